@@ -1,0 +1,115 @@
+"""Public op API. GPU tensors run the hand-written CDNA4 HIP kernels (``csrc/*.hip``) and nothing else;
+CPU tensors run the fp32 PyTorch references in ``reference.py`` (unit tests / CPU-only tooling).
+
+Kernel inventory:
+  rmsnorm / fused_add_rmsnorm / silu_mul        csrc/norm_act.hip
+  rope_kv_write (RoPE + paged KV write)         csrc/rope_kv.hip
+  attn_decode / attn_prefill / attn_merge       csrc/attention.hip   (MFMA 32x32x16 bf16, paged, split-K, cascade)
+  sample (greedy / temperature / top-k / top-p) csrc/sampling.hip
+  moe_* / grouped GEMM                          csrc/moe.hip
+  custom all-reduce                             csrc/allreduce.hip
+"""
+from __future__ import annotations
+
+import torch
+
+from . import reference as ref
+from ._ext import ext
+
+PAGE = ref.PAGE
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | None = None) -> torch.Tensor:
+    if out is None:
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+    if _gpu(x):
+        ext().rmsnorm(out.view(-1, x.shape[-1]), x.reshape(-1, x.shape[-1]), w, float(eps))
+    else:
+        out.copy_(ref.rmsnorm(x, w, eps))
+    return out
+
+
+def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                      out: torch.Tensor | None = None) -> torch.Tensor:
+    """residual <- x + residual (in place); returns rmsnorm(residual) * w (into ``out`` or a new tensor)."""
+    if out is None:
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+    if _gpu(x):
+        ext().fused_add_rmsnorm(out.view(-1, x.shape[-1]), x.reshape(-1, x.shape[-1]),
+                                residual.view(-1, x.shape[-1]), w, float(eps))
+    else:
+        y, s = ref.fused_add_rmsnorm(x, residual, w, eps)
+        residual.copy_(s)
+        out.copy_(y)
+    return out
+
+
+def silu_mul(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    F = x.shape[-1] // 2
+    if out is None:
+        out = torch.empty(*x.shape[:-1], F, dtype=x.dtype, device=x.device)
+    if _gpu(x):
+        ext().silu_mul(out.view(-1, F), x.reshape(-1, 2 * F))
+    else:
+        out.copy_(ref.silu_mul(x))
+    return out
+
+
+def rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq: int, Hkv: int) -> None:
+    if _gpu(qkv):
+        ext().rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, int(Hq), int(Hkv))
+    else:
+        ref.rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq, Hkv)
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part, lse_part, num_splits: int,
+                split_offset: int, scale: float) -> None:
+    """Split-K paged decode attention writing (O, lse2) partials [B, Hq, S_total, D] at splits
+    [split_offset, split_offset + num_splits)."""
+    if _gpu(q):
+        ext().attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part, lse_part,
+                          int(num_splits), int(split_offset), float(scale))
+        return
+    o, l2 = ref.attn_decode_full(q, k_cache, v_cache, block_tables, seq_lens, scale, kv_start)
+    B = q.shape[0]
+    S_total = out_part.shape[2]
+    lp = lse_part.view(out_part.shape[0], out_part.shape[1], S_total)
+    out_part[:B, :, split_offset:split_offset + num_splits] = 0
+    lp[:B, :, split_offset:split_offset + num_splits] = float("-inf")
+    out_part[:B, :, split_offset] = o
+    lp[:B, :, split_offset] = l2
+
+
+def attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, scale: float, out=None, out_part=None,
+                 lse_part=None) -> None:
+    """Work-item paged attention (chunked prefill / cascade prefix). ``items`` is int32 [n, 8]:
+    (q_start, q_count, bt_row, kv_lo, kv_hi, split, 0, 0)."""
+    if _gpu(q):
+        ext().attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, out, out_part, lse_part, float(scale))
+    else:
+        ref.attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale, out, out_part, lse_part)
+
+
+def attn_merge(part, lse, out, lse_out=None) -> None:
+    if _gpu(part):
+        ext().attn_merge(part, lse, out, lse_out)
+    else:
+        ref.attn_merge(part, lse, out, lse_out)
+
+
+def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, step=None, out=None) -> torch.Tensor:
+    B = logits.shape[0]
+    if out is None:
+        out = torch.empty(B, dtype=torch.long, device=logits.device)
+    if _gpu(logits):
+        ext().sample(logits, temperature, top_p, top_k, seeds, step, out)
+    else:
+        ref.sample(logits, temperature, top_p, top_k, seeds, step, out)
+    return out
+
+
+rope_cos_sin = ref.rope_cos_sin

@@ -1,0 +1,240 @@
+// Python bindings for the CDNA4 kernels. Host-side shape / dtype / device checks live here so that a malformed
+// call fails with a Python exception instead of launching a kernel on a shape it does not assume.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+typedef unsigned short bf16;  // raw bf16 storage on the host side
+
+extern "C" {
+hipError_t kafka_launch_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs, const bf16* w, int T, int d, float eps,
+                          hipStream_t st);
+hipError_t kafka_launch_fused_add_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs, bf16* resid, int64_t rs,
+                                    const bf16* w, int T, int d, float eps, hipStream_t st);
+hipError_t kafka_launch_silu_mul(bf16* out, const bf16* x, int64_t xs, int T, int F, hipStream_t st);
+hipError_t kafka_launch_rope_kv(const bf16* qkv, int64_t qkv_stride, const int64_t* positions, const float* cos_sin,
+                          bf16* q_out, int64_t q_stride, bf16* k_cache, bf16* v_cache, const int64_t* slot_mapping,
+                          int T, int Hq, int Hkv, int D, int block_size, hipStream_t st);
+hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const bf16* k_cache, const bf16* v_cache, int B,
+                              int Hkv, int G, int D, const int* block_tables, int bt_stride, const int* seq_lens,
+                              const int* kv_start, float* out_part, float* lse_part, int S, int S_total,
+                              int split_offset, float scale, hipStream_t st);
+hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride, const bf16* k_cache,
+                               const bf16* v_cache, int Hkv, int G, int D, const int* block_tables, int bt_stride,
+                               const int* q_limit, bf16* out, int64_t out_stride, float* out_part, float* lse_part,
+                               int S_total, float scale, hipStream_t st);
+hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows, int Hq, int S, int D, bf16* out,
+                             int64_t out_stride, float* lse_out, hipStream_t st);
+hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
+                         const float* top_p, const int* top_k, const int64_t* seeds, const int64_t* step,
+                         int64_t* out_tokens, hipStream_t st);
+}  // extern "C"
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_DT(x, dt) TORCH_CHECK((x).scalar_type() == (dt), #x " has wrong dtype")
+#define CHECK_LASTDIM(x) TORCH_CHECK((x).stride(-1) == 1, #x " must be contiguous in its last dim")
+#define CHECK_HIP(e)                                                                 \
+  do {                                                                               \
+    hipError_t _e = (e);                                                             \
+    TORCH_CHECK(_e == hipSuccess, "HIP launch failed: ", hipGetErrorString(_e));    \
+  } while (0)
+
+static hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+static bf16* bptr(const at::Tensor& t) { return reinterpret_cast<bf16*>(t.data_ptr()); }
+
+static void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
+  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(w, at::kBFloat16); CHECK_DT(out, at::kBFloat16);
+  CHECK_LASTDIM(x); CHECK_LASTDIM(out);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && w.is_contiguous(), "rmsnorm: x/out must be 2-D");
+  const int d = x.size(1);
+  TORCH_CHECK(d % 8 == 0 && d <= 16384 && w.numel() == d && out.size(0) == x.size(0) && out.size(1) == d,
+              "rmsnorm: bad shapes");
+  CHECK_HIP(kafka_launch_rmsnorm(bptr(out), out.stride(0), bptr(x), x.stride(0), bptr(w), x.size(0), d, eps,
+                                  cur_stream()));
+}
+
+static void fused_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor residual, at::Tensor w, double eps) {
+  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(residual, at::kBFloat16); CHECK_DT(w, at::kBFloat16);
+  CHECK_DT(out, at::kBFloat16);
+  CHECK_LASTDIM(x); CHECK_LASTDIM(out); CHECK_LASTDIM(residual);
+  TORCH_CHECK(x.dim() == 2 && residual.dim() == 2 && out.dim() == 2, "fused_add_rmsnorm: 2-D tensors expected");
+  const int d = x.size(1);
+  TORCH_CHECK(d % 8 == 0 && d <= 16384 && w.numel() == d && residual.size(0) == x.size(0) &&
+                  residual.size(1) == d && out.size(0) == x.size(0) && out.size(1) == d,
+              "fused_add_rmsnorm: bad shapes");
+  CHECK_HIP(kafka_launch_fused_add_rmsnorm(bptr(out), out.stride(0), bptr(x), x.stride(0), bptr(residual),
+                                            residual.stride(0), bptr(w), x.size(0), d, eps, cur_stream()));
+}
+
+static void silu_mul(at::Tensor out, at::Tensor x) {
+  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(out, at::kBFloat16);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && out.is_contiguous() && x.stride(1) == 1, "silu_mul: 2-D");
+  const int F = out.size(1);
+  TORCH_CHECK(x.size(1) == 2 * F && F % 8 == 0 && out.size(0) == x.size(0), "silu_mul: bad shapes");
+  CHECK_HIP(kafka_launch_silu_mul(bptr(out), bptr(x), x.stride(0), x.size(0), F, cur_stream()));
+}
+
+static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin, at::Tensor q_out,
+                          at::Tensor k_cache, at::Tensor v_cache, c10::optional<at::Tensor> slot_mapping, int64_t Hq,
+                          int64_t Hkv) {
+  CHECK_CUDA(qkv); CHECK_DT(qkv, at::kBFloat16); CHECK_DT(q_out, at::kBFloat16);
+  CHECK_DT(positions, at::kLong); CHECK_DT(cos_sin, at::kFloat);
+  CHECK_DT(k_cache, at::kBFloat16); CHECK_DT(v_cache, at::kBFloat16);
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && cos_sin.is_contiguous() &&
+                  positions.is_contiguous(), "rope_kv_write: caches/positions/cos_sin must be contiguous");
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4, "k/v cache must be [blocks, Hkv, ., .]");
+  const int D = k_cache.size(3);
+  const int bs = k_cache.size(2);
+  TORCH_CHECK(k_cache.size(1) == Hkv && v_cache.size(1) == Hkv && v_cache.size(2) == D && v_cache.size(3) == bs &&
+                  v_cache.size(0) == k_cache.size(0), "rope_kv_write: cache shape mismatch");
+  TORCH_CHECK(bs == 16, "page size must be 16");
+  TORCH_CHECK(D == 128 || D == 64, "head dim must be 64 or 128");
+  const int T = qkv.size(0);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv shape");
+  TORCH_CHECK(positions.numel() == T && cos_sin.dim() == 2 && cos_sin.size(1) == D, "positions/cos_sin shape");
+  TORCH_CHECK(q_out.dim() == 3 && q_out.size(0) == T && q_out.size(1) == Hq && q_out.size(2) == D &&
+                  q_out.stride(2) == 1 && q_out.stride(1) == D, "q_out shape");
+  const int64_t* sm = nullptr;
+  if (slot_mapping.has_value()) {
+    CHECK_DT(slot_mapping.value(), at::kLong);
+    TORCH_CHECK(slot_mapping->numel() == T && slot_mapping->is_contiguous(), "slot_mapping shape");
+    sm = slot_mapping->data_ptr<int64_t>();
+  }
+  CHECK_HIP(kafka_launch_rope_kv(bptr(qkv), qkv.stride(0), positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
+                                  bptr(q_out), q_out.stride(0), bptr(k_cache), bptr(v_cache), sm, T, Hq, Hkv, D, bs,
+                                  cur_stream()));
+}
+
+static void check_cache_pair(const at::Tensor& k_cache, const at::Tensor& v_cache) {
+  CHECK_DT(k_cache, at::kBFloat16); CHECK_DT(v_cache, at::kBFloat16);
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous(), "caches must be contiguous");
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4 && k_cache.size(2) == 16 && k_cache.size(3) == 128 &&
+                  v_cache.size(2) == 128 && v_cache.size(3) == 16 && k_cache.size(0) == v_cache.size(0) &&
+                  k_cache.size(1) == v_cache.size(1),
+              "paged caches must be K[blocks,Hkv,16,128] / V[blocks,Hkv,128,16]");
+}
+
+static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
+                        at::Tensor seq_lens, c10::optional<at::Tensor> kv_start, at::Tensor out_part,
+                        at::Tensor lse_part, int64_t num_splits, int64_t split_offset, double scale) {
+  CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
+  CHECK_DT(block_tables, at::kInt); CHECK_DT(seq_lens, at::kInt); CHECK_DT(out_part, at::kFloat);
+  CHECK_DT(lse_part, at::kFloat);
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == 128 && q.size(2) == 128, "q must be [B, Hq, 128]");
+  const int B = q.size(0), Hq = q.size(1), Hkv = k_cache.size(1);
+  TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 8, "decode kernel needs Hq/Hkv <= 8");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.stride(1) == 1, "block_tables");
+  TORCH_CHECK(seq_lens.numel() >= B && seq_lens.is_contiguous(), "seq_lens");
+  TORCH_CHECK(out_part.is_contiguous() && out_part.dim() == 4 && out_part.size(0) >= B && out_part.size(1) == Hq &&
+                  out_part.size(3) == 128, "out_part must be [B, Hq, S_total, 128]");
+  const int S_total = out_part.size(2);
+  TORCH_CHECK(split_offset >= 0 && num_splits >= 1 && split_offset + num_splits <= S_total, "split range");
+  TORCH_CHECK(lse_part.is_contiguous() && lse_part.numel() >= (int64_t)B * Hq * S_total, "lse_part");
+  const int* ks = nullptr;
+  if (kv_start.has_value()) {
+    CHECK_DT(kv_start.value(), at::kInt);
+    TORCH_CHECK(kv_start->numel() >= B && kv_start->is_contiguous(), "kv_start");
+    ks = kv_start->data_ptr<int>();
+  }
+  CHECK_HIP(kafka_launch_attn_decode(bptr(q), q.stride(0), bptr(k_cache), bptr(v_cache), B, Hkv, Hq / Hkv, 128,
+                                      block_tables.data_ptr<int>(), block_tables.stride(0), seq_lens.data_ptr<int>(),
+                                      ks, out_part.data_ptr<float>(), lse_part.data_ptr<float>(), num_splits,
+                                      S_total, split_offset, scale, cur_stream()));
+}
+
+static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
+                         at::Tensor block_tables, at::Tensor q_limit, c10::optional<at::Tensor> out,
+                         c10::optional<at::Tensor> out_part, c10::optional<at::Tensor> lse_part, double scale) {
+  CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
+  CHECK_DT(items, at::kInt); CHECK_DT(block_tables, at::kInt); CHECK_DT(q_limit, at::kInt);
+  TORCH_CHECK(items.is_contiguous() && items.dim() == 2 && items.size(1) == 8, "items must be [n, 8] int32");
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == 128 && q.size(2) == 128, "q must be [T, Hq, 128]");
+  const int T = q.size(0), Hq = q.size(1), Hkv = k_cache.size(1);
+  TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
+  const int G = Hq / Hkv;
+  TORCH_CHECK(G <= 32 && 128 % G == 0, "prefill kernel needs Hq/Hkv dividing 128");
+  TORCH_CHECK(q_limit.numel() >= T && q_limit.is_contiguous(), "q_limit");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.stride(1) == 1, "block_tables");
+  bf16* op = nullptr;
+  int64_t os = 0;
+  if (out.has_value()) {
+    CHECK_DT(out.value(), at::kBFloat16);
+    TORCH_CHECK(out->dim() == 3 && out->size(0) >= T && out->size(1) == Hq && out->size(2) == 128 &&
+                    out->stride(2) == 1 && out->stride(1) == 128, "out must be [T, Hq, 128]");
+    op = bptr(out.value());
+    os = out->stride(0);
+  }
+  float* pp = nullptr;
+  float* lp = nullptr;
+  int S_total = 0;
+  if (out_part.has_value()) {
+    TORCH_CHECK(lse_part.has_value(), "lse_part required with out_part");
+    CHECK_DT(out_part.value(), at::kFloat); CHECK_DT(lse_part.value(), at::kFloat);
+    TORCH_CHECK(out_part->is_contiguous() && out_part->dim() == 4 && out_part->size(0) >= T &&
+                    out_part->size(1) == Hq && out_part->size(3) == 128, "out_part must be [T, Hq, S, 128]");
+    S_total = out_part->size(2);
+    TORCH_CHECK(lse_part->is_contiguous() && lse_part->numel() >= (int64_t)T * Hq * S_total, "lse_part");
+    pp = out_part->data_ptr<float>();
+    lp = lse_part->data_ptr<float>();
+  }
+  TORCH_CHECK(op != nullptr || pp != nullptr, "attn_prefill needs out or out_part");
+  CHECK_HIP(kafka_launch_attn_prefill(items.data_ptr<int>(), items.size(0), bptr(q), q.stride(0), bptr(k_cache),
+                                       bptr(v_cache), Hkv, G, 128, block_tables.data_ptr<int>(),
+                                       block_tables.stride(0), q_limit.data_ptr<int>(), op, os, pp, lp, S_total,
+                                       scale, cur_stream()));
+}
+
+static void attn_merge(at::Tensor part, at::Tensor lse, at::Tensor out, c10::optional<at::Tensor> lse_out) {
+  CHECK_CUDA(part); CHECK_DT(part, at::kFloat); CHECK_DT(lse, at::kFloat); CHECK_DT(out, at::kBFloat16);
+  TORCH_CHECK(part.is_contiguous() && part.dim() == 4 && part.size(3) == 128, "part must be [rows, Hq, S, 128]");
+  const int rows = out.size(0), Hq = part.size(1), S = part.size(2);
+  TORCH_CHECK(part.size(0) >= rows && out.dim() == 3 && out.size(1) == Hq && out.size(2) == 128 &&
+                  out.stride(2) == 1 && out.stride(1) == 128, "out must be [rows, Hq, 128]");
+  TORCH_CHECK(lse.is_contiguous() && lse.numel() >= (int64_t)rows * Hq * S, "lse");
+  float* lo = nullptr;
+  if (lse_out.has_value()) {
+    CHECK_DT(lse_out.value(), at::kFloat);
+    TORCH_CHECK(lse_out->numel() >= (int64_t)rows * Hq, "lse_out");
+    lo = lse_out->data_ptr<float>();
+  }
+  CHECK_HIP(kafka_launch_attn_merge(part.data_ptr<float>(), lse.data_ptr<float>(), rows, Hq, S, 128, bptr(out),
+                                     out.stride(0), lo, cur_stream()));
+}
+
+static void sample(at::Tensor logits, c10::optional<at::Tensor> temperature, c10::optional<at::Tensor> top_p,
+                   c10::optional<at::Tensor> top_k, c10::optional<at::Tensor> seeds, c10::optional<at::Tensor> step,
+                   at::Tensor out) {
+  CHECK_CUDA(logits); CHECK_DT(out, at::kLong);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [B, V]");
+  const bool is_bf16 = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(is_bf16 || logits.scalar_type() == at::kFloat, "logits must be bf16 or fp32");
+  const int B = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(out.numel() >= B && out.is_contiguous(), "out");
+  TORCH_CHECK(logits.stride(0) % 8 == 0, "logits row stride must be a multiple of 8");
+  auto fp = [&](const c10::optional<at::Tensor>& t, at::ScalarType dt) -> void* {
+    if (!t.has_value()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == dt && t->is_contiguous() && t->numel() >= B, "sampling param dtype/shape");
+    return t->data_ptr();
+  };
+  void* st = nullptr;
+  if (step.has_value()) {
+    TORCH_CHECK(step->scalar_type() == at::kLong && step->numel() >= 1, "step must be int64[1]");
+    st = step->data_ptr();
+  }
+  CHECK_HIP(kafka_launch_sample(logits.data_ptr(), is_bf16, logits.stride(0), B, V,
+                                 (const float*)fp(temperature, at::kFloat), (const float*)fp(top_p, at::kFloat),
+                                 (const int*)fp(top_k, at::kInt), (const int64_t*)fp(seeds, at::kLong),
+                                 (const int64_t*)st, out.data_ptr<int64_t>(), cur_stream()));
+}
+
+PYBIND11_MODULE(_kafka_ops, m) {
+  m.doc() = "kafka_llm_service_amd CDNA4 (gfx950) HIP kernels";
+  m.def("rmsnorm", &rmsnorm);
+  m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
+  m.def("silu_mul", &silu_mul);
+  m.def("rope_kv_write", &rope_kv_write);
+  m.def("attn_decode", &attn_decode);
+  m.def("attn_prefill", &attn_prefill);
+  m.def("attn_merge", &attn_merge);
+  m.def("sample", &sample);
+}

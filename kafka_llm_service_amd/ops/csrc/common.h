@@ -1,0 +1,82 @@
+// Shared device helpers for the CDNA4 (gfx950) kernels of kafka_llm_service_amd.
+//
+// Conventions used by every kernel in this directory:
+//   * wave = 64 lanes; block sizes are multiples of 64.
+//   * bf16 is the clang `__bf16` scalar type; casts f32->bf16 lower to v_cvt_pk_bf16_f32 (RNE, NaN-preserving).
+//   * bf16/f32 global traffic is vectorised to 16 B per lane (bf16x8 / f32x4).
+//   * MFMA fragments follow the gfx950 maps of v_mfma_f32_32x32x16_bf16:
+//       A: lane l holds A[row l&31][k = 8*(l>>5) + j], j = 0..7
+//       B: lane l holds B[k = 8*(l>>5) + j][col l&31]
+//       C/D: lane l, reg i -> row (i&3) + 8*(i>>2) + 4*(l>>5), col l&31
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define KAFKA_WAVE 64
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `red` must hold NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  __syncthreads();
+  return t;
+}
+
+template <int NT>
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float t = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t = fmaxf(t, red[i]);
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ bf16x8 load_bf16x8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ void store_bf16x8(bf16* p, bf16x8 v) { *reinterpret_cast<bf16x8*>(p) = v; }
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Counter-based RNG (splitmix64 finaliser): deterministic given (seed, stream, index).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// Uniform in (0, 1].
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t stream, uint64_t idx) {
+  uint64_t r = mix64(seed ^ mix64(stream * 0x632BE59BD9B4E019ull + idx));
+  return ((float)(r >> 40) + 1.0f) * (1.0f / 16777216.0f);
+}

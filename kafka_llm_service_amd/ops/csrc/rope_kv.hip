@@ -1,0 +1,96 @@
+// Rotary embedding on Q/K fused with the paged KV-cache write (gfx950).
+//
+// Input is the fused QKV projection output [T, (Hq + 2*Hkv) * D]. One workgroup per token:
+//   * Q heads: rotate-half RoPE -> q_out[T, Hq, D]
+//   * K heads: rotate-half RoPE -> k_cache page  [num_blocks, Hkv, 16, D]   (key-major rows, 256 B per key)
+//   * V heads: copy            -> v_cache page  [num_blocks, Hkv, D, 16]   (d-major: V^T per page)
+// The V^T page stores key offset o at position swap_bits_2_3(o). With that permutation the PV step of the
+// attention kernels (O^T = V^T . P, P taken straight from the S^T accumulator registers of
+// v_mfma_f32_32x32x16_bf16) reads each lane's 8-key A-fragment as ONE contiguous 16-byte load:
+// accumulator element j of lane-half h holds key 8*(j>>2) + 4*h + (j&3) of a 16-key page, which lands at
+// page position 8*h + j.
+// cos/sin come from a host-built table [max_pos, D] (cos in [0, D/2), sin in [D/2, D)) so the kernel does no
+// transcendental math (llama3 / linear / none scaling is folded into the table on the host).
+#include "common.h"
+
+namespace kafka {
+
+__device__ __forceinline__ int vt_pos(int o) { return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1); }
+
+template <int D>
+__global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ qkv, int64_t qkv_stride,
+                                                       const int64_t* __restrict__ positions,
+                                                       const float* __restrict__ cos_sin,
+                                                       bf16* __restrict__ q_out, int64_t q_stride,
+                                                       bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
+                                                       const int64_t* __restrict__ slot_mapping, int Hq, int Hkv,
+                                                       int block_size) {
+  constexpr int HALF = D / 2;
+  constexpr int RU = HALF / 8;  // rope units (8 rotation pairs each) per head
+  constexpr int VU = D / 8;     // v copy units (8 elements) per head
+  const int64_t t = blockIdx.x;
+  const int64_t pos = positions[t];
+  const int64_t slot = slot_mapping ? slot_mapping[t] : -1;
+  const bf16* row = qkv + t * qkv_stride;
+  const float* cs = cos_sin + pos * D;
+  const int n_rope = (Hq + Hkv) * RU;
+  const int n_total = n_rope + Hkv * VU;
+  const int64_t blk = slot >= 0 ? slot / block_size : 0;
+  const int off = slot >= 0 ? (int)(slot % block_size) : 0;
+  for (int u = threadIdx.x; u < n_total; u += 256) {
+    if (u < n_rope) {
+      const int head = u / RU;
+      const int c = (u % RU) * 8;
+      const bf16* src = row + head * D;
+      bf16x8 x1 = load_bf16x8(src + c);
+      bf16x8 x2 = load_bf16x8(src + HALF + c);
+      f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + c);
+      f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + c + 4);
+      f32x4 s0 = *reinterpret_cast<const f32x4*>(cs + HALF + c);
+      f32x4 s1 = *reinterpret_cast<const f32x4*>(cs + HALF + c + 4);
+      float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+      float sv[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+      bf16x8 o1, o2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = (float)x1[j], b = (float)x2[j];
+        o1[j] = (bf16)(a * cv[j] - b * sv[j]);
+        o2[j] = (bf16)(b * cv[j] + a * sv[j]);
+      }
+      if (head < Hq) {
+        bf16* dst = q_out + t * q_stride + head * D;
+        store_bf16x8(dst + c, o1);
+        store_bf16x8(dst + HALF + c, o2);
+      } else if (slot >= 0) {
+        const int kh = head - Hq;
+        bf16* dst = k_cache + ((blk * Hkv + kh) * block_size + off) * D;
+        store_bf16x8(dst + c, o1);
+        store_bf16x8(dst + HALF + c, o2);
+      }
+    } else if (slot >= 0) {
+      const int v = u - n_rope;
+      const int vh = v / VU;
+      const int c = (v % VU) * 8;
+      bf16x8 x = load_bf16x8(row + (Hq + Hkv + vh) * D + c);
+      bf16* dst = v_cache + (blk * Hkv + vh) * (int64_t)D * block_size + vt_pos(off);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dst[(int64_t)(c + j) * block_size] = x[j];
+    }
+  }
+}
+
+extern "C" hipError_t kafka_launch_rope_kv(const bf16* qkv, int64_t qkv_stride, const int64_t* positions, const float* cos_sin,
+                          bf16* q_out, int64_t q_stride, bf16* k_cache, bf16* v_cache, const int64_t* slot_mapping,
+                          int T, int Hq, int Hkv, int D, int block_size, hipStream_t st) {
+  if (T == 0) return hipSuccess;
+  if (D != 128 && D != 64) return hipErrorInvalidValue;
+  if (D == 128)
+    rope_kv_kernel<128><<<T, 256, 0, st>>>(qkv, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache, v_cache,
+                                           slot_mapping, Hq, Hkv, block_size);
+  else
+    rope_kv_kernel<64><<<T, 256, 0, st>>>(qkv, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache, v_cache,
+                                          slot_mapping, Hq, Hkv, block_size);
+  return hipGetLastError();
+}
+
+}  // namespace kafka

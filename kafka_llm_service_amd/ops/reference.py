@@ -1,0 +1,224 @@
+"""Plain-PyTorch fp32 reference implementations of every HIP kernel.
+
+They define the numerics the CDNA4 kernels are tested against, and they are the CPU execution path used by the
+unit tests (no GPU in CI). They use exactly the same tensor layouts as the kernels, including the paged KV layout
+  K page: [num_blocks, Hkv, 16, D]      V page: [num_blocks, Hkv, D, 16]  (V^T, key offset o at vt_pos(o)).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+PAGE = 16
+LOG2E = 1.4426950408889634
+
+
+def vt_pos(o: torch.Tensor | int):
+    """Position of key offset ``o`` inside a V^T page (swap bits 2 and 3)."""
+    if isinstance(o, int):
+        return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1)
+    return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1)
+
+
+_VT_PERM = torch.tensor([vt_pos(o) for o in range(PAGE)], dtype=torch.long)
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (xf * r * w.float()).to(x.dtype)
+
+
+def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float):
+    s = (x.float() + residual.float()).to(x.dtype)
+    return rmsnorm(s, w, eps), s
+
+
+def silu_mul(x: torch.Tensor) -> torch.Tensor:
+    F = x.shape[-1] // 2
+    g, u = x[..., :F].float(), x[..., F:].float()
+    return (torch.nn.functional.silu(g) * u).to(x.dtype)
+
+
+def rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq: int, Hkv: int) -> None:
+    T = qkv.shape[0]
+    D = k_cache.shape[-1]
+    half = D // 2
+    x = qkv.float().view(T, Hq + 2 * Hkv, D)
+    cs = cos_sin[positions.long()].float()  # [T, D]
+    cos, sin = cs[:, None, :half], cs[:, None, half:]
+    qk = x[:, : Hq + Hkv]
+    x1, x2 = qk[..., :half], qk[..., half:]
+    rot = torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(qkv.dtype)
+    q_out.copy_(rot[:, :Hq])
+    if slot_mapping is None:
+        return
+    k = rot[:, Hq:]
+    v = x[:, Hq + Hkv:].to(qkv.dtype)
+    for t in range(T):
+        s = int(slot_mapping[t])
+        if s < 0:
+            continue
+        blk, off = divmod(s, PAGE)
+        k_cache[blk, :, off, :] = k[t]
+        v_cache[blk, :, :, vt_pos(off)] = v[t]
+
+
+def gather_kv(k_cache, v_cache, block_table, length: int):
+    """Materialise [length, Hkv, D] K and V for one sequence from the paged caches (fp32)."""
+    nb = (length + PAGE - 1) // PAGE
+    ids = block_table[:nb].long()
+    k = k_cache[ids].float()  # [nb, Hkv, 16, D]
+    v = v_cache[ids].float()  # [nb, Hkv, D, 16]
+    v = v[..., _VT_PERM.to(v.device)]  # undo the page permutation -> [nb, Hkv, D, 16] natural key order
+    k = k.permute(0, 2, 1, 3).reshape(nb * PAGE, k.shape[1], k.shape[3])[:length]
+    v = v.permute(0, 3, 1, 2).reshape(nb * PAGE, v.shape[1], v.shape[2])[:length]
+    return k, v
+
+
+def _attend(q, k, v, mask, scale):
+    """q [M, G, D], k/v [N, D] (one kv head), mask [M, N] bool -> (o [M, G, D], lse2 [M, G])."""
+    s = torch.einsum("mgd,nd->mgn", q, k) * scale
+    s = s.masked_fill(~mask[:, None, :], float("-inf"))
+    m = s.amax(-1, keepdim=True)
+    m_use = torch.where(torch.isinf(m), torch.zeros_like(m), m)
+    p = torch.exp(s - m_use)
+    l = p.sum(-1, keepdim=True)
+    o = torch.einsum("mgn,nd->mgd", p, v) / torch.where(l > 0, l, torch.ones_like(l))
+    lse = torch.where(l[..., 0] > 0, (m_use[..., 0] + torch.log(l[..., 0])) * LOG2E,
+                      torch.full_like(l[..., 0], float("-inf")))
+    return o, lse
+
+
+def attn_decode_full(q, k_cache, v_cache, block_tables, seq_lens, scale, kv_start=None):
+    """Reference single-token paged attention over keys [kv_start, seq_len). q [B, Hq, D] -> (o fp32, lse2)."""
+    B, Hq, D = q.shape
+    Hkv = k_cache.shape[1]
+    G = Hq // Hkv
+    out = torch.zeros(B, Hq, D, dtype=torch.float32, device=q.device)
+    lse = torch.full((B, Hq), float("-inf"), dtype=torch.float32, device=q.device)
+    for b in range(B):
+        L = int(seq_lens[b])
+        s0 = int(kv_start[b]) if kv_start is not None else 0
+        if L <= s0:
+            continue
+        k, v = gather_kv(k_cache, v_cache, block_tables[b], L)
+        for h in range(Hkv):
+            qh = q[b, h * G:(h + 1) * G].float()[None]
+            mask = torch.zeros(1, L, dtype=torch.bool, device=q.device)
+            mask[:, s0:L] = True
+            o, l2 = _attend(qh, k[:, h], v[:, h], mask, scale)
+            out[b, h * G:(h + 1) * G] = o[0]
+            lse[b, h * G:(h + 1) * G] = l2[0]
+    return out, lse
+
+
+def attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale, out=None, out_part=None,
+                       lse_part=None):
+    """Reference for the work-item prefill / cascade kernel (see ops/csrc/attention.hip)."""
+    T, Hq, D = q.shape
+    Hkv = k_cache.shape[1]
+    G = Hq // Hkv
+    for it in items.tolist():
+        q_start, q_count, bt_row, lo, hi, split = it[:6]
+        if q_count <= 0:
+            continue
+        toks = torch.arange(q_start, q_start + q_count, device=q.device)
+        lim = q_limit[toks].long()
+        kmax = int(min(hi, int(lim.max()) + 1))
+        if kmax <= lo:
+            o = torch.zeros(q_count, Hq, D, device=q.device)
+            l2 = torch.full((q_count, Hq), float("-inf"), device=q.device)
+        else:
+            k, v = gather_kv(k_cache, v_cache, block_tables[bt_row], kmax)
+            pos = torch.arange(kmax, device=q.device)
+            mask = (pos[None] >= lo) & (pos[None] < hi) & (pos[None] <= lim[:, None])
+            o = torch.zeros(q_count, Hq, D, device=q.device)
+            l2 = torch.zeros(q_count, Hq, device=q.device)
+            for h in range(Hkv):
+                oh, lh = _attend(q[toks, h * G:(h + 1) * G].float(), k[:, h], v[:, h], mask, scale)
+                o[:, h * G:(h + 1) * G] = oh
+                l2[:, h * G:(h + 1) * G] = lh
+        if split < 0:
+            out[toks] = o.to(out.dtype)
+        else:
+            out_part[toks, :, split] = o
+            lse_part.view(out_part.shape[0], Hq, out_part.shape[2])[toks, :, split] = l2
+
+
+def attn_merge(part, lse, out, lse_out=None):
+    rows = out.shape[0]
+    p = part[:rows]
+    l = lse.view(part.shape[0], part.shape[1], part.shape[2])[:rows]
+    M = l.amax(-1, keepdim=True)
+    Mu = torch.where(torch.isinf(M), torch.zeros_like(M), M)
+    f = torch.exp2(l - Mu)
+    L = f.sum(-1, keepdim=True)
+    o = (f[..., None] * p).sum(2) / torch.where(L > 0, L, torch.ones_like(L))
+    out.copy_(o.to(out.dtype))
+    if lse_out is not None:
+        lse_out.view(rows, -1).copy_(torch.where(L[..., 0] > 0, Mu[..., 0] + torch.log2(L[..., 0]),
+                                                 torch.full_like(L[..., 0], float("-inf"))))
+
+
+def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, step=None, out=None):
+    """CPU sampler with the same semantics (not the same random stream) as the HIP kernel."""
+    B, V = logits.shape
+    x = logits.float()
+    res = torch.empty(B, dtype=torch.long, device=logits.device)
+    for b in range(B):
+        t = float(temperature[b]) if temperature is not None else 0.0
+        if not t > 0:
+            res[b] = int(torch.argmax(x[b]))
+            continue
+        z = x[b] / t
+        p = torch.softmax(z, -1)
+        tp = float(top_p[b]) if top_p is not None else 1.0
+        tk = int(top_k[b]) if top_k is not None else 0
+        order = torch.argsort(p, descending=True)
+        ps = p[order]
+        keep = torch.ones(V, dtype=torch.bool, device=p.device)
+        if tk > 0:
+            keep[tk:] = False
+        if tp < 1.0:
+            above = torch.cumsum(ps, 0) - ps
+            keep &= above < tp
+        ps = torch.where(keep, ps, torch.zeros_like(ps))
+        gen = torch.Generator(device="cpu")
+        seed = int(seeds[b]) if seeds is not None else 0x1234
+        stepv = int(step[0]) if step is not None else 0
+        gen.manual_seed((seed * 1000003 + stepv) & 0x7FFFFFFFFFFFFFFF)
+        idx = torch.multinomial(ps.cpu() / ps.sum().cpu(), 1, generator=gen)
+        res[b] = order[idx.to(order.device)]
+    if out is not None:
+        out[:B].copy_(res)
+        return out
+    return res
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float, scaling: dict | None = None,
+                 device="cpu") -> torch.Tensor:
+    """[max_pos, D] fp32 table: cos of the D/2 frequencies then sin (rotate-half / NeoX convention).
+
+    ``scaling`` follows the HF ``rope_scaling`` dict: ``{"rope_type": "llama3", "factor", "low_freq_factor",
+    "high_freq_factor", "original_max_position_embeddings"}`` or ``{"rope_type": "linear", "factor"}``.
+    """
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling:
+        kind = scaling.get("rope_type", scaling.get("type"))
+        if kind == "llama3":
+            factor = scaling["factor"]
+            lf, hf = scaling["low_freq_factor"], scaling["high_freq_factor"]
+            old = scaling["original_max_position_embeddings"]
+            low_wl, high_wl = old / lf, old / hf
+            wl = 2 * math.pi / inv
+            smooth = (old / wl - lf) / (hf - lf)
+            scaled = torch.where(wl > low_wl, inv / factor, inv)
+            mid = (wl <= low_wl) & (wl >= high_wl)
+            inv = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+        elif kind == "linear":
+            inv = inv / scaling["factor"]
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return torch.cat([f.cos(), f.sin()], dim=-1).float().to(device)

@@ -1,0 +1,218 @@
+"""Numerics of every HIP kernel against the plain-PyTorch fp32 reference of the same op (ops/reference.py)."""
+import math
+
+import pytest
+import torch
+
+from kafka_llm_service_amd import ops
+from kafka_llm_service_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, atol, rtol=0.0, msg=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    tol = atol + rtol * b.abs().max().item()
+    assert err <= tol, f"{msg} max err {err} > {tol}"
+
+
+@pytest.mark.parametrize("T,d", [(1, 4096), (64, 4096), (37, 8192), (5, 1024), (3, 4104)])
+def test_rmsnorm(cuda, T, d):
+    torch.manual_seed(0)
+    x = torch.randn(T, d, device=cuda, dtype=torch.bfloat16)
+    w = torch.randn(d, device=cuda, dtype=torch.bfloat16)
+    y = ops.rmsnorm(x, w, 1e-5)
+    _close(y, ref.rmsnorm(x.cpu(), w.cpu(), 1e-5), atol=0.05, rtol=0.01, msg="rmsnorm")
+
+
+@pytest.mark.parametrize("T,d", [(1, 4096), (64, 4096), (130, 8192)])
+def test_fused_add_rmsnorm(cuda, T, d):
+    torch.manual_seed(1)
+    x = torch.randn(T, d, device=cuda, dtype=torch.bfloat16)
+    r = torch.randn(T, d, device=cuda, dtype=torch.bfloat16)
+    w = torch.randn(d, device=cuda, dtype=torch.bfloat16)
+    y_ref, s_ref = ref.fused_add_rmsnorm(x.cpu(), r.cpu(), w.cpu(), 1e-5)
+    y = ops.fused_add_rmsnorm(x, r, w, 1e-5)
+    _close(r, s_ref, atol=1e-2, msg="residual")
+    _close(y, y_ref, atol=0.05, rtol=0.01, msg="norm")
+
+
+@pytest.mark.parametrize("T,F", [(1, 14336), (64, 14336), (7, 1024)])
+def test_silu_mul(cuda, T, F):
+    x = torch.randn(T, 2 * F, device=cuda, dtype=torch.bfloat16)
+    _close(ops.silu_mul(x), ref.silu_mul(x.cpu()), atol=0.03, rtol=0.01)
+
+
+def _make_cache(nb, Hkv, D=128, device="cpu"):
+    k = torch.zeros(nb, Hkv, 16, D, dtype=torch.bfloat16, device=device)
+    v = torch.zeros(nb, Hkv, D, 16, dtype=torch.bfloat16, device=device)
+    return k, v
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1)])
+def test_rope_kv_write(cuda, Hq, Hkv):
+    torch.manual_seed(2)
+    D, T, nb = 128, 40, 16
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=cuda, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=cuda, dtype=torch.long)
+    cs = ref.rope_cos_sin(8192, D, 500000.0, {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                               "high_freq_factor": 4.0, "original_max_position_embeddings": 8192},
+                          device=cuda)
+    slots = torch.randperm(nb * 16, device=cuda)[:T].long()
+    slots[3] = -1
+    q = torch.empty(T, Hq, D, device=cuda, dtype=torch.bfloat16)
+    k, v = _make_cache(nb, Hkv, D, cuda)
+    ops.rope_kv_write(qkv, pos, cs, q, k, v, slots, Hq, Hkv)
+    q2 = torch.empty(T, Hq, D, dtype=torch.bfloat16)
+    k2, v2 = _make_cache(nb, Hkv, D)
+    ref.rope_kv_write(qkv.cpu(), pos.cpu(), cs.cpu(), q2, k2, v2, slots.cpu(), Hq, Hkv)
+    _close(q, q2, atol=0.03, rtol=0.01, msg="q")
+    _close(k, k2, atol=0.03, rtol=0.01, msg="k")
+    assert torch.equal(v.cpu(), v2), "v cache"
+
+
+def _random_paged(B, lens, Hkv, device, seed=0, D=128):
+    g = torch.Generator().manual_seed(seed)
+    max_nb = max((l + 15) // 16 for l in lens)
+    nb_total = sum((l + 15) // 16 for l in lens) + 4
+    perm = torch.randperm(nb_total, generator=g)
+    bt = torch.zeros(B, max_nb + 2, dtype=torch.int32)
+    c = 0
+    for b, l in enumerate(lens):
+        n = (l + 15) // 16
+        bt[b, :n] = perm[c:c + n].int()
+        c += n
+    k = torch.randn(nb_total, Hkv, 16, D, generator=g).to(torch.bfloat16)
+    v = torch.randn(nb_total, Hkv, D, 16, generator=g).to(torch.bfloat16)
+    return k.to(device), v.to(device), bt.to(device)
+
+
+@pytest.mark.parametrize("Hq,Hkv,lens,S", [
+    (32, 8, [1, 17, 300, 2049], 4),
+    (32, 8, [4096] * 3, 8),
+    (8, 1, [33, 1000], 2),
+    (32, 8, [5, 64], 1),
+])
+def test_attn_decode(cuda, Hq, Hkv, lens, S):
+    torch.manual_seed(3)
+    B, D = len(lens), 128
+    k, v, bt = _random_paged(B, lens, Hkv, cuda)
+    q = torch.randn(B, Hq, D, device=cuda, dtype=torch.bfloat16)
+    sl = torch.tensor(lens, dtype=torch.int32, device=cuda)
+    scale = 1 / math.sqrt(D)
+    part = torch.empty(B, Hq, S, D, device=cuda)
+    lse = torch.empty(B, Hq, S, device=cuda)
+    ops.attn_decode(q, k, v, bt, sl, None, part, lse, S, 0, scale)
+    out = torch.empty(B, Hq, D, device=cuda, dtype=torch.bfloat16)
+    lse_o = torch.empty(B, Hq, device=cuda)
+    ops.attn_merge(part, lse, out, lse_o)
+    o_ref, l_ref = ref.attn_decode_full(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), sl.cpu(), scale)
+    _close(out, o_ref, atol=0.02, msg="decode out")
+    _close(lse_o, l_ref, atol=0.02, msg="decode lse")
+
+
+def test_attn_decode_kv_start_cascade(cuda):
+    """Cascade: prefix partial from attn_prefill (rows = decode seqs) + suffix partial from attn_decode == full."""
+    torch.manual_seed(4)
+    Hq, Hkv, D = 32, 8, 128
+    P = 160  # shared prefix length (multiple of 16)
+    suffix = [3, 40, 257]
+    B = len(suffix)
+    lens = [P + s for s in suffix]
+    g = torch.Generator().manual_seed(5)
+    n_pref = P // 16
+    nb_total = n_pref + sum((s + 15) // 16 + 1 for s in suffix) + 2
+    k = torch.randn(nb_total, Hkv, 16, D, generator=g).to(torch.bfloat16).to(cuda)
+    v = torch.randn(nb_total, Hkv, D, 16, generator=g).to(torch.bfloat16).to(cuda)
+    bt = torch.zeros(B, 64, dtype=torch.int32)
+    c = n_pref
+    for b, s in enumerate(suffix):
+        bt[b, :n_pref] = torch.arange(n_pref)
+        n = (lens[b] + 15) // 16 - n_pref
+        bt[b, n_pref:n_pref + n] = torch.arange(c, c + n)
+        c += n
+    bt = bt.to(cuda)
+    q = torch.randn(B, Hq, D, device=cuda, dtype=torch.bfloat16)
+    sl = torch.tensor(lens, dtype=torch.int32, device=cuda)
+    ks = torch.full((B,), P, dtype=torch.int32, device=cuda)
+    scale = 1 / math.sqrt(D)
+    S_pre, S_suf = 2, 3
+    S_total = S_pre + S_suf
+    part = torch.empty(B, Hq, S_total, D, device=cuda)
+    lse = torch.empty(B, Hq, S_total, device=cuda)
+    # prefix: rows are the B decode sequences, all using block table row 0 restricted to [0, P), split in 2 chunks
+    items = torch.tensor([[0, B, 0, 0, 96, 0, 0, 0], [0, B, 0, 96, P, 1, 0, 0]], dtype=torch.int32, device=cuda)
+    q_limit = torch.full((B,), 1 << 30, dtype=torch.int32, device=cuda)
+    ops.attn_prefill(items, q, k, v, bt, q_limit, scale, out_part=part, lse_part=lse)
+    ops.attn_decode(q, k, v, bt, sl, ks, part, lse, S_suf, S_pre, scale)
+    out = torch.empty(B, Hq, D, device=cuda, dtype=torch.bfloat16)
+    ops.attn_merge(part, lse, out)
+    o_ref, _ = ref.attn_decode_full(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), sl.cpu(), scale)
+    _close(out, o_ref, atol=0.02, msg="cascade")
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8)])
+def test_attn_prefill_causal(cuda, Hq, Hkv):
+    torch.manual_seed(6)
+    D = 128
+    G = Hq // Hkv
+    ctx = [0, 37, 512]     # cached context per sequence
+    qlen = [70, 1, 33]     # new tokens per sequence
+    B = len(ctx)
+    lens = [c + n for c, n in zip(ctx, qlen)]
+    k, v, bt = _random_paged(B, lens, Hkv, cuda, seed=7)
+    T = sum(qlen)
+    q = torch.randn(T, Hq, D, device=cuda, dtype=torch.bfloat16)
+    q_limit = torch.empty(T, dtype=torch.int32)
+    items = []
+    tile = 128 // G
+    t0 = 0
+    for b in range(B):
+        for i in range(qlen[b]):
+            q_limit[t0 + i] = ctx[b] + i
+        for s in range(0, qlen[b], tile):
+            items.append([t0 + s, min(tile, qlen[b] - s), b, 0, lens[b], -1, 0, 0])
+        t0 += qlen[b]
+    items = torch.tensor(items, dtype=torch.int32, device=cuda)
+    q_limit = q_limit.to(cuda)
+    out = torch.zeros(T, Hq, D, device=cuda, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    ops.attn_prefill(items, q, k, v, bt, q_limit, scale, out=out)
+    out_ref = torch.zeros(T, Hq, D, dtype=torch.bfloat16)
+    ref.attn_prefill_items(items.cpu(), q.cpu(), k.cpu(), v.cpu(), bt.cpu(), q_limit.cpu(), scale, out=out_ref)
+    _close(out, out_ref, atol=0.02, msg="prefill")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_sample_greedy(cuda, dtype):
+    torch.manual_seed(8)
+    B, V = 17, 128256
+    logits = torch.randn(B, V, device=cuda).to(dtype)
+    temp = torch.zeros(B, device=cuda)
+    tok = ops.sample(logits, temp)
+    assert torch.equal(tok.cpu(), torch.argmax(logits.float(), -1).cpu())
+
+
+def test_sample_distribution(cuda):
+    """Gumbel-max with temperature reproduces softmax(x/T); top-k / top-p never leave their sets."""
+    V = 64
+    logits = torch.randn(1, V, device=cuda) * 2
+    n = 4000
+    lg = logits.expand(n, V).contiguous()
+    temp = torch.full((n,), 0.8, device=cuda)
+    seeds = torch.arange(n, device=cuda, dtype=torch.long)
+    tok = ops.sample(lg, temp, seeds=seeds).cpu()
+    emp = torch.bincount(tok, minlength=V).float() / n
+    p = torch.softmax(logits[0].cpu() / 0.8, -1)
+    assert (emp - p).abs().max().item() < 0.05
+    topk = torch.full((n,), 5, device=cuda, dtype=torch.int32)
+    tok = ops.sample(lg, temp, top_k=topk, seeds=seeds).cpu()
+    allowed = set(torch.topk(logits[0].cpu(), 5).indices.tolist())
+    assert set(tok.tolist()) <= allowed
+    topp = torch.full((n,), 0.5, device=cuda)
+    tok = ops.sample(lg, temp, top_p=topp, seeds=seeds).cpu()
+    ps, order = torch.sort(p, descending=True)
+    keep = (torch.cumsum(ps, 0) - ps) < 0.5
+    allowed = set(order[keep].tolist())
+    assert set(tok.tolist()) <= allowed
