@@ -1,0 +1,201 @@
+"""LLMEngine: KV cache allocation + scheduler + model runner + output processing (one replica, one TP group).
+
+Synchronous core API (used by bench.py, tests and the async driver):
+    eng = LLMEngine(EngineConfig(model="llama3-8b"))
+    eng.add_request("r1", prompt_ids, SamplingParams(max_tokens=64))
+    while eng.has_unfinished(): outs = eng.step()       # -> list[StepOutput]
+
+The async driver (``engine/async_engine.py``) runs ``step()`` on a dedicated thread so the API event loop never
+blocks on the GPU (SURVEY.md §2.4 "Engine step loop must not run on the API event loop").
+"""
+from __future__ import annotations
+
+import logging
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from kafka_llm_service_amd.engine.model_runner import ModelRunner
+from kafka_llm_service_amd.engine.scheduler import Scheduler, SchedulerConfig
+from kafka_llm_service_amd.engine.sequence import SamplingParams, Sequence, SeqStatus, StepOutput
+from kafka_llm_service_amd.models.config import ModelConfig, get_config
+from kafka_llm_service_amd.models.weights import build_model
+from kafka_llm_service_amd.runtime import KVManager
+
+log = logging.getLogger("kafka.engine")
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama3-8b"
+    weights: str | None = None          # safetensors dir/file; None = seeded random init
+    seed: int = 0
+    device: str | None = None           # default cuda:<local rank> when a GPU is present, else cpu
+    tp: int = 1
+    tp_rank: int = 0
+    kv_fraction: float = 0.80           # of free device memory after weights
+    num_kv_blocks: int | None = None    # explicit pool size (pages of 16 tokens)
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 8192
+    max_prefill_chunk: int = 8192
+    max_model_len: int = 131072
+    enable_prefix_cache: bool = True
+    use_cascade: bool = True
+    cascade_min_prefix: int = 512
+    target_wgs: int = 768               # attention work decomposition target (256 CUs x ~3)
+    prefill_kv_chunk: int = 2048        # key-range split for long-context prefill tiles
+    use_graphs: bool = False
+    eos_token_ids: list[int] = field(default_factory=list)
+
+    def resolve_device(self) -> torch.device:
+        if self.device:
+            return torch.device(self.device)
+        if torch.cuda.is_available():
+            import os
+
+            return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+        return torch.device("cpu")
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, model_cfg: ModelConfig | None = None, model=None):
+        self.cfg = cfg
+        self.model_cfg = model_cfg or get_config(cfg.model)
+        self.device = cfg.resolve_device()
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        mc = self.model_cfg
+        t0 = time.perf_counter()
+        self.model = model or build_model(mc, self.device, tp=cfg.tp, tp_rank=cfg.tp_rank, seed=cfg.seed,
+                                          weights=cfg.weights, max_positions=min(cfg.max_model_len,
+                                                                                 mc.max_position_embeddings))
+        self.load_s = time.perf_counter() - t0
+        self.eos = set(cfg.eos_token_ids or mc.eos_token_ids)
+        hkv, D, L = self.model.hkv, self.model.D, mc.num_layers
+        page_bytes = 2 * L * hkv * 16 * D * 2
+        if cfg.num_kv_blocks:
+            nb = cfg.num_kv_blocks
+        elif self.device.type == "cuda":
+            free, _ = torch.cuda.mem_get_info(self.device)
+            nb = int(free * cfg.kv_fraction) // page_bytes
+        else:
+            nb = 4096
+        self.num_blocks = nb
+        self.k_cache = torch.empty(L, nb, hkv, 16, D, dtype=torch.bfloat16, device=self.device)
+        self.v_cache = torch.empty(L, nb, hkv, D, 16, dtype=torch.bfloat16, device=self.device)
+        self.kvm = KVManager(nb, 16, cfg.enable_prefix_cache)
+        max_blocks = (cfg.max_model_len + 15) // 16
+        self.sched = Scheduler(SchedulerConfig(max_num_seqs=cfg.max_num_seqs,
+                                               max_num_batched_tokens=cfg.max_num_batched_tokens,
+                                               max_prefill_chunk=cfg.max_prefill_chunk,
+                                               max_model_len=cfg.max_model_len, max_blocks_per_seq=max_blocks),
+                               self.kvm)
+        kc = [self.k_cache[i] for i in range(L)]
+        vc = [self.v_cache[i] for i in range(L)]
+        self.runner = ModelRunner(self.model, kc, vc, self.kvm, cfg.max_num_seqs, max_blocks,
+                                  cascade_min_prefix=cfg.cascade_min_prefix, use_cascade=cfg.use_cascade,
+                                  target_wgs=cfg.target_wgs, prefill_kv_chunk=cfg.prefill_kv_chunk)
+        self.requests: dict[str, Sequence] = {}
+        self.stats = {"steps": 0, "prompt_tokens": 0, "cached_tokens": 0, "output_tokens": 0, "step_time": 0.0}
+        self.stop_checker_factory = None  # set by the frontend: (request params) -> incremental stop-string checker
+        log.info("engine ready: %s tp=%d kv pages=%d (%.1f GB) load %.1fs", mc.name, cfg.tp, nb,
+                 nb * page_bytes / 1e9, self.load_s)
+
+    # ------------------------------------------------------------------------------------------------------------
+    def add_request(self, request_id: str, prompt_ids: list[int], params: SamplingParams | None = None,
+                    meta: dict | None = None) -> Sequence:
+        if request_id in self.requests:
+            raise ValueError(f"duplicate request id {request_id}")
+        params = params or SamplingParams()
+        if len(prompt_ids) + 1 > self.cfg.max_model_len:
+            raise ValueError(f"This model's maximum context length is {self.cfg.max_model_len} tokens. However, "
+                             f"your messages resulted in {len(prompt_ids)} tokens.")
+        seq = Sequence(request_id, prompt_ids, params, meta)
+        if self.stop_checker_factory is not None and params.stop:
+            seq.stop_checker = self.stop_checker_factory(params)
+        self.requests[request_id] = seq
+        self.sched.add(seq)
+        return seq
+
+    def abort(self, request_id: str) -> None:
+        seq = self.requests.pop(request_id, None)
+        if seq is not None and not seq.finished:
+            self.sched.finish(seq, "abort")
+
+    def has_unfinished(self) -> bool:
+        return self.sched.has_work()
+
+    @property
+    def num_running(self) -> int:
+        return len(self.sched.running)
+
+    @property
+    def num_waiting(self) -> int:
+        return len(self.sched.waiting)
+
+    # ------------------------------------------------------------------------------------------------------------
+    def step(self) -> list[StepOutput]:
+        batch = self.sched.schedule()
+        if batch.empty:
+            return []
+        t0 = time.perf_counter()
+        sampled_seqs, toks = self.runner.execute(batch)
+        now = time.perf_counter()
+        self.stats["step_time"] += now - t0
+        self.stats["steps"] += 1
+        # advance computed counts + register completed pages in the prefix tree
+        for s in batch.decode:
+            s.num_computed = s.total_len
+        for s, a, b in batch.prefill:
+            s.num_computed = b
+        for s in batch.decode:
+            self.kvm.commit(s.seq_id, s.num_computed)
+        for s, a, b in batch.prefill:
+            self.kvm.commit(s.seq_id, s.num_computed)
+        outs: list[StepOutput] = []
+        for s, t in zip(sampled_seqs, toks):
+            s.output_ids.append(t)
+            self.kvm.append_token(s.seq_id, t)
+            if s.first_token_time is None:
+                s.first_token_time = now
+                self.stats["prompt_tokens"] += len(s.prompt_ids)
+                self.stats["cached_tokens"] += s.num_cached
+            s.last_token_time = now
+            self.stats["output_tokens"] += 1
+            reason = self._check_stop(s, t)
+            if reason:
+                self.sched.finish(s, reason)
+                self.requests.pop(s.request_id, None)
+            outs.append(StepOutput(s.request_id, [t], reason is not None, reason, len(s.prompt_ids),
+                                   len(s.output_ids), s.num_cached))
+        return outs
+
+    def _check_stop(self, s: Sequence, t: int) -> str | None:
+        p = s.params
+        if not p.ignore_eos and t in self.eos:
+            return "stop"
+        if t in p.stop_token_ids:
+            return "stop"
+        if s.stop_checker is not None and s.stop_checker(t):
+            return "stop"
+        if len(s.output_ids) >= p.max_tokens:
+            return "length"
+        if s.total_len >= self.cfg.max_model_len:
+            return "length"
+        return None
+
+    # ------------------------------------------------------------------------------------------------------------
+    def generate(self, prompts: list[list[int]], params: SamplingParams | list[SamplingParams]) -> list[list[int]]:
+        """Blocking helper: run prompts to completion, return output token ids (tests, smoke, offline use)."""
+        ps = params if isinstance(params, list) else [params] * len(prompts)
+        ids = [f"gen-{time.perf_counter_ns()}-{i}" for i in range(len(prompts))]
+        seqs = [self.add_request(i, p, sp) for i, p, sp in zip(ids, prompts, ps)]
+        while any(not s.finished for s in seqs):
+            self.step()
+        return [s.output_ids for s in seqs]
+
+    def kv_stats(self) -> dict:
+        d = dict(self.kvm.stats())
+        d["num_blocks"] = self.num_blocks
+        return d

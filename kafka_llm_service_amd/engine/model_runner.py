@@ -1,0 +1,242 @@
+"""Turns a ScheduledBatch into device tensors, runs the model and samples (one engine step on one GPU/TP rank).
+
+Host->device traffic per step is two packed pinned buffers (one int64: tokens / positions / slots / logit rows;
+one int32: block tables / seq lens / kv_start / work items / causal limits) copied with one async H2D each; the only
+device->host traffic is the sampled token ids (SURVEY.md §3.2 "device→host: sampled token ids only").
+
+Decode-only batches can be replayed from hipGraphs captured per batch-size bucket (``engine/graphs.py``); mixed
+batches run eagerly.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from kafka_llm_service_amd import ops
+from kafka_llm_service_amd.engine.scheduler import ScheduledBatch
+from kafka_llm_service_amd.engine.sequence import Sequence
+from kafka_llm_service_amd.models.attention import AttnMeta
+from kafka_llm_service_amd.models.llama import StepInput, TransformerLM
+
+PAGE = 16
+
+
+def decode_splits(B: int, hkv: int, max_keys: int, target_wgs: int = 1024, min_keys_per_split: int = 256) -> int:
+    """Split-K factor for the decode kernel: enough workgroups to fill 256 CUs, >= min_keys_per_split keys each."""
+    if B <= 0:
+        return 1
+    s = max(1, math.ceil(target_wgs / (B * hkv)))
+    s = min(s, max(1, max_keys // min_keys_per_split), 32)
+    return s
+
+
+class ModelRunner:
+    def __init__(self, model: TransformerLM, k_caches, v_caches, kvm, max_num_seqs: int, max_blocks_per_seq: int,
+                 cascade_min_prefix: int = 512, use_cascade: bool = True, target_wgs: int = 768,
+                 prefill_kv_chunk: int = 2048):
+        self.model = model
+        self.k_caches, self.v_caches = k_caches, v_caches
+        self.kvm = kvm
+        self.device = model.device
+        self.max_num_seqs = max_num_seqs
+        self.max_blocks = max_blocks_per_seq
+        self.G = model.hq // model.hkv
+        self.tile = 128 // self.G
+        self.cascade_min_prefix = cascade_min_prefix
+        self.target_wgs = target_wgs
+        self.prefill_kv_chunk = prefill_kv_chunk
+        self.use_cascade = use_cascade
+        self.vocab = model.cfg.vocab_size
+        pin = self.device.type == "cuda"
+        self._bt = np.zeros((max_num_seqs * 2, max_blocks_per_seq), dtype=np.int32)
+        self._pin = pin
+        self.last_stats: dict = {}
+
+    # ------------------------------------------------------------------------------------------------------------
+    def prepare(self, batch: ScheduledBatch) -> tuple[StepInput, list[Sequence]]:
+        dec = batch.decode
+        B = len(dec)
+        pre = batch.prefill
+        T = B + sum(e - s for _, s, e in pre)
+        rows = B + len(pre)
+        nbt = max(1, rows)
+        # ---- int64 pack: tokens | positions | slots | logit_rows
+        tokens = np.empty(T, dtype=np.int64)
+        positions = np.empty(T, dtype=np.int64)
+        slots = np.empty(T, dtype=np.int64)
+        q_limit = np.empty(T, dtype=np.int32)
+        sample_seqs: list[Sequence] = []
+        logit_rows: list[int] = []
+        seq_ids = []
+        for i, s in enumerate(dec):
+            p = s.total_len - 1
+            tokens[i] = s.token_at(p)
+            positions[i] = p
+            q_limit[i] = p
+            self.kvm.fill_slots(s.seq_id, p, p + 1, slots, i)
+            sample_seqs.append(s)
+            logit_rows.append(i)
+            seq_ids.append(s.seq_id)
+        items = []
+        r = B
+        for j, (s, a, b) in enumerate(pre):
+            n = b - a
+            tokens[r:r + n] = s.tokens_range(a, b)
+            positions[r:r + n] = np.arange(a, b)
+            q_limit[r:r + n] = np.arange(a, b, dtype=np.int32)
+            self.kvm.fill_slots(s.seq_id, a, b, slots, r)
+            bt_row = B + j
+            for t0 in range(0, n, self.tile):
+                items.append((r + t0 - B, min(self.tile, n - t0), bt_row, 0, b, -1, 0, 0))
+            if b == s.total_len:
+                sample_seqs.append(s)
+                logit_rows.append(r + n - 1)
+            seq_ids.append(s.seq_id)
+            r += n
+        bt = self._bt[:nbt]
+        self.kvm.fill_block_tables(seq_ids, bt)
+        # ---- decode metadata (+ cascade over the shared prefix)
+        meta = AttnMeta(num_decode=B, num_tokens=T, scale=self.model.scale)
+        i32_parts = [bt.reshape(-1), q_limit]
+        seq_lens = kv_start = prefix_items = None
+        n_pref_splits = 0
+        if B:
+            seq_lens = np.fromiter((s.total_len for s in dec), dtype=np.int32, count=B)
+            P = 0
+            if self.use_cascade and B >= 2:
+                P = self.kvm.common_prefix_blocks([s.seq_id for s in dec]) * PAGE
+                P = min(P, (int(seq_lens.min()) - 1) // PAGE * PAGE)
+                if P < self.cascade_min_prefix:
+                    P = 0
+            max_suffix = int(seq_lens.max()) - P
+            S = decode_splits(B, self.model.hkv, max_suffix)
+            if P:
+                # key chunks sized so the prefix pass alone launches ~target_wgs workgroups
+                groups = math.ceil(B / self.tile)
+                want = max(1, self.target_wgs // (groups * self.model.hkv))
+                chunk = max(256, math.ceil(P / want / 32) * 32)
+                nc = math.ceil(P / chunk)
+                pit = []
+                for g0 in range(0, B, self.tile):
+                    for c in range(nc):
+                        pit.append((g0, min(self.tile, B - g0), 0, c * chunk, min(P, (c + 1) * chunk), c, 0, 0))
+                prefix_items = np.asarray(pit, dtype=np.int32)
+                n_pref_splits = nc
+                kv_start = np.full(B, P, dtype=np.int32)
+            meta.num_splits = S
+            meta.num_prefix_splits = n_pref_splits
+            i32_parts += [seq_lens]
+            if kv_start is not None:
+                i32_parts += [kv_start, prefix_items.reshape(-1)]
+            meta.extra["cascade_prefix"] = P
+        p_splits = 0
+        if items:
+            # few query tiles against a long key range (a new turn of a thread with a ~20k-token cached context):
+            # split every tile's key range so the pass fills the GPU, merge the partials afterwards
+            max_kv = max(b for _, _, b in pre)
+            if len(items) * self.model.hkv < self.target_wgs // 2 and max_kv > 2 * self.prefill_kv_chunk:
+                ck = self.prefill_kv_chunk
+                split_items = []
+                for (q0, cnt, btr, lo, hi, _, _, _) in items:
+                    for c in range(math.ceil(hi / ck)):
+                        split_items.append((q0, cnt, btr, c * ck, min(hi, (c + 1) * ck), c, 0, 0))
+                items = split_items
+                p_splits = math.ceil(max_kv / ck)
+            items_np = np.asarray(items, dtype=np.int32)
+            i32_parts.append(items_np.reshape(-1))
+        i64 = np.concatenate([tokens, positions, slots, np.asarray(logit_rows, dtype=np.int64)])
+        i32 = np.concatenate(i32_parts)
+        d64 = self._h2d(i64)
+        d32 = self._h2d(i32)
+        o = 0
+        t_tokens, t_pos, t_slots = d64[0:T], d64[T:2 * T], d64[2 * T:3 * T]
+        t_rows = d64[3 * T:3 * T + len(logit_rows)]
+        o = 0
+        meta.block_tables = d32[o:o + bt.size].view(nbt, self.max_blocks)
+        o += bt.size
+        meta.q_limit = d32[o:o + T]
+        o += T
+        if B:
+            meta.seq_lens = d32[o:o + B]
+            o += B
+            if kv_start is not None:
+                meta.kv_start = d32[o:o + B]
+                o += B
+                meta.prefix_items = d32[o:o + prefix_items.size].view(-1, 8)
+                o += prefix_items.size
+            Hq, D = self.model.hq, self.model.D
+            meta.part = torch.empty(B, Hq, meta.s_total, D, dtype=torch.float32, device=self.device)
+            meta.lse = torch.empty(B, Hq, meta.s_total, dtype=torch.float32, device=self.device)
+        if items:
+            meta.prefill_items = d32[o:o + len(items) * 8].view(-1, 8)
+            o += len(items) * 8
+            if p_splits:
+                Tp, Hq, D = T - B, self.model.hq, self.model.D
+                meta.prefill_splits = p_splits
+                meta.prefill_part = torch.empty(Tp, Hq, p_splits, D, dtype=torch.float32, device=self.device)
+                meta.prefill_lse = torch.full((Tp, Hq, p_splits), float("-inf"), dtype=torch.float32,
+                                              device=self.device)
+        self.last_stats = {"B": B, "T": T, "cascade_prefix": meta.extra.get("cascade_prefix", 0),
+                           "splits": meta.num_splits, "prefix_splits": meta.num_prefix_splits,
+                           "prefill_splits": p_splits}
+        return StepInput(t_tokens, t_pos, t_slots, meta, t_rows), sample_seqs
+
+    def _h2d(self, a: np.ndarray) -> torch.Tensor:
+        t = torch.from_numpy(a)
+        if self.device.type == "cuda":
+            return t.pin_memory().to(self.device, non_blocking=True)
+        return t.to(self.device)
+
+    # ------------------------------------------------------------------------------------------------------------
+    def sample(self, logits: torch.Tensor, seqs: list[Sequence]) -> torch.Tensor:
+        n = len(seqs)
+        temp = np.empty(n, dtype=np.float32)
+        topp = np.empty(n, dtype=np.float32)
+        topk = np.empty(n, dtype=np.int32)
+        seeds = np.empty(n, dtype=np.int64)
+        need_proc = False
+        for i, s in enumerate(seqs):
+            p = s.params
+            temp[i] = p.temperature
+            topp[i] = p.top_p
+            topk[i] = p.top_k
+            base = p.seed if p.seed is not None else (s.seq_id * 7919)
+            seeds[i] = (base * 1000003 + len(s.output_ids)) & 0x7FFFFFFFFFFFFFFF
+            if p.presence_penalty or p.frequency_penalty or p.allowed_tokens_fn is not None:
+                need_proc = True
+        if need_proc:
+            logits = self._process_logits(logits, seqs)
+        all_greedy = not temp.any()
+        dev = logits.device
+        if all_greedy:
+            return ops.sample(logits, torch.zeros(n, device=dev))
+        f32 = torch.from_numpy(np.concatenate([temp, topp])).to(dev, non_blocking=True)
+        return ops.sample(logits, f32[:n], f32[n:], torch.from_numpy(topk).to(dev, non_blocking=True),
+                          torch.from_numpy(seeds).to(dev, non_blocking=True))
+
+    def _process_logits(self, logits: torch.Tensor, seqs: list[Sequence]) -> torch.Tensor:
+        logits = logits.float().clone()
+        for i, s in enumerate(seqs):
+            p = s.params
+            if (p.presence_penalty or p.frequency_penalty) and s.output_ids:
+                ids = torch.tensor(s.output_ids, device=logits.device)
+                cnt = torch.bincount(ids, minlength=logits.shape[1]).float()
+                logits[i] -= p.frequency_penalty * cnt + p.presence_penalty * (cnt > 0).float()
+            if p.allowed_tokens_fn is not None:
+                allowed = p.allowed_tokens_fn(s.output_ids)
+                if allowed is not None:
+                    mask = torch.full((logits.shape[1],), float("-inf"), device=logits.device)
+                    idx = torch.as_tensor(allowed, device=logits.device, dtype=torch.long)
+                    mask[idx] = 0.0
+                    logits[i] += mask
+        return logits
+
+    # ------------------------------------------------------------------------------------------------------------
+    @torch.inference_mode()
+    def execute(self, batch: ScheduledBatch) -> tuple[list[Sequence], list[int]]:
+        inp, sample_seqs = self.prepare(batch)
+        logits = self.model.forward(inp, self.k_caches, self.v_caches)
+        toks = self.sample(logits, sample_seqs)
+        return sample_seqs, toks.tolist()

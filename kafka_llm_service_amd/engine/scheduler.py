@@ -1,0 +1,147 @@
+"""Continuous-batching scheduler (iteration level) with chunked prefill, prefix-cache admission and preemption.
+
+Every engine step the scheduler builds one mixed batch under a token budget:
+  1. every RUNNING sequence that has exactly its last sampled token left to compute contributes one DECODE token
+     (decode has priority, so a long cold prefill never stalls the streams of other threads);
+  2. RUNNING sequences that are part-way through their prompt continue their prefill chunk;
+  3. WAITING sequences are admitted FCFS: the KV manager matches their prompt against the prefix tree (shared system
+     prompt + the thread's own history), allocates pages for the uncached tail, and the tail is
+     prefilled in chunks of at most the remaining budget.
+When the KV pool cannot grow a running sequence, the most recently admitted sequence is preempted by recompute: its
+private pages are freed, its committed pages stay in the prefix tree, so its re-admission is mostly a cache hit.
+
+The reference service has no scheduler — concurrency is one asyncio loop forwarding requests to a remote API
+(/root/reference/server.py:384-523); this component replaces that.
+"""
+from __future__ import annotations
+
+from collections import deque
+from dataclasses import dataclass, field
+
+from kafka_llm_service_amd.engine.sequence import Sequence, SeqStatus
+
+
+@dataclass
+class SchedulerConfig:
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 8192
+    max_prefill_chunk: int = 8192
+    max_model_len: int = 131072
+    max_blocks_per_seq: int = 8192
+
+
+@dataclass
+class ScheduledBatch:
+    decode: list[Sequence] = field(default_factory=list)
+    # (seq, start, end): compute tokens [start, end) of seq; samples iff end == seq.total_len
+    prefill: list[tuple[Sequence, int, int]] = field(default_factory=list)
+    preempted: list[Sequence] = field(default_factory=list)
+
+    @property
+    def num_tokens(self) -> int:
+        return len(self.decode) + sum(e - s for _, s, e in self.prefill)
+
+    @property
+    def empty(self) -> bool:
+        return not self.decode and not self.prefill
+
+
+class Scheduler:
+    def __init__(self, cfg: SchedulerConfig, kv):
+        self.cfg = cfg
+        self.kv = kv
+        self.page = kv.page
+        self.waiting: deque[Sequence] = deque()
+        self.running: list[Sequence] = []
+        self.num_preemptions = 0
+
+    def add(self, seq: Sequence) -> None:
+        if seq.total_len >= self.cfg.max_model_len:
+            raise ValueError(f"prompt of {seq.total_len} tokens exceeds max_model_len={self.cfg.max_model_len}")
+        self.waiting.append(seq)
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def _preempt_one(self, batch: ScheduledBatch, protect: Sequence) -> bool:
+        for victim in reversed(self.running):
+            if victim is protect:
+                continue
+            self._evict(victim)
+            batch.preempted.append(victim)
+            if victim in batch.decode:
+                batch.decode.remove(victim)
+            return True
+        return False
+
+    def _evict(self, seq: Sequence) -> None:
+        self.kv.free_sequence(seq.seq_id)
+        self.running.remove(seq)
+        seq.status = SeqStatus.WAITING
+        seq.num_computed = 0
+        seq.preemptions += 1
+        self.num_preemptions += 1
+        self.waiting.appendleft(seq)
+
+    def finish(self, seq: Sequence, reason: str) -> None:
+        seq.status = SeqStatus.FINISHED
+        seq.finish_reason = reason
+        if seq in self.running:
+            self.running.remove(seq)
+        else:
+            try:
+                self.waiting.remove(seq)
+            except ValueError:
+                pass
+        if self.kv.has_seq(seq.seq_id):
+            self.kv.free_sequence(seq.seq_id)
+
+    def schedule(self) -> ScheduledBatch:
+        cfg = self.cfg
+        batch = ScheduledBatch()
+        budget = cfg.max_num_batched_tokens
+        # 1. decodes (and their page growth, preempting from the tail if the pool is dry)
+        for seq in list(self.running):
+            if seq.status != SeqStatus.RUNNING or seq.remaining != 1:
+                continue
+            while not self.kv.ensure_capacity(seq.seq_id, seq.total_len):
+                if not self._preempt_one(batch, seq):
+                    raise RuntimeError("KV cache too small for a single sequence")
+            if seq.status != SeqStatus.RUNNING:
+                continue
+            batch.decode.append(seq)
+            budget -= 1
+        # 2. running prefills
+        for seq in list(self.running):
+            if budget <= 0:
+                break
+            # remaining == 1 sequences were scheduled as decodes in phase 1
+            if seq.status != SeqStatus.RUNNING or seq.remaining <= 1:
+                continue
+            n = min(seq.remaining, budget, cfg.max_prefill_chunk)
+            end = seq.num_computed + n
+            if not self.kv.ensure_capacity(seq.seq_id, end):
+                continue
+            batch.prefill.append((seq, seq.num_computed, end))
+            budget -= n
+        # 3. admissions
+        while self.waiting and budget > 0 and len(self.running) < cfg.max_num_seqs:
+            seq = self.waiting[0]
+            toks = seq.all_ids()
+            cached = self.kv.add_sequence(seq.seq_id, toks)
+            n = min(seq.total_len - cached, budget, cfg.max_prefill_chunk)
+            end = cached + n
+            if not self.kv.ensure_capacity(seq.seq_id, end):
+                self.kv.free_sequence(seq.seq_id)
+                break
+            self.waiting.popleft()
+            seq.num_cached = cached if seq.preemptions == 0 else seq.num_cached
+            seq.num_computed = cached
+            seq.status = SeqStatus.RUNNING
+            self.running.append(seq)
+            if end - cached == 1 and end == seq.total_len:
+                batch.decode.append(seq)
+            else:
+                batch.prefill.append((seq, cached, end))
+            budget -= n
+        return batch

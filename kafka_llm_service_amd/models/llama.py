@@ -1,0 +1,135 @@
+"""Llama-3 / Llama-3.1 / Mixtral decoder for the serving engine (TP-sharded, paged KV, CDNA4 kernels).
+
+Per layer (SURVEY.md §3.2 "Target equivalent"):
+    fused_add_rmsnorm -> QKV GEMM (column-parallel) -> rope_kv_write (RoPE + paged KV write, HIP)
+    -> paged attention (decode / cascade / chunked prefill, HIP MFMA) -> O GEMM (row-parallel) -> [TP all-reduce]
+    -> fused_add_rmsnorm -> gate_up GEMM (column-parallel) -> silu_mul (HIP) -> down GEMM (row-parallel)
+    -> [TP all-reduce]                                     (Mixtral: router -> expert MLPs, models/moe.py)
+Dense GEMMs are hipBLASLt through ``torch.nn.functional.linear`` (bf16, fp32 accumulate). The elementwise / norm /
+attention / sampling work runs in the hand-written kernels of ``ops/csrc``.
+
+Weights are stored HF-style ``[out, in]`` so safetensors checkpoints load without transposes; random init (seeded,
+synthetic benchmarks — no checkpoints are downloadable here) is the default.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from kafka_llm_service_amd import ops
+from kafka_llm_service_amd.models.attention import AttnMeta, paged_attention
+from kafka_llm_service_amd.models.config import ModelConfig
+from kafka_llm_service_amd.parallel import state as pstate
+
+
+@dataclass
+class StepInput:
+    """Device tensors of one engine step."""
+    tokens: torch.Tensor          # int64 [T]
+    positions: torch.Tensor       # int64 [T]
+    slot_mapping: torch.Tensor    # int64 [T] (-1 = do not write KV)
+    attn: AttnMeta
+    logit_rows: torch.Tensor      # int64 [n] rows whose next-token logits are needed
+
+
+class LayerWeights:
+    __slots__ = ("input_norm", "post_norm", "qkv", "o", "gate_up", "down", "router", "w13", "w2", "expert_ids")
+
+    def __init__(self):
+        for s in self.__slots__:
+            setattr(self, s, None)
+
+
+class TransformerLM:
+    """Functional model: holds weight tensors + the RoPE table and runs one step over paged KV caches."""
+
+    def __init__(self, cfg: ModelConfig, device: torch.device, dtype=torch.bfloat16, tp: int = 1, tp_rank: int = 0,
+                 max_positions: int | None = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.tp, self.tp_rank = tp, tp_rank
+        if cfg.num_heads % tp or cfg.num_kv_heads % tp:
+            raise ValueError(f"heads ({cfg.num_heads}/{cfg.num_kv_heads}) not divisible by tp={tp}")
+        self.hq = cfg.num_heads // tp
+        self.hkv = cfg.num_kv_heads // tp
+        self.D = cfg.head_dim
+        self.ffn = cfg.intermediate_size // tp if not cfg.num_experts else cfg.intermediate_size
+        self.vocab_local = (cfg.vocab_size + tp - 1) // tp
+        self.layers: list[LayerWeights] = [LayerWeights() for _ in range(cfg.num_layers)]
+        self.embed = None       # [V_local, d]
+        self.lm_head = None     # [V_local, d]
+        self.final_norm = None  # [d]
+        maxp = max_positions or cfg.max_position_embeddings
+        self.cos_sin = ops.rope_cos_sin(maxp, self.D, cfg.rope_theta, cfg.rope_scaling, device=self.device)
+        self.scale = self.D ** -0.5
+        self.moe = None
+
+    # ------------------------------------------------------------------------------------------------------------
+    def forward(self, inp: StepInput, k_caches: list[torch.Tensor], v_caches: list[torch.Tensor]) -> torch.Tensor:
+        """Returns logits [n, V] (bf16) for ``inp.logit_rows``."""
+        cfg = self.cfg
+        T = inp.tokens.shape[0]
+        h = self._embed(inp.tokens)
+        residual = h
+        x = torch.empty_like(h)
+        q = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
+        attn_out = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
+        eps = cfg.rms_norm_eps
+        delta = None
+        for i, lw in enumerate(self.layers):
+            if delta is None:
+                ops.rmsnorm(h, lw.input_norm, eps, out=x)
+                residual = h.clone()
+            else:
+                ops.fused_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x)
+            qkv = F.linear(x, lw.qkv)
+            ops.rope_kv_write(qkv, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i], inp.slot_mapping,
+                              self.hq, self.hkv)
+            paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out)
+            o = F.linear(attn_out.view(T, -1), lw.o)
+            o = pstate.tp_all_reduce(o)
+            ops.fused_add_rmsnorm(o, residual, lw.post_norm, eps, out=x)
+            if lw.router is not None:
+                delta = self.moe(x, lw)
+            else:
+                gu = F.linear(x, lw.gate_up)
+                a = ops.silu_mul(gu)
+                delta = F.linear(a, lw.down)
+                delta = pstate.tp_all_reduce(delta)
+        rows = inp.logit_rows
+        d_sel = delta.index_select(0, rows)
+        r_sel = residual.index_select(0, rows)
+        hf = ops.fused_add_rmsnorm(d_sel, r_sel, self.final_norm, eps)
+        logits = F.linear(hf, self.lm_head)
+        if self.tp > 1:
+            logits = pstate.tp_all_gather_lastdim(logits)
+        return logits[:, :cfg.vocab_size]
+
+    def _embed(self, tokens: torch.Tensor) -> torch.Tensor:
+        if self.tp == 1:
+            return F.embedding(tokens, self.embed)
+        lo = self.tp_rank * self.vocab_local
+        local = tokens - lo
+        mask = (local < 0) | (local >= self.vocab_local)
+        h = F.embedding(local.clamp(0, self.vocab_local - 1), self.embed)
+        h = h.masked_fill(mask[:, None], 0)
+        return pstate.tp_all_reduce(h)
+
+    # ------------------------------------------------------------------------------------------------------------
+    def weight_bytes(self) -> int:
+        n = 0
+        for t in self.named_tensors().values():
+            n += t.numel() * t.element_size()
+        return n
+
+    def named_tensors(self) -> dict[str, torch.Tensor]:
+        out = {"embed": self.embed, "lm_head": self.lm_head, "final_norm": self.final_norm}
+        for i, lw in enumerate(self.layers):
+            for s in LayerWeights.__slots__:
+                t = getattr(lw, s)
+                if isinstance(t, torch.Tensor):
+                    out[f"layers.{i}.{s}"] = t
+        return {k: v for k, v in out.items() if v is not None}

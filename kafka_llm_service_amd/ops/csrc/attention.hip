@@ -44,28 +44,48 @@ struct WaveAcc {
   float l;
 };
 
-// One 32-key step for one wave. key0 is 32-aligned; page0/page1 hold keys [key0, key0+16) and [key0+16, key0+32).
+// K/V fragments of one 32-key block for one wave (register-staged; the next block is prefetched while the
+// current one is computed: loads for block i+1 are issued before the MFMAs of block i, so HBM/L2 latency hides
+// under the QK^T / softmax / PV work instead of stalling every 32-key step).
 template <int D>
-__device__ __forceinline__ void attn_step(const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache, int Hkv,
-                                          int kvh, int page0, int page1, int key0, int lo, int hi, int limit,
-                                          const bf16x8 (&qf)[D / 16], float scale_log2, WaveAcc<D>& acc, int lane) {
+struct KVFrag {
+  bf16x8 k[D / 16];
+  bf16x8 v[2][D / 32];
+};
+
+template <int D>
+__device__ __forceinline__ void load_kv(KVFrag<D>& f, const bf16* __restrict__ k_cache,
+                                        const bf16* __restrict__ v_cache, int Hkv, int kvh, int page0, int page1,
+                                        int lane) {
   const int r = lane & 31, h = lane >> 5;
   const int kp = (r >> 4) ? page1 : page0;
   const bf16* kptr = k_cache + ((int64_t)kp * Hkv + kvh) * (PAGE * D) + (r & 15) * D + 8 * h;
-  bf16x8 kf[D / 16];
 #pragma unroll
-  for (int kk = 0; kk < D / 16; ++kk) kf[kk] = load_bf16x8(kptr + 16 * kk);
-  bf16x8 vf[2][D / 32];
+  for (int kk = 0; kk < D / 16; ++kk) f.k[kk] = load_bf16x8(kptr + 16 * kk);
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
     const int vp = s2 ? page1 : page0;
     const bf16* vptr = v_cache + ((int64_t)vp * Hkv + kvh) * (D * PAGE) + r * PAGE + 8 * h;
 #pragma unroll
-    for (int t = 0; t < D / 32; ++t) vf[s2][t] = load_bf16x8(vptr + 32 * t * PAGE);
+    for (int t = 0; t < D / 32; ++t) f.v[s2][t] = load_bf16x8(vptr + 32 * t * PAGE);
   }
+}
+
+// Pages holding keys [key0, key0 + 32) (key0 32-aligned); the second page is only dereferenced below `end`.
+__device__ __forceinline__ void block_pages(const int* __restrict__ bt, int key0, int end, int& p0, int& p1) {
+  p0 = bt[key0 >> 4];
+  p1 = (key0 + 16 < end) ? bt[(key0 >> 4) + 1] : p0;
+}
+
+// One 32-key step for one wave on already-loaded fragments.
+template <int D>
+__device__ __forceinline__ void attn_compute(const KVFrag<D>& f, int key0, int lo, int hi, int limit,
+                                             const bf16x8 (&qf)[D / 16], float scale_log2, WaveAcc<D>& acc,
+                                             int lane) {
+  const int h = lane >> 5;
   f32x16 s = {};
 #pragma unroll
-  for (int kk = 0; kk < D / 16; ++kk) s = mfma32(kf[kk], qf[kk], s);
+  for (int kk = 0; kk < D / 16; ++kk) s = mfma32(f.k[kk], qf[kk], s);
 
   float mx = -INFINITY;
 #pragma unroll
@@ -101,7 +121,31 @@ __device__ __forceinline__ void attn_step(const bf16* __restrict__ k_cache, cons
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-    for (int t = 0; t < D / 32; ++t) acc.o[t] = mfma32(vf[s2][t], pf[s2], acc.o[t]);
+    for (int t = 0; t < D / 32; ++t) acc.o[t] = mfma32(f.v[s2][t], pf[s2], acc.o[t]);
+}
+
+// Key blocks first, first+stride, ... < nblk (block b covers keys [base + 32 b, base + 32 b + 32)), software
+// pipelined one block deep. The prefetch of the block after the last one is clamped to the last block (pad, don't
+// branch: no divergent load, no extra waitcnt).
+template <int D>
+__device__ __forceinline__ void attn_blocks(const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+                                            int Hkv, int kvh, const int* __restrict__ bt, int base, int first,
+                                            int nblk, int stride, int end, int lo, int hi, int limit,
+                                            const bf16x8 (&qf)[D / 16], float scale_log2, WaveAcc<D>& acc,
+                                            int lane) {
+  if (first >= nblk) return;
+  int p0, p1;
+  KVFrag<D> cur;
+  block_pages(bt, base + 32 * first, end, p0, p1);
+  load_kv<D>(cur, k_cache, v_cache, Hkv, kvh, p0, p1, lane);
+  for (int b = first; b < nblk; b += stride) {
+    const int nb = (b + stride < nblk) ? b + stride : b;
+    KVFrag<D> nxt;
+    block_pages(bt, base + 32 * nb, end, p0, p1);
+    load_kv<D>(nxt, k_cache, v_cache, Hkv, kvh, p0, p1, lane);
+    attn_compute<D>(cur, base + 32 * b, lo, hi, limit, qf, scale_log2, acc, lane);
+    cur = nxt;
+  }
 }
 
 template <int D>
@@ -159,12 +203,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16* __restrict
   if (blo + w < bhi) {
     bf16x8 qf[D / 16];
     load_q_frags<D>(qf, q + (int64_t)b * q_stride + (int64_t)(kvh * G + r) * D, r < G, h);
-    for (int blk = blo + w; blk < bhi; blk += 4) {
-      const int key0 = a0 + blk * 32;
-      const int p0 = bt[key0 >> 4];
-      const int p1 = (key0 + 16 < len) ? bt[(key0 >> 4) + 1] : p0;
-      attn_step<D>(k_cache, v_cache, Hkv, kvh, p0, p1, key0, lo, hi, 0x7fffffff, qf, scale_log2, acc, lane);
-    }
+    attn_blocks<D>(k_cache, v_cache, Hkv, kvh, bt, a0, blo + w, bhi, 4, len, lo, hi, 0x7fffffff, qf, scale_log2,
+                   acc, lane);
   }
   // cross-wave combine
   if (r < G) {
@@ -238,11 +278,9 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const AttnWorkItem* _
   if (hi > lo) {
     bf16x8 qf[D / 16];
     load_q_frags<D>(qf, q + (int64_t)token * q_stride + (int64_t)(kvh * G + g) * D, valid, h);
-    for (int key0 = lo & ~31; key0 < hi; key0 += 32) {
-      const int p0 = bt[key0 >> 4];
-      const int p1 = (key0 + 16 < hi) ? bt[(key0 >> 4) + 1] : p0;
-      attn_step<D>(k_cache, v_cache, Hkv, kvh, p0, p1, key0, lo, hi, limit, qf, scale_log2, acc, lane);
-    }
+    const int base = lo & ~31;
+    attn_blocks<D>(k_cache, v_cache, Hkv, kvh, bt, base, 0, (hi - base + 31) >> 5, 1, hi, lo, hi, limit, qf,
+                   scale_log2, acc, lane);
   }
   if (!valid) return;
   const int head = kvh * G + g;
@@ -277,27 +315,54 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const AttnWorkItem* _
 }
 
 // ------------------------------------------------------------------------------------------------------------------
-// Merge S partials: grid (rows * Hq), D threads.
+// Merge S partials of every head of one row: grid (rows), 256 threads. The per-(head, split) merge weights
+// exp2(lse - M) / L are computed once into LDS; then every thread combines float4 columns of its heads.
+constexpr int MERGE_MAX_HS = 4096;  // Hq * S
 template <int D>
-__global__ __launch_bounds__(D) void attn_merge_kernel(const float* __restrict__ part, const float* __restrict__ lse,
-                                                        int S, bf16* __restrict__ out, int64_t out_stride, int Hq,
-                                                        float* __restrict__ lse_out) {
-  const int64_t rh = blockIdx.x;
-  const int row = (int)(rh / Hq), head = (int)(rh % Hq);
-  const int d = threadIdx.x;
-  const float* l = lse + rh * S;
-  float M = -INFINITY;
-  for (int s = 0; s < S; ++s) M = fmaxf(M, l[s]);
-  float L = 0.f, O = 0.f;
-  if (M != -INFINITY) {
-    for (int s = 0; s < S; ++s) {
-      const float f = exp2f(l[s] - M);
-      L += f;
-      O += f * part[(rh * S + s) * D + d];
-    }
+__global__ __launch_bounds__(256) void attn_merge_kernel(const float* __restrict__ part, const float* __restrict__ lse,
+                                                          int S, bf16* __restrict__ out, int64_t out_stride, int Hq,
+                                                          float* __restrict__ lse_out) {
+  __shared__ float wgt[MERGE_MAX_HS];
+  __shared__ float sM[64], sL[64];
+  const int64_t row = blockIdx.x;
+  const float* l = lse + row * Hq * S;
+  for (int hh = threadIdx.x; hh < Hq; hh += 256) {
+    float M = -INFINITY;
+    for (int s = 0; s < S; ++s) M = fmaxf(M, l[hh * S + s]);
+    float L = 0.f;
+    if (M != -INFINITY)
+      for (int s = 0; s < S; ++s) L += exp2f(l[hh * S + s] - M);
+    sM[hh] = M;
+    sL[hh] = L;
+    if (lse_out) lse_out[row * Hq + hh] = L > 0.f ? M + log2f(L) : -INFINITY;
   }
-  out[(int64_t)row * out_stride + (int64_t)head * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
-  if (lse_out && d == 0) lse_out[rh] = L > 0.f ? M + log2f(L) : -INFINITY;
+  __syncthreads();
+  for (int i = threadIdx.x; i < Hq * S; i += 256) {
+    const int hh = i / S;
+    const float L = sL[hh];
+    wgt[i] = L > 0.f ? exp2f(l[i] - sM[hh]) / L : 0.f;
+  }
+  __syncthreads();
+  constexpr int D4 = D / 4;
+  for (int i = threadIdx.x; i < Hq * D4; i += 256) {
+    const int hh = i / D4, c = (i % D4) * 4;
+    const float* p = part + ((row * Hq + hh) * S) * D + c;
+    const float* w = wgt + hh * S;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int s = 0;
+    for (; s + 4 <= S; s += 4) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(p + (s + 0) * D);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(p + (s + 1) * D);
+      const f32x4 cc = *reinterpret_cast<const f32x4*>(p + (s + 2) * D);
+      const f32x4 d = *reinterpret_cast<const f32x4*>(p + (s + 3) * D);
+      acc += a * w[s] + b * w[s + 1] + cc * w[s + 2] + d * w[s + 3];
+    }
+    for (; s < S; ++s) acc += *reinterpret_cast<const f32x4*>(p + s * D) * w[s];
+    bf16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = (bf16)acc[j];
+    *reinterpret_cast<bf16x4*>(out + row * out_stride + (int64_t)hh * D + c) = o;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -330,8 +395,8 @@ extern "C" hipError_t kafka_launch_attn_prefill(const void* items, int n_items, 
 extern "C" hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows, int Hq, int S, int D, bf16* out,
                              int64_t out_stride, float* lse_out, hipStream_t st) {
   if (rows == 0) return hipSuccess;
-  if (D != 128) return hipErrorInvalidValue;
-  attn_merge_kernel<128><<<rows * Hq, 128, 0, st>>>(part, lse, S, out, out_stride, Hq, lse_out);
+  if (D != 128 || Hq > 64 || Hq * S > MERGE_MAX_HS) return hipErrorInvalidValue;
+  attn_merge_kernel<128><<<rows, 256, 0, st>>>(part, lse, S, out, out_stride, Hq, lse_out);
   return hipGetLastError();
 }
 

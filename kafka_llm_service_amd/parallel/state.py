@@ -1,0 +1,113 @@
+"""Process-group state: one process per GPU, ``torch.distributed`` over RCCL (backend "nccl" on ROCm) / gloo on CPU.
+
+Layout of a node of ``world`` ranks:
+  * ``tp`` consecutive ranks form one tensor-parallel group (Megatron column/row split, 2 all-reduces per layer),
+  * the remaining factor ``dp = world // tp`` are independent engine replicas (DP) — each replica owns its own KV
+    cache and its own threads (thread-affinity routing, ``engine/dp_router.py``); replicas never communicate on the
+    hot path.
+  * ``ep`` (Mixtral) re-uses the TP group: experts are partitioned over its ranks and tokens are exchanged with
+    all-to-all (``parallel/moe_ep.py``).
+
+The reference service has no collectives at all; this module is new.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class ParallelState:
+    world: int = 1
+    rank: int = 0
+    local_rank: int = 0
+    tp: int = 1
+    tp_rank: int = 0
+    dp: int = 1
+    dp_rank: int = 0
+    tp_group: object = None  # torch ProcessGroup over the tp ranks (None when tp == 1)
+    cpu_group: object = None  # gloo group over the tp ranks for host-side broadcasts (scheduler decisions)
+    backend: str = "none"
+
+    @property
+    def is_tp_leader(self) -> bool:
+        return self.tp_rank == 0
+
+
+_STATE = ParallelState()
+
+
+def get() -> ParallelState:
+    return _STATE
+
+
+def env_world() -> tuple[int, int, int]:
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0"))))
+
+
+def init(tp: int = 1, backend: str | None = None, device: str | None = None) -> ParallelState:
+    """Initialise torch.distributed from the torchrun env (no-op for a single process) and build the TP/DP groups."""
+    global _STATE
+    world, rank, local_rank = env_world()
+    if world % tp != 0:
+        raise ValueError(f"world size {world} not divisible by tp={tp}")
+    st = ParallelState(world=world, rank=rank, local_rank=local_rank, tp=tp, tp_rank=rank % tp, dp=world // tp,
+                       dp_rank=rank // tp)
+    if world > 1:
+        if backend is None:
+            backend = "nccl" if (device or "").startswith("cuda") or (device is None and torch.cuda.is_available()) \
+                else "gloo"
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            kw = {}
+            if backend == "nccl":
+                torch.cuda.set_device(local_rank)
+                kw["device_id"] = torch.device("cuda", local_rank)
+            dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+        st.backend = backend
+        if tp > 1:
+            for g in range(world // tp):
+                ranks = list(range(g * tp, (g + 1) * tp))
+                pg = dist.new_group(ranks, backend=backend)
+                cpg = dist.new_group(ranks, backend="gloo") if backend != "gloo" else pg
+                if rank in ranks:
+                    st.tp_group, st.cpu_group = pg, cpg
+    _STATE = st
+    return st
+
+
+def set_state(st: ParallelState) -> None:
+    global _STATE
+    _STATE = st
+
+
+def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
+    st = _STATE
+    if st.tp == 1:
+        return x
+    from . import comm
+
+    return comm.all_reduce(x, st.tp_group)
+
+
+def tp_all_gather_lastdim(x: torch.Tensor) -> torch.Tensor:
+    st = _STATE
+    if st.tp == 1:
+        return x
+    parts = [torch.empty_like(x) for _ in range(st.tp)]
+    dist.all_gather(parts, x.contiguous(), group=st.tp_group)
+    return torch.cat(parts, dim=-1)
+
+
+def barrier() -> None:
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def destroy() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()

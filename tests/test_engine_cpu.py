@@ -1,0 +1,136 @@
+"""Engine integration on CPU (reference ops): paged + prefix-cached + continuously-batched greedy decoding must agree
+with the dense cache-free oracle; cold vs warm prefix, cascade, chunked prefill and preemption must not change
+the result (SURVEY.md §4.4 "Engine integration")."""
+import pytest
+import torch
+
+from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
+from kafka_llm_service_amd.engine.sequence import SamplingParams
+from kafka_llm_service_amd.models.oracle import dense_logits
+
+GREEDY = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
+
+
+@pytest.fixture(scope="module")
+def base_engine():
+    return LLMEngine(EngineConfig(model="tiny-llama", device="cpu", num_kv_blocks=256, max_model_len=2048))
+
+
+def _engine(model=None, **kw):
+    cfg = dict(model="tiny-llama", device="cpu", num_kv_blocks=256, max_model_len=2048)
+    cfg.update(kw)
+    return LLMEngine(EngineConfig(**cfg), model=model)
+
+
+def _prompts(seed=1, shared=70, tails=(5, 17, 40)):
+    g = torch.Generator().manual_seed(seed)
+    prefix = torch.randint(0, 5000, (shared,), generator=g).tolist()
+    return [prefix + torch.randint(0, 5000, (n,), generator=g).tolist() for n in tails]
+
+
+def _check_against_oracle(model, prompts, outs, tol=0.05):
+    for p, o in zip(prompts, outs):
+        lg = dense_logits(model, p + o)
+        for i, tok in enumerate(o):
+            row = lg[len(p) - 1 + i]
+            assert (row.max() - row[tok]).item() < tol, f"token {i}: not the oracle's argmax"
+
+
+def test_greedy_matches_oracle(base_engine):
+    prompts = _prompts()
+    outs = base_engine.generate(prompts, GREEDY)
+    _check_against_oracle(base_engine.model, prompts, outs)
+
+
+def test_prefix_hit_equals_cold(base_engine):
+    prompts = _prompts(seed=2, shared=100)
+    cold = _engine(model=base_engine.model, enable_prefix_cache=False).generate(prompts, GREEDY)
+    warm_eng = _engine(model=base_engine.model)
+    warm_eng.generate([prompts[0][:90] + [1, 2, 3]], GREEDY)  # seeds the tree with the shared prefix
+    warm = warm_eng.generate(prompts, GREEDY)
+    assert warm_eng.kv_stats()["hit_tokens"] >= 3 * 80
+    assert warm == cold
+
+
+def test_cascade_equals_plain(base_engine):
+    prompts = _prompts(seed=3, shared=96, tails=(3, 9, 30, 31))
+    e1 = _engine(model=base_engine.model, use_cascade=False)
+    e2 = _engine(model=base_engine.model, use_cascade=True, cascade_min_prefix=16)
+    e2.generate([prompts[0][:96] + [7]], GREEDY)
+    plain = e1.generate(prompts, GREEDY)
+    casc = e2.generate(prompts, GREEDY)
+    assert e2.runner.last_stats["cascade_prefix"] >= 80
+    assert casc == plain
+
+
+def test_chunked_prefill_and_small_budget(base_engine):
+    prompts = _prompts(seed=4, shared=50, tails=(60, 3))
+    ref = _engine(model=base_engine.model).generate(prompts, GREEDY)
+    chunked = _engine(model=base_engine.model, max_num_batched_tokens=24, max_prefill_chunk=16).generate(prompts,
+                                                                                                       GREEDY)
+    assert chunked == ref
+
+
+def test_preemption_recompute(base_engine):
+    prompts = _prompts(seed=5, shared=20, tails=(30, 30, 30, 30))
+    params = SamplingParams(temperature=0.0, max_tokens=20, ignore_eos=True)
+    ref = _engine(model=base_engine.model).generate(prompts, params)
+    small = _engine(model=base_engine.model, num_kv_blocks=12)
+    out = small.generate(prompts, params)
+    assert small.sched.num_preemptions > 0
+    assert out == ref
+
+
+def test_sampling_params_validation():
+    with pytest.raises(ValueError):
+        SamplingParams(temperature=-1)
+    with pytest.raises(ValueError):
+        SamplingParams(top_p=0)
+    assert SamplingParams(temperature=0).greedy
+
+
+def test_stop_tokens_and_abort(base_engine):
+    eng = _engine(model=base_engine.model)
+    p = _prompts(seed=6)[0]
+    first = eng.generate([p], GREEDY)[0]
+    s = eng.add_request("x", p, SamplingParams(temperature=0, max_tokens=10, stop_token_ids=[first[2]]))
+    while not s.finished:
+        eng.step()
+    k = first.index(first[2])
+    assert s.finish_reason == "stop" and s.output_ids == first[:k + 1]
+    s2 = eng.add_request("y", p, SamplingParams(temperature=0, max_tokens=10))
+    eng.step()
+    eng.abort("y")
+    assert s2.finish_reason == "abort" and not eng.has_unfinished()
+    assert eng.kvm.check_invariants()
+
+
+def test_context_length_error(base_engine):
+    eng = _engine(model=base_engine.model, max_model_len=64)
+    with pytest.raises(ValueError, match="maximum context length"):
+        eng.add_request("z", list(range(100)), GREEDY)
+
+
+def test_sampling_temperature_reproducible(base_engine):
+    eng = _engine(model=base_engine.model)
+    p = _prompts(seed=7)[:2]
+    sp = SamplingParams(temperature=0.8, top_p=0.9, top_k=50, max_tokens=5, seed=123, ignore_eos=True)
+    a = eng.generate(p, sp)
+    b = _engine(model=base_engine.model).generate(p, sp)
+    assert a == b
+
+
+def test_split_kv_prefill_equals_plain(base_engine):
+    """A new turn on a long cached context: key-range-split prefill tiles + merge == one pass."""
+    prompts = _prompts(seed=8, shared=300, tails=(9,))
+    ref_eng = _engine(model=base_engine.model)
+    ref_eng.generate([prompts[0][:290] + [3]], GREEDY)
+    ref = ref_eng.generate(prompts, GREEDY)
+    e = _engine(model=base_engine.model, prefill_kv_chunk=32)
+    e.generate([prompts[0][:290] + [3]], GREEDY)
+    s = e.add_request("q", prompts[0], GREEDY)
+    e.step()
+    assert e.runner.last_stats["prefill_splits"] >= 9
+    while not s.finished:
+        e.step()
+    assert s.output_ids == ref[0]

@@ -1,0 +1,120 @@
+"""Native KV block manager + prefix cache (runtime/csrc/kv_manager.cpp): unit + property tests (CPU)."""
+import random
+
+import numpy as np
+import pytest
+from hypothesis import given, settings, strategies as st
+
+from kafka_llm_service_amd.runtime import KVManager
+
+
+def test_prefix_match_and_commit():
+    kv = KVManager(64, 16, True)
+    toks = list(range(100))
+    assert kv.add_sequence(1, toks) == 0
+    assert kv.ensure_capacity(1, 100)
+    assert len(kv.block_table(1)) == 7
+    kv.commit(1, 100)
+    assert kv.num_cached_pages() == 6  # only full pages
+    kv.free_sequence(1)
+    assert kv.num_evictable() == 6  # the whole unreferenced chain
+    # a new prompt sharing 70 tokens re-uses 4 full pages
+    assert kv.add_sequence(2, toks[:70] + [999] * 10) == 64
+    # a prompt identical to a cached prefix always leaves >= 1 token to compute
+    assert kv.add_sequence(3, toks[:96]) == 80
+    assert kv.check_invariants()
+
+
+def test_dedup_on_commit():
+    kv = KVManager(32, 16, True)
+    toks = list(range(40))
+    kv.add_sequence(1, toks)
+    kv.add_sequence(2, toks)
+    kv.ensure_capacity(1, 40)
+    kv.ensure_capacity(2, 40)
+    kv.commit(1, 40)
+    kv.commit(2, 40)  # identical pages: seq 2 adopts seq 1's blocks
+    assert kv.block_table(1)[:2] == kv.block_table(2)[:2]
+    assert kv.common_prefix_blocks([1, 2]) == 2
+    assert kv.check_invariants()
+    kv.free_sequence(1)
+    kv.free_sequence(2)
+    assert kv.check_invariants()
+    assert kv.num_free() + kv.num_evictable() + (kv.num_cached_pages() - kv.num_evictable()) == 32
+
+
+def test_eviction_lru():
+    kv = KVManager(8, 16, True)
+    for sid, base in ((1, 0), (2, 1000)):
+        t = list(range(base, base + 64))
+        kv.add_sequence(sid, t)
+        assert kv.ensure_capacity(sid, 64)
+        kv.commit(sid, 64)
+        kv.free_sequence(sid)
+    assert kv.num_free() == 0 and kv.available() == 8
+    # need 5 fresh blocks: evicts leaves LRU-first, seq 1's chain (older) first
+    kv.add_sequence(3, list(range(5000, 5080)))
+    assert kv.ensure_capacity(3, 80)
+    assert kv.stats()["evictions"] == 5
+    assert kv.check_invariants()
+    assert kv.add_sequence(4, list(range(1000, 1064)) + [1]) == 48  # seq 2's chain survived (3 of 4 pages)
+
+
+def test_capacity_failure_is_atomic():
+    kv = KVManager(4, 16, False)
+    kv.add_sequence(1, list(range(10)))
+    assert not kv.ensure_capacity(1, 16 * 5)
+    assert kv.num_free() == 4
+    assert kv.ensure_capacity(1, 64)
+    assert kv.num_free() == 0
+
+
+def test_fill_helpers():
+    kv = KVManager(16, 16, True)
+    kv.add_sequence(7, list(range(40)))
+    kv.ensure_capacity(7, 40)
+    bt = np.zeros((2, 8), dtype=np.int32)
+    kv.fill_block_tables([7], bt)
+    assert list(bt[0, :3]) == kv.block_table(7)
+    slots = np.zeros(5, dtype=np.int64)
+    kv.fill_slots(7, 14, 19, slots, 0)
+    b = kv.block_table(7)
+    assert list(slots) == [b[0] * 16 + 14, b[0] * 16 + 15, b[1] * 16, b[1] * 16 + 1, b[1] * 16 + 2]
+    with pytest.raises(RuntimeError):
+        kv.fill_slots(7, 40, 60, np.zeros(20, dtype=np.int64), 0)
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.lists(st.tuples(st.integers(0, 3), st.integers(0, 5), st.integers(1, 90)), min_size=1, max_size=60),
+       st.booleans())
+def test_random_ops_keep_invariants(ops, prefix_cache):
+    """Random admit / grow / commit / free traffic never double-owns or leaks a block."""
+    kv = KVManager(24, 16, prefix_cache)
+    live = {}
+    rng = random.Random(0)
+    base = [rng.randrange(50) for _ in range(200)]
+    sid = 0
+    for op, a, n in ops:
+        if op == 0 and len(live) < 6:
+            sid += 1
+            toks = base[:n] if a % 2 == 0 else [rng.randrange(50) for _ in range(n)]
+            kv.add_sequence(sid, toks)
+            live[sid] = len(toks)
+        elif op == 1 and live:
+            s = sorted(live)[a % len(live)]
+            if kv.ensure_capacity(s, live[s] + a):
+                kv.append_tokens(s, np.arange(a, dtype=np.int32))
+                live[s] += a
+        elif op == 2 and live:
+            s = sorted(live)[a % len(live)]
+            if kv.ensure_capacity(s, live[s]):
+                kv.commit(s, live[s])
+        elif op == 3 and live:
+            s = sorted(live)[a % len(live)]
+            kv.free_sequence(s)
+            del live[s]
+        assert kv.check_invariants()
+    for s in list(live):
+        kv.free_sequence(s)
+    assert kv.check_invariants()
+    assert kv.available() == 24
