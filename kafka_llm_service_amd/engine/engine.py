@@ -43,8 +43,8 @@ class EngineConfig:
     enable_prefix_cache: bool = True
     use_cascade: bool = True
     cascade_min_prefix: int = 512
-    target_wgs: int = 768               # attention work decomposition target (256 CUs x ~3)
-    prefill_kv_chunk: int = 2048        # key-range split for long-context prefill tiles
+    target_wgs: int = 256               # tile-kernel workgroups per pass (8-wave WGs, one per CU)
+    prefill_kv_chunk: int = 1024        # key-range split for long-context prefill tiles
     use_graphs: bool = False
     eos_token_ids: list[int] = field(default_factory=list)
 

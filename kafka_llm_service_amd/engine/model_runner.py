@@ -21,9 +21,10 @@ from kafka_llm_service_amd.models.attention import AttnMeta
 from kafka_llm_service_amd.models.llama import StepInput, TransformerLM
 
 PAGE = 16
+MAX_ITEM_KEYS = 32000  # key range of one attention work item (page ids of an item are staged in 8 KB of LDS)
 
 
-def decode_splits(B: int, hkv: int, max_keys: int, target_wgs: int = 1024, min_keys_per_split: int = 256) -> int:
+def decode_splits(B: int, hkv: int, max_keys: int, target_wgs: int = 512, min_keys_per_split: int = 256) -> int:
     """Split-K factor for the decode kernel: enough workgroups to fill 256 CUs, >= min_keys_per_split keys each."""
     if B <= 0:
         return 1
@@ -34,8 +35,8 @@ def decode_splits(B: int, hkv: int, max_keys: int, target_wgs: int = 1024, min_k
 
 class ModelRunner:
     def __init__(self, model: TransformerLM, k_caches, v_caches, kvm, max_num_seqs: int, max_blocks_per_seq: int,
-                 cascade_min_prefix: int = 512, use_cascade: bool = True, target_wgs: int = 768,
-                 prefill_kv_chunk: int = 2048):
+                 cascade_min_prefix: int = 512, use_cascade: bool = True, target_wgs: int = 256,
+                 prefill_kv_chunk: int = 1024):
         self.model = model
         self.k_caches, self.v_caches = k_caches, v_caches
         self.kvm = kvm
@@ -43,7 +44,7 @@ class ModelRunner:
         self.max_num_seqs = max_num_seqs
         self.max_blocks = max_blocks_per_seq
         self.G = model.hq // model.hkv
-        self.tile = 128 // self.G
+        self.tile = ops.tile_rows(0) // self.G  # tokens per attention work item
         self.cascade_min_prefix = cascade_min_prefix
         self.target_wgs = target_wgs
         self.prefill_kv_chunk = prefill_kv_chunk
@@ -116,7 +117,7 @@ class ModelRunner:
                 # key chunks sized so the prefix pass alone launches ~target_wgs workgroups
                 groups = math.ceil(B / self.tile)
                 want = max(1, self.target_wgs // (groups * self.model.hkv))
-                chunk = max(256, math.ceil(P / want / 32) * 32)
+                chunk = min(MAX_ITEM_KEYS, max(256, math.ceil(P / want / 32) * 32))
                 nc = math.ceil(P / chunk)
                 pit = []
                 for g0 in range(0, B, self.tile):
@@ -136,8 +137,9 @@ class ModelRunner:
             # few query tiles against a long key range (a new turn of a thread with a ~20k-token cached context):
             # split every tile's key range so the pass fills the GPU, merge the partials afterwards
             max_kv = max(b for _, _, b in pre)
-            if len(items) * self.model.hkv < self.target_wgs // 2 and max_kv > 2 * self.prefill_kv_chunk:
-                ck = self.prefill_kv_chunk
+            few = len(items) * self.model.hkv < self.target_wgs // 2 and max_kv > 2 * self.prefill_kv_chunk
+            if few or max_kv > MAX_ITEM_KEYS:
+                ck = self.prefill_kv_chunk if few else MAX_ITEM_KEYS
                 split_items = []
                 for (q0, cnt, btr, lo, hi, _, _, _) in items:
                     for c in range(math.ceil(hi / ck)):

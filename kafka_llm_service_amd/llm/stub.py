@@ -1,0 +1,73 @@
+"""Test / plumbing providers.
+
+``StubEchoProvider`` — BASELINE config 1 (the reference's plumbing measured with an instant LLM):
+echoes the last user message back as ``n_chunks`` content chunks with no delay.
+``ScriptedProvider`` — replays scripted turns (text and/or tool calls split into streaming deltas), the fake-LLM seam
+the survey used to capture the reference's golden SSE traces.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import uuid
+from typing import Any, AsyncGenerator
+
+from kafka_llm_service_amd.llm.base import LLMProvider
+from kafka_llm_service_amd.llm.types import LLMProviderError, Message, StreamChunk, Usage
+
+
+class StubEchoProvider(LLMProvider):
+    def __init__(self, n_chunks: int = 128, delay_s: float = 0.0, tool_provider=None):
+        super().__init__(tool_provider)
+        self.n_chunks = n_chunks
+        self.delay_s = delay_s
+
+    async def stream_completion(self, messages, *, temperature=None, max_tokens=None, stop=None,
+                                **kwargs) -> AsyncGenerator[StreamChunk, None]:
+        last = next((m.content for m in reversed(messages) if m.role == "user" and m.content), "") or "ok"
+        cid = f"chatcmpl-{uuid.uuid4().hex[:24]}"
+        yield StreamChunk(role="assistant", id=cid)
+        n = self.n_chunks if max_tokens is None else min(self.n_chunks, max_tokens)
+        for i in range(n):
+            if self.delay_s:
+                await asyncio.sleep(self.delay_s)
+            yield StreamChunk(content=last[i % len(last)] if last else "x", id=cid)
+        yield StreamChunk(finish_reason="stop", id=cid, usage=Usage(prompt_tokens=sum(len(m.content or "")
+                                                                                        for m in messages),
+                                                                     completion_tokens=n,
+                                                                     total_tokens=n))
+
+
+class ScriptedProvider(LLMProvider):
+    """Each call pops the next scripted turn: {"text": str} and/or {"tool_calls": [{"name", "arguments"}]},
+    or {"error": "message"} to raise an LLMProviderError (e.g. a context-length error for compaction tests)."""
+
+    def __init__(self, turns: list[dict[str, Any]], split: int = 7, tool_provider=None):
+        super().__init__(tool_provider)
+        self.turns = list(turns)
+        self.split = split
+        self.calls: list[list[Message]] = []
+
+    async def stream_completion(self, messages, *, temperature=None, max_tokens=None, stop=None,
+                                **kwargs) -> AsyncGenerator[StreamChunk, None]:
+        self.calls.append(list(messages))
+        turn = self.turns.pop(0) if self.turns else {"text": "done"}
+        if "error" in turn:
+            raise LLMProviderError(turn["error"], provider="scripted", status_code=400)
+        cid = f"chatcmpl-{uuid.uuid4().hex[:24]}"
+        yield StreamChunk(role="assistant", id=cid)
+        text = turn.get("text", "")
+        for i in range(0, len(text), self.split):
+            yield StreamChunk(content=text[i:i + self.split], id=cid)
+        calls = turn.get("tool_calls") or []
+        for idx, tc in enumerate(calls):
+            tid = tc.get("id") or f"call_{uuid.uuid4().hex[:24]}"
+            yield StreamChunk(tool_calls=[{"index": idx, "id": tid, "type": "function",
+                                           "function": {"name": tc["name"], "arguments": ""}}], id=cid)
+            args = tc.get("arguments", {})
+            s = args if isinstance(args, str) else json.dumps(args)
+            for i in range(0, len(s), self.split):
+                yield StreamChunk(tool_calls=[{"index": idx, "function": {"arguments": s[i:i + self.split]}}],
+                                  id=cid)
+        yield StreamChunk(finish_reason="tool_calls" if calls else "stop", id=cid,
+                          usage=Usage(completion_tokens=len(text), total_tokens=len(text)))

@@ -85,13 +85,19 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part,
 
 
 def attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, scale: float, out=None, out_part=None,
-                 lse_part=None) -> None:
+                 lse_part=None, variant: int = 0) -> None:
     """Work-item paged attention (chunked prefill / cascade prefix). ``items`` is int32 [n, 8]:
     (q_start, q_count, bt_row, kv_lo, kv_hi, split, 0, 0)."""
     if _gpu(q):
-        ext().attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, out, out_part, lse_part, float(scale))
+        ext().attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, out, out_part, lse_part, float(scale),
+                           int(variant))
     else:
         ref.attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale, out, out_part, lse_part)
+
+
+def tile_rows(variant: int = 0) -> int:
+    """Query rows ((token, head) pairs of one KV head) per attn_prefill work item for a kernel variant."""
+    return 256 if variant == 0 else 128
 
 
 def attn_merge(part, lse, out, lse_out=None) -> None:

@@ -21,6 +21,8 @@
 //                        chunked prefill and for the cascade pass where the rows are the decode sequences of a
 //                        batch and the keys are the shared system-prompt prefix (read once for all sequences).
 //   attn_merge_kernel    log-sum-exp merge of S partials per (row, head) -> bf16.
+//   (attn_prefill_kernel variants: 0 = 8 waves / 256 rows per item, K/V staged once per workgroup in LDS;
+//    1 = 4 waves / 128 rows, LDS; 2 = 4 waves / 128 rows, per-wave register loads. ops.tile_rows(variant).)
 #include "common.h"
 
 namespace kafka {
@@ -77,41 +79,46 @@ __device__ __forceinline__ void block_pages(const int* __restrict__ bt, int key0
   p1 = (key0 + 16 < end) ? bt[(key0 >> 4) + 1] : p0;
 }
 
-// One 32-key step for one wave on already-loaded fragments.
+// Online softmax of one 32-key S^T tile (raw scores, lane = query column) + the P.V MFMAs.
+//   * `masked` (wave-uniform) is false for interior blocks: no per-element range / causal test at all;
+//   * the O / l rescale runs only when some row's running max moved (wave vote) — exact, and after the first few
+//     blocks of a row it almost never fires;
+//   * the softmax scale is folded into one FMA in front of exp2.
+// acc.m is kept in the scaled log2 domain.
 template <int D>
-__device__ __forceinline__ void attn_compute(const KVFrag<D>& f, int key0, int lo, int hi, int limit,
-                                             const bf16x8 (&qf)[D / 16], float scale_log2, WaveAcc<D>& acc,
-                                             int lane) {
+__device__ __forceinline__ void softmax_pv(f32x16& s, bool masked, int key0, int lo, int hi, int limit,
+                                           float scale_log2, const bf16x8 (&vf)[2][D / 32], WaveAcc<D>& acc,
+                                           int lane) {
   const int h = lane >> 5;
-  f32x16 s = {};
+  if (masked) {
 #pragma unroll
-  for (int kk = 0; kk < D / 16; ++kk) s = mfma32(f.k[kk], qf[kk], s);
-
-  float mx = -INFINITY;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int key = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-    const bool ok = (key >= lo) & (key < hi) & (key <= limit);
-    const float v = ok ? s[i] * scale_log2 : -INFINITY;
-    s[i] = v;
-    mx = fmaxf(mx, v);
+    for (int i = 0; i < 16; ++i) {
+      const int key = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (!((key >= lo) & (key < hi) & (key <= limit))) s[i] = -INFINITY;
+    }
   }
+  float mx = s[0];
+#pragma unroll
+  for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[i]);
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  const float m_new = fmaxf(acc.m, mx);
+  const float m_new = fmaxf(acc.m, mx * scale_log2);
   const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-  const float alpha = exp2f(acc.m - m_use);
+  if (!__all(m_new == acc.m)) {
+    const float alpha = exp2f(acc.m - m_use);
+    acc.l *= alpha;
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t) acc.o[t] *= alpha;
+  }
+  acc.m = m_new;
   float psum = 0.f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const float p = exp2f(s[i] - m_use);
+    const float p = exp2f(fmaf(s[i], scale_log2, -m_use));
     s[i] = p;
     psum += p;
   }
   psum += __shfl_xor(psum, 32, 64);
-  acc.l = acc.l * alpha + psum;
-  acc.m = m_new;
-#pragma unroll
-  for (int t = 0; t < D / 32; ++t) acc.o[t] *= alpha;
+  acc.l += psum;
   bf16x8 pf[2];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -121,7 +128,18 @@ __device__ __forceinline__ void attn_compute(const KVFrag<D>& f, int key0, int l
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-    for (int t = 0; t < D / 32; ++t) acc.o[t] = mfma32(f.v[s2][t], pf[s2], acc.o[t]);
+    for (int t = 0; t < D / 32; ++t) acc.o[t] = mfma32(vf[s2][t], pf[s2], acc.o[t]);
+}
+
+// One 32-key step for one wave on already-loaded fragments.
+template <int D>
+__device__ __forceinline__ void attn_compute(const KVFrag<D>& f, int key0, int lo, int hi, int limit,
+                                             const bf16x8 (&qf)[D / 16], float scale_log2, WaveAcc<D>& acc,
+                                             int lane, bool masked = true) {
+  f32x16 s = {};
+#pragma unroll
+  for (int kk = 0; kk < D / 16; ++kk) s = mfma32(f.k[kk], qf[kk], s);
+  softmax_pv<D>(s, masked, key0, lo, hi, limit, scale_log2, f.v, acc, lane);
 }
 
 // Key blocks first, first+stride, ... < nblk (block b covers keys [base + 32 b, base + 32 b + 32)), software
@@ -143,7 +161,9 @@ __device__ __forceinline__ void attn_blocks(const bf16* __restrict__ k_cache, co
     KVFrag<D> nxt;
     block_pages(bt, base + 32 * nb, end, p0, p1);
     load_kv<D>(nxt, k_cache, v_cache, Hkv, kvh, p0, p1, lane);
-    attn_compute<D>(cur, base + 32 * b, lo, hi, limit, qf, scale_log2, acc, lane);
+    const int key0 = base + 32 * b;
+    attn_compute<D>(cur, key0, lo, hi, limit, qf, scale_log2, acc, lane,
+                    (key0 < lo) | (key0 + 32 > hi) | (key0 + 31 > limit));
     cur = nxt;
   }
 }
@@ -245,8 +265,99 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16* __restrict
 // ------------------------------------------------------------------------------------------------------------------
 // Prefill / cascade: grid (num_items, Hkv), 256 threads; wave w owns tile rows [32w, 32w+32), row R -> token R / G,
 // head kvh*G + R % G.
+// LDS staging for the tile kernel: every 32-key block is loaded ONCE per workgroup (256 threads x 4 x 16 B) and
+// read by all 4 waves from LDS, instead of once per wave from L2 (the 4 waves own different query rows but need the
+// same keys). Two 16 KB buffers; the global loads of block b+1 are issued before the MFMAs of block b and written to
+// LDS after them (issue-early / write-late), one barrier per block.
+//   K tile  [32 keys][128 d] bf16, 256-B rows, 16-B chunk c of key k stored at chunk c ^ (k & 15) (XOR swizzle:
+//           the A-fragment reads of 16 lanes on 16 different keys hit 16 different bank groups)
+//   V tile  [2 pages][128 d][16 pos] bf16, 32-B rows, 16-B half j of row d stored at half j ^ ((d >> 3) & 1)
+constexpr int KT_BYTES = 32 * 128 * 2;
+constexpr int VT_BYTES = 2 * 128 * 16 * 2;
+constexpr int STAGE_BYTES = KT_BYTES + VT_BYTES;
+constexpr int MAX_STAGED_PAGES = 2048;  // keys [base, base + 32k) have their page ids staged in LDS
+
+// NT threads stage one block: K 512 chunks + V 512 chunks of 16 B -> 1024 / NT chunks of each per thread.
+template <int NT>
+struct StageRegs {
+  bf16x8 k[512 / NT];
+  bf16x8 v[512 / NT];
+};
+
+// Staging loads are issued with inline asm so hipcc's waitcnt pass does not see them: it would otherwise drain
+// vmcnt(0) before the LDS store of the OLDER register stage and collapse the 2-deep prefetch to 1 (ROCm 7.2). The
+// loop waits for them itself with a counted `s_waitcnt vmcnt(N)` (N = loads of the younger stage still in flight).
+__device__ __forceinline__ bf16x8 asm_load16(const bf16* p) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  i32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+template <int NT>
+__device__ __forceinline__ void stage_load(StageRegs<NT>& sr, const bf16* __restrict__ k_cache,
+                                           const bf16* __restrict__ v_cache, int Hkv, int kvh, int p0, int p1,
+                                           int tid) {
+  constexpr int D = 128;
+#pragma unroll
+  for (int i = 0; i < 512 / NT; ++i) {
+    const int qd = tid + NT * i;
+    const int key = qd >> 4, c = qd & 15;
+    const int page = key < 16 ? p0 : p1;
+    sr.k[i] = asm_load16(k_cache + ((int64_t)page * Hkv + kvh) * (PAGE * D) + (key & 15) * D + c * 8);
+    const int vp = (qd >> 8) ? p1 : p0;
+    sr.v[i] = asm_load16(v_cache + ((int64_t)vp * Hkv + kvh) * (D * PAGE) + (qd & 255) * 8);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int NT>
+__device__ __forceinline__ void stage_store(const StageRegs<NT>& sr, char* lds, int tid) {
+#pragma unroll
+  for (int i = 0; i < 512 / NT; ++i) {
+    const int qd = tid + NT * i;
+    const int key = qd >> 4, c = qd & 15;
+    *reinterpret_cast<bf16x8*>(lds + key * 256 + 16 * (c ^ (key & 15))) = sr.k[i];
+    const int vq = qd & 255, d = vq >> 1, half = vq & 1;
+    *reinterpret_cast<bf16x8*>(lds + KT_BYTES + (qd >> 8) * 4096 + d * 32 + 16 * (half ^ ((d >> 3) & 1))) =
+        sr.v[i];
+  }
+}
+
+// One 32-key step reading K/V fragments from an LDS stage. All 8 K-fragment reads are issued before the first
+// QK^T MFMA and all 8 V-fragment reads right behind the QK^T MFMAs (sched_barrier pins the order; left alone hipcc
+// issues one ds_read at a time, each waited with lgkmcnt(0) before its MFMA).
 template <int D>
-__global__ __launch_bounds__(256) void attn_prefill_kernel(const AttnWorkItem* __restrict__ items,
+__device__ __forceinline__ void attn_compute_lds(const char* lds, int key0, int lo, int hi, int limit,
+                                                 const bf16x8 (&qf)[D / 16], float scale_log2, WaveAcc<D>& acc,
+                                                 int lane, bool masked) {
+  const int r = lane & 31, h = lane >> 5;
+  bf16x8 kf[D / 16];
+#pragma unroll
+  for (int kk = 0; kk < D / 16; ++kk)
+    kf[kk] = *reinterpret_cast<const bf16x8*>(lds + r * 256 + 16 * ((2 * kk + h) ^ (r & 15)));
+  __builtin_amdgcn_sched_barrier(0);
+  f32x16 s = {};
+#pragma unroll
+  for (int kk = 0; kk < D / 16; ++kk) s = mfma32(kf[kk], qf[kk], s);
+  bf16x8 vf[2][D / 32];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t) {
+      const int d = 32 * t + r;
+      vf[s2][t] = *reinterpret_cast<const bf16x8*>(lds + KT_BYTES + s2 * 4096 + d * 32 + 16 * (h ^ ((d >> 3) & 1)));
+    }
+  __builtin_amdgcn_sched_barrier(0);
+  softmax_pv<D>(s, masked, key0, lo, hi, limit, scale_log2, vf, acc, lane);
+}
+
+template <int D, int NW, bool LDS>
+__global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkItem* __restrict__ items,
                                                             const bf16* __restrict__ q, int64_t q_stride,
                                                             const bf16* __restrict__ k_cache,
                                                             const bf16* __restrict__ v_cache, int Hkv, int G,
@@ -269,18 +380,98 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const AttnWorkItem* _
   int wmax = limit;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o, 64));
+  int wmin = valid ? limit : 0x7fffffff;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wmin = min(wmin, __shfl_xor(wmin, o, 64));
   const int lo = it.kv_lo;
   const int hi = min(it.kv_hi, wmax + 1);
   const int* bt = block_tables + (int64_t)it.bt_row * bt_stride;
 
   WaveAcc<D> acc;
   init_acc<D>(acc);
-  if (hi > lo) {
-    bf16x8 qf[D / 16];
-    load_q_frags<D>(qf, q + (int64_t)token * q_stride + (int64_t)(kvh * G + g) * D, valid, h);
-    const int base = lo & ~31;
-    attn_blocks<D>(k_cache, v_cache, Hkv, kvh, bt, base, 0, (hi - base + 31) >> 5, 1, hi, lo, hi, limit, qf,
-                   scale_log2, acc, lane);
+  if constexpr (!LDS) {
+    if (hi > lo) {
+      bf16x8 qf[D / 16];
+      load_q_frags<D>(qf, q + (int64_t)token * q_stride + (int64_t)(kvh * G + g) * D, valid, h);
+      const int base = lo & ~31;
+      attn_blocks<D>(k_cache, v_cache, Hkv, kvh, bt, base, 0, (hi - base + 31) >> 5, 1, hi, lo, hi, limit, qf,
+                     scale_log2, acc, lane);
+    }
+  } else {
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE_BYTES];
+    __shared__ int s_hi[NW];
+    __shared__ int s_pages[MAX_STAGED_PAGES];
+    if (lane == 0) s_hi[w] = hi;
+    __syncthreads();
+    int hi_wg = s_hi[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) hi_wg = max(hi_wg, s_hi[i]);
+    if (hi_wg > lo) {  // workgroup-uniform
+      bf16x8 qf[D / 16];
+      load_q_frags<D>(qf, q + (int64_t)token * q_stride + (int64_t)(kvh * G + g) * D, valid, h);
+      // retire the Q loads here: otherwise hipcc keeps a vmcnt(0) for them inside the loop, which would also
+      // drain the (compiler-invisible) staging loads every block
+#pragma unroll
+      for (int kk = 0; kk < D / 16; ++kk) asm volatile("" ::"v"(qf[kk]));
+      const int base = lo & ~31;
+      const int nblk = (hi_wg - base + 31) >> 5;
+      const int tid = threadIdx.x;
+      constexpr int LOADS = 2 * (512 / (NW * 64));  // asm loads per register stage per thread
+      // page indices of the item's key range staged in LDS once: no scalar global load (and no lgkmcnt(0) on it)
+      // inside the block loop
+      // (the host never builds an LDS-variant item spanning more than MAX_STAGED_PAGES pages: model_runner splits
+      // longer key ranges; a violating item produces NaN instead of reading out of bounds)
+      const int pg0 = base >> 4;
+      const int npg = ((hi_wg + 15) >> 4) - pg0;
+      const bool fits = npg <= MAX_STAGED_PAGES;
+      for (int i = tid; i < npg && i < MAX_STAGED_PAGES; i += NW * 64) s_pages[i] = bt[pg0 + i];
+      __syncthreads();
+      auto pages_of = [&](int key0, int& a, int& b2) {
+        const int i0 = min((key0 >> 4) - pg0, MAX_STAGED_PAGES - 2);
+        a = s_pages[i0];
+        b2 = (key0 + 16 < hi_wg) ? s_pages[i0 + 1] : a;
+      };
+      if (!fits) acc.m = acc.l = __builtin_nanf("");
+      // two register stages in flight (A: odd blocks, B: even blocks >= 2): the load of block b+3 is issued right
+      // after block b's MFMAs and written to LDS two blocks later, so HBM latency has two compute phases of cover.
+      StageRegs<NW * 64> ra, rb;
+      int p0, p1;
+      pages_of(base, p0, p1);
+      stage_load<NW * 64>(ra, k_cache, v_cache, Hkv, kvh, p0, p1, tid);
+      wait_vmcnt<0>();
+      stage_store<NW * 64>(ra, lds, tid);
+      if (nblk > 1) {
+        pages_of(base + 32, p0, p1);
+        stage_load<NW * 64>(ra, k_cache, v_cache, Hkv, kvh, p0, p1, tid);
+      }
+      if (nblk > 2) {
+        pages_of(base + 64, p0, p1);
+        stage_load<NW * 64>(rb, k_cache, v_cache, Hkv, kvh, p0, p1, tid);
+      }
+      __syncthreads();
+      auto body = [&](int b, StageRegs<NW * 64>& regs) {
+        const int key0 = base + 32 * b;
+        if (key0 < hi) {  // wave-uniform: skip blocks past this wave's causal limit
+          const bool masked = (key0 < lo) | (key0 + 32 > hi) | (key0 + 31 > wmin);
+          attn_compute_lds<D>(lds + (b & 1) * STAGE_BYTES, key0, lo, hi, limit, qf, scale_log2, acc, lane, masked);
+        }
+        if (b + 1 < nblk) {
+          // regs hold block b+1; the other stage (block b+2) may still be in flight
+          if (b + 2 < nblk) wait_vmcnt<LOADS>();
+          else wait_vmcnt<0>();
+          stage_store<NW * 64>(regs, lds + ((b + 1) & 1) * STAGE_BYTES, tid);
+        }
+        if (b + 3 < nblk) {
+          pages_of(key0 + 96, p0, p1);
+          stage_load<NW * 64>(regs, k_cache, v_cache, Hkv, kvh, p0, p1, tid);
+        }
+        __syncthreads();
+      };
+      for (int b = 0; b < (fits ? nblk : 0); b += 2) {
+        body(b, ra);
+        if (b + 1 < nblk) body(b + 1, rb);
+      }
+    }
   }
   if (!valid) return;
   const int head = kvh * G + g;
@@ -315,54 +506,48 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const AttnWorkItem* _
 }
 
 // ------------------------------------------------------------------------------------------------------------------
-// Merge S partials of every head of one row: grid (rows), 256 threads. The per-(head, split) merge weights
-// exp2(lse - M) / L are computed once into LDS; then every thread combines float4 columns of its heads.
-constexpr int MERGE_MAX_HS = 4096;  // Hq * S
+// Merge S partials: grid (rows, ceil(Hq / 8)), 256 threads = 8 heads x 32 lanes x float4 columns. Each lane
+// recomputes its head's max / sum over the S lse values (L1-resident broadcast reads), then accumulates its 4 columns.
+constexpr int MERGE_MAX_S = 256;
 template <int D>
 __global__ __launch_bounds__(256) void attn_merge_kernel(const float* __restrict__ part, const float* __restrict__ lse,
                                                           int S, bf16* __restrict__ out, int64_t out_stride, int Hq,
                                                           float* __restrict__ lse_out) {
-  __shared__ float wgt[MERGE_MAX_HS];
-  __shared__ float sM[64], sL[64];
+  static_assert(D == 128, "merge maps 32 lanes x float4 onto one head");
   const int64_t row = blockIdx.x;
-  const float* l = lse + row * Hq * S;
-  for (int hh = threadIdx.x; hh < Hq; hh += 256) {
-    float M = -INFINITY;
-    for (int s = 0; s < S; ++s) M = fmaxf(M, l[hh * S + s]);
-    float L = 0.f;
-    if (M != -INFINITY)
-      for (int s = 0; s < S; ++s) L += exp2f(l[hh * S + s] - M);
-    sM[hh] = M;
-    sL[hh] = L;
-    if (lse_out) lse_out[row * Hq + hh] = L > 0.f ? M + log2f(L) : -INFINITY;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < Hq * S; i += 256) {
-    const int hh = i / S;
-    const float L = sL[hh];
-    wgt[i] = L > 0.f ? exp2f(l[i] - sM[hh]) / L : 0.f;
-  }
-  __syncthreads();
-  constexpr int D4 = D / 4;
-  for (int i = threadIdx.x; i < Hq * D4; i += 256) {
-    const int hh = i / D4, c = (i % D4) * 4;
+  const int hh = blockIdx.y * 8 + (threadIdx.x >> 5);
+  if (hh >= Hq) return;
+  const int c = (threadIdx.x & 31) * 4;
+  const float* l = lse + (row * Hq + hh) * S;
+  float M = -INFINITY;
+  for (int s = 0; s < S; ++s) M = fmaxf(M, l[s]);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float L = 0.f;
+  if (M != -INFINITY) {
     const float* p = part + ((row * Hq + hh) * S) * D + c;
-    const float* w = wgt + hh * S;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     int s = 0;
     for (; s + 4 <= S; s += 4) {
+      const float w0 = exp2f(l[s] - M), w1 = exp2f(l[s + 1] - M), w2 = exp2f(l[s + 2] - M),
+                  w3 = exp2f(l[s + 3] - M);
       const f32x4 a = *reinterpret_cast<const f32x4*>(p + (s + 0) * D);
       const f32x4 b = *reinterpret_cast<const f32x4*>(p + (s + 1) * D);
       const f32x4 cc = *reinterpret_cast<const f32x4*>(p + (s + 2) * D);
       const f32x4 d = *reinterpret_cast<const f32x4*>(p + (s + 3) * D);
-      acc += a * w[s] + b * w[s + 1] + cc * w[s + 2] + d * w[s + 3];
+      acc += a * w0 + b * w1 + cc * w2 + d * w3;
+      L += (w0 + w1) + (w2 + w3);
     }
-    for (; s < S; ++s) acc += *reinterpret_cast<const f32x4*>(p + s * D) * w[s];
-    bf16x4 o;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = (bf16)acc[j];
-    *reinterpret_cast<bf16x4*>(out + row * out_stride + (int64_t)hh * D + c) = o;
+    for (; s < S; ++s) {
+      const float w0 = exp2f(l[s] - M);
+      acc += *reinterpret_cast<const f32x4*>(p + s * D) * w0;
+      L += w0;
+    }
   }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  bf16x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = (bf16)(acc[j] * inv);
+  *reinterpret_cast<bf16x4*>(out + row * out_stride + (int64_t)hh * D + c) = o;
+  if (lse_out && (threadIdx.x & 31) == 0) lse_out[row * Hq + hh] = L > 0.f ? M + log2f(L) : -INFINITY;
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -382,21 +567,31 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
 extern "C" hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride, const bf16* k_cache,
                                const bf16* v_cache, int Hkv, int G, int D, const int* block_tables, int bt_stride,
                                const int* q_limit, bf16* out, int64_t out_stride, float* out_part, float* lse_part,
-                               int S_total, float scale, hipStream_t st) {
+                               int S_total, float scale, int variant, hipStream_t st) {
   if (n_items == 0) return hipSuccess;
   if (D != 128 || G < 1 || G > 32 || (128 % G) != 0) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
-  attn_prefill_kernel<128><<<dim3(n_items, Hkv), 256, 0, st>>>(
-      reinterpret_cast<const AttnWorkItem*>(items), q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride,
-      q_limit, out, out_stride, out_part, lse_part, S_total, scale_log2);
+  const auto* it = reinterpret_cast<const AttnWorkItem*>(items);
+  if (variant == 0)  // 8 waves, 256 query rows per item, K/V staged in LDS
+    attn_prefill_kernel<128, 8, true><<<dim3(n_items, Hkv), 512, 0, st>>>(
+        it, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
+        lse_part, S_total, scale_log2);
+  else if (variant == 1)  // 4 waves, 128 rows, LDS
+    attn_prefill_kernel<128, 4, true><<<dim3(n_items, Hkv), 256, 0, st>>>(
+        it, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
+        lse_part, S_total, scale_log2);
+  else  // 4 waves, 128 rows, per-wave register loads
+    attn_prefill_kernel<128, 4, false><<<dim3(n_items, Hkv), 256, 0, st>>>(
+        it, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
+        lse_part, S_total, scale_log2);
   return hipGetLastError();
 }
 
 extern "C" hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows, int Hq, int S, int D, bf16* out,
                              int64_t out_stride, float* lse_out, hipStream_t st) {
   if (rows == 0) return hipSuccess;
-  if (D != 128 || Hq > 64 || Hq * S > MERGE_MAX_HS) return hipErrorInvalidValue;
-  attn_merge_kernel<128><<<rows, 256, 0, st>>>(part, lse, S, out, out_stride, Hq, lse_out);
+  if (D != 128 || S > MERGE_MAX_S) return hipErrorInvalidValue;
+  attn_merge_kernel<128><<<dim3(rows, (Hq + 7) / 8), 256, 0, st>>>(part, lse, S, out, out_stride, Hq, lse_out);
   return hipGetLastError();
 }
 

@@ -22,7 +22,7 @@ hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const bf16*
 hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride, const bf16* k_cache,
                                const bf16* v_cache, int Hkv, int G, int D, const int* block_tables, int bt_stride,
                                const int* q_limit, bf16* out, int64_t out_stride, float* out_part, float* lse_part,
-                               int S_total, float scale, hipStream_t st);
+                               int S_total, float scale, int variant, hipStream_t st);
 hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows, int Hq, int S, int D, bf16* out,
                              int64_t out_stride, float* lse_out, hipStream_t st);
 hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
@@ -144,7 +144,8 @@ static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at
 
 static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                          at::Tensor block_tables, at::Tensor q_limit, c10::optional<at::Tensor> out,
-                         c10::optional<at::Tensor> out_part, c10::optional<at::Tensor> lse_part, double scale) {
+                         c10::optional<at::Tensor> out_part, c10::optional<at::Tensor> lse_part, double scale,
+                         int64_t variant) {
   CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
   CHECK_DT(items, at::kInt); CHECK_DT(block_tables, at::kInt); CHECK_DT(q_limit, at::kInt);
   TORCH_CHECK(items.is_contiguous() && items.dim() == 2 && items.size(1) == 8, "items must be [n, 8] int32");
@@ -181,7 +182,7 @@ static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at:
   CHECK_HIP(kafka_launch_attn_prefill(items.data_ptr<int>(), items.size(0), bptr(q), q.stride(0), bptr(k_cache),
                                        bptr(v_cache), Hkv, G, 128, block_tables.data_ptr<int>(),
                                        block_tables.stride(0), q_limit.data_ptr<int>(), op, os, pp, lp, S_total,
-                                       scale, cur_stream()));
+                                       scale, (int)variant, cur_stream()));
 }
 
 static void attn_merge(at::Tensor part, at::Tensor lse, at::Tensor out, c10::optional<at::Tensor> lse_out) {
@@ -234,7 +235,9 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("silu_mul", &silu_mul);
   m.def("rope_kv_write", &rope_kv_write);
   m.def("attn_decode", &attn_decode);
-  m.def("attn_prefill", &attn_prefill);
+  m.def("attn_prefill", &attn_prefill, py::arg("items"), py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
+        py::arg("block_tables"), py::arg("q_limit"), py::arg("out"), py::arg("out_part"), py::arg("lse_part"),
+        py::arg("scale"), py::arg("variant") = 0);
   m.def("attn_merge", &attn_merge);
   m.def("sample", &sample);
 }

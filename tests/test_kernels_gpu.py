@@ -112,7 +112,8 @@ def test_attn_decode(cuda, Hq, Hkv, lens, S):
     _close(lse_o, l_ref, atol=0.02, msg="decode lse")
 
 
-def test_attn_decode_kv_start_cascade(cuda):
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_attn_decode_kv_start_cascade(cuda, variant):
     """Cascade: prefix partial from attn_prefill (rows = decode seqs) + suffix partial from attn_decode == full."""
     torch.manual_seed(4)
     Hq, Hkv, D = 32, 8, 128
@@ -144,7 +145,7 @@ def test_attn_decode_kv_start_cascade(cuda):
     # prefix: rows are the B decode sequences, all using block table row 0 restricted to [0, P), split in 2 chunks
     items = torch.tensor([[0, B, 0, 0, 96, 0, 0, 0], [0, B, 0, 96, P, 1, 0, 0]], dtype=torch.int32, device=cuda)
     q_limit = torch.full((B,), 1 << 30, dtype=torch.int32, device=cuda)
-    ops.attn_prefill(items, q, k, v, bt, q_limit, scale, out_part=part, lse_part=lse)
+    ops.attn_prefill(items, q, k, v, bt, q_limit, scale, out_part=part, lse_part=lse, variant=variant)
     ops.attn_decode(q, k, v, bt, sl, ks, part, lse, S_suf, S_pre, scale)
     out = torch.empty(B, Hq, D, device=cuda, dtype=torch.bfloat16)
     ops.attn_merge(part, lse, out)
@@ -152,8 +153,9 @@ def test_attn_decode_kv_start_cascade(cuda):
     _close(out, o_ref, atol=0.02, msg="cascade")
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8)])
-def test_attn_prefill_causal(cuda, Hq, Hkv):
+def test_attn_prefill_causal(cuda, Hq, Hkv, variant):
     torch.manual_seed(6)
     D = 128
     G = Hq // Hkv
@@ -166,7 +168,7 @@ def test_attn_prefill_causal(cuda, Hq, Hkv):
     q = torch.randn(T, Hq, D, device=cuda, dtype=torch.bfloat16)
     q_limit = torch.empty(T, dtype=torch.int32)
     items = []
-    tile = 128 // G
+    tile = ops.tile_rows(variant) // G
     t0 = 0
     for b in range(B):
         for i in range(qlen[b]):
@@ -178,7 +180,7 @@ def test_attn_prefill_causal(cuda, Hq, Hkv):
     q_limit = q_limit.to(cuda)
     out = torch.zeros(T, Hq, D, device=cuda, dtype=torch.bfloat16)
     scale = 1 / math.sqrt(D)
-    ops.attn_prefill(items, q, k, v, bt, q_limit, scale, out=out)
+    ops.attn_prefill(items, q, k, v, bt, q_limit, scale, out=out, variant=variant)
     out_ref = torch.zeros(T, Hq, D, dtype=torch.bfloat16)
     ref.attn_prefill_items(items.cpu(), q.cpu(), k.cpu(), v.cpu(), bt.cpu(), q_limit.cpu(), scale, out=out_ref)
     _close(out, out_ref, atol=0.02, msg="prefill")
