@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Decode-shaped GEMMs of Llama-3-8B (y = x W^T, bf16): hipBLASLt vs rocBLAS vs the in-tree skinny GEMM.
+
+Reports us/call and the weight-streaming bandwidth (weights are read once per call; x is tiny)."""
+from __future__ import annotations
+
+import json
+import statistics
+import sys
+
+import torch
+import torch.nn.functional as F
+
+SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+          "lm_head": (128256, 4096)}
+
+
+def timeit(fn, iters=30, rounds=5):
+    res = []
+    for _ in range(rounds):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        fn()
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        res.append(s.elapsed_time(e) * 1e3 / iters)
+    return statistics.median(res)
+
+
+def main():
+    Ms = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,16,32,64,128").split(",")]
+    dev = torch.device("cuda:0")
+    have_custom = False
+    try:
+        from kafka_llm_service_amd import ops
+
+        have_custom = hasattr(ops, "skinny_gemm")
+    except Exception:
+        pass
+    for name, (N, K) in SHAPES.items():
+        w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
+        for M in Ms:
+            x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            row = {"gemm": name, "M": M, "N": N, "K": K}
+            for lib in ("cublaslt", "cublas"):
+                torch.backends.cuda.preferred_blas_library(lib)
+                us = timeit(lambda: F.linear(x, w))
+                row[f"{'hipblaslt' if lib == 'cublaslt' else 'rocblas'}_us"] = round(us, 1)
+            torch.backends.cuda.preferred_blas_library("cublaslt")
+            if have_custom and M <= 128:
+                ref = F.linear(x, w).float()
+                y = ops.skinny_gemm(x, w)
+                err = (y.float() - ref).abs().max().item()
+                us = timeit(lambda: ops.skinny_gemm(x, w))
+                row["skinny_us"] = round(us, 1)
+                row["skinny_err"] = round(err, 4)
+            best = min(v for k, v in row.items() if k.endswith("_us"))
+            row["best_TB/s"] = round(N * K * 2 / best / 1e6, 2)
+            print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,254 @@
+"""Thread / message store on SQLite — the source of truth for conversation state.
+
+Interface parity with /root/reference/src/db/local.py:20-370 and the Supabase client's thread-config surface
+(/root/reference/src/db/supabase.py:458-707): get_thread_messages / add_message(s) / create_thread / thread_exists /
+get_thread_metadata / delete_thread_messages / get|update_thread_sandbox_id / get_thread_config /
+get_or_create_vm_api_key / get_playbooks_for_kafka_profile.
+
+Fixed vs the reference:
+  * ordering is a monotonic per-thread ``seq`` (the reference ordered by ``created_at`` with 1-second resolution, so
+    same-second messages could come back in any order — quirk Q10),
+  * ``thread_lock(thread_id)`` serialises read-modify-write of one thread across concurrent requests (Q11),
+  * every message row keeps the engine token ids of generated assistant turns (``token_ids`` column): the chat
+    template re-renders history from them exactly, which keeps the thread's KV prefix cache hot,
+  * all SQLite work runs on one dedicated thread (sqlite3 connections are not thread-safe; aiosqlite is not
+    installed) so the API event loop never blocks on disk I/O (the reference's Supabase client blocked the loop).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import secrets
+import sqlite3
+import uuid
+from collections import defaultdict
+from concurrent.futures import ThreadPoolExecutor
+from datetime import datetime, timezone
+from typing import Any
+
+from kafka_llm_service_amd.llm.types import Message
+
+SCHEMA = """
+CREATE TABLE IF NOT EXISTS threads (
+    id TEXT PRIMARY KEY, created_at TEXT NOT NULL, metadata TEXT, sandbox_id TEXT, user_id TEXT,
+    kafka_profile_id TEXT, next_seq INTEGER NOT NULL DEFAULT 0);
+CREATE TABLE IF NOT EXISTS messages (
+    id TEXT PRIMARY KEY, thread_id TEXT NOT NULL REFERENCES threads(id), seq INTEGER NOT NULL,
+    message TEXT NOT NULL, token_ids TEXT, metadata TEXT, created_at TEXT NOT NULL);
+CREATE UNIQUE INDEX IF NOT EXISTS idx_messages_thread_seq ON messages(thread_id, seq);
+CREATE TABLE IF NOT EXISTS kafka_profiles (
+    id TEXT PRIMARY KEY, user_id TEXT, global_prompt TEXT, memory_dsn TEXT, virtual_keys TEXT);
+CREATE TABLE IF NOT EXISTS playbooks (
+    id TEXT PRIMARY KEY, kafka_profile_id TEXT, name TEXT, description TEXT, created_at TEXT);
+CREATE TABLE IF NOT EXISTS vm_api_keys (
+    id TEXT PRIMARY KEY, thread_id TEXT, user_id TEXT, api_key TEXT, status TEXT, created_at TEXT);
+"""
+
+
+def _now() -> str:
+    return datetime.now(timezone.utc).isoformat()
+
+
+class LocalDBClient:
+    def __init__(self, db_path: str | None = None):
+        self.db_path = db_path or os.environ.get("LOCAL_DB_PATH", "data/threads.db")
+        self._exec = ThreadPoolExecutor(max_workers=1, thread_name_prefix="kafka-sqlite")
+        self._conn: sqlite3.Connection | None = None
+        self._locks: dict[str, asyncio.Lock] = defaultdict(asyncio.Lock)
+        self._initialized = False
+
+    # --- plumbing ---------------------------------------------------------------------------------------------
+    def _connect(self) -> sqlite3.Connection:
+        if self._conn is None:
+            if self.db_path != ":memory:":
+                os.makedirs(os.path.dirname(os.path.abspath(self.db_path)), exist_ok=True)
+            self._conn = sqlite3.connect(self.db_path, check_same_thread=False)
+            self._conn.row_factory = sqlite3.Row
+            self._conn.execute("PRAGMA journal_mode=WAL")
+            self._conn.execute("PRAGMA synchronous=NORMAL")
+            self._conn.executescript(SCHEMA)
+        return self._conn
+
+    async def _run(self, fn, *args):
+        return await asyncio.get_running_loop().run_in_executor(self._exec, fn, *args)
+
+    async def initialize(self) -> None:
+        await self._run(self._connect)
+        self._initialized = True
+
+    async def close(self) -> None:
+        def _close():
+            if self._conn is not None:
+                self._conn.close()
+                self._conn = None
+        await self._run(_close)
+
+    def thread_lock(self, thread_id: str) -> asyncio.Lock:
+        """Per-thread lock: hold it across read-history -> run -> persist for one request."""
+        return self._locks[thread_id]
+
+    # --- threads ----------------------------------------------------------------------------------------------
+    async def create_thread(self, thread_id: str | None = None, system_message: str | None = None,
+                            user_id: str | None = None, kafka_profile_id: str | None = None,
+                            metadata: dict | None = None) -> dict[str, Any]:
+        tid = thread_id or str(uuid.uuid4())
+        created = _now()
+
+        def _do():
+            c = self._connect()
+            c.execute("INSERT OR IGNORE INTO threads(id, created_at, metadata, user_id, kafka_profile_id) "
+                      "VALUES (?,?,?,?,?)", (tid, created, json.dumps(metadata or {}), user_id, kafka_profile_id))
+            c.commit()
+        await self._run(_do)
+        if system_message:
+            await self.add_message(tid, Message(role="system", content=system_message))
+        return {"id": tid, "thread_id": tid, "created_at": created}
+
+    async def thread_exists(self, thread_id: str) -> bool:
+        def _do():
+            return self._connect().execute("SELECT 1 FROM threads WHERE id=?", (thread_id,)).fetchone() is not None
+        return await self._run(_do)
+
+    async def get_thread_metadata(self, thread_id: str) -> dict[str, Any] | None:
+        def _do():
+            r = self._connect().execute("SELECT * FROM threads WHERE id=?", (thread_id,)).fetchone()
+            if r is None:
+                return None
+            d = dict(r)
+            d["metadata"] = json.loads(d["metadata"] or "{}")
+            return d
+        return await self._run(_do)
+
+    # --- messages ---------------------------------------------------------------------------------------------
+    async def get_thread_messages(self, thread_id: str, limit: int | None = None,
+                                  include_system: bool = True) -> list[Message]:
+        def _do():
+            q = "SELECT message, token_ids FROM messages WHERE thread_id=? ORDER BY seq ASC"
+            args: list[Any] = [thread_id]
+            if limit:
+                q += " LIMIT ?"
+                args.append(limit)
+            return self._connect().execute(q, args).fetchall()
+        rows = await self._run(_do)
+        out = []
+        for r in rows:
+            d = json.loads(r["message"])
+            if not include_system and d.get("role") == "system":
+                continue
+            if r["token_ids"]:
+                d["token_ids"] = json.loads(r["token_ids"])
+            out.append(Message.from_dict(d))
+        return out
+
+    def _insert(self, c: sqlite3.Connection, thread_id: str, m: Message, metadata: dict | None) -> str:
+        mid = str(uuid.uuid4())
+        c.execute("INSERT OR IGNORE INTO threads(id, created_at, metadata) VALUES (?,?,?)",
+                  (thread_id, _now(), "{}"))
+        seq = c.execute("UPDATE threads SET next_seq = next_seq + 1 WHERE id=? RETURNING next_seq - 1",
+                        (thread_id,)).fetchone()[0]
+        c.execute("INSERT INTO messages(id, thread_id, seq, message, token_ids, metadata, created_at) "
+                  "VALUES (?,?,?,?,?,?,?)",
+                  (mid, thread_id, seq, json.dumps(m.to_dict()), json.dumps(m.token_ids) if m.token_ids else None,
+                   json.dumps(metadata or {}), _now()))
+        return mid
+
+    async def add_message(self, thread_id: str, message: Message, metadata: dict | None = None) -> str:
+        def _do():
+            c = self._connect()
+            mid = self._insert(c, thread_id, message, metadata)
+            c.commit()
+            return mid
+        return await self._run(_do)
+
+    async def add_messages(self, thread_id: str, messages: list[Message], metadata: dict | None = None) -> list[str]:
+        def _do():
+            c = self._connect()
+            ids = [self._insert(c, thread_id, m, metadata) for m in messages]
+            c.commit()
+            return ids
+        return await self._run(_do)
+
+    async def delete_thread_messages(self, thread_id: str) -> int:
+        def _do():
+            c = self._connect()
+            n = c.execute("DELETE FROM messages WHERE thread_id=?", (thread_id,)).rowcount
+            c.commit()
+            return n
+        return await self._run(_do)
+
+    # --- sandbox / config -------------------------------------------------------------------------------------
+    async def get_thread_sandbox_id(self, thread_id: str) -> str | None:
+        meta = await self.get_thread_metadata(thread_id)
+        return meta.get("sandbox_id") if meta else None
+
+    async def update_thread_sandbox_id(self, thread_id: str, sandbox_id: str | None) -> bool:
+        def _do():
+            c = self._connect()
+            n = c.execute("UPDATE threads SET sandbox_id=? WHERE id=?", (sandbox_id, thread_id)).rowcount
+            c.commit()
+            return n > 0
+        return await self._run(_do)
+
+    async def upsert_kafka_profile(self, profile_id: str, user_id: str | None = None, global_prompt: str | None = None,
+                                   memory_dsn: str | None = None, virtual_keys: dict | None = None) -> None:
+        def _do():
+            c = self._connect()
+            c.execute("INSERT OR REPLACE INTO kafka_profiles(id, user_id, global_prompt, memory_dsn, virtual_keys) "
+                      "VALUES (?,?,?,?,?)", (profile_id, user_id, global_prompt, memory_dsn,
+                                             json.dumps(virtual_keys or {})))
+            c.commit()
+        await self._run(_do)
+
+    async def add_playbook(self, kafka_profile_id: str, name: str, description: str) -> str:
+        pid = str(uuid.uuid4())
+
+        def _do():
+            c = self._connect()
+            c.execute("INSERT INTO playbooks(id, kafka_profile_id, name, description, created_at) VALUES (?,?,?,?,?)",
+                      (pid, kafka_profile_id, name, description, _now()))
+            c.commit()
+        await self._run(_do)
+        return pid
+
+    async def get_thread_config(self, thread_id: str) -> dict[str, Any] | None:
+        """Thread -> kafka profile join: global_prompt, memory_dsn, virtual keys, user id (None if no profile)."""
+        def _do():
+            r = self._connect().execute(
+                "SELECT t.user_id, t.kafka_profile_id, p.global_prompt, p.memory_dsn, p.virtual_keys "
+                "FROM threads t LEFT JOIN kafka_profiles p ON p.id = t.kafka_profile_id WHERE t.id=?",
+                (thread_id,)).fetchone()
+            return dict(r) if r else None
+        r = await self._run(_do)
+        if r is None or not r.get("kafka_profile_id"):
+            return None
+        r["virtual_keys"] = json.loads(r.get("virtual_keys") or "{}")
+        return r
+
+    async def get_playbooks_for_kafka_profile(self, kafka_profile_id: str) -> list[dict[str, Any]]:
+        def _do():
+            return [dict(r) for r in self._connect().execute(
+                "SELECT id, name, description, created_at FROM playbooks WHERE kafka_profile_id=? "
+                "ORDER BY created_at, id", (kafka_profile_id,)).fetchall()]
+        return await self._run(_do)
+
+    async def get_or_create_vm_api_key(self, thread_id: str, user_id: str | None = None) -> str:
+        def _do():
+            c = self._connect()
+            r = c.execute("SELECT api_key FROM vm_api_keys WHERE thread_id=? AND status='active'",
+                          (thread_id,)).fetchone()
+            if r:
+                return r["api_key"]
+            key = "vmk_" + secrets.token_hex(24)
+            c.execute("INSERT INTO vm_api_keys(id, thread_id, user_id, api_key, status, created_at) "
+                      "VALUES (?,?,?,?,?,?)", (str(uuid.uuid4()), thread_id, user_id, key, "active", _now()))
+            c.commit()
+            return key
+        return await self._run(_do)
+
+
+class MemoryDBClient(LocalDBClient):
+    """Same store on an in-memory SQLite database (tests, benchmarks, stateless deployments)."""
+
+    def __init__(self):
+        super().__init__(db_path=":memory:")

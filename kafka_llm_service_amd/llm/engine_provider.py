@@ -1,0 +1,120 @@
+"""EngineLLMProvider: the LLMProvider backed by the on-node MI355X engine (replaces the Portkey gateway provider,
+/root/reference/src/llm/portkey.py:62-701, per the north star).
+
+Per call: render the chat template (system prompt + tool schemas + history, re-using stored engine token ids) to
+token ids -> refuse up front with an OpenAI-style "maximum context length" error if it cannot fit (the agent's
+compaction path recognises it, /root/reference/src/llm/context_compaction/base.py:42-43) -> submit to the engine
+(routed by thread id for KV affinity) -> detokenize incrementally and yield live content chunks -> a generation that
+opens with the tool-call token (``<|python_tag|>`` / ``[TOOL_CALLS]``) is parsed into OpenAI ``tool_calls`` deltas
+(``index``/``id``/``type``/``function{name, arguments}``, the normalised shape the Portkey provider produced,
+portkey.py:447-464) -> a final chunk with ``finish_reason`` and real ``usage``. Every chunk carries the generated
+token ids so the agent can store them with the message (thread token cache).
+"""
+from __future__ import annotations
+
+import json
+import uuid
+from typing import Any, AsyncGenerator
+
+from kafka_llm_service_amd.engine.chat_template import ChatTemplate, parse_tool_calls
+from kafka_llm_service_amd.engine.sequence import SamplingParams
+from kafka_llm_service_amd.engine.tokenizer import IncrementalDetokenizer, tokenizer_for_model
+from kafka_llm_service_amd.llm.base import LLMProvider
+from kafka_llm_service_amd.llm.types import LLMProviderError, Message, StreamChunk, Usage
+
+
+class EngineLLMProvider(LLMProvider):
+    def __init__(self, client, default_max_tokens: int = 1024, model_name: str = "llama3-8b", tool_provider=None,
+                 ignore_eos: bool = False):
+        super().__init__(tool_provider)
+        self.client = client
+        self.tok = tokenizer_for_model(client.model_cfg)
+        self.template = ChatTemplate(self.tok)
+        self.default_max_tokens = default_max_tokens
+        self.model_name = model_name
+        self.ignore_eos = ignore_eos
+        self._tool_start = self.template.tool_call_start_ids()
+
+    def render(self, messages: list[Message], tools: list[dict] | None) -> list[int]:
+        return self.template.render(messages, tools)
+
+    async def stream_completion(self, messages: list[Message], *, temperature: float | None = None,
+                                max_tokens: int | None = None, stop: list[str] | None = None,
+                                tools: list[dict] | None = None, top_p: float | None = None,
+                                frequency_penalty: float | None = None, presence_penalty: float | None = None,
+                                seed: int | None = None, routing_key: str | None = None,
+                                **kwargs: Any) -> AsyncGenerator[StreamChunk, None]:
+        self.validate_messages(messages)
+        if tools is None:
+            tools = await self.get_tools()
+        prompt = self.render(messages, tools)
+        limit = self.client.max_model_len
+        if len(prompt) + 1 > limit:
+            raise LLMProviderError(f"This model's maximum context length is {limit} tokens. However, your messages "
+                                   f"resulted in {len(prompt)} tokens.", provider="engine", status_code=400)
+        max_new = min(max_tokens or self.default_max_tokens, limit - len(prompt))
+        params = SamplingParams(temperature=0.7 if temperature is None else float(temperature),
+                                top_p=1.0 if not top_p else float(top_p), max_tokens=max_new,
+                                frequency_penalty=float(frequency_penalty or 0.0),
+                                presence_penalty=float(presence_penalty or 0.0), seed=seed,
+                                ignore_eos=self.ignore_eos)
+        stops = [s for s in (stop or []) if s]
+        hold = max((len(s) for s in stops), default=1) - 1
+        rid = f"req-{uuid.uuid4().hex}"
+        cid = f"chatcmpl-{uuid.uuid4().hex[:24]}"
+        yield StreamChunk(role="assistant", id=cid, model=self.model_name)
+        detok = IncrementalDetokenizer(self.tok)
+        mode = None
+        tool_ids: list[int] = []
+        all_ids: list[int] = []
+        pending = ""
+        finish = "stop"
+        cached = 0
+        n_out = 0
+        stopped = False
+        async for out in self.client.generate(rid, prompt, params, routing_key):
+            ids = out.new_token_ids
+            all_ids.extend(ids)
+            n_out = out.num_output_tokens
+            cached = out.num_cached_tokens
+            if mode is None and ids:
+                mode = "tool" if ids[0] in self._tool_start else "text"
+            if mode == "tool":
+                tool_ids.extend(i for i in ids if not self.tok.is_special(i))
+            else:
+                text = detok.add(ids)
+                if text:
+                    pending += text
+                    if stops:
+                        cut = min((pending.find(s) for s in stops if s in pending), default=-1)
+                        if cut >= 0:
+                            if pending[:cut]:
+                                yield StreamChunk(content=pending[:cut], id=cid)
+                            finish, stopped = "stop", True
+                            break
+                    emit = pending[:len(pending) - hold] if hold else pending
+                    if emit:
+                        pending = pending[len(emit):]
+                        yield StreamChunk(content=emit, id=cid)
+            if out.finished:
+                finish = out.finish_reason or "stop"
+        if mode != "tool" and pending and not stopped:
+            yield StreamChunk(content=pending, id=cid)
+        calls = None
+        if mode == "tool":
+            body = self.tok.decode(tool_ids)
+            calls = parse_tool_calls(body)
+            if calls is None:  # malformed call: surface the raw text instead of inventing arguments
+                yield StreamChunk(content=body, id=cid)
+            else:
+                for c in calls:
+                    yield StreamChunk(tool_calls=[{"index": c["index"], "id": c["id"], "type": "function",
+                                                   "function": {"name": c["function"]["name"], "arguments": ""}}],
+                                      id=cid)
+                    yield StreamChunk(tool_calls=[{"index": c["index"],
+                                                   "function": {"arguments": c["function"]["arguments"]}}], id=cid)
+        if finish == "abort":
+            finish = "stop"
+        yield StreamChunk(finish_reason="tool_calls" if calls else finish, id=cid, token_ids=all_ids,
+                          usage=Usage(prompt_tokens=len(prompt), completion_tokens=n_out,
+                                      total_tokens=len(prompt) + n_out, cached_tokens=cached))

@@ -32,10 +32,9 @@ class StubEchoProvider(LLMProvider):
             if self.delay_s:
                 await asyncio.sleep(self.delay_s)
             yield StreamChunk(content=last[i % len(last)] if last else "x", id=cid)
-        yield StreamChunk(finish_reason="stop", id=cid, usage=Usage(prompt_tokens=sum(len(m.content or "")
-                                                                                        for m in messages),
-                                                                     completion_tokens=n,
-                                                                     total_tokens=n))
+        npt = sum(len(m.content or "") for m in messages)
+        yield StreamChunk(finish_reason="stop", id=cid, usage=Usage(prompt_tokens=npt, completion_tokens=n,
+                                                                     total_tokens=npt + n))
 
 
 class ScriptedProvider(LLMProvider):

@@ -1,0 +1,33 @@
+"""Prometheus metrics: request counts, TTFT / end-to-end latency histograms, and engine gauges
+(running / waiting sequences, KV pages used / free, prefix-cache hit tokens, output tokens) scraped from the engine
+client at render time. The reference exposed only /health (server.py:617-620)."""
+from __future__ import annotations
+
+from prometheus_client import CollectorRegistry, Counter, Histogram, generate_latest
+
+REGISTRY = CollectorRegistry(auto_describe=True)
+_BUCKETS = (0.005, 0.01, 0.02, 0.05, 0.1, 0.2, 0.5, 1.0, 2.0, 5.0, 10.0, 30.0, 60.0)
+REQUESTS = Counter("kafka_requests_total", "HTTP requests by route", ["route"], registry=REGISTRY)
+TTFT = Histogram("kafka_ttft_seconds", "time to first streamed content token", buckets=_BUCKETS, registry=REGISTRY)
+E2E = Histogram("kafka_request_seconds", "end-to-end streamed request latency", buckets=_BUCKETS, registry=REGISTRY)
+
+
+def render(state) -> str:
+    out = generate_latest(REGISTRY).decode()
+    health = state.engine_health() if state is not None else {}
+    lines = []
+    for k, v in sorted(_flatten(health).items()):
+        if isinstance(v, (int, float)) and not isinstance(v, bool):
+            lines.append(f"kafka_engine_{k} {v}")
+    return out + "\n".join(lines) + ("\n" if lines else "")
+
+
+def _flatten(d, prefix=""):
+    out = {}
+    for k, v in (d or {}).items():
+        key = f"{prefix}{k}".replace(".", "_").replace("-", "_")
+        if isinstance(v, dict):
+            out.update(_flatten(v, key + "_"))
+        else:
+            out[key] = v
+    return out
