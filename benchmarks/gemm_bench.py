@@ -16,14 +16,15 @@ SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "dow
 
 
 def timeit(fn, iters=30, rounds=5):
+    """fn(i) is called with the iteration index (used to rotate weight copies so every call streams from HBM)."""
     res = []
     for _ in range(rounds):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        fn()
+        fn(0)
         torch.cuda.synchronize()
         s.record()
-        for _ in range(iters):
-            fn()
+        for i in range(iters):
+            fn(i)
         e.record()
         torch.cuda.synchronize()
         res.append(s.elapsed_time(e) * 1e3 / iters)
@@ -41,25 +42,44 @@ def main():
     except Exception:
         pass
     for name, (N, K) in SHAPES.items():
-        w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
+        nrot = max(1, -(-640 * 2**20 // (N * K * 2)))  # > 256 MB Infinity Cache in total
+        ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) for _ in range(nrot)]
+        w = ws[0]
         for M in Ms:
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             row = {"gemm": name, "M": M, "N": N, "K": K}
             for lib in ("cublaslt", "cublas"):
                 torch.backends.cuda.preferred_blas_library(lib)
-                us = timeit(lambda: F.linear(x, w))
+                us = timeit(lambda i: F.linear(x, ws[i % nrot]))
                 row[f"{'hipblaslt' if lib == 'cublaslt' else 'rocblas'}_us"] = round(us, 1)
             torch.backends.cuda.preferred_blas_library("cublaslt")
-            if have_custom and M <= 128:
+            for S in (2, 4, 8):
+                if K % S:
+                    continue
+                xs = x.view(M, S, K // S).transpose(0, 1)
+
+                def f(i, S=S, xs=xs):
+                    wv = ws[i % nrot].view(N, S, K // S).permute(1, 2, 0)  # [S, K/S, N]
+                    return torch.bmm(xs, wv).sum(0)
                 ref = F.linear(x, w).float()
-                y = ops.skinny_gemm(x, w)
-                err = (y.float() - ref).abs().max().item()
-                us = timeit(lambda: ops.skinny_gemm(x, w))
-                row["skinny_us"] = round(us, 1)
-                row["skinny_err"] = round(err, 4)
+                err = (f(0).float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
+                row[f"bmm_splitk{S}_us"] = round(timeit(f), 1)
+                row[f"bmm_splitk{S}_err"] = round(err, 4)
+            if have_custom and M <= 64:
+                ref = F.linear(x, w).float()
+                for U in (4, 8):
+                    if not ops.skinny_supported(M, N, K, U):
+                        continue
+                    y = ops.skinny_gemm(x, w, U=U)
+                    err = (y.float() - ref).abs().max().item()
+                    us = timeit(lambda i: ops.skinny_gemm(x, ws[i % nrot], U=U))
+                    row[f"skinny{U}_us"] = round(us, 1)
+                    row[f"skinny{U}_err"] = round(err / (ref.abs().max().item() + 1e-6), 4)
             best = min(v for k, v in row.items() if k.endswith("_us"))
             row["best_TB/s"] = round(N * K * 2 / best / 1e6, 2)
             print(json.dumps(row), flush=True)
+        del ws, w
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":

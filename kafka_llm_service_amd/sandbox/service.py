@@ -20,11 +20,13 @@ import sys
 import uuid
 from typing import Any, AsyncGenerator
 
+from contextlib import asynccontextmanager
+
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, StreamingResponse
 
 _KERNEL_SRC = r'''
-import sys, json, traceback, io, contextlib
+import sys, json, traceback, io, contextlib, ast
 g = {"__name__": "__main__"}
 out = sys.stdout
 while True:
@@ -42,12 +44,13 @@ while True:
     code = 0
     with contextlib.redirect_stdout(w), contextlib.redirect_stderr(w):
         try:
-            try:
-                val = eval(compile(req["code"], "<cell>", "eval"), g)
+            tree = ast.parse(req["code"], "<cell>", "exec")
+            last = tree.body.pop() if tree.body and isinstance(tree.body[-1], ast.Expr) else None
+            exec(compile(tree, "<cell>", "exec"), g)
+            if last is not None:  # like a notebook: show the value of a trailing expression
+                val = eval(compile(ast.Expression(last.value), "<cell>", "eval"), g)
                 if val is not None:
                     print(repr(val))
-            except SyntaxError:
-                exec(compile(req["code"], "<cell>", "exec"), g)
         except BaseException:
             traceback.print_exc()
             code = 1
@@ -210,7 +213,13 @@ class SandboxService:
 
 def create_app(workdir: str) -> FastAPI:
     svc = SandboxService(workdir)
-    app = FastAPI(title="kafka sandbox service")
+
+    @asynccontextmanager
+    async def lifespan(app):
+        yield
+        await svc.reset()
+
+    app = FastAPI(title="kafka sandbox service", lifespan=lifespan)
     app.state.svc = svc
 
     @app.get("/health")
@@ -241,10 +250,6 @@ def create_app(workdir: str) -> FastAPI:
             yield "data: [DONE]\n\n"
         return StreamingResponse(gen(), media_type="text/event-stream",
                                  headers={"Cache-Control": "no-cache", "X-Accel-Buffering": "no"})
-
-    @app.on_event("shutdown")
-    async def _shutdown():
-        await svc.reset()
 
     return app
 

@@ -1,0 +1,71 @@
+"""Tokenizer / chat template / tool-call parsing: the prefix-stability property the prefix cache depends on
+ and the OpenAI tool_calls shape (portkey.py:447-464 normalisation)."""
+import asyncio
+import json
+
+from hypothesis import given, settings, strategies as st
+
+from kafka_llm_service_amd.engine.chat_template import ChatTemplate, parse_tool_calls
+from kafka_llm_service_amd.engine.tokenizer import IncrementalDetokenizer, get_tokenizer
+from kafka_llm_service_amd.llm.types import Message
+from kafka_llm_service_amd.server_tools import count_tool, get_weather_tool
+
+TOK = get_tokenizer("llama3", 128256)
+TPL = ChatTemplate(TOK)
+TOOLS = [get_weather_tool.definition, count_tool.definition]
+
+texts = st.text(alphabet=st.characters(blacklist_categories=("Cs",)), min_size=0, max_size=40)
+msgs = st.lists(st.tuples(st.sampled_from(["user", "assistant", "tool"]), texts), min_size=1, max_size=6)
+
+
+@settings(max_examples=80, deadline=None)
+@given(msgs, texts)
+def test_history_render_is_token_prefix(history, new_text):
+    hist = [Message(role="system", content="SYS")] + [
+        Message(role=r, content=t, tool_call_id="c1" if r == "tool" else None) for r, t in history]
+    a = TPL.render(hist, TOOLS, add_generation_prompt=False)
+    b = TPL.render(hist + [Message(role="user", content=new_text)], TOOLS)
+    assert b[:len(a)] == a
+
+
+def test_generated_tokens_reused_verbatim():
+    prompt_msgs = [Message(role="system", content="S"), Message(role="user", content="q")]
+    p = TPL.render(prompt_msgs, TOOLS)
+    gen = [500, 70000, 91234, TOK.special_id("<|eot_id|>")]  # arbitrary ids incl. pseudo-words + eot
+    hist = prompt_msgs + [Message(role="assistant", content=TOK.decode(gen), token_ids=gen)]
+    nxt = TPL.render(hist + [Message(role="user", content="more")], TOOLS)
+    assert nxt[:len(p) + len(gen)] == p + gen
+
+
+def test_special_tokens_and_roundtrip():
+    ids = TOK.encode("Hello, MI355X world!")
+    assert TOK.decode(ids) == "Hello, MI355X world!"
+    assert TOK.decode([TOK.special_id("<|eot_id|>")]) == ""
+    assert TOK.decode([TOK.special_id("<|eot_id|>")], skip_special_tokens=False) == "<|eot_id|>"
+    assert TOK.decode([120000]).strip()  # unused id -> deterministic pseudo-word
+    d = IncrementalDetokenizer(TOK)
+    s = "".join(d.add([i]) for i in TOK.encode("héllo wörld ✓ done"))
+    assert s == "héllo wörld ✓ done"
+
+
+def test_tool_call_render_and_parse():
+    m = Message(role="assistant", tool_calls=[{"id": "a", "type": "function",
+                                               "function": {"name": "get_weather", "arguments": '{"location":"X"}'}}])
+    ids = TPL.render_message(m)
+    assert TOK.special_id("<|python_tag|>") in ids
+    body = TOK.decode(ids[ids.index(TOK.special_id("<|python_tag|>")) + 1:])
+    calls = parse_tool_calls(body)
+    assert calls[0]["function"]["name"] == "get_weather"
+    assert json.loads(calls[0]["function"]["arguments"]) == {"location": "X"}
+    assert calls[0]["type"] == "function" and calls[0]["id"].startswith("call_") and calls[0]["index"] == 0
+    two = parse_tool_calls('{"name": "a", "parameters": {}}\n{"name": "b", "parameters": {"x": 1}}')
+    assert [c["function"]["name"] for c in two] == ["a", "b"] and two[1]["index"] == 1
+    assert parse_tool_calls("not a call") is None
+
+
+def test_mistral_template():
+    tok = get_tokenizer("mistral", 32000)
+    tpl = ChatTemplate(tok)
+    ids = tpl.render([Message(role="user", content="hi")], TOOLS)
+    assert ids[0] == 1 and tok.special_id("[INST]") in ids and tok.special_id("[AVAILABLE_TOOLS]") in ids
+    assert tok.decode(tok.encode("abc def")) == "abc def"
