@@ -33,6 +33,7 @@ def timeit(fn, iters=30, rounds=5):
 
 def main():
     Ms = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,16,32,64,128").split(",")]
+    libs_only = "--libs-only" in sys.argv  # TunableOp runs: plain F.linear only (strided bmm faults while tuning)
     dev = torch.device("cuda:0")
     have_custom = False
     try:
@@ -53,7 +54,7 @@ def main():
                 us = timeit(lambda i: F.linear(x, ws[i % nrot]))
                 row[f"{'hipblaslt' if lib == 'cublaslt' else 'rocblas'}_us"] = round(us, 1)
             torch.backends.cuda.preferred_blas_library("cublaslt")
-            for S in (2, 4, 8):
+            for S in (() if libs_only else (2, 4, 8)):
                 if K % S:
                     continue
                 xs = x.view(M, S, K // S).transpose(0, 1)
@@ -65,7 +66,7 @@ def main():
                 err = (f(0).float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
                 row[f"bmm_splitk{S}_us"] = round(timeit(f), 1)
                 row[f"bmm_splitk{S}_err"] = round(err, 4)
-            if have_custom and M <= 64:
+            if have_custom and M <= 64 and not libs_only:
                 ref = F.linear(x, w).float()
                 for U in (4, 8):
                     if not ops.skinny_supported(M, N, K, U):
