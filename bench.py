@@ -35,6 +35,7 @@ BASELINE_TOKS = 22300.0  # stub chunks/s, 64 threads, stream (r
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel size per replica (e.g. 8 for llama3-70b)")
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=60)
     ap.add_argument("--model", default="llama3-8b")
@@ -87,16 +88,27 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     from kafka_llm_service_amd.parallel import state as pstate
 
-    if world > 1:
-        pstate.init(tp=1)
+    dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
+    tp = args.tp
+    st = pstate.init(tp=tp, device=dev) if world > 1 else pstate.get()
+    from kafka_llm_service_amd.engine import tp_worker
     from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
     from kafka_llm_service_amd.engine.sequence import SamplingParams
 
-    dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
     cfg = EngineConfig(model=args.model, device=dev, seed=args.seed, max_num_seqs=max(256, 2 * args.threads),
                        max_num_batched_tokens=8192, use_cascade=not args.no_cascade, use_graphs=args.graphs,
-                       max_model_len=131072 if args.prefix_tokens > 6000 else 8192)
+                       max_model_len=131072 if args.prefix_tokens > 6000 else 8192, tp=tp, tp_rank=st.tp_rank)
     eng = LLMEngine(cfg)
+    leaders = None
+    if tp > 1:
+        import torch.distributed as dist
+
+        # TP followers mirror their leader's steps; the timing barriers run among the leaders only
+        leaders = dist.new_group(list(range(0, world, tp)), backend="gloo")
+        if not st.is_tp_leader:
+            tp_worker.follower_loop(eng)
+            return _report(args, world, rank, dev, eng, {"out_tokens": 0, "ttft": []}, 0.0, 0.0)
+        tp_worker.attach_leader(eng)
     V = eng.model_cfg.vocab_size
     rng = random.Random(args.seed * 7919 + rank)
     prefix = [rng.randrange(1000, min(V, 120000)) for _ in range(args.prefix_tokens)]
@@ -150,7 +162,7 @@ def main():
         run_step(False)
     if dev.startswith("cuda"):
         torch.cuda.synchronize()
-    pstate.barrier()
+    _barrier(leaders)
     t0 = time.perf_counter()
     window[0] = t0
     for _ in range(args.steps):
@@ -158,8 +170,21 @@ def main():
     if dev.startswith("cuda"):
         torch.cuda.synchronize()
     t1 = time.perf_counter()
-    pstate.barrier()
-    elapsed = t1 - t0
+    _barrier(leaders)
+    if tp > 1:
+        tp_worker.release_followers()
+    return _report(args, world, rank, dev, eng, timing, t1 - t0, setup_s)
+
+
+def _barrier(group) -> None:
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        dist.barrier(group=group)
+
+
+def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
+    from kafka_llm_service_amd.parallel import state as pstate
 
     local_stats = torch.tensor([timing["out_tokens"], elapsed], dtype=torch.float64)
     ttfts = sorted(timing["ttft"])
@@ -196,9 +221,9 @@ def main():
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": round(value / BASELINE_TOKS, 3), "dtype": "bf16",
         "data": "synthetic (random-init weights, random token ids)",
-        "config": {"model": args.model, "global_batch": args.threads * world, "seq_len": args.prefix_tokens
+        "config": {"model": args.model, "global_batch": args.threads * (world // args.tp), "seq_len": args.prefix_tokens
                    + args.history_turns * (args.user_tokens + args.reply_tokens) + args.user_tokens,
-                   "parallelism": f"dp{world}", "threads_per_gpu": args.threads,
+                   "parallelism": f"dp{world // args.tp}" + (f"-tp{args.tp}" if args.tp > 1 else ""), "threads_per_gpu": args.threads,
                    "shared_prefix_tokens": args.prefix_tokens, "history_turns": args.history_turns,
                    "max_out": [args.min_out, args.max_out], "temperature": args.temperature,
                    "cascade": not args.no_cascade, "graphs": args.graphs},

@@ -63,7 +63,7 @@ class InProcessClient:
 
 # ---------------------------------------------------------------------------------------------------------------
 def _worker_main(rank: int, cfg_dict: dict, conn) -> None:
-    """One DP replica: owns one GPU, steps its engine, exchanges small pickled messages over a pipe."""
+    """One DP replica (tp = 1): owns one GPU, steps its engine, exchanges small pickled messages over a pipe."""
     import torch
 
     from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
@@ -77,6 +77,11 @@ def _worker_main(rank: int, cfg_dict: dict, conn) -> None:
         conn.send(("fatal", repr(e)))
         return
     conn.send(("ready", {"device": str(eng.device), "kv_pages": eng.num_blocks}))
+    serve_pipe(eng, conn)
+
+
+def serve_pipe(eng, conn) -> None:
+    """Request loop of a replica (or TP-group leader): drain control messages, step while there is work."""
     while True:
         busy = eng.has_unfinished()
         while conn.poll(0 if busy else 0.05):
@@ -108,10 +113,15 @@ def _worker_main(rank: int, cfg_dict: dict, conn) -> None:
 
 
 class DPClient:
-    def __init__(self, engine_cfg, n_replicas: int, start_timeout: float = 900.0):
+    """``n_replicas`` independent engines; with ``tp > 1`` each replica is a TP group of ``tp`` processes
+    (``engine/tp_worker.py``) whose leader owns the request pipe."""
+
+    def __init__(self, engine_cfg, n_replicas: int, start_timeout: float = 900.0, tp: int = 1,
+                 base_port: int | None = None):
         ctx = mp.get_context("spawn")
         self.engine_cfg = engine_cfg
         self.n_replicas = n_replicas
+        self.tp = tp
         self.max_model_len = engine_cfg.max_model_len
         from kafka_llm_service_amd.models.config import get_config
 
@@ -119,25 +129,40 @@ class DPClient:
         cfg = asdict(engine_cfg)
         cfg["device"] = None
         self.conns, self.procs = [], []
+        self._followers: list = []
         self._send_locks = [threading.Lock() for _ in range(n_replicas)]
         self._streams: dict[str, tuple[asyncio.AbstractEventLoop, asyncio.Queue, int]] = {}
         self._lock = threading.Lock()
         self._loads = [0] * n_replicas
         self._health: list[dict] = [{} for _ in range(n_replicas)]
         self._ids = itertools.count()
+        follower_conns = []
+        if base_port is None:
+            base_port = _free_port_base(n_replicas)
         for r in range(n_replicas):
-            parent, child = ctx.Pipe()
-            p = ctx.Process(target=_worker_main, args=(r, cfg, child), daemon=True, name=f"kafka-replica{r}")
-            p.start()
-            self.conns.append(parent)
-            self.procs.append(p)
+            if tp == 1:
+                parent, child = ctx.Pipe()
+                p = ctx.Process(target=_worker_main, args=(r, cfg, child), daemon=True, name=f"kafka-replica{r}")
+                p.start()
+                self.conns.append(parent)
+                self.procs.append(p)
+                continue
+            from kafka_llm_service_amd.engine.tp_worker import tp_worker_main
+
+            for t in range(tp):
+                parent, child = ctx.Pipe()
+                p = ctx.Process(target=tp_worker_main, args=(r, t, tp, base_port + r, cfg, child), daemon=True,
+                                name=f"kafka-replica{r}-tp{t}")
+                p.start()
+                (self.conns if t == 0 else follower_conns).append(parent)
+                (self.procs if t == 0 else self._followers).append(p)
         deadline = time.monotonic() + start_timeout
-        for r, c in enumerate(self.conns):
+        for r, c in enumerate(self.conns + follower_conns):
             if not c.poll(max(1.0, deadline - time.monotonic())):
-                raise RuntimeError(f"replica {r} did not start")
+                raise RuntimeError(f"engine process {r} did not start")
             msg = c.recv()
             if msg[0] != "ready":
-                raise RuntimeError(f"replica {r} failed: {msg[1]}")
+                raise RuntimeError(f"engine process {r} failed: {msg[1]}")
         self._readers = [threading.Thread(target=self._reader, args=(r,), daemon=True) for r in range(n_replicas)]
         for t in self._readers:
             t.start()
@@ -239,10 +264,33 @@ class DPClient:
                 self._send(r, ("stop",))
             except (OSError, BrokenPipeError):
                 pass
-        for p in self.procs:
+        for p in self.procs + self._followers:
             p.join(timeout=30)
             if p.is_alive():
                 p.terminate()
+
+
+def _free_port_base(n: int) -> int:
+    """A base port with n free consecutive ports on 127.0.0.1 (one rendezvous per TP replica)."""
+    import socket
+
+    for _ in range(64):
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            base = sk.getsockname()[1]
+        if base + n >= 65535:
+            continue
+        ok = True
+        for i in range(1, n):
+            with socket.socket() as sk:
+                try:
+                    sk.bind(("127.0.0.1", base + i))
+                except OSError:
+                    ok = False
+                    break
+        if ok:
+            return base
+    raise RuntimeError("no free port range")
 
 
 def _put_all(items) -> None:
@@ -259,8 +307,4 @@ async def make_engine_client(server_cfg):
     n = max(1, server_cfg.dp)
     if n == 1 and server_cfg.tp == 1:
         return await asyncio.to_thread(InProcessClient, ecfg)
-    if server_cfg.tp > 1:
-        from kafka_llm_service_amd.engine.tp_worker import TPClient
-
-        return await asyncio.to_thread(TPClient, ecfg, server_cfg.tp, n)
-    return await asyncio.to_thread(DPClient, ecfg, n)
+    return await asyncio.to_thread(DPClient, ecfg, n, 900.0, max(1, server_cfg.tp))

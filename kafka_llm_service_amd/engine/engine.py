@@ -58,6 +58,19 @@ class EngineConfig:
         return torch.device("cpu")
 
 
+def _agree_min(n: int) -> int:
+    import torch.distributed as dist
+
+    from kafka_llm_service_amd.parallel import state as pstate
+
+    st = pstate.get()
+    if st.tp == 1 or not dist.is_initialized():
+        return n
+    t = torch.tensor([n], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=st.cpu_group)
+    return int(t.item())
+
+
 class LLMEngine:
     def __init__(self, cfg: EngineConfig, model_cfg: ModelConfig | None = None, model=None):
         self.cfg = cfg
@@ -81,6 +94,8 @@ class LLMEngine:
             nb = int(free * cfg.kv_fraction) // page_bytes
         else:
             nb = 4096
+        if cfg.tp > 1:
+            nb = _agree_min(nb)  # every rank of the TP group indexes the same page ids
         self.num_blocks = nb
         self.k_cache = torch.empty(L, nb, hkv, 16, D, dtype=torch.bfloat16, device=self.device)
         self.v_cache = torch.empty(L, nb, hkv, D, 16, dtype=torch.bfloat16, device=self.device)

@@ -10,6 +10,7 @@ batches run eagerly.
 from __future__ import annotations
 
 import math
+from dataclasses import dataclass
 
 import numpy as np
 import torch
@@ -22,6 +23,24 @@ from kafka_llm_service_amd.models.llama import StepInput, TransformerLM
 
 PAGE = 16
 MAX_ITEM_KEYS = 32000  # key range of one attention work item (page ids of an item are staged in 8 KB of LDS)
+
+
+@dataclass
+class HostStep:
+    """Host-side plan of one step: packed int64 (tokens | positions | slots | logit rows) and int32 (block tables |
+    causal limits | decode seq lens | cascade kv_start + prefix items | prefill items) buffers plus their layout."""
+    B: int = 0
+    T: int = 0
+    nbt: int = 1
+    n_rows: int = 0
+    splits: int = 1
+    prefix_splits: int = 0
+    n_prefix_items: int = 0
+    cascade_prefix: int = 0
+    n_items: int = 0
+    prefill_splits: int = 0
+    i64: np.ndarray | None = None
+    i32: np.ndarray | None = None
 
 
 def decode_splits(B: int, hkv: int, max_keys: int, target_wgs: int = 512, min_keys_per_split: int = 256) -> int:
@@ -54,9 +73,16 @@ class ModelRunner:
         self._bt = np.zeros((max_num_seqs * 2, max_blocks_per_seq), dtype=np.int32)
         self._pin = pin
         self.last_stats: dict = {}
+        self.broadcast = None  # set on a TP leader: callable(HostStep) (engine/tp_worker.py)
 
     # ------------------------------------------------------------------------------------------------------------
     def prepare(self, batch: ScheduledBatch) -> tuple[StepInput, list[Sequence]]:
+        host, sample_seqs = self.build_host(batch)
+        return self.to_device(host), sample_seqs
+
+    def build_host(self, batch: ScheduledBatch) -> tuple[HostStep, list[Sequence]]:
+        """All host-side work of a step: token/slot/page-table packing and attention work-item planning. The result
+        is a few numpy arrays + scalars — what a TP leader broadcasts to its followers (``engine/tp_worker.py``)."""
         dec = batch.decode
         B = len(dec)
         pre = batch.prefill
@@ -99,10 +125,8 @@ class ModelRunner:
         bt = self._bt[:nbt]
         self.kvm.fill_block_tables(seq_ids, bt)
         # ---- decode metadata (+ cascade over the shared prefix)
-        meta = AttnMeta(num_decode=B, num_tokens=T, scale=self.model.scale)
+        h = HostStep(B=B, T=T, nbt=nbt, n_rows=len(logit_rows))
         i32_parts = [bt.reshape(-1), q_limit]
-        seq_lens = kv_start = prefix_items = None
-        n_pref_splits = 0
         if B:
             seq_lens = np.fromiter((s.total_len for s in dec), dtype=np.int32, count=B)
             P = 0
@@ -112,7 +136,8 @@ class ModelRunner:
                 if P < self.cascade_min_prefix:
                     P = 0
             max_suffix = int(seq_lens.max()) - P
-            S = decode_splits(B, self.model.hkv, max_suffix)
+            h.splits = decode_splits(B, self.model.hkv, max_suffix)
+            i32_parts += [seq_lens]
             if P:
                 # key chunks sized so the prefix pass alone launches ~target_wgs workgroups
                 groups = math.ceil(B / self.tile)
@@ -123,16 +148,10 @@ class ModelRunner:
                 for g0 in range(0, B, self.tile):
                     for c in range(nc):
                         pit.append((g0, min(self.tile, B - g0), 0, c * chunk, min(P, (c + 1) * chunk), c, 0, 0))
-                prefix_items = np.asarray(pit, dtype=np.int32)
-                n_pref_splits = nc
-                kv_start = np.full(B, P, dtype=np.int32)
-            meta.num_splits = S
-            meta.num_prefix_splits = n_pref_splits
-            i32_parts += [seq_lens]
-            if kv_start is not None:
-                i32_parts += [kv_start, prefix_items.reshape(-1)]
-            meta.extra["cascade_prefix"] = P
-        p_splits = 0
+                h.prefix_splits = nc
+                h.n_prefix_items = len(pit)
+                i32_parts += [np.full(B, P, dtype=np.int32), np.asarray(pit, dtype=np.int32).reshape(-1)]
+            h.cascade_prefix = P
         if items:
             # few query tiles against a long key range (a new turn of a thread with a ~20k-token cached context):
             # split every tile's key range so the pass fills the GPU, merge the partials afterwards
@@ -145,45 +164,54 @@ class ModelRunner:
                     for c in range(math.ceil(hi / ck)):
                         split_items.append((q0, cnt, btr, c * ck, min(hi, (c + 1) * ck), c, 0, 0))
                 items = split_items
-                p_splits = math.ceil(max_kv / ck)
-            items_np = np.asarray(items, dtype=np.int32)
-            i32_parts.append(items_np.reshape(-1))
-        i64 = np.concatenate([tokens, positions, slots, np.asarray(logit_rows, dtype=np.int64)])
-        i32 = np.concatenate(i32_parts)
-        d64 = self._h2d(i64)
-        d32 = self._h2d(i32)
-        o = 0
+                h.prefill_splits = math.ceil(max_kv / ck)
+            h.n_items = len(items)
+            i32_parts.append(np.asarray(items, dtype=np.int32).reshape(-1))
+        h.i64 = np.concatenate([tokens, positions, slots, np.asarray(logit_rows, dtype=np.int64)])
+        h.i32 = np.concatenate(i32_parts)
+        self.last_stats = {"B": B, "T": T, "cascade_prefix": h.cascade_prefix, "splits": h.splits,
+                           "prefix_splits": h.prefix_splits, "prefill_splits": h.prefill_splits}
+        return h, sample_seqs
+
+    def to_device(self, h: HostStep) -> StepInput:
+        """One H2D copy per packed buffer, then views into it (identical on every TP rank)."""
+        B, T, nbt = h.B, h.T, h.nbt
+        d64 = self._h2d(h.i64)
+        d32 = self._h2d(h.i32)
         t_tokens, t_pos, t_slots = d64[0:T], d64[T:2 * T], d64[2 * T:3 * T]
-        t_rows = d64[3 * T:3 * T + len(logit_rows)]
+        t_rows = d64[3 * T:3 * T + h.n_rows]
+        meta = AttnMeta(num_decode=B, num_tokens=T, scale=self.model.scale)
         o = 0
-        meta.block_tables = d32[o:o + bt.size].view(nbt, self.max_blocks)
-        o += bt.size
+        n_bt = nbt * self.max_blocks
+        meta.block_tables = d32[o:o + n_bt].view(nbt, self.max_blocks)
+        o += n_bt
         meta.q_limit = d32[o:o + T]
         o += T
+        Hq, D = self.model.hq, self.model.D
         if B:
+            meta.num_splits = h.splits
+            meta.num_prefix_splits = h.prefix_splits
             meta.seq_lens = d32[o:o + B]
             o += B
-            if kv_start is not None:
+            if h.cascade_prefix:
                 meta.kv_start = d32[o:o + B]
                 o += B
-                meta.prefix_items = d32[o:o + prefix_items.size].view(-1, 8)
-                o += prefix_items.size
-            Hq, D = self.model.hq, self.model.D
+                meta.prefix_items = d32[o:o + h.n_prefix_items * 8].view(-1, 8)
+                o += h.n_prefix_items * 8
             meta.part = torch.empty(B, Hq, meta.s_total, D, dtype=torch.float32, device=self.device)
             meta.lse = torch.empty(B, Hq, meta.s_total, dtype=torch.float32, device=self.device)
-        if items:
-            meta.prefill_items = d32[o:o + len(items) * 8].view(-1, 8)
-            o += len(items) * 8
-            if p_splits:
-                Tp, Hq, D = T - B, self.model.hq, self.model.D
-                meta.prefill_splits = p_splits
-                meta.prefill_part = torch.empty(Tp, Hq, p_splits, D, dtype=torch.float32, device=self.device)
-                meta.prefill_lse = torch.full((Tp, Hq, p_splits), float("-inf"), dtype=torch.float32,
+            meta.extra["cascade_prefix"] = h.cascade_prefix
+        if h.n_items:
+            meta.prefill_items = d32[o:o + h.n_items * 8].view(-1, 8)
+            o += h.n_items * 8
+            if h.prefill_splits:
+                Tp = T - B
+                meta.prefill_splits = h.prefill_splits
+                meta.prefill_part = torch.empty(Tp, Hq, h.prefill_splits, D, dtype=torch.float32,
+                                                device=self.device)
+                meta.prefill_lse = torch.full((Tp, Hq, h.prefill_splits), float("-inf"), dtype=torch.float32,
                                               device=self.device)
-        self.last_stats = {"B": B, "T": T, "cascade_prefix": meta.extra.get("cascade_prefix", 0),
-                           "splits": meta.num_splits, "prefix_splits": meta.num_prefix_splits,
-                           "prefill_splits": p_splits}
-        return StepInput(t_tokens, t_pos, t_slots, meta, t_rows), sample_seqs
+        return StepInput(t_tokens, t_pos, t_slots, meta, t_rows)
 
     def _h2d(self, a: np.ndarray) -> torch.Tensor:
         t = torch.from_numpy(a)
@@ -238,7 +266,10 @@ class ModelRunner:
     # ------------------------------------------------------------------------------------------------------------
     @torch.inference_mode()
     def execute(self, batch: ScheduledBatch) -> tuple[list[Sequence], list[int]]:
-        inp, sample_seqs = self.prepare(batch)
+        host, sample_seqs = self.build_host(batch)
+        if self.broadcast is not None:  # TP leader: followers run the same step on their shards
+            self.broadcast(host)
+        inp = self.to_device(host)
         logits = self.model.forward(inp, self.k_caches, self.v_caches)
         toks = self.sample(logits, sample_seqs)
         return sample_seqs, toks.tolist()
