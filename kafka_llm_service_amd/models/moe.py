@@ -6,9 +6,10 @@ its own experts over the tokens routed to them and the per-rank partial outputs 
 that a dense row-parallel MLP would use (one collective per layer, [T, d] bf16). With ep = 1 the whole block is
 local (Mixtral 8x7B bf16 = 93 GB fits one 288 GB MI355X).
 
-GPU path: ``ops.moe_route`` (HIP: softmax + top-k + renormalise + expert histogram + permutation, one kernel) and
-``ops.grouped_gemm`` (HIP MFMA grouped GEMM over the expert-sorted rows) when the extension provides them; the CPU
-path is the plain PyTorch reference of the same math.
+Per layer: router GEMM (hipBLASLt) -> ``ops.moe_route`` (HIP, one workgroup: softmax + top-k + renormalise + stable
+expert sort, no host sync) -> ``ops.grouped_gemm`` gate_up (HIP MFMA, A rows gathered through the permutation) ->
+``ops.silu_mul`` -> ``ops.grouped_gemm`` down with the routing-weighted scatter-combine fused into its epilogue
+(fp32 atomics onto a zeroed [T, d] buffer). On CPU the same calls run the fp32 references of ``ops/reference.py``.
 """
 from __future__ import annotations
 
@@ -41,37 +42,14 @@ class MoEBlock:
     def __call__(self, x: torch.Tensor, lw) -> torch.Tensor:
         T, d = x.shape
         logits = F.linear(x, lw.router)
-        w, e = route(logits, self.k)
-        out = self._experts(x, w, e, lw)
+        r = ops.moe_route(logits, self.k)
+        # gate_up for every (token, expert) entry routed to a local expert, rows gathered from x by the kernel
+        h = ops.grouped_gemm(x, lw.w13, r, gather=True, e_lo=self.e0)
+        a = ops.silu_mul(h)
+        # down projection with the routing-weighted scatter-combine fused into the epilogue
+        out = torch.zeros(T, d, dtype=torch.float32, device=x.device)
+        ops.grouped_gemm(a, lw.w2, r, gather=False, e_lo=self.e0, combine_out=out)
+        out = out.to(x.dtype)
         if self.ep > 1:
             out = pstate.tp_all_reduce(out)
         return out
-
-    def _experts(self, x, w, e, lw) -> torch.Tensor:
-        T, d = x.shape
-        flat_e = e.reshape(-1)
-        flat_w = w.reshape(-1)
-        tok = torch.arange(T, device=x.device).repeat_interleave(self.k)
-        local = (flat_e >= self.e0) & (flat_e < self.e0 + self.e_local)
-        le = flat_e[local] - self.e0
-        order = torch.argsort(le, stable=True)
-        le, ltok, lw_ = le[order], tok[local][order], flat_w[local][order]
-        counts = torch.bincount(le, minlength=self.e_local)
-        xs = x.index_select(0, ltok)
-        if x.is_cuda and hasattr(ops, "grouped_gemm") and ops.has_grouped_gemm():
-            offs = torch.zeros(self.e_local + 1, dtype=torch.int32, device=x.device)
-            offs[1:] = torch.cumsum(counts, 0)
-            h = ops.grouped_gemm(xs, lw.w13, offs)
-            a = ops.silu_mul(h)
-            y = ops.grouped_gemm(a, lw.w2, offs)
-        else:
-            y = torch.empty(xs.shape[0], d, dtype=x.dtype, device=x.device)
-            start = 0
-            for j, c in enumerate(counts.tolist()):
-                if c:
-                    h = F.linear(xs[start:start + c], lw.w13[j])
-                    y[start:start + c] = F.linear(ops.silu_mul(h), lw.w2[j])
-                start += c
-        out = torch.zeros(T, d, dtype=torch.float32, device=x.device)
-        out.index_add_(0, ltok, y.float() * lw_[:, None])
-        return out.to(x.dtype)

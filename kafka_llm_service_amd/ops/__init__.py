@@ -134,3 +134,54 @@ def skinny_gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = Non
 
 
 rope_cos_sin = ref.rope_cos_sin
+
+
+class MoERouting:
+    """Device-side routing of one MoE layer (csrc/moe.hip ``moe_route``): everything the grouped GEMMs need."""
+    __slots__ = ("topk_w", "topk_e", "perm_tok", "perm_w", "expert_off", "tile_off", "num_experts", "max_tiles")
+
+    def __init__(self, topk_w, topk_e, perm_tok, perm_w, expert_off, tile_off, num_experts):
+        self.topk_w, self.topk_e = topk_w, topk_e
+        self.perm_tok, self.perm_w = perm_tok, perm_w
+        self.expert_off, self.tile_off = expert_off, tile_off
+        self.num_experts = num_experts
+        self.max_tiles = (perm_tok.numel() + GG_BM - 1) // GG_BM + num_experts
+
+
+GG_BM = 64  # row tile of the grouped GEMM (a routing bound the kernel and the host agree on)
+
+
+def moe_route(logits: torch.Tensor, k: int) -> MoERouting:
+    """softmax -> top-k -> renormalise, then a stable sort of the T*k entries by expert (token order inside)."""
+    T, E = logits.shape
+    dev = logits.device
+    if _gpu(logits):
+        tw = torch.empty(T, k, dtype=torch.float32, device=dev)
+        te = torch.empty(T, k, dtype=torch.int32, device=dev)
+        pt = torch.empty(T * k, dtype=torch.int32, device=dev)
+        pw = torch.empty(T * k, dtype=torch.float32, device=dev)
+        eo = torch.empty(E + 1, dtype=torch.int32, device=dev)
+        to = torch.empty(E + 1, dtype=torch.int32, device=dev)
+        ext().moe_route(logits, int(k), GG_BM, tw, te, pt, pw, eo, to)
+        return MoERouting(tw, te, pt, pw, eo, to, E)
+    tw, te, pt, pw, eo, to = ref.moe_route(logits, k, GG_BM)
+    return MoERouting(tw, te, pt, pw, eo, to, E)
+
+
+def grouped_gemm(x: torch.Tensor, w: torch.Tensor, r: MoERouting, gather: bool, e_lo: int = 0,
+                 y: torch.Tensor | None = None, combine_out: torch.Tensor | None = None) -> torch.Tensor:
+    """Per expert segment of the routed entries: Y = X_e . W_e^T (W = [E_local, N, K], experts [e_lo, e_lo+E_local)).
+
+    gather=True reads A rows as x[perm_tok[r]] (token activations), else x[r] (expert-sorted rows).
+    combine_out (f32 [T, N], zeroed by the caller) receives out[perm_tok[r]] += perm_w[r] * Y[r] instead of Y."""
+    n_ent = r.perm_tok.numel()
+    if combine_out is not None and combine_out.shape[0] != r.topk_w.shape[0]:
+        raise ValueError("combine_out must have one row per routed token")
+    if combine_out is None and y is None:
+        y = torch.empty(n_ent, w.shape[1], dtype=x.dtype, device=x.device)
+    if _gpu(x):
+        ext().grouped_gemm(x, w, r.perm_tok, r.perm_w, r.expert_off, r.tile_off, int(e_lo), int(r.max_tiles),
+                           bool(gather), y, combine_out)
+    else:
+        ref.grouped_gemm(x, w, r.perm_tok, r.perm_w, r.expert_off, e_lo, gather, y, combine_out)
+    return combine_out if combine_out is not None else y

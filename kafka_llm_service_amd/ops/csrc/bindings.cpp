@@ -32,6 +32,13 @@ int kafka_skinny_gemm_plan(int M, int N, int K, int U, int* splitk, int* k_per_w
 hipError_t kafka_launch_skinny_gemm(const bf16* X, int64_t ldx, const bf16* W, int64_t ldw, bf16* Y, int64_t ldy,
                                     float* slab, int M, int N, int K, int U, int splitk, int k_per_wave,
                                     hipStream_t st);
+hipError_t kafka_launch_moe_route(const bf16* logits, int64_t ld, int T, int E, int K, int BM, float* topk_w,
+                                  int* topk_e, int* perm_tok, float* perm_w, int* expert_off, int* tile_off,
+                                  hipStream_t st);
+hipError_t kafka_launch_grouped_gemm(const bf16* X, int64_t ldx, const bf16* W, int N, int Kd, const int* perm_tok,
+                                     const float* perm_w, const int* expert_off, const int* tile_off, int e_lo,
+                                     int e_n, int max_tiles, int gather, bf16* Y, int64_t ldy, float* out,
+                                     int64_t ldo, hipStream_t st);
 }  // extern "C"
 
 #define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
@@ -257,6 +264,62 @@ static void skinny_gemm(at::Tensor x, at::Tensor w, at::Tensor out, int64_t U) {
                                      K, (int)U, splitk, kpw, cur_stream()));
 }
 
+// softmax -> top-k -> renormalise + stable expert sort (one kernel, no host sync)
+static void moe_route(at::Tensor logits, int64_t k, int64_t bm, at::Tensor topk_w, at::Tensor topk_e,
+                      at::Tensor perm_tok, at::Tensor perm_w, at::Tensor expert_off, at::Tensor tile_off) {
+  CHECK_CUDA(logits); CHECK_DT(logits, at::kBFloat16); CHECK_LASTDIM(logits);
+  CHECK_DT(topk_w, at::kFloat); CHECK_DT(perm_w, at::kFloat);
+  CHECK_DT(topk_e, at::kInt); CHECK_DT(perm_tok, at::kInt); CHECK_DT(expert_off, at::kInt); CHECK_DT(tile_off, at::kInt);
+  const int T = logits.size(0), E = logits.size(1);
+  TORCH_CHECK(T >= 1 && E <= 16 && k >= 1 && k <= 4 && k <= E, "moe_route: unsupported T/E/k");
+  TORCH_CHECK(topk_w.numel() == (int64_t)T * k && topk_e.numel() == (int64_t)T * k &&
+                  perm_tok.numel() == (int64_t)T * k && perm_w.numel() == (int64_t)T * k &&
+                  expert_off.numel() == E + 1 && tile_off.numel() == E + 1,
+              "moe_route: output sizes");
+  TORCH_CHECK(topk_w.is_contiguous() && topk_e.is_contiguous() && perm_tok.is_contiguous() && perm_w.is_contiguous(),
+              "moe_route: contiguous outputs");
+  CHECK_HIP(kafka_launch_moe_route(bptr(logits), logits.stride(0), T, E, (int)k, (int)bm, topk_w.data_ptr<float>(),
+                                   topk_e.data_ptr<int>(), perm_tok.data_ptr<int>(), perm_w.data_ptr<float>(),
+                                   expert_off.data_ptr<int>(), tile_off.data_ptr<int>(), cur_stream()));
+}
+
+// Y (or out += w * Y) = X_e . W_e^T per expert segment of the routed entries; W = [e_n, N, K] local experts
+static void grouped_gemm(at::Tensor x, at::Tensor w, at::Tensor perm_tok, at::Tensor perm_w, at::Tensor expert_off,
+                         at::Tensor tile_off, int64_t e_lo, int64_t max_tiles, bool gather,
+                         c10::optional<at::Tensor> y, c10::optional<at::Tensor> out) {
+  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(w, at::kBFloat16); CHECK_LASTDIM(x);
+  TORCH_CHECK(w.dim() == 3 && w.is_contiguous(), "grouped_gemm: w must be contiguous [E_local, N, K]");
+  const int e_n = w.size(0), N = w.size(1), Kd = w.size(2);
+  const int E = expert_off.numel() - 1;
+  TORCH_CHECK(x.size(1) == Kd && N % 128 == 0 && Kd % 64 == 0 && x.stride(0) % 8 == 0,
+              "grouped_gemm: need N % 128 == 0, K % 64 == 0, 16-B rows");
+  TORCH_CHECK(e_lo >= 0 && e_lo + e_n <= E, "grouped_gemm: expert range");
+  const int64_t entries = perm_tok.numel();
+  TORCH_CHECK(max_tiles >= (entries + 63) / 64 + E, "grouped_gemm: max_tiles below the routing bound");
+  TORCH_CHECK(gather || x.size(0) >= entries, "grouped_gemm: direct mode needs one x row per routed entry");
+  bf16* yp = nullptr;
+  int64_t ldy = 0;
+  float* op = nullptr;
+  int64_t ldo = 0;
+  if (out.has_value()) {
+    CHECK_DT(out.value(), at::kFloat); CHECK_LASTDIM(out.value());
+    TORCH_CHECK(out.value().size(1) == N, "grouped_gemm: out width");
+    op = out.value().data_ptr<float>();
+    ldo = out.value().stride(0);
+  } else {
+    TORCH_CHECK(y.has_value(), "grouped_gemm: y or out required");
+    CHECK_DT(y.value(), at::kBFloat16); CHECK_LASTDIM(y.value());
+    TORCH_CHECK(y.value().size(0) >= entries && y.value().size(1) == N && y.value().stride(0) % 8 == 0,
+                "grouped_gemm: y shape");
+    yp = bptr(y.value());
+    ldy = y.value().stride(0);
+  }
+  CHECK_HIP(kafka_launch_grouped_gemm(bptr(x), x.stride(0), bptr(w), N, Kd, perm_tok.data_ptr<int>(),
+                                      perm_w.data_ptr<float>(), expert_off.data_ptr<int>(), tile_off.data_ptr<int>(),
+                                      (int)e_lo, e_n, (int)max_tiles, gather ? 1 : 0, yp, ldy, op, ldo,
+                                      cur_stream()));
+}
+
 PYBIND11_MODULE(_kafka_ops, m) {
   m.doc() = "kafka_llm_service_amd CDNA4 (gfx950) HIP kernels";
   m.def("rmsnorm", &rmsnorm);
@@ -271,4 +334,6 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("sample", &sample);
   m.def("skinny_supported", &skinny_supported);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("moe_route", &moe_route);
+  m.def("grouped_gemm", &grouped_gemm);
 }

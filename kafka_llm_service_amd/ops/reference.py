@@ -222,3 +222,37 @@ def rope_cos_sin(max_pos: int, head_dim: int, theta: float, scaling: dict | None
     t = torch.arange(max_pos, dtype=torch.float64)
     f = torch.outer(t, inv)
     return torch.cat([f.cos(), f.sin()], dim=-1).float().to(device)
+
+
+def moe_route(logits: torch.Tensor, k: int, bm: int = 64):
+    """fp32 reference of csrc/moe.hip moe_route: (topk_w, topk_e, perm_tok, perm_w, expert_off, tile_off)."""
+    T, E = logits.shape
+    p = torch.softmax(logits.float(), dim=-1)
+    # descending by probability, lowest expert index first on ties (the kernel's order)
+    order = torch.argsort(-p + torch.arange(E, device=p.device) * 1e-12, dim=-1, stable=True)[:, :k]
+    w = torch.gather(p, 1, order)
+    w = w / w.sum(-1, keepdim=True)
+    te = order.to(torch.int32)
+    flat = te.reshape(-1).long()
+    perm = torch.argsort(flat, stable=True)
+    counts = torch.bincount(flat, minlength=E)
+    eo = torch.zeros(E + 1, dtype=torch.int32, device=p.device)
+    eo[1:] = torch.cumsum(counts, 0)
+    to = torch.zeros(E + 1, dtype=torch.int32, device=p.device)
+    to[1:] = torch.cumsum((counts + bm - 1) // bm, 0)
+    return w.float(), te, (perm // k).to(torch.int32), w.reshape(-1)[perm].float(), eo, to
+
+
+def grouped_gemm(x, w, perm_tok, perm_w, expert_off, e_lo, gather, y, out):
+    e_n = w.shape[0]
+    eo = expert_off.tolist()
+    for j in range(e_n):
+        a, b = eo[e_lo + j], eo[e_lo + j + 1]
+        if a == b:
+            continue
+        rows = x[perm_tok[a:b].long()] if gather else x[a:b]
+        yy = rows.float() @ w[j].float().t()
+        if out is not None:
+            out.index_add_(0, perm_tok[a:b].long(), yy * perm_w[a:b, None])
+        else:
+            y[a:b] = yy.to(y.dtype)

@@ -134,3 +134,11 @@ def test_split_kv_prefill_equals_plain(base_engine):
     while not s.finished:
         e.step()
     assert s.output_ids == ref[0]
+
+
+def test_mixtral_greedy_matches_oracle():
+    """MoE engine path (router -> grouped GEMMs -> weighted combine, ops references on CPU) vs the dense oracle."""
+    eng = LLMEngine(EngineConfig(model="tiny-mixtral", device="cpu", num_kv_blocks=256, max_model_len=2048))
+    prompts = _prompts(seed=5, shared=40, tails=(4, 19))
+    outs = eng.generate(prompts, GREEDY)
+    _check_against_oracle(eng.model, prompts, outs)

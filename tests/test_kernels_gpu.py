@@ -218,3 +218,41 @@ def test_sample_distribution(cuda):
     keep = (torch.cumsum(ps, 0) - ps) < 0.5
     allowed = set(order[keep].tolist())
     assert set(tok.tolist()) <= allowed
+
+
+@pytest.mark.parametrize("T,E,k", [(1, 8, 2), (128, 8, 2), (3000, 8, 2), (77, 16, 4)])
+def test_moe_route(cuda, T, E, k):
+    torch.manual_seed(7)
+    logits = torch.randn(T, E, device=cuda).to(torch.bfloat16)
+    r = ops.moe_route(logits, k)
+    tw, te, pt, pw, eo, to = ref.moe_route(logits.cpu(), k, ops.GG_BM)
+    assert torch.equal(r.topk_e.cpu(), te) and torch.equal(r.expert_off.cpu(), eo)
+    assert torch.equal(r.tile_off.cpu(), to) and torch.equal(r.perm_tok.cpu(), pt)
+    _close(r.topk_w, tw, atol=1e-5, msg="topk_w")
+    _close(r.perm_w, pw, atol=1e-5, msg="perm_w")
+
+
+@pytest.mark.parametrize("T,d,N,E,e_lo,e_n", [(128, 512, 1024, 8, 0, 8), (300, 1024, 512, 8, 2, 4),
+                                              (1, 256, 384, 8, 0, 8), (64, 4096, 2048, 8, 0, 8)])
+def test_grouped_gemm(cuda, T, d, N, E, e_lo, e_n):
+    torch.manual_seed(8)
+    x = torch.randn(T, d, device=cuda, dtype=torch.bfloat16)
+    w = (torch.randn(e_n, N, d, device=cuda) * d ** -0.5).to(torch.bfloat16)
+    w2 = (torch.randn(e_n, d, N, device=cuda) * N ** -0.5).to(torch.bfloat16)
+    r = ops.moe_route(torch.randn(T, E, device=cuda).to(torch.bfloat16), 2)
+    rc = ops.MoERouting(*(t.cpu() for t in (r.topk_w, r.topk_e, r.perm_tok, r.perm_w, r.expert_off, r.tile_off)),
+                        E)
+    # gather mode -> bf16 rows (only the local experts' segments are defined)
+    y = ops.grouped_gemm(x, w, r, gather=True, e_lo=e_lo)
+    y_ref = torch.zeros(T * 2, N)
+    ref.grouped_gemm(x.cpu(), w.cpu(), rc.perm_tok, rc.perm_w, rc.expert_off, e_lo, True, y_ref, None)
+    eo = rc.expert_off.tolist()
+    a, b = eo[e_lo], eo[e_lo + e_n]
+    _close(y[a:b], y_ref[a:b], atol=0.03, rtol=0.01, msg="gather")
+    # direct mode with the fused weighted scatter-combine
+    h = torch.randn(T * 2, N, device=cuda, dtype=torch.bfloat16)
+    out = torch.zeros(T, d, device=cuda)
+    ops.grouped_gemm(h, w2, r, gather=False, e_lo=e_lo, combine_out=out)
+    out_ref = torch.zeros(T, d)
+    ref.grouped_gemm(h.cpu(), w2.cpu(), rc.perm_tok, rc.perm_w, rc.expert_off, e_lo, False, None, out_ref)
+    _close(out, out_ref, atol=0.02, rtol=0.01, msg="combine")
