@@ -1,0 +1,231 @@
+"""Schema-constrained tool-call decoding (random-init models never emit a valid tool call, so the
+agent / tool-calling configurations force well-formed calls with logit masks in the sampler).
+
+A ``ToolCallConstraint`` is a per-request ``SamplingParams.allowed_tokens_fn``: before every sampled token the model
+runner asks it for the allowed set (``None`` = unconstrained, a list of ids, or a cached boolean vocab mask) and masks
+the other logits to -inf. The constraint is a small program (a Python generator) that walks the chat template's tool
+call grammar token by token:
+
+    llama3:  <|python_tag|> {"name":"<tool>","parameters":<object per the tool's JSON schema>} <|eom_id|>
+    mistral: [TOOL_CALLS] [{"name":"<tool>","arguments":<object>}] </s>
+
+* fixed JSON punctuation / keys are FORCED (one allowed id), tokenized segment by segment — byte-level BPE decodes a
+  concatenation of separately encoded segments to the concatenated text, so the result is exactly
+  ``json.dumps(..., separators=(",", ":"))`` shaped;
+* the tool name and ``enum`` values are CHOICES over the tokenizations of the alternatives (a trie walk);
+* free values are bounded: strings take "string-safe" tokens (no ``"``, ``\\`` or control bytes, checked on the token's
+  bytes) and may close after >= 1 token, integers / numbers are one digit-only token (no leading zero), booleans are
+  a choice, arrays hold one item, nested objects emit their required properties.
+The model's own probabilities still pick among the allowed tokens (temperature / top-p apply), so with real weights
+the constraint only removes malformed continuations. ``tool_choice``: ``"auto"`` lets the first token decide (the
+constraint engages only once the model opens a tool call), ``"required"`` forces a call to any tool, a named function
+forces that tool, ``"none"`` forbids the tool-call token.
+"""
+from __future__ import annotations
+
+import json
+from functools import lru_cache
+from typing import Any, Iterator
+
+import numpy as np
+
+from kafka_llm_service_amd.engine.tokenizer import KafkaTokenizer
+
+MAX_STR_TOKENS = 12
+
+
+@lru_cache(maxsize=1)
+def _byte_decoder() -> dict[str, int]:
+    """Inverse of the GPT-2 byte-level alphabet used by the byte-level BPE (unicode char -> byte)."""
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) + \
+        list(range(ord("®"), ord("ÿ") + 1))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return {chr(c): b for b, c in zip(bs, cs)}
+
+
+class VocabClasses:
+    """Boolean masks over the vocabulary, computed once per tokenizer."""
+
+    def __init__(self, tok: KafkaTokenizer):
+        V = tok.vocab_size
+        dec = _byte_decoder()
+        self.str_safe = np.zeros(V, dtype=bool)
+        self.digits = np.zeros(V, dtype=bool)
+        self.digits_nz = np.zeros(V, dtype=bool)  # digit-only tokens not starting with '0'
+        for j in range(tok.n_base):
+            piece = tok.base.id_to_token(j)
+            if piece is None:
+                continue
+            try:
+                bs = bytes(dec[c] for c in piece)
+            except KeyError:
+                continue
+            i = j + tok.offset
+            if i >= V or tok.is_special(i):
+                continue
+            if bs and all(b >= 0x20 and b not in (0x22, 0x5C, 0x7F) for b in bs):
+                self.str_safe[i] = True
+            if bs and all(0x30 <= b <= 0x39 for b in bs):
+                self.digits[i] = True
+                self.digits_nz[i] = bs[0] != 0x30
+        # unused ids above the trained vocabulary decode to pseudo words (letters + a space): string-safe
+        for i in range(tok.n_base + tok.offset, V):
+            if not tok.is_special(i):
+                self.str_safe[i] = True
+
+
+_CLASSES: dict[int, VocabClasses] = {}
+
+
+def vocab_classes(tok: KafkaTokenizer) -> VocabClasses:
+    c = _CLASSES.get(id(tok))
+    if c is None:
+        c = _CLASSES[id(tok)] = VocabClasses(tok)
+    return c
+
+
+class Mask:
+    """An allowed set given as a cached vocab mask plus a few extra ids (cache key lets the runner reuse the device
+    copy of the base mask)."""
+    __slots__ = ("key", "base", "extra")
+
+    def __init__(self, key: str, base: np.ndarray, extra: list[int]):
+        self.key, self.base, self.extra = key, base, extra
+
+
+class ToolCallConstraint:
+    def __init__(self, tok: KafkaTokenizer, tools: list[dict], tool_choice: Any = "auto"):
+        self.tok = tok
+        self.cls = vocab_classes(tok)
+        self.llama = tok.family == "llama3"
+        self.start = tok.special_id("<|python_tag|>") if self.llama else tok.special_id("[TOOL_CALLS]")
+        self.end = tok.special_id("<|eom_id|>") if self.llama else tok.eos_ids[0]
+        self.tools = {t["function"]["name"]: t["function"].get("parameters") or {} for t in tools
+                      if t.get("type", "function") == "function" and "function" in t}
+        self.mode, names = self._mode(tool_choice)
+        self.names = names
+        self._gen: Iterator | None = None
+        self._spec: Any = None
+        self._n = 0
+        self.done = False
+
+    def _mode(self, tc):
+        if isinstance(tc, dict):
+            name = (tc.get("function") or {}).get("name")
+            if name not in self.tools:
+                raise ValueError(f"tool_choice names an unknown tool: {name}")
+            return "forced", [name]
+        if tc in (None, "auto"):
+            return "auto", list(self.tools)
+        if tc == "required":
+            return "forced", list(self.tools)
+        if tc == "none":
+            return "none", []
+        raise ValueError(f"unsupported tool_choice: {tc!r}")
+
+    # ---- runner protocol ----------------------------------------------------------------------------------------
+    def __call__(self, output_ids: list[int]):
+        if self._gen is None:
+            self._gen = self._program()
+            self._spec = next(self._gen)
+        while self._n < len(output_ids):
+            t = output_ids[self._n]
+            self._n += 1
+            if self._spec is _FREE_FOREVER:
+                return None
+            try:
+                self._spec = self._gen.send(t)
+            except StopIteration:
+                self._spec = _FREE_FOREVER
+                self.done = True
+        return None if self._spec is _FREE_FOREVER else self._spec
+
+    # ---- grammar -------------------------------------------------------------------------------------------------
+    def _program(self):
+        if self.mode == "none":
+            m = np.ones(self.tok.vocab_size, dtype=bool)
+            m[self.start] = False
+            yield Mask("no_tool_start", m, [])
+            return
+        if self.mode == "auto":
+            first = yield None
+            if first != self.start:
+                return
+        else:
+            yield [self.start]
+        yield from self._forced('[{"name":"' if not self.llama else '{"name":"')
+        name = yield from self._choice([n + '"' for n in self.names])
+        name = name[:-1]
+        yield from self._forced(',"parameters":' if self.llama else ',"arguments":')
+        yield from self._value(self.tools.get(name) or {"type": "object"})
+        yield from self._forced("}" if self.llama else "}]")
+        yield [self.end]
+        self.done = True
+
+    def _forced(self, text: str):
+        for i in self.tok.encode(text):
+            yield [i]
+
+    def _choice(self, alts: list[str]):
+        """Trie walk over the tokenizations of ``alts``; returns the chosen alternative."""
+        seqs = [(a, self.tok.encode(a)) for a in alts]
+        pos = 0
+        while True:
+            live = [(a, s) for a, s in seqs if len(s) > pos]
+            t = yield sorted({s[pos] for _, s in live})
+            seqs = [(a, s) for a, s in live if s[pos] == t]
+            pos += 1
+            done = [a for a, s in seqs if len(s) == pos]
+            if done:
+                return done[0]
+
+    def _value(self, schema: dict):
+        """Emit one JSON value for ``schema`` (every value is self-delimiting, so no look-ahead is needed)."""
+        if "enum" in schema and schema["enum"]:
+            yield from self._choice([json.dumps(v, separators=(",", ":")) for v in schema["enum"]])
+            return
+        typ = schema.get("type", "string")
+        if isinstance(typ, list):
+            typ = next((t for t in typ if t != "null"), "string")
+        if typ == "object":
+            props = schema.get("properties") or {}
+            req = [k for k in (schema.get("required") or []) if k in props]
+            yield from self._forced("{")
+            for j, k in enumerate(req):
+                if j:
+                    yield from self._forced(",")
+                yield from self._forced(json.dumps(k) + ":")
+                yield from self._value(props[k])
+            yield from self._forced("}")
+        elif typ == "array":
+            # one item (the minimal non-empty array; enough for a well-formed call)
+            yield from self._forced("[")
+            yield from self._value(schema.get("items") or {"type": "string"})
+            yield from self._forced("]")
+        elif typ in ("integer", "number"):
+            # one digit-only token without a leading zero (BPE digit runs cover 1..3 digits), or a lone "0"
+            yield Mask("digits_nz", self.cls.digits_nz, self.tok.encode("0")[:1])
+        elif typ == "boolean":
+            yield from self._choice(["true", "false"])
+        elif typ == "null":
+            yield from self._forced("null")
+        else:  # string (and anything unrecognised): 1..MAX_STR_TOKENS string-safe tokens, then the closing quote
+            q = self.tok.encode('"')
+            yield from self._forced('"')
+            yield Mask("str", self.cls.str_safe, [])
+            for _ in range(MAX_STR_TOKENS - 1):
+                t = yield Mask("str", self.cls.str_safe, q[:1])
+                if t == q[0]:
+                    for i in q[1:]:
+                        yield [i]
+                    return
+            yield from self._forced('"')
+
+
+_FREE_FOREVER = object()

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import logging
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 
 import torch
 
@@ -126,6 +126,13 @@ class LLMEngine:
         if len(prompt_ids) + 1 > self.cfg.max_model_len:
             raise ValueError(f"This model's maximum context length is {self.cfg.max_model_len} tokens. However, "
                              f"your messages resulted in {len(prompt_ids)} tokens.")
+        if params.tool_grammar is not None and params.allowed_tokens_fn is None:
+            from kafka_llm_service_amd.engine.constrained import ToolCallConstraint
+            from kafka_llm_service_amd.engine.tokenizer import tokenizer_for_model
+
+            g = params.tool_grammar
+            c = ToolCallConstraint(tokenizer_for_model(self.model_cfg), g.get("tools") or [], g.get("tool_choice"))
+            params = replace(params, allowed_tokens_fn=c, stop_token_ids=list(params.stop_token_ids) + [c.end])
         seq = Sequence(request_id, prompt_ids, params, meta)
         if self.stop_checker_factory is not None and params.stop:
             seq.stop_checker = self.stop_checker_factory(params)

@@ -226,7 +226,7 @@ class ModelRunner:
         topp = np.empty(n, dtype=np.float32)
         topk = np.empty(n, dtype=np.int32)
         seeds = np.empty(n, dtype=np.int64)
-        need_proc = False
+        procs = []  # (row, seq, allowed) for rows that need penalties or a token constraint
         for i, s in enumerate(seqs):
             p = s.params
             temp[i] = p.temperature
@@ -234,10 +234,11 @@ class ModelRunner:
             topk[i] = p.top_k
             base = p.seed if p.seed is not None else (s.seq_id * 7919)
             seeds[i] = (base * 1000003 + len(s.output_ids)) & 0x7FFFFFFFFFFFFFFF
-            if p.presence_penalty or p.frequency_penalty or p.allowed_tokens_fn is not None:
-                need_proc = True
-        if need_proc:
-            logits = self._process_logits(logits, seqs)
+            allowed = p.allowed_tokens_fn(s.output_ids) if p.allowed_tokens_fn is not None else None
+            if allowed is not None or p.presence_penalty or p.frequency_penalty:
+                procs.append((i, s, allowed))
+        if procs:
+            logits = self._process_logits(logits, procs)
         all_greedy = not temp.any()
         dev = logits.device
         if all_greedy:
@@ -246,21 +247,37 @@ class ModelRunner:
         return ops.sample(logits, f32[:n], f32[n:], torch.from_numpy(topk).to(dev, non_blocking=True),
                           torch.from_numpy(seeds).to(dev, non_blocking=True))
 
-    def _process_logits(self, logits: torch.Tensor, seqs: list[Sequence]) -> torch.Tensor:
+    def _mask_tensor(self, m) -> torch.Tensor:
+        """Device copy of a constrained.Mask's base vocab mask (cached by key) with its extra ids allowed."""
+        cache = self.__dict__.setdefault("_masks", {})
+        base = cache.get(m.key)
+        if base is None or base.numel() != m.base.shape[0]:
+            base = cache[m.key] = torch.from_numpy(m.base).to(self.device)
+        if not m.extra:
+            return base
+        t = base.clone()
+        t[torch.as_tensor(m.extra, device=self.device, dtype=torch.long)] = True
+        return t
+
+    def _process_logits(self, logits: torch.Tensor, procs) -> torch.Tensor:
+        from kafka_llm_service_amd.engine.constrained import Mask
+
         logits = logits.float().clone()
-        for i, s in enumerate(seqs):
+        V = logits.shape[1]
+        for i, s, allowed in procs:
             p = s.params
             if (p.presence_penalty or p.frequency_penalty) and s.output_ids:
                 ids = torch.tensor(s.output_ids, device=logits.device)
-                cnt = torch.bincount(ids, minlength=logits.shape[1]).float()
+                cnt = torch.bincount(ids, minlength=V)[:V].float()
                 logits[i] -= p.frequency_penalty * cnt + p.presence_penalty * (cnt > 0).float()
-            if p.allowed_tokens_fn is not None:
-                allowed = p.allowed_tokens_fn(s.output_ids)
-                if allowed is not None:
-                    mask = torch.full((logits.shape[1],), float("-inf"), device=logits.device)
-                    idx = torch.as_tensor(allowed, device=logits.device, dtype=torch.long)
-                    mask[idx] = 0.0
-                    logits[i] += mask
+            if allowed is None:
+                continue
+            if isinstance(allowed, Mask):
+                keep = self._mask_tensor(allowed)[:V]
+            else:
+                keep = torch.zeros(V, dtype=torch.bool, device=logits.device)
+                keep[torch.as_tensor(allowed, device=logits.device, dtype=torch.long)] = True
+            logits[i].masked_fill_(~keep, float("-inf"))
         return logits
 
     # ------------------------------------------------------------------------------------------------------------

@@ -27,8 +27,11 @@ class SamplingParams:
     seed: int | None = None
     presence_penalty: float = 0.0
     frequency_penalty: float = 0.0
-    # called with (output_token_ids) -> allowed token ids (list/tensor) or None for "no constraint"
+    # called with (output_token_ids) -> allowed token ids (list / constrained.Mask) or None for "no constraint"
     allowed_tokens_fn: Callable | None = None
+    # picklable tool-call grammar {"tools": [...], "tool_choice": ...}: the engine builds the constraint
+    # (engine/constrained.py) on its own side, so it also works through the DP / TP worker pipes
+    tool_grammar: dict | None = None
 
     def __post_init__(self):
         if self.temperature < 0:

@@ -7,7 +7,8 @@ compaction path recognises it, /root/reference/src/llm/context_compaction/base.p
 (routed by thread id for KV affinity) -> detokenize incrementally and yield live content chunks -> a generation that
 opens with the tool-call token (``<|python_tag|>`` / ``[TOOL_CALLS]``) is parsed into OpenAI ``tool_calls`` deltas
 (``index``/``id``/``type``/``function{name, arguments}``, the normalised shape the Portkey provider produced,
-portkey.py:447-464) -> a final chunk with ``finish_reason`` and real ``usage``. Every chunk carries the generated
+portkey.py:447-464); with tools present the sampler runs the tool-call grammar of ``engine/constrained.py``, so a call
+is always well-formed, and ``tool_choice`` ("auto" / "required" / "none" / a named function) is honoured -> a final chunk with ``finish_reason`` and real ``usage``. Every chunk carries the generated
 token ids so the agent can store them with the message (thread token cache).
 """
 from __future__ import annotations
@@ -25,8 +26,12 @@ from kafka_llm_service_amd.llm.types import LLMProviderError, Message, StreamChu
 
 class EngineLLMProvider(LLMProvider):
     def __init__(self, client, default_max_tokens: int = 1024, model_name: str = "llama3-8b", tool_provider=None,
-                 ignore_eos: bool = False):
+                 ignore_eos: bool = False, constrain_tools: bool = True, tool_choice: Any = "auto"):
         super().__init__(tool_provider)
+        # schema-constrained tool calls (engine/constrained.py): every call the model opens is well-formed JSON
+        # matching the tool's schema; tool_choice "required" / a named function forces one (random-init weights)
+        self.constrain_tools = constrain_tools
+        self.tool_choice = tool_choice
         self.client = client
         self.tok = tokenizer_for_model(client.model_cfg)
         self.template = ChatTemplate(self.tok)
@@ -43,7 +48,7 @@ class EngineLLMProvider(LLMProvider):
                                 tools: list[dict] | None = None, top_p: float | None = None,
                                 frequency_penalty: float | None = None, presence_penalty: float | None = None,
                                 seed: int | None = None, routing_key: str | None = None,
-                                **kwargs: Any) -> AsyncGenerator[StreamChunk, None]:
+                                tool_choice: Any = None, **kwargs: Any) -> AsyncGenerator[StreamChunk, None]:
         self.validate_messages(messages)
         if tools is None:
             tools = await self.get_tools()
@@ -57,7 +62,9 @@ class EngineLLMProvider(LLMProvider):
                                 top_p=1.0 if not top_p else float(top_p), max_tokens=max_new,
                                 frequency_penalty=float(frequency_penalty or 0.0),
                                 presence_penalty=float(presence_penalty or 0.0), seed=seed,
-                                ignore_eos=self.ignore_eos)
+                                ignore_eos=self.ignore_eos,
+                                tool_grammar=({"tools": tools, "tool_choice": tool_choice or self.tool_choice}
+                                              if tools and self.constrain_tools else None))
         stops = [s for s in (stop or []) if s]
         hold = max((len(s) for s in stops), default=1) - 1
         rid = f"req-{uuid.uuid4().hex}"

@@ -12,6 +12,7 @@ LOCAL_SANDBOX_URL, LOCAL_DB_PATH) and adds the engine's:
 from __future__ import annotations
 
 import logging
+import json
 import os
 from dataclasses import dataclass, field
 from typing import Any, AsyncGenerator
@@ -36,6 +37,9 @@ class ServerConfig:
     mcp: bool = False
     max_model_len: int = 131072
     default_max_tokens: int = 1024
+    # default tool_choice of engine-backed generations ("auto" | "required" | "none" | a JSON function object);
+    # "required" makes random-init models drive the agent/tool loop with well-formed calls (BASELINE config 4)
+    tool_choice: Any = "auto"
     engine_kwargs: dict[str, Any] = field(default_factory=dict)
 
     @staticmethod
@@ -49,7 +53,13 @@ class ServerConfig:
                             sandbox_url=e.get("LOCAL_SANDBOX_URL", "http://localhost:8081"),
                             mcp=e.get("KAFKA_MCP", "0") == "1",
                             max_model_len=int(e.get("KAFKA_MAX_MODEL_LEN", "131072")),
-                            default_max_tokens=int(e.get("KAFKA_DEFAULT_MAX_TOKENS", "1024")))
+                            default_max_tokens=int(e.get("KAFKA_DEFAULT_MAX_TOKENS", "1024")),
+                            tool_choice=_tool_choice(e.get("KAFKA_TOOL_CHOICE", "auto")))
+
+
+def _tool_choice(v: str) -> Any:
+    v = v.strip()
+    return json.loads(v) if v.startswith("{") else v
 
 
 class ServerState:
@@ -107,7 +117,7 @@ class ServerState:
 
         self.engine_client = await make_engine_client(cfg)
         return EngineLLMProvider(self.engine_client, default_max_tokens=cfg.default_max_tokens,
-                                 model_name=self.model_ids()[0])
+                                 model_name=self.model_ids()[0], tool_choice=cfg.tool_choice)
 
     async def stop(self) -> None:
         self.ready = False
