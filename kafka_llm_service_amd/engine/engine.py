@@ -17,8 +17,8 @@ from dataclasses import dataclass, field, replace
 import torch
 
 from kafka_llm_service_amd.engine.model_runner import ModelRunner
-from kafka_llm_service_amd.engine.scheduler import Scheduler, SchedulerConfig
-from kafka_llm_service_amd.engine.sequence import SamplingParams, Sequence, SeqStatus, StepOutput
+from kafka_llm_service_amd.engine.scheduler import NeedSync, Scheduler, SchedulerConfig
+from kafka_llm_service_amd.engine.sequence import PENDING, SamplingParams, Sequence, SeqStatus, StepOutput
 from kafka_llm_service_amd.models.config import ModelConfig, get_config
 from kafka_llm_service_amd.models.weights import build_model
 from kafka_llm_service_amd.runtime import KVManager
@@ -46,6 +46,7 @@ class EngineConfig:
     target_wgs: int = 256               # tile-kernel workgroups per pass (8-wave WGs, one per CU)
     prefill_kv_chunk: int = 1024        # key-range split for long-context prefill tiles
     use_graphs: bool = False
+    async_scheduling: bool = True       # plan step n+1 on the host while step n runs on the GPU
     eos_token_ids: list[int] = field(default_factory=list)
 
     def resolve_device(self) -> torch.device:
@@ -56,6 +57,15 @@ class EngineConfig:
 
             return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
         return torch.device("cpu")
+
+
+@dataclass
+class _Plan:
+    batch: object
+    host: object
+    sampled: list
+    seqs: list
+    n_added: int
 
 
 def _agree_min(n: int) -> int:
@@ -112,7 +122,10 @@ class LLMEngine:
                                   cascade_min_prefix=cfg.cascade_min_prefix, use_cascade=cfg.use_cascade,
                                   target_wgs=cfg.target_wgs, prefill_kv_chunk=cfg.prefill_kv_chunk)
         self.requests: dict[str, Sequence] = {}
-        self.stats = {"steps": 0, "prompt_tokens": 0, "cached_tokens": 0, "output_tokens": 0, "step_time": 0.0}
+        self.stats = {"steps": 0, "prompt_tokens": 0, "cached_tokens": 0, "output_tokens": 0, "step_time": 0.0,
+                      "replans": 0, "planned_ahead": 0}
+        self._plan: _Plan | None = None
+        self._n_added = 0
         self.stop_checker_factory = None  # set by the frontend: (request params) -> incremental stop-string checker
         log.info("engine ready: %s tp=%d kv pages=%d (%.1f GB) load %.1fs", mc.name, cfg.tp, nb,
                  nb * page_bytes / 1e9, self.load_s)
@@ -138,6 +151,7 @@ class LLMEngine:
             seq.stop_checker = self.stop_checker_factory(params)
         self.requests[request_id] = seq
         self.sched.add(seq)
+        self._n_added += 1
         return seq
 
     def abort(self, request_id: str) -> None:
@@ -158,15 +172,31 @@ class LLMEngine:
 
     # ------------------------------------------------------------------------------------------------------------
     def step(self) -> list[StepOutput]:
-        batch = self.sched.schedule()
-        if batch.empty:
-            return []
+        """Run one engine iteration and return the tokens it produced.
+
+        With ``async_scheduling`` the host work of the NEXT iteration (scheduling, page allocation, block tables,
+        attention work items: ~1 ms of Python/C++ for 64 long-context threads) is done while the GPU runs this one:
+        the sequences sampled by the in-flight step carry a PENDING placeholder token, their decode rows are patched
+        with the real ids at launch. A plan is dropped (and redone after the step lands) when requests arrived or
+        sequences finished in between, so new turns are never delayed and no row is computed for a finished
+        sequence; sequences that will finish by length are left out of speculative plans up front."""
+        plan = self._plan
+        self._plan = None
+        if plan is not None and (plan.n_added != self._n_added or any(s.finished for s in plan.seqs)):
+            plan = None
+            self.stats["replans"] += 1
+        if plan is None:
+            batch = self.sched.schedule()
+            if batch.empty:
+                return []
+            host, sampled = self.runner.build_host(batch)
+        else:
+            batch, host, sampled = plan.batch, plan.host, plan.sampled
+            self.stats["planned_ahead"] += 1
         t0 = time.perf_counter()
-        sampled_seqs, toks = self.runner.execute(batch)
-        now = time.perf_counter()
-        self.stats["step_time"] += now - t0
-        self.stats["steps"] += 1
-        # advance computed counts + register completed pages in the prefix tree
+        launched = self.runner.launch(host, sampled)
+        # advance computed counts + register completed pages in the prefix tree (the step's KV writes are ordered
+        # before any later reader on the stream); the sampled tokens are pending until the step lands
         for s in batch.decode:
             s.num_computed = s.total_len
         for s, a, b in batch.prefill:
@@ -175,9 +205,17 @@ class LLMEngine:
             self.kvm.commit(s.seq_id, s.num_computed)
         for s, a, b in batch.prefill:
             self.kvm.commit(s.seq_id, s.num_computed)
+        for s in sampled:
+            s.output_ids.append(PENDING)
+        if self.cfg.async_scheduling:
+            self._plan = self._speculate()
+        toks = self.runner.collect(launched)
+        now = time.perf_counter()
+        self.stats["step_time"] += now - t0
+        self.stats["steps"] += 1
         outs: list[StepOutput] = []
-        for s, t in zip(sampled_seqs, toks):
-            s.output_ids.append(t)
+        for s, t in zip(sampled, toks):
+            s.output_ids[-1] = t
             self.kvm.append_token(s.seq_id, t)
             if s.first_token_time is None:
                 s.first_token_time = now
@@ -192,6 +230,17 @@ class LLMEngine:
             outs.append(StepOutput(s.request_id, [t], reason is not None, reason, len(s.prompt_ids),
                                    len(s.output_ids), s.num_cached))
         return outs
+
+    def _speculate(self) -> _Plan | None:
+        try:
+            batch = self.sched.schedule(speculative=True)
+        except NeedSync:
+            return None
+        if batch.empty:
+            return None
+        host, sampled = self.runner.build_host(batch)
+        seqs = list(batch.decode) + [s for s, _, _ in batch.prefill]
+        return _Plan(batch, host, sampled, seqs, self._n_added)
 
     def _check_stop(self, s: Sequence, t: int) -> str | None:
         p = s.params

@@ -10,7 +10,7 @@ batches run eagerly.
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 import torch
@@ -41,6 +41,15 @@ class HostStep:
     prefill_splits: int = 0
     i64: np.ndarray | None = None
     i32: np.ndarray | None = None
+    # (row, seq, position): decode inputs whose token was still being sampled at planning time, filled at launch
+    patch: list = field(default_factory=list)
+    stats: dict = field(default_factory=dict)
+
+
+@dataclass
+class Launched:
+    tokens: torch.Tensor            # sampled ids (pinned host buffer on GPU, plain tensor on CPU)
+    event: object = None            # completion event of the D2H copy
 
 
 def decode_splits(B: int, hkv: int, max_keys: int, target_wgs: int = 512, min_keys_per_split: int = 256) -> int:
@@ -74,6 +83,7 @@ class ModelRunner:
         self._pin = pin
         self.last_stats: dict = {}
         self.broadcast = None  # set on a TP leader: callable(HostStep) (engine/tp_worker.py)
+        self._tok_host = None  # pinned landing buffer of the sampled ids
 
     # ------------------------------------------------------------------------------------------------------------
     def prepare(self, batch: ScheduledBatch) -> tuple[StepInput, list[Sequence]]:
@@ -97,9 +107,13 @@ class ModelRunner:
         sample_seqs: list[Sequence] = []
         logit_rows: list[int] = []
         seq_ids = []
+        patch = []
         for i, s in enumerate(dec):
             p = s.total_len - 1
-            tokens[i] = s.token_at(p)
+            t = s.token_at(p)
+            if t < 0:  # PENDING: sampled by the step still in flight (async scheduling)
+                patch.append((i, s, p))
+            tokens[i] = t
             positions[i] = p
             q_limit[i] = p
             self.kvm.fill_slots(s.seq_id, p, p + 1, slots, i)
@@ -125,7 +139,7 @@ class ModelRunner:
         bt = self._bt[:nbt]
         self.kvm.fill_block_tables(seq_ids, bt)
         # ---- decode metadata (+ cascade over the shared prefix)
-        h = HostStep(B=B, T=T, nbt=nbt, n_rows=len(logit_rows))
+        h = HostStep(B=B, T=T, nbt=nbt, n_rows=len(logit_rows), patch=patch)
         i32_parts = [bt.reshape(-1), q_limit]
         if B:
             seq_lens = np.fromiter((s.total_len for s in dec), dtype=np.int32, count=B)
@@ -169,8 +183,8 @@ class ModelRunner:
             i32_parts.append(np.asarray(items, dtype=np.int32).reshape(-1))
         h.i64 = np.concatenate([tokens, positions, slots, np.asarray(logit_rows, dtype=np.int64)])
         h.i32 = np.concatenate(i32_parts)
-        self.last_stats = {"B": B, "T": T, "cascade_prefix": h.cascade_prefix, "splits": h.splits,
-                           "prefix_splits": h.prefix_splits, "prefill_splits": h.prefill_splits}
+        h.stats = {"B": B, "T": T, "cascade_prefix": h.cascade_prefix, "splits": h.splits,
+                   "prefix_splits": h.prefix_splits, "prefill_splits": h.prefill_splits}
         return h, sample_seqs
 
     def to_device(self, h: HostStep) -> StepInput:
@@ -284,9 +298,33 @@ class ModelRunner:
     @torch.inference_mode()
     def execute(self, batch: ScheduledBatch) -> tuple[list[Sequence], list[int]]:
         host, sample_seqs = self.build_host(batch)
+        return sample_seqs, self.collect(self.launch(host, sample_seqs))
+
+    @torch.inference_mode()
+    def launch(self, host: HostStep, sample_seqs: list[Sequence]) -> "Launched":
+        """Enqueue one step on the GPU without waiting for it: (TP broadcast) -> H2D -> forward -> sample -> async
+        D2H of the sampled ids into pinned memory. ``collect`` waits for them."""
+        for row, s, pos in host.patch:  # decode inputs that were still being sampled when the step was planned
+            host.i64[row] = s.token_at(pos)
+        host.patch = []
+        self.last_stats = host.stats
         if self.broadcast is not None:  # TP leader: followers run the same step on their shards
             self.broadcast(host)
         inp = self.to_device(host)
         logits = self.model.forward(inp, self.k_caches, self.v_caches)
         toks = self.sample(logits, sample_seqs)
-        return sample_seqs, toks.tolist()
+        if self.device.type != "cuda":
+            return Launched(toks, None)
+        n = toks.shape[0]
+        if self._tok_host is None or self._tok_host.shape[0] < n:
+            self._tok_host = torch.empty(max(n, 256), dtype=torch.int64, pin_memory=True)
+        out = self._tok_host[:n]
+        out.copy_(toks, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return Launched(out, ev)
+
+    def collect(self, h: "Launched") -> list[int]:
+        if h.event is not None:
+            h.event.synchronize()
+        return h.tokens.tolist()

@@ -46,6 +46,10 @@ class ScheduledBatch:
         return not self.decode and not self.prefill
 
 
+class NeedSync(Exception):
+    """A speculative plan would have to preempt: plan again once the in-flight step has landed."""
+
+
 class Scheduler:
     def __init__(self, cfg: SchedulerConfig, kv):
         self.cfg = cfg
@@ -96,7 +100,10 @@ class Scheduler:
         if self.kv.has_seq(seq.seq_id):
             self.kv.free_sequence(seq.seq_id)
 
-    def schedule(self) -> ScheduledBatch:
+    def schedule(self, speculative: bool = False) -> ScheduledBatch:
+        """Build the next batch. ``speculative``: planned while the previous step is still on the GPU (its sampled
+        tokens are PENDING placeholders): sequences whose pending token is their last by length are left out, and a
+        plan that would need a preemption is abandoned (``NeedSync``) — the engine then plans after the step lands."""
         cfg = self.cfg
         batch = ScheduledBatch()
         budget = cfg.max_num_batched_tokens
@@ -104,7 +111,11 @@ class Scheduler:
         for seq in list(self.running):
             if seq.status != SeqStatus.RUNNING or seq.remaining != 1:
                 continue
+            if speculative and (len(seq.output_ids) >= seq.params.max_tokens or seq.total_len >= cfg.max_model_len):
+                continue
             while not self.kv.ensure_capacity(seq.seq_id, seq.total_len):
+                if speculative:
+                    raise NeedSync()
                 if not self._preempt_one(batch, seq):
                     raise RuntimeError("KV cache too small for a single sequence")
             if seq.status != SeqStatus.RUNNING:

@@ -15,6 +15,9 @@ from dataclasses import dataclass, field
 from typing import Callable
 
 
+PENDING = -1  # placeholder of a token still being sampled by the in-flight engine step (async scheduling)
+
+
 @dataclass
 class SamplingParams:
     temperature: float = 1.0

@@ -142,3 +142,30 @@ def test_mixtral_greedy_matches_oracle():
     prompts = _prompts(seed=5, shared=40, tails=(4, 19))
     outs = eng.generate(prompts, GREEDY)
     _check_against_oracle(eng.model, prompts, outs)
+
+
+def test_async_scheduling_equals_sync(base_engine):
+    """Planning step n+1 while step n is in flight (PENDING tokens patched at launch, plans dropped when requests
+    arrive or sequences finish) must not change any output; requests join mid-run and finish at different times."""
+    import random
+
+    prompts = _prompts(seed=9, shared=60, tails=(2, 30, 7, 55, 11))
+    lens = [3, 9, 5, 12, 7]
+
+    def run(async_on):
+        eng = _engine(model=base_engine.model, async_scheduling=async_on)
+        rng = random.Random(0)
+        pending = list(range(len(prompts)))
+        seqs = {}
+        while pending or any(not s.finished for s in seqs.values()):
+            if pending and rng.random() < 0.4:
+                i = pending.pop(0)
+                sp = SamplingParams(temperature=0.0, max_tokens=lens[i], ignore_eos=True)
+                seqs[i] = eng.add_request(f"r{i}", prompts[i], sp)
+            eng.step()
+        return [seqs[i].output_ids for i in range(len(prompts))], eng.stats
+
+    sync_out, _ = run(False)
+    async_out, st = run(True)
+    assert async_out == sync_out
+    assert st["planned_ahead"] > 0 and st["replans"] > 0
