@@ -27,6 +27,7 @@ SSE behaviour (SURVEY.md §2.5.1/2.5.2, quirks Q1-Q3, Q6-Q8 fixed):
 """
 from __future__ import annotations
 
+import asyncio
 import json
 import logging
 import time
@@ -59,6 +60,40 @@ def _chunk(cid: str, created: int, model: str, delta: dict, finish: Optional[str
     d = {"role": delta.get("role"), "content": delta.get("content"), "tool_calls": delta.get("tool_calls")}
     return _sse({"id": cid, "object": "chat.completion.chunk", "created": created, "model": model,
                  "choices": [{"index": 0, "delta": d, "finish_reason": finish}]})
+
+
+async def _coalesce(gen: AsyncGenerator[str, None]) -> AsyncGenerator[str, None]:
+    """Write every SSE frame that is ready in ONE transport send: a producer task drains ``gen`` into a queue and the
+    response yields everything queued since the last write. A live token stream (one frame per engine step) is
+    unchanged; bursts (usage + finish + [DONE], tool output, the stub provider's instant replies) stop costing one
+    ASGI send each (~25 us of event-loop time per frame — the plumbing overhead SURVEY.md §6.2 measured)."""
+    q: asyncio.Queue = asyncio.Queue()
+    done = object()
+
+    async def pump():
+        try:
+            async for frame in gen:
+                q.put_nowait(frame)
+        finally:
+            q.put_nowait(done)
+
+    task = asyncio.create_task(pump())
+    try:
+        while True:
+            parts = [await q.get()]
+            while not q.empty():
+                parts.append(q.get_nowait())
+            end = parts[-1] is done
+            if end:
+                parts.pop()
+            if parts:
+                yield "".join(parts)
+            if end:
+                break
+        await task  # re-raise a producer failure
+    finally:
+        if not task.done():
+            task.cancel()  # client went away: cancel the generation (engine abort runs in its finally blocks)
 
 
 def _sampling_kwargs(req: ChatCompletionRequest) -> dict[str, Any]:
@@ -163,7 +198,7 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
         new = [convert_to_internal_message(m) for m in req.messages]
         tool_events = request.headers.get("x-kafka-tool-events") == "1"
         if req.stream:
-            return StreamingResponse(completion_events(new, req, thread_id, tool_events),
+            return StreamingResponse(_coalesce(completion_events(new, req, thread_id, tool_events)),
                                      media_type="text/event-stream", headers=SSE_HEADERS)
         return await completion_json(new, req, thread_id)
 
@@ -174,7 +209,8 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
         msgs = [convert_to_internal_message(m) for m in req.messages]
         tool_events = request.headers.get("x-kafka-tool-events") == "1"
         if req.stream:
-            return StreamingResponse(completion_events(msgs, req, None, tool_events), media_type="text/event-stream",
+            return StreamingResponse(_coalesce(completion_events(msgs, req, None, tool_events)),
+                                     media_type="text/event-stream",
                                      headers=SSE_HEADERS)
         return await completion_json(msgs, req, None)
 
@@ -192,7 +228,8 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
         _require()
         M.REQUESTS.labels(route="agent_run").inc()
         msgs = [convert_to_internal_message(m) for m in req.messages]
-        return StreamingResponse(agent_events(st.run_agent(msgs, req.model, req.temperature, req.max_tokens, None)),
+        return StreamingResponse(_coalesce(agent_events(st.run_agent(msgs, req.model, req.temperature, req.max_tokens,
+                                                                     None))),
                                  media_type="text/event-stream", headers=SSE_HEADERS)
 
     @app.post("/v1/threads/{thread_id}/agent/run")
@@ -202,8 +239,8 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
         if not await st.db.thread_exists(thread_id):
             await st.db.create_thread(thread_id=thread_id)
         msgs = [convert_to_internal_message(m) for m in req.messages]
-        return StreamingResponse(agent_events(st.run_thread_agent(thread_id, msgs, req.model, req.temperature,
-                                                                  req.max_tokens)),
+        return StreamingResponse(_coalesce(agent_events(st.run_thread_agent(thread_id, msgs, req.model,
+                                                                            req.temperature, req.max_tokens))),
                                  media_type="text/event-stream", headers=SSE_HEADERS)
 
     @app.post("/v1/threads/{thread_id}/messages")

@@ -40,6 +40,7 @@ class ServerConfig:
     # default tool_choice of engine-backed generations ("auto" | "required" | "none" | a JSON function object);
     # "required" makes random-init models drive the agent/tool loop with well-formed calls (BASELINE config 4)
     tool_choice: Any = "auto"
+    ignore_eos: bool = False  # benchmarks: generate exactly max_tokens (random-init weights emit EOS at random)
     engine_kwargs: dict[str, Any] = field(default_factory=dict)
 
     @staticmethod
@@ -54,7 +55,8 @@ class ServerConfig:
                             mcp=e.get("KAFKA_MCP", "0") == "1",
                             max_model_len=int(e.get("KAFKA_MAX_MODEL_LEN", "131072")),
                             default_max_tokens=int(e.get("KAFKA_DEFAULT_MAX_TOKENS", "1024")),
-                            tool_choice=_tool_choice(e.get("KAFKA_TOOL_CHOICE", "auto")))
+                            tool_choice=_tool_choice(e.get("KAFKA_TOOL_CHOICE", "auto")),
+                            ignore_eos=e.get("KAFKA_IGNORE_EOS", "0") == "1")
 
 
 def _tool_choice(v: str) -> Any:
@@ -117,7 +119,8 @@ class ServerState:
 
         self.engine_client = await make_engine_client(cfg)
         return EngineLLMProvider(self.engine_client, default_max_tokens=cfg.default_max_tokens,
-                                 model_name=self.model_ids()[0], tool_choice=cfg.tool_choice)
+                                 model_name=self.model_ids()[0], tool_choice=cfg.tool_choice,
+                                 ignore_eos=cfg.ignore_eos)
 
     async def stop(self) -> None:
         self.ready = False
