@@ -24,6 +24,17 @@ from kafka_llm_service_amd.llm.compaction import is_context_length_error
 from kafka_llm_service_amd.llm.types import Message
 from kafka_llm_service_amd.tools.types import Tool
 
+
+def _tool_done(name: str, t0: float) -> None:
+    """Tool time (SURVEY.md §5.1 spans / §5.5 metrics)."""
+    from kafka_llm_service_amd.obs import metrics, trace
+
+    t1 = time.perf_counter()
+    metrics.TOOL_SECONDS.labels(tool=name).observe(t1 - t0)
+    tr = trace.tracer()
+    if tr is not None:
+        tr.complete(f"tool:{name}", "agent", t0, t1)
+
 IDLE_TOOL_NAME = "idle"
 
 
@@ -175,10 +186,12 @@ class Agent:
                                       "iteration": iteration})
                     return
                 result = ""
+                t_tool = time.perf_counter()
                 async for chunk in self.tool_provider.run_tool_stream(name, args, call["id"]):
                     result += chunk.delta
                     yield {"type": "tool_result", "tool_call_id": call["id"], "tool_name": name,
                            "delta": chunk.delta, "is_complete": chunk.is_complete}
+                _tool_done(name, t_tool)
                 working.append(Message(role="tool", content=result, tool_call_id=call["id"], name=name))
                 if emit_messages:
                     yield {"type": "_message", "message": working[-1]}

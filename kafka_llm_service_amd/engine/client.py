@@ -23,14 +23,23 @@ from typing import AsyncIterator
 from kafka_llm_service_amd.engine.sequence import SamplingParams, StepOutput
 
 log = logging.getLogger("kafka.engine")
+HEARTBEAT_S = 1.0
 
 
-def route(key: str | None, n: int, loads: list[int]) -> int:
-    if n == 1:
-        return 0
+def route(key: str | None, n: int, loads: list[int], alive: list[bool] | None = None) -> int:
+    """Replica for a request: the thread's home replica (stable hash of the thread id, so its KV prefix is reused);
+    if that one is down, the next live replica in hash order; keyless requests go to the least-loaded live replica.
+    Returns -1 when no replica is up."""
+    live = [i for i in range(n) if alive is None or alive[i]]
+    if not live:
+        return -1
     if key is None:
-        return min(range(n), key=lambda i: loads[i])
-    return int(hashlib.blake2b(key.encode(), digest_size=8).hexdigest(), 16) % n
+        return min(live, key=lambda i: loads[i])
+    h = int(hashlib.blake2b(key.encode(), digest_size=8).hexdigest(), 16) % n
+    for j in range(n):
+        if alive is None or alive[(h + j) % n]:
+            return (h + j) % n
+    return -1
 
 
 class InProcessClient:
@@ -81,8 +90,19 @@ def _worker_main(rank: int, cfg_dict: dict, conn) -> None:
 
 
 def serve_pipe(eng, conn) -> None:
-    """Request loop of a replica (or TP-group leader): drain control messages, step while there is work."""
+    """Request loop of a replica (or TP-group leader): drain control messages, step while there is work, send a
+    heartbeat at least every HEARTBEAT_S (the parent's stall detector, ``DPClient._monitor``)."""
+    from kafka_llm_service_amd.utils import faults
+
+    fi = faults.get()
+    last_hb = 0.0
     while True:
+        now = time.monotonic()
+        if now - last_hb >= HEARTBEAT_S:
+            conn.send(("hb", eng.stats["steps"]))
+            last_hb = now
+        if fi.worker_should_exit(eng.stats["steps"]):
+            os._exit(3)  # injected replica crash (KAFKA_FI_WORKER_EXIT_AFTER)
         busy = eng.has_unfinished()
         while conn.poll(0 if busy else 0.05):
             msg = conn.recv()
@@ -114,11 +134,17 @@ def serve_pipe(eng, conn) -> None:
 
 class DPClient:
     """``n_replicas`` independent engines; with ``tp > 1`` each replica is a TP group of ``tp`` processes
-    (``engine/tp_worker.py``) whose leader owns the request pipe."""
+    (``engine/tp_worker.py``) whose leader owns the request pipe.
+
+    Supervision (SURVEY.md §5.3 "engine watchdog ... the DP router drains and re-routes threads"): a replica whose
+    process dies fails its in-flight streams with an error (the API turns it into an error frame), is marked down —
+    its threads are routed to the next live replica and re-prefill from the thread store there — and is respawned in
+    the background; a replica whose heartbeat stops for ``stall_timeout`` seconds is killed and handled the same way.
+    """
 
     def __init__(self, engine_cfg, n_replicas: int, start_timeout: float = 900.0, tp: int = 1,
-                 base_port: int | None = None):
-        ctx = mp.get_context("spawn")
+                 base_port: int | None = None, respawn: bool = True, stall_timeout: float | None = None):
+        self._ctx = mp.get_context("spawn")
         self.engine_cfg = engine_cfg
         self.n_replicas = n_replicas
         self.tp = tp
@@ -126,61 +152,122 @@ class DPClient:
         from kafka_llm_service_amd.models.config import get_config
 
         self.model_cfg = get_config(engine_cfg.model)
-        cfg = asdict(engine_cfg)
-        cfg["device"] = None
-        self.conns, self.procs = [], []
-        self._followers: list = []
+        self._cfg = asdict(engine_cfg)
+        self._cfg["device"] = None
+        self.start_timeout = start_timeout
+        self.respawn = respawn
+        self.stall_timeout = stall_timeout if stall_timeout is not None else \
+            float(os.environ.get("KAFKA_STALL_TIMEOUT_S", "600"))
+        self.conns: list = [None] * n_replicas
+        self.procs: list = [None] * n_replicas
+        self._group_procs: list[list] = [[] for _ in range(n_replicas)]
         self._send_locks = [threading.Lock() for _ in range(n_replicas)]
         self._streams: dict[str, tuple[asyncio.AbstractEventLoop, asyncio.Queue, int]] = {}
         self._lock = threading.Lock()
         self._loads = [0] * n_replicas
         self._health: list[dict] = [{} for _ in range(n_replicas)]
+        self._alive = [False] * n_replicas
+        self._last_hb = [time.monotonic()] * n_replicas
+        self._gen = [0] * n_replicas
+        self.restarts = [0] * n_replicas
+        self._closing = False
         self._ids = itertools.count()
-        follower_conns = []
-        if base_port is None:
-            base_port = _free_port_base(n_replicas)
-        for r in range(n_replicas):
-            if tp == 1:
-                parent, child = ctx.Pipe()
-                p = ctx.Process(target=_worker_main, args=(r, cfg, child), daemon=True, name=f"kafka-replica{r}")
-                p.start()
-                self.conns.append(parent)
-                self.procs.append(p)
-                continue
-            from kafka_llm_service_amd.engine.tp_worker import tp_worker_main
+        ports = base_port if base_port is not None else _free_port_base(n_replicas)
+        pending = [self._spawn(r, ports + r) for r in range(n_replicas)]
+        for r, conns in enumerate(pending):
+            self._await_ready(r, conns)
+        self._monitor_thread = threading.Thread(target=self._monitor, daemon=True, name="kafka-dp-monitor")
+        self._monitor_thread.start()
 
-            for t in range(tp):
-                parent, child = ctx.Pipe()
-                p = ctx.Process(target=tp_worker_main, args=(r, t, tp, base_port + r, cfg, child), daemon=True,
-                                name=f"kafka-replica{r}-tp{t}")
-                p.start()
-                (self.conns if t == 0 else follower_conns).append(parent)
-                (self.procs if t == 0 else self._followers).append(p)
-        deadline = time.monotonic() + start_timeout
-        for r, c in enumerate(self.conns + follower_conns):
+    # ---- replica lifecycle -------------------------------------------------------------------------------------
+    def _spawn(self, r: int, port: int) -> list:
+        """Start replica r's processes; returns [leader_conn, follower_conns...] (not yet ready)."""
+        ctx, cfg = self._ctx, self._cfg
+        if self.tp == 1:
+            parent, child = ctx.Pipe()
+            p = ctx.Process(target=_worker_main, args=(r, cfg, child), daemon=True, name=f"kafka-replica{r}")
+            p.start()
+            self.procs[r], self._group_procs[r] = p, [p]
+            return [parent]
+        from kafka_llm_service_amd.engine.tp_worker import tp_worker_main
+
+        conns, group = [], []
+        for t in range(self.tp):
+            parent, child = ctx.Pipe()
+            p = ctx.Process(target=tp_worker_main, args=(r, t, self.tp, port, cfg, child), daemon=True,
+                            name=f"kafka-replica{r}-tp{t}")
+            p.start()
+            conns.append(parent)
+            group.append(p)
+        self.procs[r], self._group_procs[r] = group[0], group
+        return conns
+
+    def _await_ready(self, r: int, conns: list) -> None:
+        deadline = time.monotonic() + self.start_timeout
+        for c in conns:
             if not c.poll(max(1.0, deadline - time.monotonic())):
-                raise RuntimeError(f"engine process {r} did not start")
+                raise RuntimeError(f"engine replica {r} did not start")
             msg = c.recv()
             if msg[0] != "ready":
-                raise RuntimeError(f"engine process {r} failed: {msg[1]}")
-        self._readers = [threading.Thread(target=self._reader, args=(r,), daemon=True) for r in range(n_replicas)]
-        for t in self._readers:
-            t.start()
+                raise RuntimeError(f"engine replica {r} failed: {msg[1]}")
+        with self._lock:
+            self.conns[r] = conns[0]
+            self._gen[r] += 1
+            self._alive[r] = True
+            self._last_hb[r] = time.monotonic()
+        threading.Thread(target=self._reader, args=(r, conns[0], self._gen[r]), daemon=True,
+                         name=f"kafka-dp-reader{r}").start()
+
+    def _respawn(self, r: int) -> None:
+        for p in self._group_procs[r]:
+            if p.is_alive():
+                p.terminate()
+            p.join(timeout=30)
+        if self._closing or not self.respawn:
+            return
+        try:
+            self._await_ready(r, self._spawn(r, _free_port_base(1)))
+            self.restarts[r] += 1
+            log.warning("engine replica %d restarted", r)
+        except Exception:
+            log.exception("engine replica %d failed to restart", r)
+
+    def _monitor(self) -> None:
+        while not self._closing:
+            time.sleep(1.0)
+            now = time.monotonic()
+            for r in range(self.n_replicas):
+                if self._alive[r] and now - self._last_hb[r] > self.stall_timeout:
+                    log.error("engine replica %d stalled (no heartbeat for %.0fs): killing it", r,
+                              now - self._last_hb[r])
+                    for p in self._group_procs[r]:
+                        if p.is_alive():
+                            p.kill()
 
     def _send(self, r: int, msg) -> None:
         with self._send_locks[r]:
             self.conns[r].send(msg)
 
-    def _reader(self, r: int) -> None:
-        conn = self.conns[r]
+    def _send_quiet(self, r: int, msg) -> None:
+        """Best-effort control message (aborts): a replica that is down has nothing to abort."""
+        try:
+            self._send(r, msg)
+        except (OSError, BrokenPipeError, EOFError):
+            pass
+
+    def _reader(self, r: int, conn, gen: int) -> None:
         while True:
             try:
                 msg = conn.recv()
             except (EOFError, OSError):
-                self._fail_replica(r)
+                if gen == self._gen[r] and not self._closing:
+                    self._fail_replica(r)
+                    threading.Thread(target=self._respawn, args=(r,), daemon=True).start()
                 return
             kind = msg[0]
-            if kind == "out":
+            if kind == "hb":
+                self._last_hb[r] = time.monotonic()
+            elif kind == "out":
                 batches: dict = {}
                 with self._lock:
                     for rid, toks, fin, reason, npt, nout, ncached in msg[1]:
@@ -208,9 +295,11 @@ class DPClient:
 
     def _fail_replica(self, r: int) -> None:
         with self._lock:
+            self._alive[r] = False
             dead = [(rid, s) for rid, s in self._streams.items() if s[2] == r]
             for rid, _ in dead:
                 self._streams.pop(rid, None)
+            self._loads[r] = 0
         for rid, (loop, q, _) in dead:
             loop.call_soon_threadsafe(q.put_nowait, RuntimeError(f"engine replica {r} died"))
 
@@ -219,11 +308,18 @@ class DPClient:
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
         with self._lock:
-            r = route(routing_key, self.n_replicas, self._loads)
+            r = route(routing_key, self.n_replicas, self._loads, self._alive)
+            if r < 0:
+                raise RuntimeError("no engine replica available (all replicas are restarting)")
             self._streams[request_id] = (loop, q, r)
             self._loads[r] += 1
         pd = {k: v for k, v in params.__dict__.items() if k != "allowed_tokens_fn"}
-        self._send(r, ("add", request_id, list(prompt_ids), pd))
+        try:
+            self._send(r, ("add", request_id, list(prompt_ids), pd))
+        except (OSError, BrokenPipeError):
+            with self._lock:
+                self._streams.pop(request_id, None)
+            raise RuntimeError(f"engine replica {r} is down")
         done = False
         try:
             while True:
@@ -239,13 +335,13 @@ class DPClient:
                 with self._lock:
                     if self._streams.pop(request_id, None) is not None:
                         self._loads[r] -= 1
-                self._send(r, ("abort", request_id))
+                self._send_quiet(r, ("abort", request_id))
 
     def abort(self, request_id: str) -> None:
         with self._lock:
             s = self._streams.get(request_id)
         if s is not None:
-            self._send(s[2], ("abort", request_id))
+            self._send_quiet(s[2], ("abort", request_id))
 
     def health(self) -> dict:
         for r in range(self.n_replicas):
@@ -255,19 +351,22 @@ class DPClient:
                 pass
         out = {"replicas": self.n_replicas}
         for r in range(self.n_replicas):
-            out[f"replica{r}"] = dict(self._health[r], active=self._loads[r], alive=self.procs[r].is_alive())
+            out[f"replica{r}"] = dict(self._health[r], active=self._loads[r], alive=bool(self._alive[r]),
+                                      restarts=self.restarts[r])
         return out
 
     async def close(self) -> None:
+        self._closing = True
         for r in range(self.n_replicas):
             try:
                 self._send(r, ("stop",))
-            except (OSError, BrokenPipeError):
+            except (OSError, BrokenPipeError, AttributeError):
                 pass
-        for p in self.procs + self._followers:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.terminate()
+        for group in self._group_procs:
+            for p in group:
+                p.join(timeout=30)
+                if p.is_alive():
+                    p.terminate()
 
 
 def _free_port_base(n: int) -> int:

@@ -22,6 +22,8 @@ from kafka_llm_service_amd.engine.sequence import PENDING, SamplingParams, Seque
 from kafka_llm_service_amd.models.config import ModelConfig, get_config
 from kafka_llm_service_amd.models.weights import build_model
 from kafka_llm_service_amd.runtime import KVManager
+from kafka_llm_service_amd.obs import trace
+from kafka_llm_service_amd.utils import faults
 
 log = logging.getLogger("kafka.engine")
 
@@ -97,7 +99,10 @@ class LLMEngine:
         self.eos = set(cfg.eos_token_ids or mc.eos_token_ids)
         hkv, D, L = self.model.hkv, self.model.D, mc.num_layers
         page_bytes = 2 * L * hkv * 16 * D * 2
-        if cfg.num_kv_blocks:
+        self.fi = faults.get()
+        if self.fi.kv_blocks:
+            nb = self.fi.kv_blocks
+        elif cfg.num_kv_blocks:
             nb = cfg.num_kv_blocks
         elif self.device.type == "cuda":
             free, _ = torch.cuda.mem_get_info(self.device)
@@ -180,21 +185,25 @@ class LLMEngine:
         with the real ids at launch. A plan is dropped (and redone after the step lands) when requests arrived or
         sequences finished in between, so new turns are never delayed and no row is computed for a finished
         sequence; sequences that will finish by length are left out of speculative plans up front."""
+        if self.fi.active:
+            self.fi.on_step()
         plan = self._plan
         self._plan = None
         if plan is not None and (plan.n_added != self._n_added or any(s.finished for s in plan.seqs)):
             plan = None
             self.stats["replans"] += 1
         if plan is None:
-            batch = self.sched.schedule()
-            if batch.empty:
-                return []
-            host, sampled = self.runner.build_host(batch)
+            with trace.span("schedule"):
+                batch = self.sched.schedule()
+                if batch.empty:
+                    return []
+                host, sampled = self.runner.build_host(batch)
         else:
             batch, host, sampled = plan.batch, plan.host, plan.sampled
             self.stats["planned_ahead"] += 1
         t0 = time.perf_counter()
-        launched = self.runner.launch(host, sampled)
+        with trace.span("launch", B=host.B, T=host.T):
+            launched = self.runner.launch(host, sampled)
         # advance computed counts + register completed pages in the prefix tree (the step's KV writes are ordered
         # before any later reader on the stream); the sampled tokens are pending until the step lands
         for s in batch.decode:
@@ -208,8 +217,10 @@ class LLMEngine:
         for s in sampled:
             s.output_ids.append(PENDING)
         if self.cfg.async_scheduling:
-            self._plan = self._speculate()
-        toks = self.runner.collect(launched)
+            with trace.span("plan_ahead"):
+                self._plan = self._speculate()
+        with trace.span("collect"):
+            toks = self.runner.collect(launched)
         now = time.perf_counter()
         self.stats["step_time"] += now - t0
         self.stats["steps"] += 1
@@ -227,6 +238,7 @@ class LLMEngine:
             if reason:
                 self.sched.finish(s, reason)
                 self.requests.pop(s.request_id, None)
+                trace.request_span(s, now)
             outs.append(StepOutput(s.request_id, [t], reason is not None, reason, len(s.prompt_ids),
                                    len(s.output_ids), s.num_cached))
         return outs

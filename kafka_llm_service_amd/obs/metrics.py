@@ -10,6 +10,11 @@ _BUCKETS = (0.005, 0.01, 0.02, 0.05, 0.1, 0.2, 0.5, 1.0, 2.0, 5.0, 10.0, 30.0, 6
 REQUESTS = Counter("kafka_requests_total", "HTTP requests by route", ["route"], registry=REGISTRY)
 TTFT = Histogram("kafka_ttft_seconds", "time to first streamed content token", buckets=_BUCKETS, registry=REGISTRY)
 E2E = Histogram("kafka_request_seconds", "end-to-end streamed request latency", buckets=_BUCKETS, registry=REGISTRY)
+TPOT = Histogram("kafka_tpot_seconds", "time per output token after the first (streamed requests)",
+                 buckets=(0.001, 0.002, 0.005, 0.01, 0.02, 0.05, 0.1, 0.2, 0.5), registry=REGISTRY)
+OUTPUT_TOKENS = Counter("kafka_output_tokens_total", "generated tokens returned to clients", registry=REGISTRY)
+TOOL_SECONDS = Histogram("kafka_tool_seconds", "tool execution time by tool", ["tool"], buckets=_BUCKETS,
+                         registry=REGISTRY)
 
 
 def render(state) -> str:

@@ -13,6 +13,7 @@ from typing import Any, AsyncGenerator, Optional
 
 import httpx
 
+from kafka_llm_service_amd.utils import faults
 from kafka_llm_service_amd.sandbox.base import Sandbox, SandboxError, SandboxInfo, SandboxState, ToolEvent
 
 
@@ -59,6 +60,8 @@ class LocalSandbox(Sandbox):
             self._client = None
 
     async def get_health_status(self) -> Optional[dict[str, Any]]:
+        if faults.get().sandbox_down:
+            return None
         try:
             r = await (await self._get_client()).get(self.health_url, timeout=5.0)
             if r.status_code == 200:
@@ -86,6 +89,8 @@ class LocalSandbox(Sandbox):
             await asyncio.sleep(min(self.HEALTH_INTERVAL, max(0.0, deadline - time.monotonic())))
 
     async def run_tool(self, tool_name: str, arguments: dict[str, Any]) -> AsyncGenerator[ToolEvent, None]:
+        if faults.get().sandbox_down:
+            raise SandboxError("Failed to connect to sandbox: injected fault (KAFKA_FI_SANDBOX_DOWN)", self._id)
         if self._state != SandboxState.RUNNING:
             raise SandboxError(f"Sandbox is not running (state: {self._state.value})", self._id)
         client = await self._get_client()

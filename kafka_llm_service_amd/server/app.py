@@ -135,6 +135,7 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
         model = req.model
         t0 = time.perf_counter()
         first = True
+        t_first = None
         finish = "stop"
         usage = None
         try:
@@ -159,7 +160,8 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
                 text = delta.get("content")
                 if text:
                     if first:
-                        M.TTFT.observe(time.perf_counter() - t0)
+                        t_first = time.perf_counter()
+                        M.TTFT.observe(t_first - t0)
                         first = False
                     yield _chunk(cid, created, model, {"content": text}, None)
                 if ch[0].get("finish_reason") == "length":
@@ -173,7 +175,13 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
         except Exception as e:  # the reference's error frame (server.py:375-377)
             log.exception("completion stream failed")
             yield _sse({"error": {"message": str(e), "type": "server_error"}})
-        M.E2E.observe(time.perf_counter() - t0)
+        t_end = time.perf_counter()
+        M.E2E.observe(t_end - t0)
+        n_out = (usage or {}).get("completion_tokens", 0)
+        if n_out:
+            M.OUTPUT_TOKENS.inc(n_out)
+            if n_out > 1 and t_first is not None:
+                M.TPOT.observe((t_end - t_first) / (n_out - 1))
         yield "data: [DONE]\n\n"
 
     async def completion_json(messages, req: ChatCompletionRequest, thread_id: str | None) -> ChatCompletionResponse:

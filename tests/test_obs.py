@@ -1,0 +1,49 @@
+"""Observability: Chrome-trace spans of engine phases / requests / tools when
+KAFKA_TRACE_FILE is set, and the Prometheus histograms the server exports."""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+from pathlib import Path
+
+
+def test_trace_file_has_engine_and_request_spans(tmp_path):
+    code = textwrap.dedent("""
+        from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
+        from kafka_llm_service_amd.engine.sequence import SamplingParams
+        from kafka_llm_service_amd.obs import trace
+        e = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", num_kv_blocks=128, max_model_len=1024))
+        e.generate([list(range(100, 130)), list(range(200, 220))],
+                   SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True))
+        trace.tracer().close()
+    """)
+    env = dict(os.environ, KAFKA_TRACE_FILE=str(tmp_path / "tr"),
+               PYTHONPATH=str(Path(__file__).resolve().parents[1]))
+    subprocess.run([sys.executable, "-c", code], check=True, env=env, timeout=300)
+    files = list(tmp_path.glob("tr.*.json"))
+    assert len(files) == 1
+    evs = [e for e in json.loads(files[0].read_text()) if e]
+    names = {e["name"] for e in evs}
+    assert {"schedule", "launch", "collect", "request", "first_token", "decode"} <= names
+    req = [e for e in evs if e["name"] == "request"]
+    assert len(req) == 2 and all(e["args"]["output_tokens"] == 4 and e["dur"] > 0 for e in req)
+
+
+def test_metrics_histograms_exported():
+    from fastapi.testclient import TestClient
+
+    from kafka_llm_service_amd.db.local import MemoryDBClient
+    from kafka_llm_service_amd.llm.stub import ScriptedProvider
+    from kafka_llm_service_amd.server.app import create_app
+    from kafka_llm_service_amd.server.state import ServerConfig, ServerState
+
+    llm = ScriptedProvider([{"tool_calls": [{"name": "count_slowly", "arguments": {"count": 1, "delay": 0}}]},
+                            {"text": "done and dusted"}])
+    st = ServerState(ServerConfig(backend="stub", sandbox="none"), llm_provider=llm, db=MemoryDBClient())
+    with TestClient(create_app(state=st)) as c:
+        c.post("/v1/chat/completions", json={"model": "m", "messages": [{"role": "user", "content": "x"}],
+                                             "stream": True, "stream_options": {"include_usage": True}})
+        m = c.get("/metrics").text
+    assert 'kafka_tool_seconds_count{tool="count_slowly"} 1.0' in m
+    assert "kafka_tpot_seconds_bucket" in m and "kafka_output_tokens_total" in m
