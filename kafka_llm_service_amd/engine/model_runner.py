@@ -316,8 +316,8 @@ class ModelRunner:
         if self.device.type != "cuda":
             return Launched(toks, None)
         n = toks.shape[0]
-        if self._tok_host is None or self._tok_host.shape[0] < n:
-            self._tok_host = torch.empty(max(n, 256), dtype=torch.int64, pin_memory=True)
+        if self._tok_host is None or self._tok_host.shape[0] < n or self._tok_host.dtype != toks.dtype:
+            self._tok_host = torch.empty(max(n, 256), dtype=toks.dtype, pin_memory=True)
         out = self._tok_host[:n]
         out.copy_(toks, non_blocking=True)
         ev = torch.cuda.Event()
