@@ -31,6 +31,7 @@ class ServerConfig:
     served_model_name: str | None = None
     dp: int = 1
     tp: int = 1
+    db: str = "local"                    # "local" (SQLite, LOCAL_DB_PATH) | "supabase" (SUPABASE_URL / SUPABASE_KEY)
     db_path: str = "data/threads.db"
     sandbox: str = "shared"
     sandbox_url: str = "http://localhost:8081"
@@ -50,6 +51,7 @@ class ServerConfig:
                             weights=e.get("KAFKA_WEIGHTS") or None,
                             served_model_name=e.get("DEFAULT_MODEL") or None, dp=int(e.get("KAFKA_DP", "1")),
                             tp=int(e.get("KAFKA_TP", "1")), db_path=e.get("LOCAL_DB_PATH", "data/threads.db"),
+                            db=e.get("KAFKA_DB", "local"),
                             sandbox=e.get("KAFKA_SANDBOX", "shared"),
                             sandbox_url=e.get("LOCAL_SANDBOX_URL", "http://localhost:8081"),
                             mcp=e.get("KAFKA_MCP", "0") == "1",
@@ -84,7 +86,12 @@ class ServerState:
 
         cfg = self.config
         if self.db is None:
-            self.db = LocalDBClient(cfg.db_path)
+            if cfg.db == "supabase":
+                from kafka_llm_service_amd.db.supabase import SupabaseDBClient
+
+                self.db = SupabaseDBClient()
+            else:
+                self.db = LocalDBClient(cfg.db_path)
         await self.db.initialize()
         if self.llm is None:
             self.llm = await self._make_llm()

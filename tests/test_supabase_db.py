@@ -1,0 +1,115 @@
+"""The Supabase (PostgREST) thread store against an in-process fake PostgREST (eq filters, select, order, limit,
+upsert-ignore, PATCH/DELETE with representation, RPC) — same behaviour as the SQLite store, plus the reference's
+thread-config join."""
+import asyncio
+import json
+
+import httpx
+import pytest
+
+from kafka_llm_service_amd.db.supabase import SupabaseDBClient
+from kafka_llm_service_amd.llm.types import Message
+
+
+class FakePostgREST:
+    def __init__(self):
+        self.tables: dict[str, list[dict]] = {}
+
+    def _match(self, row, params):
+        for k, v in params.items():
+            if k in ("select", "order", "limit"):
+                continue
+            op, _, val = v.partition(".")
+            if op == "eq" and str(row.get(k)) != val:
+                return False
+        return True
+
+    def handler(self, req: httpx.Request) -> httpx.Response:
+        path = req.url.path.split("/rest/v1/")[1]
+        params = dict(req.url.params)
+        if path.startswith("rpc/"):
+            return httpx.Response(200, json="vmk_from_rpc")
+        rows = self.tables.setdefault(path, [])
+        prefer = req.headers.get("prefer", "")
+        if req.method == "GET":
+            out = [r for r in rows if self._match(r, params)]
+            if "order" in params:
+                for key in reversed(params["order"].split(",")):
+                    col, _, d = key.partition(".")
+                    out.sort(key=lambda r: str(r.get(col)), reverse=(d == "desc"))
+            if "limit" in params:
+                out = out[:int(params["limit"])]
+            if params.get("select", "*") != "*":
+                cols = params["select"].split(",")
+                out = [{c: r.get(c) for c in cols} for r in out]
+            return httpx.Response(200, json=out)
+        if req.method == "POST":
+            body = json.loads(req.content)
+            new = body if isinstance(body, list) else [body]
+            added = []
+            for r in new:
+                if "ignore-duplicates" in prefer and any(x.get("id") == r.get("id") for x in rows):
+                    continue
+                rows.append(dict(r))
+                added.append(r)
+            return httpx.Response(201, json=added if "representation" in prefer else None)
+        if req.method == "PATCH":
+            body = json.loads(req.content)
+            hit = [r for r in rows if self._match(r, params)]
+            for r in hit:
+                r.update(body)
+            return httpx.Response(200, json=hit if "representation" in prefer else None)
+        if req.method == "DELETE":
+            hit = [r for r in rows if self._match(r, params)]
+            self.tables[path] = [r for r in rows if r not in hit]
+            return httpx.Response(200, json=hit)
+        return httpx.Response(405)
+
+
+@pytest.fixture()
+def db():
+    fake = FakePostgREST()
+    c = SupabaseDBClient(url="http://supabase.test", key="k", transport=httpx.MockTransport(fake.handler))
+    c.fake = fake
+    return c
+
+
+def test_thread_and_message_roundtrip(db):
+    async def go():
+        t = await db.create_thread(system_message="be brief", user_id="u1")
+        tid = t["id"]
+        assert await db.thread_exists(tid) and not await db.thread_exists("nope")
+        await db.add_messages(tid, [Message(role="user", content="hi"),
+                                    Message(role="assistant", content="yo", token_ids=[1, 2, 3])])
+        msgs = await db.get_thread_messages(tid)
+        assert [m.role for m in msgs] == ["system", "user", "assistant"] and msgs[2].token_ids == [1, 2, 3]
+        assert [m.role for m in await db.get_thread_messages(tid, include_system=False)] == ["user", "assistant"]
+        assert await db.update_thread_sandbox_id(tid, "sb-1") and await db.get_thread_sandbox_id(tid) == "sb-1"
+        assert await db.delete_thread_messages(tid) == 3 and await db.get_thread_messages(tid) == []
+        # auto-created thread on add_message
+        await db.add_message("auto-1", Message(role="user", content="x"))
+        assert await db.thread_exists("auto-1")
+        await db.close()
+    asyncio.run(go())
+
+
+def test_thread_config_join_playbooks_and_vm_key(db):
+    f = db.fake
+    f.tables["kafka_profiles"] = [{"id": "kp1", "user_id": "owner", "memory_dsn": "pg://m", "global_prompt": "GP"}]
+    f.tables["profiles"] = [{"id": "owner", "openai_pk_virtual_key": "vk-oa"}]
+    f.tables["playbooks"] = [{"id": "b", "kafka_profile_id": "kp1", "name": "N2", "description": "D2",
+                              "created_at": "2"},
+                             {"id": "a", "kafka_profile_id": "kp1", "name": "N1", "description": "D1",
+                              "created_at": "1"}]
+
+    async def go():
+        await db.create_thread(thread_id="t1", kafka_profile_id="kp1")
+        cfg = await db.get_thread_config("t1")
+        assert cfg["global_prompt"] == "GP" and cfg["memory_dsn"] == "pg://m"
+        assert cfg["openai_pk_virtual_key"] == "vk-oa" and cfg["virtual_keys"] == {"openai_pk_virtual_key": "vk-oa"}
+        assert [p["name"] for p in await db.get_playbooks_for_kafka_profile("kp1")] == ["N1", "N2"]
+        k1 = await db.get_or_create_vm_api_key("t1", "owner")
+        assert k1 == "vmk_from_rpc" and await db.get_or_create_vm_api_key("t1") == k1
+        assert (await db.get_thread_config("t1"))["vm_api_key"] == k1
+        await db.close()
+    asyncio.run(go())
