@@ -1,3 +1,4 @@
+#include <cstring>
 // Python bindings for the CDNA4 kernels. Host-side shape / dtype / device checks live here so that a malformed
 // call fails with a Python exception instead of launching a kernel on a shape it does not assume.
 #include <torch/extension.h>
@@ -39,6 +40,14 @@ hipError_t kafka_launch_grouped_gemm(const bf16* X, int64_t ldx, const bf16* W, 
                                      const float* perm_w, const int* expert_off, const int* tile_off, int e_lo,
                                      int e_n, int max_tiles, int gather, bf16* Y, int64_t ldy, float* out,
                                      int64_t ldo, hipStream_t st);
+hipError_t kafka_car_alloc(int64_t bytes, void** out);
+int64_t kafka_car_header_bytes();
+hipError_t kafka_car_ipc_handle(void* p, hipIpcMemHandle_t* h);
+hipError_t kafka_car_open(const hipIpcMemHandle_t* h, void** out);
+hipError_t kafka_car_close(void* p);
+hipError_t kafka_car_free(void* p);
+hipError_t kafka_launch_car_allreduce(char* const* bases, int nranks, int rank, int epoch, bf16* x, int64_t n8,
+                                      int64_t max_bytes, int nblocks, hipStream_t st);
 }  // extern "C"
 
 #define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
@@ -320,6 +329,44 @@ static void grouped_gemm(at::Tensor x, at::Tensor w, at::Tensor perm_tok, at::Te
                                       cur_stream()));
 }
 
+// ---- custom one-shot all-reduce (csrc/allreduce.hip): raw device allocations + IPC handles
+static int64_t car_alloc(int64_t bytes) {
+  void* p = nullptr;
+  CHECK_HIP(kafka_car_alloc(bytes, &p));
+  return reinterpret_cast<int64_t>(p);
+}
+static py::bytes car_ipc_handle(int64_t ptr) {
+  hipIpcMemHandle_t h;
+  CHECK_HIP(kafka_car_ipc_handle(reinterpret_cast<void*>(ptr), &h));
+  return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+static int64_t car_open(py::bytes handle) {
+  std::string s = handle;
+  TORCH_CHECK(s.size() == sizeof(hipIpcMemHandle_t), "car_open: bad handle size");
+  hipIpcMemHandle_t h;
+  memcpy(&h, s.data(), sizeof(h));
+  void* p = nullptr;
+  CHECK_HIP(kafka_car_open(&h, &p));
+  return reinterpret_cast<int64_t>(p);
+}
+static void car_close(int64_t ptr) { CHECK_HIP(kafka_car_close(reinterpret_cast<void*>(ptr))); }
+static void car_free(int64_t ptr) { CHECK_HIP(kafka_car_free(reinterpret_cast<void*>(ptr))); }
+static int64_t car_error(int64_t own) {
+  int v = 0;
+  CHECK_HIP(hipMemcpy(&v, reinterpret_cast<char*>(own) + 8 * 128 * 4, sizeof(int), hipMemcpyDeviceToHost));
+  return v;
+}
+static void car_all_reduce(at::Tensor x, std::vector<int64_t> bases, int64_t rank, int64_t epoch, int64_t max_bytes,
+                           int64_t nblocks) {
+  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 8 == 0, "car_all_reduce: contiguous bf16, numel % 8 == 0");
+  TORCH_CHECK(x.numel() * 2 <= max_bytes, "car_all_reduce: message larger than the registered buffer");
+  std::vector<char*> b(bases.size());
+  for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<char*>(bases[i]);
+  CHECK_HIP(kafka_launch_car_allreduce(b.data(), (int)b.size(), (int)rank, (int)epoch, bptr(x), x.numel() / 8,
+                                       max_bytes, (int)nblocks, cur_stream()));
+}
+
 PYBIND11_MODULE(_kafka_ops, m) {
   m.doc() = "kafka_llm_service_amd CDNA4 (gfx950) HIP kernels";
   m.def("rmsnorm", &rmsnorm);
@@ -335,5 +382,12 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("skinny_supported", &skinny_supported);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("moe_route", &moe_route);
+  m.def("car_alloc", &car_alloc);
+  m.def("car_ipc_handle", &car_ipc_handle);
+  m.def("car_open", &car_open);
+  m.def("car_close", &car_close);
+  m.def("car_free", &car_free);
+  m.def("car_error", &car_error);
+  m.def("car_all_reduce", &car_all_reduce);
   m.def("grouped_gemm", &grouped_gemm);
 }

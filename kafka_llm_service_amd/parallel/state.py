@@ -76,6 +76,11 @@ def init(tp: int = 1, backend: str | None = None, device: str | None = None) -> 
                 cpg = dist.new_group(ranks, backend="gloo") if backend != "gloo" else pg
                 if rank in ranks:
                     st.tp_group, st.cpu_group = pg, cpg
+            if backend == "nccl" and os.environ.get("KAFKA_CUSTOM_AR", "0") == "1":
+                from . import comm
+                from .custom_allreduce import CustomAllReduce
+
+                comm.register_custom(st.tp_group, CustomAllReduce(st.cpu_group, st.tp_rank, tp))
     _STATE = st
     return st
 
