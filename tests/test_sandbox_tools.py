@@ -124,3 +124,20 @@ def test_mcp_stdio_client_and_routing():
         assert out[0].delta == "hey" and out[-1].is_complete
         await tp.disconnect()
     asyncio.run(main())
+
+
+def test_daytona_sandbox_interface_offline():
+    """Daytona sandboxes are LocalSandboxes addressed by id; lifecycle calls need the SDK and say so."""
+    import asyncio
+
+    from kafka_llm_service_amd.sandbox.base import SandboxError
+    from kafka_llm_service_amd.sandbox.daytona import DaytonaSandbox
+
+    sb = DaytonaSandbox("abc123", "env")
+    assert sb.base_url == "https://8081-abc123.proxy.daytona.works" and sb.id == "abc123"
+    assert sb.health_url.endswith("/health") and sb.tool_run_url.endswith("/run")
+    try:
+        asyncio.run(DaytonaSandbox.create("snap"))
+        raise AssertionError("expected SandboxError")
+    except SandboxError as e:
+        assert "daytona_sdk" in str(e)
