@@ -82,6 +82,8 @@ class AsyncEngine:
                     self._deliver_error(rid, e)
             elif kind == "abort":
                 self.engine.abort(item[1])
+            elif kind == "pin":
+                self.engine.pin_prefix(item[1])
             try:
                 item = self._inbox.get_nowait()
             except queue.Empty:
@@ -140,6 +142,10 @@ class AsyncEngine:
 
     def abort(self, request_id: str) -> None:
         self._inbox.put(("abort", request_id))
+
+    def pin_prefix(self, token_ids: list[int]) -> None:
+        """Pin the cached pages of a hot shared prefix (applied on the driver thread, the single KV writer)."""
+        self._inbox.put(("pin", list(token_ids)))
 
     def health(self) -> dict:
         eng = self.engine

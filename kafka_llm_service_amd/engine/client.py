@@ -63,6 +63,9 @@ class InProcessClient:
     def abort(self, request_id: str) -> None:
         self.async_engine.abort(request_id)
 
+    def pin_prefix(self, token_ids: list[int]) -> None:
+        self.async_engine.pin_prefix(token_ids)
+
     def health(self) -> dict:
         return {"replicas": 1, "replica0": self.async_engine.health()}
 
@@ -115,6 +118,8 @@ def serve_pipe(eng, conn) -> None:
                     conn.send(("error", rid, str(e)))
             elif kind == "abort":
                 eng.abort(msg[1])
+            elif kind == "pin":
+                eng.pin_prefix(msg[1])
             elif kind == "health":
                 kv = eng.kv_stats()
                 conn.send(("health", {"running": eng.num_running, "waiting": eng.num_waiting,
@@ -342,6 +347,12 @@ class DPClient:
             s = self._streams.get(request_id)
         if s is not None:
             self._send_quiet(s[2], ("abort", request_id))
+
+    def pin_prefix(self, token_ids: list[int]) -> None:
+        """Every replica holds (and pins) its own copy of the shared system prefix."""
+        for r in range(self.n_replicas):
+            if self._alive[r]:
+                self._send_quiet(r, ("pin", list(token_ids)))
 
     def health(self) -> dict:
         for r in range(self.n_replicas):

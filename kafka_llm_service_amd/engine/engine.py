@@ -278,6 +278,22 @@ class LLMEngine:
             self.step()
         return [s.output_ids for s in seqs]
 
+    def pin_prefix(self, token_ids: list[int]) -> int:
+        """Hold the cached pages of ``token_ids`` (e.g. the shared Kafka system prompt + tool schemas) so LRU eviction
+        under KV pressure never drops them (SURVEY.md §2.8 "pinned hot prefix"). Returns the number of pinned tokens
+        (whole pages that are already in the prefix cache); ``unpin_prefix`` releases them."""
+        self.unpin_prefix()
+        sid = -(1 << 40)  # outside the id range of real sequences
+        n = self.kvm.add_sequence(sid, list(token_ids) + [0])  # + sentinel: a full last page can match too
+        self._pinned = sid
+        return n
+
+    def unpin_prefix(self) -> None:
+        sid = getattr(self, "_pinned", None)
+        if sid is not None and self.kvm.has_seq(sid):
+            self.kvm.free_sequence(sid)
+        self._pinned = None
+
     def kv_stats(self) -> dict:
         d = dict(self.kvm.stats())
         d["num_blocks"] = self.num_blocks

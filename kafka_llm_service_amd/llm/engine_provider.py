@@ -39,9 +39,32 @@ class EngineLLMProvider(LLMProvider):
         self.model_name = model_name
         self.ignore_eos = ignore_eos
         self._tool_start = self.template.tool_call_start_ids()
+        self._pin: list[int] | None = None
 
     def render(self, messages: list[Message], tools: list[dict] | None) -> list[int]:
         return self.template.render(messages, tools)
+
+    def _maybe_pin(self, messages: list[Message], tools: list[dict] | None) -> None:
+        """Pin the shared system prefix (system prompt + tool schemas, ~18k tokens for Kafka) in the engine's prefix
+        cache once it has been computed, so KV pressure from long threads never evicts it. With per-thread prompt
+        tails (profiles, playbooks) only the common part of all system prefixes seen so far stays pinned."""
+        if not messages or messages[0].role != "system" or not hasattr(self.client, "pin_prefix"):
+            return
+        ids = self.template.render(messages[:1], tools)
+        if self._pin is not None:
+            n = 0
+            for a, b in zip(self._pin, ids):
+                if a != b:
+                    break
+                n += 1
+            if n == len(self._pin):
+                return
+            ids = ids[:n]
+        if len(ids) < 256:  # nothing worth pinning in common
+            self._pin = ids
+            return
+        self._pin = ids
+        self.client.pin_prefix(ids)
 
     async def stream_completion(self, messages: list[Message], *, temperature: float | None = None,
                                 max_tokens: int | None = None, stop: list[str] | None = None,
@@ -122,6 +145,7 @@ class EngineLLMProvider(LLMProvider):
                                                    "function": {"arguments": c["function"]["arguments"]}}], id=cid)
         if finish == "abort":
             finish = "stop"
+        self._maybe_pin(messages, tools)
         yield StreamChunk(finish_reason="tool_calls" if calls else finish, id=cid, token_ids=all_ids,
                           usage=Usage(prompt_tokens=len(prompt), completion_tokens=n_out,
                                       total_tokens=len(prompt) + n_out, cached_tokens=cached))

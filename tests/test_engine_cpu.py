@@ -169,3 +169,18 @@ def test_async_scheduling_equals_sync(base_engine):
     async_out, st = run(True)
     assert async_out == sync_out
     assert st["planned_ahead"] > 0 and st["replans"] > 0
+
+
+def test_pinned_prefix_survives_eviction(base_engine):
+    eng = _engine(model=base_engine.model, num_kv_blocks=64)
+    prefix = list(range(3000, 3000 + 160))  # 10 full pages
+    eng.generate([prefix + [1, 2]], SamplingParams(temperature=0.0, max_tokens=2, ignore_eos=True))
+    assert eng.pin_prefix(prefix) == 160
+    eng.kvm.evict_all()
+    # a request far larger than the free pool forces eviction pressure; the pinned pages must stay cached
+    eng.generate([list(range(9000, 9000 + 700))], SamplingParams(temperature=0.0, max_tokens=2, ignore_eos=True))
+    s = eng.add_request("after", prefix + [7], SamplingParams(temperature=0.0, max_tokens=1, ignore_eos=True))
+    eng.step()
+    assert s.num_cached == 160
+    eng.unpin_prefix()
+    eng.kvm.check_invariants()
