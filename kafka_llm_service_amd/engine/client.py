@@ -26,20 +26,33 @@ log = logging.getLogger("kafka.engine")
 HEARTBEAT_S = 1.0
 
 
-def route(key: str | None, n: int, loads: list[int], alive: list[bool] | None = None) -> int:
+SPILL_FACTOR = float(os.environ.get("KAFKA_DP_SPILL_FACTOR", "2.0"))
+SPILL_MIN = int(os.environ.get("KAFKA_DP_SPILL_MIN", "48"))
+
+
+def route(key: str | None, n: int, loads: list[int], alive: list[bool] | None = None,
+          spill_factor: float = SPILL_FACTOR, spill_min: int = SPILL_MIN) -> int:
     """Replica for a request: the thread's home replica (stable hash of the thread id, so its KV prefix is reused);
     if that one is down, the next live replica in hash order; keyless requests go to the least-loaded live replica.
-    Returns -1 when no replica is up."""
+    Load-aware spill: when the home replica carries >= ``spill_min`` active requests AND more than ``spill_factor``
+    x the mean live load, the request goes to the least-loaded live replica instead (a hot spot of threads costs one
+    history re-prefill there — the shared system prefix is cached on every replica). Returns -1 when none is up."""
     live = [i for i in range(n) if alive is None or alive[i]]
     if not live:
         return -1
+    least = min(live, key=lambda i: loads[i])
     if key is None:
-        return min(live, key=lambda i: loads[i])
+        return least
     h = int(hashlib.blake2b(key.encode(), digest_size=8).hexdigest(), 16) % n
+    home = -1
     for j in range(n):
         if alive is None or alive[(h + j) % n]:
-            return (h + j) % n
-    return -1
+            home = (h + j) % n
+            break
+    mean = sum(loads[i] for i in live) / len(live)
+    if loads[home] >= spill_min and loads[home] > spill_factor * (mean + 1):
+        return least
+    return home
 
 
 class InProcessClient:

@@ -155,3 +155,19 @@ def test_sandbox_down_gives_error_tool_result():
         await sb.close()
     asyncio.run(go())
     assert os.environ.get("KAFKA_FI_SANDBOX_DOWN") is None
+
+
+def test_route_affinity_and_load_spill():
+    from kafka_llm_service_amd.engine.client import route
+
+    keys = [f"thread-{i}" for i in range(400)]
+    homes = [route(k, 4, [0] * 4) for k in keys]
+    assert homes == [route(k, 4, [0] * 4) for k in keys]            # stable
+    assert all(homes.count(r) > 60 for r in range(4))                # spread over replicas
+    k = keys[0]
+    h = homes[0]
+    loads = [0] * 4
+    loads[h] = 100
+    assert route(k, 4, loads, spill_min=48, spill_factor=2.0) != h   # hot spot spills to the least loaded
+    loads = [30, 30, 30, 30]
+    assert route(k, 4, loads, spill_min=48) == h                     # balanced: stay home
