@@ -84,8 +84,25 @@ async def _turn(client, url, tid, i, args, res):
     res["requests"] += 1
 
 
+_SYS_WORDS = ("tool shell notebook thread agent planner sandbox weather stream token cache prefix kernel wave "
+              "matrix memory schedule request reply history playbook profile idle summary context").split()
+
+
+def _system_message(chars: int) -> str | None:
+    """A deterministic synthetic system prompt of ~``chars`` characters, identical for every thread (the reference's
+    rendered Kafka prompt is ~70k characters; a thread created with a system message carries it as its prefix)."""
+    if chars <= 0:
+        return None
+    out, i = [], 0
+    while sum(len(w) + 1 for w in out) < chars:
+        out.append(_SYS_WORDS[(i * 7 + i // 13) % len(_SYS_WORDS)])
+        i += 1
+    return " ".join(out)
+
+
 async def _thread(client, url, k, args, res):
-    r = await client.post(f"{url}/v1/threads", json={})
+    body = {"system_message": _system_message(args.system_chars)} if args.system_chars > 0 else {}
+    r = await client.post(f"{url}/v1/threads", json=body)
     tid = r.json()["thread_id"]
     for i in range(args.turns):
         await _turn(client, url, tid, i, args, res)
@@ -155,7 +172,7 @@ def run(url, args):
     return {
         "metric": "serve: p50 TTFT + output tok/s, /v1/threads/{id}/chat/completions",
         "backend": args.backend, "model": args.model, "threads": args.threads, "turns": args.turns,
-        "stream": not args.no_stream, "client_procs": P, "requests": res["requests"], "wall_s": round(wall, 3),
+        "stream": not args.no_stream, "client_procs": P, "system_chars": args.system_chars, "requests": res["requests"], "wall_s": round(wall, 3),
         "client_cpu_s": round(res["client_cpu"], 3),
         "ttft_p50_ms": ms(_pct(res["ttft"], 0.5)), "ttft_p99_ms": ms(_pct(res["ttft"], 0.99)),
         "e2e_p50_ms": ms(_pct(res["e2e"], 0.5)), "e2e_p99_ms": ms(_pct(res["e2e"], 0.99)),
@@ -180,6 +197,9 @@ def main():
     ap.add_argument("--user-words", type=int, default=8)
     ap.add_argument("--no-stream", action="store_true")
     ap.add_argument("--procs", type=int, default=4, help="load-generator processes")
+    ap.add_argument("--system-chars", type=int, default=0,
+                    help="create threads with a shared synthetic system message of this many characters "
+                         "(70000 ~ the reference's rendered Kafka prompt) instead of the server's Kafka prompt")
     ap.add_argument("--ignore-eos", action="store_true", default=True)
     args = ap.parse_args()
     proc = None

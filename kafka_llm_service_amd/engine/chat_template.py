@@ -17,6 +17,7 @@ Llama-3.1 layout:
 from __future__ import annotations
 
 import json
+from collections import OrderedDict
 import uuid
 from typing import Any
 
@@ -38,6 +39,20 @@ class ChatTemplate:
     def __init__(self, tok: KafkaTokenizer):
         self.tok = tok
         self.llama = tok.family == "llama3"
+        self._enc_cache: OrderedDict[str, list[int]] = OrderedDict()
+
+    def _encode_cached(self, text: str) -> list[int]:
+        """BPE of the (system prompt + tool schemas) block, memoised: it is the same ~70k characters for every request
+        of every thread, and re-encoding it would cost the API loop milliseconds per request."""
+        ids = self._enc_cache.get(text)
+        if ids is None:
+            ids = self.tok.encode(text)
+            self._enc_cache[text] = ids
+            if len(self._enc_cache) > 64:
+                self._enc_cache.popitem(last=False)
+        else:
+            self._enc_cache.move_to_end(text)
+        return ids
 
     # --- llama 3 ----------------------------------------------------------------------------------------------
     def _hdr(self, role: str) -> list[int]:
@@ -97,7 +112,7 @@ class ChatTemplate:
             block = _tools_block(tools)
             if system or block:
                 text = system + ("\n\n" + block if system and block else block)
-                ids += self._hdr("system") + t.encode(text) + [self._eot()]
+                ids += self._hdr("system") + self._encode_cached(text) + [self._eot()]
             for m in msgs:
                 ids += self.render_message(m)
             if add_generation_prompt:
@@ -105,7 +120,8 @@ class ChatTemplate:
             return ids
         block = _tools_block(tools)
         if block:
-            ids += [t.special_id("[AVAILABLE_TOOLS]")] + t.encode(block) + [t.special_id("[/AVAILABLE_TOOLS]")]
+            ids += [t.special_id("[AVAILABLE_TOOLS]")] + self._encode_cached(block) + \
+                [t.special_id("[/AVAILABLE_TOOLS]")]
         for m in msgs:
             ids += self.render_message(m)
         return ids
