@@ -20,6 +20,7 @@ Reported (one JSON line): p50/p99 TTFT (first content frame, stream), p50/p99 en
 from __future__ import annotations
 
 import argparse
+import functools
 import asyncio
 import json
 import os
@@ -88,14 +89,17 @@ _SYS_WORDS = ("tool shell notebook thread agent planner sandbox weather stream t
               "matrix memory schedule request reply history playbook profile idle summary context").split()
 
 
+@functools.lru_cache(maxsize=4)
 def _system_message(chars: int) -> str | None:
     """A deterministic synthetic system prompt of ~``chars`` characters, identical for every thread (the reference's
     rendered Kafka prompt is ~70k characters; a thread created with a system message carries it as its prefix)."""
     if chars <= 0:
         return None
-    out, i = [], 0
-    while sum(len(w) + 1 for w in out) < chars:
-        out.append(_SYS_WORDS[(i * 7 + i // 13) % len(_SYS_WORDS)])
+    out, i, n = [], 0, 0
+    while n < chars:
+        w = _SYS_WORDS[(i * 7 + i // 13) % len(_SYS_WORDS)]
+        out.append(w)
+        n += len(w) + 1
         i += 1
     return " ".join(out)
 
