@@ -1,0 +1,72 @@
+"""Property tests of the engine loop (SURVEY.md §4.4 "scheduler policies", §5.2 "allocator invariants"): random
+arrivals, aborts, lengths and a small KV pool — after every step the KV bookkeeping is consistent, every request
+ends (finished or aborted), nothing leaks, and greedy outputs do not depend on batching / preemption / plan-ahead."""
+import random
+
+from hypothesis import HealthCheck, given, settings, strategies as st
+
+from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
+from kafka_llm_service_amd.engine.sequence import SamplingParams
+
+_MODEL = {}
+
+
+def _model():
+    if "m" not in _MODEL:
+        _MODEL["m"] = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", num_kv_blocks=64,
+                                             max_model_len=1024)).model
+    return _MODEL["m"]
+
+
+@settings(max_examples=12, deadline=None, suppress_health_check=list(HealthCheck))
+@given(seed=st.integers(0, 10_000), blocks=st.sampled_from([14, 24, 64]), async_on=st.booleans(),
+       chunk=st.sampled_from([16, 64, 4096]))
+def test_random_workload_invariants(seed, blocks, async_on, chunk):
+    rng = random.Random(seed)
+    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", num_kv_blocks=blocks, max_model_len=1024,
+                                 async_scheduling=async_on, max_prefill_chunk=chunk, max_num_batched_tokens=128),
+                    model=_model())
+    shared = [rng.randrange(1000, 5000) for _ in range(rng.choice([0, 16, 40]))]
+    reqs = {}
+    next_id = 0
+    for _ in range(60):
+        r = rng.random()
+        if r < 0.35 and len(reqs) < 6:
+            n = rng.randrange(1, 60)
+            sp = SamplingParams(temperature=rng.choice([0.0, 0.8]), max_tokens=rng.randrange(1, 12),
+                                ignore_eos=True, seed=rng.randrange(100))
+            rid = f"q{next_id}"
+            next_id += 1
+            reqs[rid] = eng.add_request(rid, shared + [rng.randrange(1000, 5000) for _ in range(n)], sp)
+        elif r < 0.42 and reqs:
+            eng.abort(rng.choice(list(reqs)))
+        eng.step()
+        eng.kvm.check_invariants()
+        for rid in [k for k, s in reqs.items() if s.finished]:
+            s = reqs.pop(rid)
+            assert s.finish_reason in ("length", "abort", "stop")
+            if s.finish_reason == "length":
+                assert len(s.output_ids) == s.params.max_tokens and -1 not in s.output_ids
+    for rid in list(reqs):
+        eng.abort(rid)
+    for _ in range(3):
+        eng.step()
+    eng.kvm.check_invariants()
+    st_ = eng.kv_stats()
+    assert st_["free"] + st_["evictable"] == blocks  # every page is free or an unreferenced cached page
+
+
+@settings(max_examples=6, deadline=None, suppress_health_check=list(HealthCheck))
+@given(seed=st.integers(0, 10_000))
+def test_greedy_outputs_independent_of_batching(seed):
+    rng = random.Random(seed)
+    prompts = [[rng.randrange(1000, 5000) for _ in range(rng.randrange(2, 50))] for _ in range(4)]
+    lens = [rng.randrange(1, 8) for _ in prompts]
+
+    def run(**kw):
+        eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_model_len=1024, **kw), model=_model())
+        return eng.generate(prompts, [SamplingParams(temperature=0.0, max_tokens=n, ignore_eos=True) for n in lens])
+
+    base = run(num_kv_blocks=256)
+    assert run(num_kv_blocks=14, max_prefill_chunk=16, max_num_batched_tokens=32) == base
+    assert run(num_kv_blocks=256, async_scheduling=False, enable_prefix_cache=False) == base
