@@ -126,6 +126,10 @@ class LLMEngine:
         self.runner = ModelRunner(self.model, kc, vc, self.kvm, cfg.max_num_seqs, max_blocks,
                                   cascade_min_prefix=cfg.cascade_min_prefix, use_cascade=cfg.use_cascade,
                                   target_wgs=cfg.target_wgs, prefill_kv_chunk=cfg.prefill_kv_chunk)
+        if cfg.use_graphs and cfg.tp == 1:
+            from kafka_llm_service_amd.engine.graphs import DecodeGraphs
+
+            self.runner.graphs = DecodeGraphs(self.runner)
         self.requests: dict[str, Sequence] = {}
         self.stats = {"steps": 0, "prompt_tokens": 0, "cached_tokens": 0, "output_tokens": 0, "step_time": 0.0,
                       "replans": 0, "planned_ahead": 0}

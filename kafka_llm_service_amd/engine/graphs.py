@@ -1,0 +1,139 @@
+"""hipGraph decode runner (SURVEY.md §2.8 "hipGraph decode runner: capture decode steps per batch-size bucket with
+static buffers", §7.4 #7 "hipGraph + dynamic paged metadata").
+
+A decode-only step (B running threads, one token each) launches ~11 kernels per layer — 364 for Llama-3-8B — from
+Python. Captured once per LAYOUT as a hipGraph, the whole step (embedding, 32 layers of GEMMs / norms / RoPE+KV
+write / cascade + split-K paged attention / merge, final norm, lm_head, sampler) becomes one ``replay``: the CPU
+cost drops from ~2 ms to ~20 us, which is what lets the host keep up with short decode steps (small batches, TP
+shards) and leaves the CPU free for the API loop.
+
+Layout key: (B, decode split-K factor, cascade prefix chunks, prefix work items, cascade on/off, packed-buffer sizes,
+greedy). Everything that changes from step to step — token ids, positions, KV slots, block tables, sequence lengths,
+cascade work items, sampling parameters and seeds — lives in STATIC device buffers that are refreshed (one async
+H2D each) before the replay; intermediates (activations, attention partials, logits) come from a graph memory pool
+shared by all captured layouts. Steps with prefill rows or host-side logits processing (penalties, tool grammars)
+run eagerly. Tensor parallelism keeps the eager path (the followers replay from the leader's broadcast plan).
+
+``backend="fake"`` re-runs the captured closure instead of a device graph: on CPU it checks the property a graph
+relies on — a replay reads ONLY the static buffers (tests/test_graphs.py).
+"""
+from __future__ import annotations
+
+import copy
+import logging
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from kafka_llm_service_amd import ops
+
+log = logging.getLogger("kafka.graphs")
+
+
+class _FakeGraph:
+    """Graph stand-in: 'capture' runs the closure once, 'replay' runs it again."""
+
+    def __init__(self, fn):
+        self.fn = fn
+        fn()
+
+    def replay(self) -> None:
+        self.fn()
+
+
+class _Entry:
+    __slots__ = ("graph", "s64", "s32", "f32", "topk", "seeds", "out", "layout")
+
+
+class DecodeGraphs:
+    def __init__(self, runner, max_graphs: int = 8, backend: str | None = None):
+        self.runner = runner
+        self.max_graphs = max_graphs
+        self.backend = backend or ("cuda" if runner.device.type == "cuda" else "fake")
+        self.graphs: OrderedDict[tuple, _Entry] = OrderedDict()
+        self.pool = torch.cuda.graph_pool_handle() if self.backend == "cuda" else None
+        self.disabled = False
+        self.stats = {"captures": 0, "replays": 0}
+
+    @staticmethod
+    def key(h, sp) -> tuple:
+        return (h.B, h.splits, h.prefix_splits, h.n_prefix_items, bool(h.cascade_prefix), h.i64.size, h.i32.size,
+                sp.greedy)
+
+    def eligible(self, h, sp) -> bool:
+        return (not self.disabled and h.B > 0 and h.T == h.B and h.n_items == 0 and not sp.procs
+                and self.runner.broadcast is None)
+
+    # ------------------------------------------------------------------------------------------------------------
+    def run(self, h, sp) -> torch.Tensor | None:
+        k = self.key(h, sp)
+        e = self.graphs.get(k)
+        if e is None:
+            try:
+                e = self._capture(k, h, sp)
+            except Exception:  # never let capture problems take the engine down: stay eager from here on
+                log.exception("hipGraph capture failed; decode steps run eagerly")
+                self.disabled = True
+                return None
+            return e.out  # the capture run computed this step
+        self.graphs.move_to_end(k)
+        self._load(e, h, sp)
+        e.graph.replay()
+        self.stats["replays"] += 1
+        return e.out
+
+    def _load(self, e: _Entry, h, sp) -> None:
+        r = self.runner
+        e.s64.copy_(r._host(h.i64), non_blocking=True)
+        e.s32.copy_(r._host(h.i32), non_blocking=True)
+        if not sp.greedy:
+            e.f32.copy_(r._host(np.concatenate([sp.temp, sp.topp])), non_blocking=True)
+            e.topk.copy_(r._host(sp.topk), non_blocking=True)
+            e.seeds.copy_(r._host(sp.seeds), non_blocking=True)
+
+    def _capture(self, k: tuple, h, sp) -> _Entry:
+        r = self.runner
+        dev = r.device
+        n = h.n_rows
+        e = _Entry()
+        e.s64 = torch.empty(h.i64.size, dtype=torch.int64, device=dev)
+        e.s32 = torch.empty(h.i32.size, dtype=torch.int32, device=dev)
+        e.f32 = torch.empty(2 * n, dtype=torch.float32, device=dev)
+        e.topk = torch.empty(n, dtype=torch.int32, device=dev)
+        e.seeds = torch.empty(n, dtype=torch.int64, device=dev)
+        e.out = torch.empty(n, dtype=torch.int64, device=dev)
+        e.layout = copy.copy(h)
+        e.layout.i64 = e.layout.i32 = None
+        e.layout.patch = []
+        greedy = sp.greedy
+
+        def step():
+            inp = r.views(e.s64, e.s32, e.layout)
+            logits = r.model.forward(inp, r.k_caches, r.v_caches)
+            if greedy:
+                toks = ops.sample(logits, torch.zeros(n, device=dev))
+            else:
+                toks = ops.sample(logits, e.f32[:n], e.f32[n:], e.topk, e.seeds)
+            e.out.copy_(toks)
+
+        self._load(e, h, sp)
+        if self.backend == "fake":
+            e.graph = _FakeGraph(step)
+        else:
+            # warm up on a side stream (library workspaces, lazy inits): this run computes THIS step (tokens and
+            # its KV writes); the capture pass that follows records the kernels without executing them
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                step()
+            torch.cuda.current_stream().wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool):
+                step()
+            e.graph = g
+        self.graphs[k] = e
+        self.stats["captures"] += 1
+        while len(self.graphs) > self.max_graphs:
+            self.graphs.popitem(last=False)
+        return e

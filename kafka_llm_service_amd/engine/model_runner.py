@@ -47,6 +47,16 @@ class HostStep:
 
 
 @dataclass
+class SampleParams:
+    temp: np.ndarray
+    topp: np.ndarray
+    topk: np.ndarray
+    seeds: np.ndarray
+    procs: list          # rows that need host-side logits processing (penalties / token constraints)
+    greedy: bool
+
+
+@dataclass
 class Launched:
     tokens: torch.Tensor            # sampled ids (pinned host buffer on GPU, plain tensor on CPU)
     event: object = None            # completion event of the D2H copy
@@ -84,6 +94,7 @@ class ModelRunner:
         self.last_stats: dict = {}
         self.broadcast = None  # set on a TP leader: callable(HostStep) (engine/tp_worker.py)
         self._tok_host = None  # pinned landing buffer of the sampled ids
+        self.graphs = None  # engine/graphs.py DecodeGraphs when hipGraph decode is enabled
 
     # ------------------------------------------------------------------------------------------------------------
     def prepare(self, batch: ScheduledBatch) -> tuple[StepInput, list[Sequence]]:
@@ -189,9 +200,12 @@ class ModelRunner:
 
     def to_device(self, h: HostStep) -> StepInput:
         """One H2D copy per packed buffer, then views into it (identical on every TP rank)."""
+        return self.views(self._h2d(h.i64), self._h2d(h.i32), h)
+
+    def views(self, d64: torch.Tensor, d32: torch.Tensor, h: HostStep) -> StepInput:
+        """StepInput over packed device buffers laid out as ``h`` describes (only h's scalars are read, so a hipGraph
+        captured over static buffers replays with any step of the same layout)."""
         B, T, nbt = h.B, h.T, h.nbt
-        d64 = self._h2d(h.i64)
-        d32 = self._h2d(h.i32)
         t_tokens, t_pos, t_slots = d64[0:T], d64[T:2 * T], d64[2 * T:3 * T]
         t_rows = d64[3 * T:3 * T + h.n_rows]
         meta = AttnMeta(num_decode=B, num_tokens=T, scale=self.model.scale)
@@ -227,6 +241,11 @@ class ModelRunner:
                                               device=self.device)
         return StepInput(t_tokens, t_pos, t_slots, meta, t_rows)
 
+    def _host(self, a: np.ndarray) -> torch.Tensor:
+        """Host tensor of ``a`` for an async copy into a device buffer (pinned on GPU hosts)."""
+        t = torch.from_numpy(a)
+        return t.pin_memory() if self.device.type == "cuda" else t
+
     def _h2d(self, a: np.ndarray) -> torch.Tensor:
         t = torch.from_numpy(a)
         if self.device.type == "cuda":
@@ -235,6 +254,9 @@ class ModelRunner:
 
     # ------------------------------------------------------------------------------------------------------------
     def sample(self, logits: torch.Tensor, seqs: list[Sequence]) -> torch.Tensor:
+        return self.sample_device(logits, self.sample_params(seqs))
+
+    def sample_params(self, seqs: list[Sequence]) -> "SampleParams":
         n = len(seqs)
         temp = np.empty(n, dtype=np.float32)
         topp = np.empty(n, dtype=np.float32)
@@ -251,15 +273,18 @@ class ModelRunner:
             allowed = p.allowed_tokens_fn(s.output_ids) if p.allowed_tokens_fn is not None else None
             if allowed is not None or p.presence_penalty or p.frequency_penalty:
                 procs.append((i, s, allowed))
-        if procs:
-            logits = self._process_logits(logits, procs)
-        all_greedy = not temp.any()
+        return SampleParams(temp, topp, topk, seeds, procs, not temp.any())
+
+    def sample_device(self, logits: torch.Tensor, sp: "SampleParams") -> torch.Tensor:
+        if sp.procs:
+            logits = self._process_logits(logits, sp.procs)
+        n = logits.shape[0]
         dev = logits.device
-        if all_greedy:
+        if sp.greedy:
             return ops.sample(logits, torch.zeros(n, device=dev))
-        f32 = torch.from_numpy(np.concatenate([temp, topp])).to(dev, non_blocking=True)
-        return ops.sample(logits, f32[:n], f32[n:], torch.from_numpy(topk).to(dev, non_blocking=True),
-                          torch.from_numpy(seeds).to(dev, non_blocking=True))
+        f32 = torch.from_numpy(np.concatenate([sp.temp, sp.topp])).to(dev, non_blocking=True)
+        return ops.sample(logits, f32[:n], f32[n:], torch.from_numpy(sp.topk).to(dev, non_blocking=True),
+                          torch.from_numpy(sp.seeds).to(dev, non_blocking=True))
 
     def _mask_tensor(self, m) -> torch.Tensor:
         """Device copy of a constrained.Mask's base vocab mask (cached by key) with its extra ids allowed."""
@@ -310,9 +335,14 @@ class ModelRunner:
         self.last_stats = host.stats
         if self.broadcast is not None:  # TP leader: followers run the same step on their shards
             self.broadcast(host)
-        inp = self.to_device(host)
-        logits = self.model.forward(inp, self.k_caches, self.v_caches)
-        toks = self.sample(logits, sample_seqs)
+        sp = self.sample_params(sample_seqs)
+        toks = None
+        if self.graphs is not None and self.graphs.eligible(host, sp):
+            toks = self.graphs.run(host, sp)
+        if toks is None:
+            inp = self.to_device(host)
+            logits = self.model.forward(inp, self.k_caches, self.v_caches)
+            toks = self.sample_device(logits, sp)
         if self.device.type != "cuda":
             return Launched(toks, None)
         n = toks.shape[0]
