@@ -75,15 +75,15 @@ def test_tp2_generate_matches_tp1():
 def _capture_logits(eng, prompt):
     """Run one prefill step through the engine and return the logits the sampler saw."""
     seen = []
-    orig = eng.runner.sample
+    orig = eng.runner.sample_device
 
-    def sample(logits, seqs):
+    def sample_device(logits, sp):
         seen.append(logits.float().clone())
-        return orig(logits, seqs)
+        return orig(logits, sp)
 
-    eng.runner.sample = sample
+    eng.runner.sample_device = sample_device
     eng.generate([prompt], SamplingParams(temperature=0.0, max_tokens=2, ignore_eos=True))
-    eng.runner.sample = orig
+    eng.runner.sample_device = orig
     return torch.cat(seen)
 
 
