@@ -64,3 +64,19 @@ def test_mixtral_engine_matches_oracle(cuda):
     prompts = _prompts(3, 64, (5, 40, 130))
     outs = e.generate(prompts, GREEDY)
     _oracle_ok(e.model, prompts, outs)
+
+
+def test_hipgraph_decode_matches_eager(eng):
+    """Decode steps replayed from hipGraphs (engine/graphs.py) == eager steps (greedy and seeded sampling)."""
+    prompts = _prompts(4, 300, (3, 40, 77))
+    sps = [SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True),
+           SamplingParams(temperature=0.8, top_p=0.9, max_tokens=10, ignore_eos=True, seed=5),
+           SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)]
+    eager = eng.generate(prompts, sps)
+    g = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", num_kv_blocks=4096, max_model_len=8192,
+                               cascade_min_prefix=64, prefill_kv_chunk=256, use_graphs=True), model=eng.model)
+    graphed = g.generate(prompts, sps)
+    st = g.runner.graphs.stats
+    assert not g.runner.graphs.disabled, "hipGraph capture failed (see log)"
+    assert st["captures"] >= 1 and st["replays"] >= 1
+    assert graphed == eager
