@@ -5,7 +5,7 @@ Builds an engine client (in-process, one GPU — or CPU with the tiny test model
 LLMProvider and runs a KafkaV1Provider agent with the weather and counter tools, printing the live event stream.
 Random-init weights never choose a tool on their own, so ``--tool-choice required`` forces a (schema-valid) call.
 
-  python examples/agent.py --model tiny-llama --device cpu --tool-choice required
+  python examples/agent.py --model tiny-llama --device cpu --tool-choice required --prompt-sections intro,core_tools
   python examples/agent.py --model llama3-8b                       # GPU 0, random-init Llama-3-8B
 """
 from __future__ import annotations
@@ -35,7 +35,9 @@ async def main(args) -> int:
     tc = json.loads(args.tool_choice) if args.tool_choice.startswith("{") else args.tool_choice
     llm = EngineLLMProvider(client, default_max_tokens=args.max_tokens, model_name=args.model, tool_choice=tc,
                             ignore_eos=True)
-    agent = KafkaV1Provider(llm, tools=[get_weather_tool, count_tool], max_iterations=args.max_iterations)
+    sections = [x for x in args.prompt_sections.split(",") if x] or None
+    agent = KafkaV1Provider(llm, tools=[get_weather_tool, count_tool], max_iterations=args.max_iterations,
+                            prompt_sections=sections)
     await agent.initialize()
     print(f"user: {args.prompt}\nagent:")
     n_tool = 0
@@ -73,4 +75,5 @@ if __name__ == "__main__":
     ap.add_argument("--temperature", type=float, default=0.7)
     ap.add_argument("--max-tokens", type=int, default=48)
     ap.add_argument("--max-iterations", type=int, default=3)
+    ap.add_argument("--prompt-sections", default="", help="comma-separated subset of the Kafka prompt sections")
     sys.exit(asyncio.run(main(ap.parse_args())))

@@ -41,6 +41,8 @@ class ServerConfig:
     # default tool_choice of engine-backed generations ("auto" | "required" | "none" | a JSON function object);
     # "required" makes random-init models drive the agent/tool loop with well-formed calls (BASELINE config 4)
     tool_choice: Any = "auto"
+    # subset of the Kafka v1 prompt sections (None = all 13, ~47k characters); small engines / CPU tests use a few
+    prompt_sections: list[str] | None = None
     ignore_eos: bool = False  # benchmarks: generate exactly max_tokens (random-init weights emit EOS at random)
     engine_kwargs: dict[str, Any] = field(default_factory=dict)
 
@@ -58,7 +60,8 @@ class ServerConfig:
                             max_model_len=int(e.get("KAFKA_MAX_MODEL_LEN", "131072")),
                             default_max_tokens=int(e.get("KAFKA_DEFAULT_MAX_TOKENS", "1024")),
                             tool_choice=_tool_choice(e.get("KAFKA_TOOL_CHOICE", "auto")),
-                            ignore_eos=e.get("KAFKA_IGNORE_EOS", "0") == "1")
+                            ignore_eos=e.get("KAFKA_IGNORE_EOS", "0") == "1",
+                            prompt_sections=[x for x in e.get("KAFKA_PROMPT_SECTIONS", "").split(",") if x] or None)
 
 
 def _tool_choice(v: str) -> Any:
@@ -110,7 +113,8 @@ class ServerState:
             self.sandbox_manager = SandboxManager(self.db, self.provisioner, warm)
         tools = [get_weather_tool, count_tool] + PlannerTools(None).tools
         self.kafka = KafkaV1Provider(self.llm, tools=tools, sandbox_tools=sandbox_tools,
-                                     mcp_servers=DEFAULT_MCP_SERVERS if cfg.mcp else [])
+                                     mcp_servers=DEFAULT_MCP_SERVERS if cfg.mcp else [],
+                                     prompt_sections=cfg.prompt_sections)
         await self.kafka.initialize()
         self.ready = True
         log.info("server ready (backend=%s model=%s)", cfg.backend, cfg.model)
@@ -186,7 +190,7 @@ class ServerState:
             sandbox_tools = ShellTools(sb).tools + NotebookTools(sb).tools
         agent = KafkaV1Provider(self.llm, thread_id=thread_id, db_client=self.db,
                                 tools=[get_weather_tool, count_tool] + PlannerTools(thread_id).tools,
-                                sandbox_tools=sandbox_tools)
+                                sandbox_tools=sandbox_tools, prompt_sections=self.config.prompt_sections)
         await agent.initialize()
         try:
             async for ev in agent.run_with_thread(messages, model=model, temperature=temperature,

@@ -150,8 +150,8 @@ def test_thread_agent_run_persists(tmp_path):
 # ---------------------------------------------------------------------------------------------------------------
 @pytest.fixture(scope="module")
 def engine_client():
-    st = ServerState(ServerConfig(backend="engine", model="tiny-llama", sandbox="none", max_model_len=4096,
-                                  default_max_tokens=12,
+    st = ServerState(ServerConfig(backend="engine", model="tiny-llama", sandbox="none", max_model_len=8192,
+                                  default_max_tokens=12, prompt_sections=["intro", "core_principles", "core_tools"],
                                   engine_kwargs={"device": "cpu", "num_kv_blocks": 1024}),
                      db=MemoryDBClient())
     with TestClient(create_app(state=st)) as c:
@@ -178,7 +178,7 @@ def test_engine_streaming_and_prefix_reuse(engine_client):
 
 def test_engine_context_length_error(engine_client):
     c, _ = engine_client
-    body = {"model": "tiny-llama", "messages": [{"role": "user", "content": "word " * 5000}], "stream": True,
+    body = {"model": "tiny-llama", "messages": [{"role": "user", "content": "word " * 9000}], "stream": True,
             "max_tokens": 4}
     f = frames(c.post("/v1/chat/completions", json=body).text)
     err = [x for x in f if isinstance(x, dict) and "error" in x]

@@ -101,6 +101,7 @@ def test_agent_loop_with_forced_idle_call():
 
     cfg = ServerConfig(backend="engine", model="tiny-llama", sandbox="none", max_model_len=32768,
                        default_max_tokens=64, tool_choice={"type": "function", "function": {"name": "idle"}},
+                       prompt_sections=["intro", "core_tools"],
                        engine_kwargs={"device": "cpu", "num_kv_blocks": 4096})
     st = ServerState(cfg, db=MemoryDBClient())
     with TestClient(create_app(state=st)) as c:

@@ -14,7 +14,7 @@ ROOT = Path(__file__).resolve().parents[1]
 @pytest.mark.timeout(600)
 def test_agent_example_forced_tool_call():
     out = subprocess.run([sys.executable, str(ROOT / "examples/agent.py"), "--model", "tiny-llama", "--device", "cpu",
-                          "--max-iterations", "2", "--tool-choice",
+                          "--max-iterations", "2", "--prompt-sections", "intro,core_tools", "--tool-choice",
                           '{"type":"function","function":{"name":"get_weather"}}'],
                          capture_output=True, text=True, timeout=600, env=dict(os.environ, KAFKA_WEATHER_MODE="offline"))
     assert out.returncode == 0, out.stderr[-2000:]
