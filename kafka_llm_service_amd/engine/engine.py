@@ -148,6 +148,11 @@ class LLMEngine:
         if len(prompt_ids) + 1 > self.cfg.max_model_len:
             raise ValueError(f"This model's maximum context length is {self.cfg.max_model_len} tokens. However, "
                              f"your messages resulted in {len(prompt_ids)} tokens.")
+        pool_tokens = self.num_blocks * 16
+        if len(prompt_ids) + 1 > pool_tokens:
+            # a sequence that can never fit the KV pool would stall the scheduler; refuse it like an over-long prompt
+            raise ValueError(f"This model's maximum context length is {pool_tokens} tokens on this replica (KV "
+                             f"pool). However, your messages resulted in {len(prompt_ids)} tokens.")
         if params.tool_grammar is not None and params.allowed_tokens_fn is None:
             from kafka_llm_service_amd.engine.constrained import ToolCallConstraint
             from kafka_llm_service_amd.engine.tokenizer import tokenizer_for_model
@@ -199,8 +204,9 @@ class LLMEngine:
         if plan is None:
             with trace.span("schedule"):
                 batch = self.sched.schedule()
+                cut = self._cut_outputs(batch)
                 if batch.empty:
-                    return []
+                    return cut
                 host, sampled = self.runner.build_host(batch)
         else:
             batch, host, sampled = plan.batch, plan.host, plan.sampled
@@ -228,7 +234,7 @@ class LLMEngine:
         now = time.perf_counter()
         self.stats["step_time"] += now - t0
         self.stats["steps"] += 1
-        outs: list[StepOutput] = []
+        outs: list[StepOutput] = [] if plan is not None else cut
         for s, t in zip(sampled, toks):
             s.output_ids[-1] = t
             self.kvm.append_token(s.seq_id, t)
@@ -245,6 +251,14 @@ class LLMEngine:
                 trace.request_span(s, now)
             outs.append(StepOutput(s.request_id, [t], reason is not None, reason, len(s.prompt_ids),
                                    len(s.output_ids), s.num_cached))
+        return outs
+
+    def _cut_outputs(self, batch) -> list[StepOutput]:
+        outs = []
+        for s in batch.cut:
+            self.requests.pop(s.request_id, None)
+            outs.append(StepOutput(s.request_id, [], True, "length", len(s.prompt_ids), len(s.output_ids),
+                                   s.num_cached))
         return outs
 
     def _speculate(self) -> _Plan | None:

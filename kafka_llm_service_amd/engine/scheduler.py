@@ -36,6 +36,7 @@ class ScheduledBatch:
     # (seq, start, end): compute tokens [start, end) of seq; samples iff end == seq.total_len
     prefill: list[tuple[Sequence, int, int]] = field(default_factory=list)
     preempted: list[Sequence] = field(default_factory=list)
+    cut: list[Sequence] = field(default_factory=list)  # finished by the scheduler (outgrew the KV pool)
 
     @property
     def num_tokens(self) -> int:
@@ -117,7 +118,10 @@ class Scheduler:
                 if speculative:
                     raise NeedSync()
                 if not self._preempt_one(batch, seq):
-                    raise RuntimeError("KV cache too small for a single sequence")
+                    # alone and still out of pages: the sequence has outgrown the whole KV pool -> end it by length
+                    self.finish(seq, "length")
+                    batch.cut.append(seq)
+                    break
             if seq.status != SeqStatus.RUNNING:
                 continue
             batch.decode.append(seq)

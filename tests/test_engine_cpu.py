@@ -184,3 +184,20 @@ def test_pinned_prefix_survives_eviction(base_engine):
     assert s.num_cached == 160
     eng.unpin_prefix()
     eng.kvm.check_invariants()
+
+
+def test_kv_pool_limits_are_handled(base_engine):
+    eng = _engine(model=base_engine.model, num_kv_blocks=8)  # 128 tokens of KV
+    with pytest.raises(ValueError, match="maximum context length"):
+        eng.add_request("big", list(range(1000, 1200)), GREEDY)
+    # a sequence that outgrows the pool while decoding ends by length instead of stalling the engine
+    s = eng.add_request("grow", list(range(1000, 1100)),
+                        SamplingParams(temperature=0.0, max_tokens=100, ignore_eos=True))
+    outs = []
+    for _ in range(200):
+        outs += eng.step()
+        if s.finished:
+            break
+    assert s.finished and s.finish_reason == "length" and 0 < len(s.output_ids) < 100
+    assert outs[-1].finished and outs[-1].request_id == "grow"
+    eng.kvm.check_invariants()
