@@ -50,3 +50,30 @@ def test_metrics_histograms_exported():
     cnt = re.search(r'kafka_tool_seconds_count\{tool="count_slowly"\} ([0-9.]+)', m)
     assert cnt and float(cnt.group(1)) >= 1
     assert "kafka_tpot_seconds_bucket" in m and "kafka_output_tokens_total" in m
+
+
+def test_json_logging_lines():
+    import io
+    import logging
+
+    from kafka_llm_service_amd.obs.logging import setup_logging
+
+    buf = io.StringIO()
+    setup_logging(json_lines=True, level="INFO", stream=buf)
+    logging.getLogger("kafka.engine").info("step done", extra={"step": 7, "ms": 9.4})
+    rec = json.loads(buf.getvalue().strip().splitlines()[-1])
+    assert rec["msg"] == "step done" and rec["step"] == 7 and rec["level"] == "INFO" and rec["logger"] == "kafka.engine"
+    setup_logging(json_lines=False, stream=io.StringIO())
+
+
+def test_server_cli_flags_map_to_config(monkeypatch):
+    from kafka_llm_service_amd.server import __main__ as m
+    from kafka_llm_service_amd.server.state import ServerConfig
+
+    for env in m.FLAGS.values():
+        monkeypatch.delenv(env, raising=False)
+    monkeypatch.setenv("KAFKA_MODEL", "tiny-llama")
+    monkeypatch.setenv("KAFKA_DP", "2")
+    monkeypatch.setenv("KAFKA_PROMPT_SECTIONS", "intro,core_tools")
+    cfg = ServerConfig.from_env()
+    assert cfg.model == "tiny-llama" and cfg.dp == 2 and cfg.prompt_sections == ["intro", "core_tools"]
