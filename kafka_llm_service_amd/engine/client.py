@@ -24,6 +24,7 @@ from kafka_llm_service_amd.engine.sequence import SamplingParams, StepOutput
 
 log = logging.getLogger("kafka.engine")
 HEARTBEAT_S = 1.0
+_WARM = itertools.count()
 
 
 SPILL_FACTOR = float(os.environ.get("KAFKA_DP_SPILL_FACTOR", "2.0"))
@@ -78,6 +79,13 @@ class InProcessClient:
 
     def pin_prefix(self, token_ids: list[int]) -> None:
         self.async_engine.pin_prefix(token_ids)
+
+    async def warm_prefix(self, token_ids: list[int]) -> None:
+        """Prefill ``token_ids`` once (one sampled token, discarded) and pin the resulting pages."""
+        sp = SamplingParams(temperature=0.0, max_tokens=1, ignore_eos=True)
+        async for _ in self.async_engine.generate(f"warm-{next(_WARM)}", list(token_ids) + [0], sp):
+            pass
+        self.pin_prefix(token_ids)
 
     def health(self) -> dict:
         return {"replicas": 1, "replica0": self.async_engine.health()}
@@ -360,6 +368,31 @@ class DPClient:
             s = self._streams.get(request_id)
         if s is not None:
             self._send_quiet(s[2], ("abort", request_id))
+
+    async def warm_prefix(self, token_ids: list[int]) -> None:
+        """Prefill the shared prefix on EVERY live replica (bypassing thread routing), then pin it everywhere."""
+        loop = asyncio.get_running_loop()
+        sp = {k: v for k, v in SamplingParams(temperature=0.0, max_tokens=1, ignore_eos=True).__dict__.items()
+              if k != "allowed_tokens_fn"}
+        waits = []
+        for r in range(self.n_replicas):
+            if not self._alive[r]:
+                continue
+            rid = f"warm-{next(_WARM)}-r{r}"
+            q: asyncio.Queue = asyncio.Queue()
+            with self._lock:
+                self._streams[rid] = (loop, q, r)
+                self._loads[r] += 1
+            self._send(r, ("add", rid, list(token_ids) + [0], sp))
+            waits.append(q)
+        for q in waits:
+            while True:
+                item = await q.get()
+                if isinstance(item, BaseException):
+                    raise item
+                if item.finished:
+                    break
+        self.pin_prefix(token_ids)
 
     def pin_prefix(self, token_ids: list[int]) -> None:
         """Every replica holds (and pins) its own copy of the shared system prefix."""

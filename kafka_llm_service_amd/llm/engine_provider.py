@@ -44,6 +44,17 @@ class EngineLLMProvider(LLMProvider):
     def render(self, messages: list[Message], tools: list[dict] | None) -> list[int]:
         return self.template.render(messages, tools)
 
+    async def warm(self, system_prompt: str, tools: list[dict] | None) -> int:
+        """Prefill the shared system prefix (system prompt + tool schemas) on every engine replica and pin it, so the
+        very first request of every thread is a prefix hit (SURVEY.md §3.1 target: "pre-fill the shared
+        system-prefix KV on each replica ... then start the API"). Returns the prefix length in tokens."""
+        ids = self.template.render([Message(role="system", content=system_prompt)], tools,
+                                   add_generation_prompt=False)
+        if hasattr(self.client, "warm_prefix"):
+            await self.client.warm_prefix(ids)
+            self._pin = ids
+        return len(ids)
+
     def _maybe_pin(self, messages: list[Message], tools: list[dict] | None) -> None:
         """Pin the shared system prefix (system prompt + tool schemas, ~18k tokens for Kafka) in the engine's prefix
         cache once it has been computed, so KV pressure from long threads never evicts it. With per-thread prompt

@@ -43,6 +43,7 @@ class ServerConfig:
     tool_choice: Any = "auto"
     # subset of the Kafka v1 prompt sections (None = all 13, ~47k characters); small engines / CPU tests use a few
     prompt_sections: list[str] | None = None
+    warm_prefix: bool = True  # prefill + pin the shared system prefix on every replica before serving
     ignore_eos: bool = False  # benchmarks: generate exactly max_tokens (random-init weights emit EOS at random)
     engine_kwargs: dict[str, Any] = field(default_factory=dict)
 
@@ -61,6 +62,7 @@ class ServerConfig:
                             default_max_tokens=int(e.get("KAFKA_DEFAULT_MAX_TOKENS", "1024")),
                             tool_choice=_tool_choice(e.get("KAFKA_TOOL_CHOICE", "auto")),
                             ignore_eos=e.get("KAFKA_IGNORE_EOS", "0") == "1",
+                            warm_prefix=e.get("KAFKA_WARM_PREFIX", "1") == "1",
                             prompt_sections=[x for x in e.get("KAFKA_PROMPT_SECTIONS", "").split(",") if x] or None)
 
 
@@ -116,6 +118,9 @@ class ServerState:
                                      mcp_servers=DEFAULT_MCP_SERVERS if cfg.mcp else [],
                                      prompt_sections=cfg.prompt_sections)
         await self.kafka.initialize()
+        if cfg.backend == "engine" and cfg.warm_prefix and hasattr(self.llm, "warm") and self.kafka.system_prompt:
+            n = await self.llm.warm(self.kafka.system_prompt, await self.kafka.get_tools())
+            log.info("shared system prefix prefilled and pinned: %d tokens", n)
         self.ready = True
         log.info("server ready (backend=%s model=%s)", cfg.backend, cfg.model)
 

@@ -167,6 +167,9 @@ def test_engine_streaming_and_prefix_reuse(engine_client):
     assert f1[-1] == "[DONE]"
     u1 = [x for x in f1 if isinstance(x, dict) and "usage" in x][0]["usage"]
     assert u1["completion_tokens"] >= 1 and u1["prompt_tokens"] > 100  # Kafka system prompt + tools rendered
+    # the shared system prefix was prefilled and pinned at start-up: even turn 1 of a new thread is a prefix hit
+    h0 = st.engine_client.health()["replica0"]
+    assert h0["prefix_hit_tokens"] >= u1["prompt_tokens"] - 64
     body["messages"] = [{"role": "user", "content": "And its HBM?"}]
     c.post(f"/v1/threads/{tid}/chat/completions", json=body)
     h = st.engine_client.health()["replica0"]

@@ -171,3 +171,28 @@ def test_route_affinity_and_load_spill():
     assert route(k, 4, loads, spill_min=48, spill_factor=2.0) != h   # hot spot spills to the least loaded
     loads = [30, 30, 30, 30]
     assert route(k, 4, loads, spill_min=48) == h                     # balanced: stay home
+
+
+@pytest.mark.timeout(300)
+def test_dp_warm_prefix_reaches_every_replica():
+    from kafka_llm_service_amd.engine.client import DPClient, route
+
+    cli = DPClient(EngineConfig(**CFG), 2)
+    prefix = list(range(4000, 4000 + 96))
+    try:
+        async def run():
+            await cli.warm_prefix(prefix)
+            keys = {}
+            for i in range(64):  # one thread key homed on each replica
+                keys.setdefault(route(f"k{i}", 2, [0, 0]), f"k{i}")
+            assert len(keys) == 2
+            for r, k in keys.items():
+                cached = 0
+                async for o in cli.generate(f"after-{r}", prefix + [7, 8],
+                                            SamplingParams(temperature=0.0, max_tokens=1, ignore_eos=True),
+                                            routing_key=k):
+                    cached = o.num_cached_tokens
+                assert cached == 96, (r, cached)
+        asyncio.run(run())
+    finally:
+        asyncio.run(cli.close())
