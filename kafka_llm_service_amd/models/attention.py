@@ -16,6 +16,7 @@ the decode path is hipGraph-capturable (fixed shapes per batch bucket).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -52,17 +53,42 @@ class AttnMeta:
         return self.num_prefix_splits + self.num_splits
 
 
+_OVERLAP = os.environ.get("KAFKA_ATTN_OVERLAP", "0") == "1"
+_SIDE: dict = {}
+
+
+def _side_stream(dev: torch.device):
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
 def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, meta: AttnMeta,
                     out: torch.Tensor) -> torch.Tensor:
-    """q [T, Hq, D] (post-RoPE) -> out [T, Hq, D] bf16."""
+    """q [T, Hq, D] (post-RoPE) -> out [T, Hq, D] bf16.
+
+    With ``KAFKA_ATTN_OVERLAP=1`` the cascade prefix pass (MFMA tile kernel, compute-heavy) runs on a side HIP stream
+    concurrently with the suffix decode pass (HBM-bound); both write disjoint split slots of the same partials and the
+    merge waits for both (fork/join with events; hipGraph-capturable). Off by default until measured."""
     B = meta.num_decode
     if B > 0:
         qd = q[:B]
-        if meta.prefix_items is not None:
+        overlap = _OVERLAP and q.is_cuda and meta.prefix_items is not None
+        if overlap:
+            main = torch.cuda.current_stream(q.device)
+            side = _side_stream(q.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                ops.attn_prefill(meta.prefix_items, qd, k_cache, v_cache, meta.block_tables, meta.q_limit,
+                                 meta.scale, out_part=meta.part, lse_part=meta.lse)
+        elif meta.prefix_items is not None:
             ops.attn_prefill(meta.prefix_items, qd, k_cache, v_cache, meta.block_tables, meta.q_limit,
                              meta.scale, out_part=meta.part, lse_part=meta.lse)
         ops.attn_decode(qd, k_cache, v_cache, meta.block_tables, meta.seq_lens, meta.kv_start, meta.part,
                         meta.lse, meta.num_splits, meta.num_prefix_splits, meta.scale)
+        if overlap:
+            main.wait_stream(side)
         ops.attn_merge(meta.part, meta.lse, out[:B])
     if meta.prefill_items is not None and meta.num_tokens > B:
         if meta.prefill_splits:
