@@ -5,6 +5,8 @@ Interface parity with /root/reference/src/llm/base.py:67-312 (tool-provider hook
 implementation that folds ``stream_completion`` (tool-call deltas accumulated by ``index`` exactly like the agent
 loop does), so a provider only has to implement streaming. Implementations here:
   * ``EngineLLMProvider`` (llm/engine_provider.py) — the on-node MI355X engine (replaces the Portkey provider),
+  * ``RemoteOpenAIProvider`` (llm/remote.py) — any OpenAI-compatible HTTP endpoint (the gateway role of the
+    reference's Portkey provider, without vendor SDKs),
   * ``StubEchoProvider`` / ``ScriptedProvider`` (llm/stub.py) — BASELINE config 1 and tests.
 """
 from __future__ import annotations

@@ -130,6 +130,11 @@ class ServerState:
             from kafka_llm_service_amd.llm.stub import StubEchoProvider
 
             return StubEchoProvider()
+        if cfg.backend == "remote":  # chain to another OpenAI-compatible server (KAFKA_REMOTE_URL / _MODEL)
+            from kafka_llm_service_amd.llm.remote import RemoteOpenAIProvider
+
+            return RemoteOpenAIProvider(os.environ["KAFKA_REMOTE_URL"], os.environ.get("KAFKA_REMOTE_MODEL", cfg.model),
+                                        default_max_tokens=cfg.default_max_tokens)
         from kafka_llm_service_amd.engine.client import make_engine_client
         from kafka_llm_service_amd.llm.engine_provider import EngineLLMProvider
 
