@@ -1,6 +1,7 @@
 """Property tests of the engine loop (SURVEY.md §4.4 "scheduler policies", §5.2 "allocator invariants"): random
 arrivals, aborts, lengths and a small KV pool — after every step the KV bookkeeping is consistent, every request
-ends (finished or aborted), nothing leaks, and greedy outputs do not depend on batching / preemption / plan-ahead."""
+ends (finished or aborted), nothing leaks, and greedy outputs stay the dense oracle's argmax whatever the batching /
+chunking / preemption / plan-ahead."""
 import random
 
 from hypothesis import HealthCheck, given, settings, strategies as st
@@ -58,7 +59,7 @@ def test_random_workload_invariants(seed, blocks, async_on, chunk):
 
 @settings(max_examples=6, deadline=None, suppress_health_check=list(HealthCheck))
 @given(seed=st.integers(0, 10_000))
-def test_greedy_outputs_independent_of_batching(seed):
+def test_greedy_outputs_consistent_across_batching(seed):
     rng = random.Random(seed)
     prompts = [[rng.randrange(1000, 5000) for _ in range(rng.randrange(2, 50))] for _ in range(4)]
     lens = [rng.randrange(1, 8) for _ in prompts]
@@ -67,6 +68,19 @@ def test_greedy_outputs_independent_of_batching(seed):
         eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_model_len=1024, **kw), model=_model())
         return eng.generate(prompts, [SamplingParams(temperature=0.0, max_tokens=n, ignore_eos=True) for n in lens])
 
+    from kafka_llm_service_amd.models.oracle import dense_logits
+
+    def oracle_ok(outs):
+        # bf16 GEMMs of different batch shapes round differently, so exact equality across configurations can flip a
+        # near-tie; what must hold is that every token is the dense oracle's argmax up to a small logit margin
+        for p, o in zip(prompts, outs):
+            lg = dense_logits(_model(), p + o)
+            for i, tok in enumerate(o):
+                row = lg[len(p) - 1 + i]
+                assert (row.max() - row[tok]).item() < 0.05
+        return True
+
     base = run(num_kv_blocks=256)
-    assert run(num_kv_blocks=14, max_prefill_chunk=16, max_num_batched_tokens=32) == base
-    assert run(num_kv_blocks=256, async_scheduling=False, enable_prefix_cache=False) == base
+    assert oracle_ok(base)
+    assert oracle_ok(run(num_kv_blocks=14, max_prefill_chunk=16, max_num_batched_tokens=32))
+    assert oracle_ok(run(num_kv_blocks=256, async_scheduling=False, enable_prefix_cache=False))
