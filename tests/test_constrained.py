@@ -111,3 +111,39 @@ def test_agent_loop_with_forced_idle_call():
     assert tr and tr[0]["tool_name"] == "idle"
     done = [f for f in frames if f.get("type") == "agent_done"]
     assert done and done[0]["reason"] == "idle"
+
+
+def test_agent_iterations_hit_the_prefix_cache(monkeypatch):
+    """Iteration k+1 of the agent = iteration k + the assistant's tool-call tokens (re-emitted verbatim from the
+    thread token cache) + the tool result, so only that suffix is prefilled (SURVEY.md §3.3 target)."""
+    from fastapi.testclient import TestClient
+
+    from kafka_llm_service_amd.db.local import MemoryDBClient
+    from kafka_llm_service_amd.server.app import create_app
+    from kafka_llm_service_amd.server.state import ServerConfig, ServerState
+
+    monkeypatch.setenv("KAFKA_WEATHER_MODE", "offline")
+    cfg = ServerConfig(backend="engine", model="tiny-llama", sandbox="none", max_model_len=32768,
+                       default_max_tokens=48,
+                       tool_choice={"type": "function", "function": {"name": "get_weather"}},
+                       prompt_sections=["intro"], warm_prefix=False,
+                       engine_kwargs={"device": "cpu", "num_kv_blocks": 4096})
+    st = ServerState(cfg, db=MemoryDBClient())
+    with TestClient(create_app(state=st)) as c:
+        eng = st.engine_client.async_engine.engine
+        seen = []
+        orig = eng.add_request
+
+        def spy(rid, prompt, params=None, meta=None):
+            s = orig(rid, prompt, params, meta)
+            seen.append(s)
+            return s
+        eng.add_request = spy
+        st.kafka._agent.max_iterations = 3  # three forced weather calls, then max_iterations ends the run
+        text = c.post("/v1/agent/run", json={"messages": [{"role": "user", "content": "weather?"}]}).text
+    assert "get_weather" in text
+    assert len(seen) >= 2
+    for prev, cur in zip(seen, seen[1:]):
+        # everything the previous iteration computed (its prompt and its generated call) is reused
+        assert cur.num_cached >= (len(prev.prompt_ids) + len(prev.output_ids)) // 16 * 16 - 16, \
+            (cur.num_cached, len(prev.prompt_ids), len(prev.output_ids))
