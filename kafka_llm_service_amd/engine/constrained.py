@@ -78,6 +78,21 @@ class VocabClasses:
         for i in range(tok.n_base + tok.offset, V):
             if not tok.is_special(i):
                 self.str_safe[i] = True
+        self._ranges: dict = {}
+
+    def digit_range(self, tok: KafkaTokenizer, lo, hi) -> np.ndarray:
+        """Mask of single digit-run tokens (no leading zero, or "0") whose integer value lies in [lo, hi]."""
+        key = (lo, hi)
+        m = self._ranges.get(key)
+        if m is None:
+            m = np.zeros(tok.vocab_size, dtype=bool)
+            zero = tok.encode("0")[:1]
+            for i in list(np.flatnonzero(self.digits_nz)) + zero:
+                v = int(tok.decode([int(i)]))
+                if (lo is None or v >= lo) and (hi is None or v <= hi):
+                    m[i] = True
+            self._ranges[key] = m
+        return m
 
 
 _CLASSES: dict[int, VocabClasses] = {}
@@ -209,8 +224,17 @@ class ToolCallConstraint:
             yield from self._value(schema.get("items") or {"type": "string"})
             yield from self._forced("]")
         elif typ in ("integer", "number"):
-            # one digit-only token without a leading zero (BPE digit runs cover 1..3 digits), or a lone "0"
-            yield Mask("digits_nz", self.cls.digits_nz, self.tok.encode("0")[:1])
+            # one digit-only token without a leading zero (BPE digit runs cover 1..3 digits), or a lone "0";
+            # "minimum" / "maximum" restrict the choice to tokens whose value is in range
+            lo, hi = schema.get("minimum"), schema.get("maximum")
+            if lo is None and hi is None:
+                yield Mask("digits_nz", self.cls.digits_nz, self.tok.encode("0")[:1])
+                return
+            m = self.cls.digit_range(self.tok, lo, hi)
+            if m.any():
+                yield Mask(f"digits[{lo},{hi}]", m, [])
+            else:  # nothing representable in one token (e.g. a negative range): emit the bound itself
+                yield from self._forced(json.dumps(lo if lo is not None else hi))
         elif typ == "boolean":
             yield from self._choice(["true", "false"])
         elif typ == "null":

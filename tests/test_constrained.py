@@ -17,7 +17,7 @@ TOOLS = [
         "properties": {"location": {"type": "string"}, "days": {"type": "integer"},
                        "units": {"type": "string", "enum": ["c", "f"]}, "tags": {"type": "array",
                                                                              "items": {"type": "string"}},
-                       "deep": {"type": "boolean"}, "opt": {"type": ["null", "number"]},
+                       "deep": {"type": "boolean"}, "opt": {"type": ["null", "number"], "minimum": 3, "maximum": 40},
                        "ignored": {"type": "string"}}}}},
     {"type": "function", "function": {"name": "get", "parameters": {"type": "object", "properties": {}}}},
     {"type": "function", "function": {"name": "idle", "parameters": {
@@ -51,6 +51,7 @@ def test_fuzz_required_calls_are_valid(family):
             assert isinstance(args["location"], str) and isinstance(args["days"], int)
             assert args["units"] in ("c", "f") and isinstance(args["tags"], list) and len(args["tags"]) == 1
             assert isinstance(args["deep"], bool) and isinstance(args["opt"], (int, float))
+            assert 3 <= args["opt"] <= 40
             assert "ignored" not in args
         elif fn["name"] == "idle":
             assert set(args) == {"summary"}
