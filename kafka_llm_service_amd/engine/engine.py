@@ -18,7 +18,7 @@ import torch
 
 from kafka_llm_service_amd.engine.model_runner import ModelRunner
 from kafka_llm_service_amd.engine.scheduler import NeedSync, Scheduler, SchedulerConfig
-from kafka_llm_service_amd.engine.sequence import PENDING, SamplingParams, Sequence, SeqStatus, StepOutput
+from kafka_llm_service_amd.engine.sequence import PENDING, SamplingParams, Sequence, StepOutput
 from kafka_llm_service_amd.models.config import ModelConfig, get_config
 from kafka_llm_service_amd.models.weights import build_model
 from kafka_llm_service_amd.runtime import KVManager

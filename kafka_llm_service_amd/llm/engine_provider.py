@@ -13,7 +13,6 @@ token ids so the agent can store them with the message (thread token cache).
 """
 from __future__ import annotations
 
-import json
 import uuid
 from typing import Any, AsyncGenerator
 

@@ -3,8 +3,6 @@ the seams SURVEY.md §4.2 lists: a scripted LLMProvider, an in-memory DB, local 
 import asyncio
 import json
 
-import pytest
-
 from kafka_llm_service_amd.agents.base import Agent
 from kafka_llm_service_amd.db.local import MemoryDBClient
 from kafka_llm_service_amd.kafka.v1 import KafkaV1Provider, format_playbooks_table
@@ -12,7 +10,7 @@ from kafka_llm_service_amd.llm.compaction import (SummarizationCompactionProvide
                                                   find_safe_split_point, is_context_length_error,
                                                   validate_message_structure)
 from kafka_llm_service_amd.llm.stub import ScriptedProvider, StubEchoProvider
-from kafka_llm_service_amd.llm.types import LLMProviderError, Message
+from kafka_llm_service_amd.llm.types import Message
 from kafka_llm_service_amd.server_tools import PlannerTools, count_tool, get_weather_tool
 from kafka_llm_service_amd.tools.agent import AgentToolProvider
 from kafka_llm_service_amd.tools.types import Tool

@@ -1,6 +1,5 @@
 """Tokenizer / chat template / tool-call parsing: the prefix-stability property the prefix cache depends on
  and the OpenAI tool_calls shape (portkey.py:447-464 normalisation)."""
-import asyncio
 import json
 
 from hypothesis import given, settings, strategies as st

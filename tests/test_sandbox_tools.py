@@ -5,7 +5,6 @@ import os
 import socket
 import subprocess
 import sys
-import time
 
 import pytest
 
@@ -13,7 +12,7 @@ from kafka_llm_service_amd.db.local import MemoryDBClient
 from kafka_llm_service_amd.sandbox.lazy import LazySandbox
 from kafka_llm_service_amd.sandbox.local import LocalSandbox, parse_sse_event
 from kafka_llm_service_amd.sandbox.manager import SandboxManager
-from kafka_llm_service_amd.sandbox.provisioner import LocalProcessProvisioner, SharedURLProvisioner
+from kafka_llm_service_amd.sandbox.provisioner import LocalProcessProvisioner
 from kafka_llm_service_amd.server_tools import NotebookTools, ShellTools
 from kafka_llm_service_amd.tools.agent import AgentToolProvider
 from kafka_llm_service_amd.tools.mcp import MCPConnection
