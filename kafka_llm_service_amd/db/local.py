@@ -7,7 +7,8 @@ get_or_create_vm_api_key / get_playbooks_for_kafka_profile.
 
 Fixed vs the reference:
   * ordering is a monotonic per-thread ``seq`` (the reference ordered by ``created_at`` with 1-second resolution, so
-    same-second messages could come back in any order — quirk Q10),
+    same-second messages could come back in any order — quirk Q10); a database written by the reference is migrated
+    in place on open (columns added, ``seq`` assigned in created_at / insertion order),
   * ``thread_lock(thread_id)`` serialises read-modify-write of one thread across concurrent requests (Q11),
   * every message row keeps the engine token ids of generated assistant turns (``token_ids`` column): the chat
     template re-renders history from them exactly, which keeps the thread's KV prefix cache hot,
@@ -36,7 +37,6 @@ CREATE TABLE IF NOT EXISTS threads (
 CREATE TABLE IF NOT EXISTS messages (
     id TEXT PRIMARY KEY, thread_id TEXT NOT NULL REFERENCES threads(id), seq INTEGER NOT NULL,
     message TEXT NOT NULL, token_ids TEXT, metadata TEXT, created_at TEXT NOT NULL);
-CREATE UNIQUE INDEX IF NOT EXISTS idx_messages_thread_seq ON messages(thread_id, seq);
 CREATE TABLE IF NOT EXISTS kafka_profiles (
     id TEXT PRIMARY KEY, user_id TEXT, global_prompt TEXT, memory_dsn TEXT, virtual_keys TEXT);
 CREATE TABLE IF NOT EXISTS playbooks (
@@ -44,6 +44,49 @@ CREATE TABLE IF NOT EXISTS playbooks (
 CREATE TABLE IF NOT EXISTS vm_api_keys (
     id TEXT PRIMARY KEY, thread_id TEXT, user_id TEXT, api_key TEXT, status TEXT, created_at TEXT);
 """
+
+
+INDEXES = """
+CREATE UNIQUE INDEX IF NOT EXISTS idx_messages_thread_seq ON messages(thread_id, seq);
+"""
+
+
+def _migrate(c: sqlite3.Connection) -> None:
+    """Open a database written by the reference service (/root/reference/src/db/local.py:51-76: threads(id,
+    created_at, metadata, sandbox_id), messages(id, thread_id, message, metadata, created_at), ordered by the
+    1-second ``created_at``): add the columns this store uses and give existing messages a ``seq`` in their original
+    order (created_at, then insertion order), so a user can switch over with their thread history intact."""
+    tcols = {r[1] for r in c.execute("PRAGMA table_info(threads)")}
+    for col, decl in (("user_id", "TEXT"), ("kafka_profile_id", "TEXT"),
+                      ("next_seq", "INTEGER NOT NULL DEFAULT 0"), ("sandbox_id", "TEXT"), ("metadata", "TEXT")):
+        if col not in tcols:
+            c.execute(f"ALTER TABLE threads ADD COLUMN {col} {decl}")
+    mcols = {r[1] for r in c.execute("PRAGMA table_info(messages)")}
+    if "token_ids" not in mcols:
+        c.execute("ALTER TABLE messages ADD COLUMN token_ids TEXT")
+    if "seq" not in mcols:
+        c.execute("ALTER TABLE messages ADD COLUMN seq INTEGER")
+        rows = c.execute("SELECT rowid, thread_id FROM messages ORDER BY thread_id, created_at, rowid").fetchall()
+        counts: dict[str, int] = {}
+        for rowid, tid in rows:
+            n = counts.get(tid, 0)
+            c.execute("UPDATE messages SET seq=? WHERE rowid=?", (n, rowid))
+            counts[tid] = n + 1
+        for tid, n in counts.items():
+            c.execute("INSERT OR IGNORE INTO threads(id, created_at, metadata) VALUES (?,?,?)", (tid, _now(), "{}"))
+            c.execute("UPDATE threads SET next_seq=? WHERE id=?", (n, tid))
+    c.commit()
+
+
+def _flatten_content(d: dict) -> dict:
+    """OpenAI multi-part content ([{"type": "text", "text": ...}, ...]) -> newline-joined text, as the reference
+    does on read (/root/reference/src/db/local.py:123-132); Message.content is a string."""
+    c = d.get("content")
+    if isinstance(c, list):
+        parts = [p["text"] if isinstance(p, dict) else str(p) for p in c
+                 if isinstance(p, str) or (isinstance(p, dict) and "text" in p)]
+        d["content"] = "\n".join(parts) if parts else None
+    return d
 
 
 def _now() -> str:
@@ -68,6 +111,8 @@ class LocalDBClient:
             self._conn.execute("PRAGMA journal_mode=WAL")
             self._conn.execute("PRAGMA synchronous=NORMAL")
             self._conn.executescript(SCHEMA)
+            _migrate(self._conn)
+            self._conn.executescript(INDEXES)
         return self._conn
 
     async def _run(self, fn, *args):
@@ -133,7 +178,7 @@ class LocalDBClient:
         rows = await self._run(_do)
         out = []
         for r in rows:
-            d = json.loads(r["message"])
+            d = _flatten_content(json.loads(r["message"]))
             if not include_system and d.get("role") == "system":
                 continue
             if r["token_ids"]:

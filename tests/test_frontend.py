@@ -68,3 +68,41 @@ def test_mistral_template():
     ids = tpl.render([Message(role="user", content="hi")], TOOLS)
     assert ids[0] == 1 and tok.special_id("[INST]") in ids and tok.special_id("[AVAILABLE_TOOLS]") in ids
     assert tok.decode(tok.encode("abc def")) == "abc def"
+
+
+def test_local_db_opens_a_reference_schema_database(tmp_path):
+    """A threads.db written by the reference (its SQLite schema, same-second created_at ties, multi-part content)
+    opens in place: history comes back in insertion order, new messages append after it."""
+    import asyncio
+    import sqlite3
+
+    from kafka_llm_service_amd.db.local import LocalDBClient
+
+    path = tmp_path / "threads.db"
+    c = sqlite3.connect(path)
+    c.executescript("""
+        CREATE TABLE threads (id TEXT PRIMARY KEY, created_at TEXT DEFAULT CURRENT_TIMESTAMP, metadata TEXT,
+                              sandbox_id TEXT);
+        CREATE TABLE messages (id TEXT PRIMARY KEY, thread_id TEXT NOT NULL, message TEXT NOT NULL, metadata TEXT,
+                               created_at TEXT DEFAULT CURRENT_TIMESTAMP, FOREIGN KEY (thread_id) REFERENCES threads(id));
+        CREATE INDEX idx_messages_thread_id ON messages(thread_id);""")
+    c.execute("INSERT INTO threads(id, created_at, metadata) VALUES ('t1', '2025-01-01 10:00:00', '{}')")
+    msgs = [{"role": "user", "content": "first"}, {"role": "assistant", "content": "second"},
+            {"role": "user", "content": [{"type": "text", "text": "multi"}, {"type": "text", "text": "part"}]},
+            {"role": "assistant", "content": "fourth"}]
+    for i, m in enumerate(msgs):  # all in the same second: only insertion order distinguishes them
+        c.execute("INSERT INTO messages(id, thread_id, message, metadata, created_at) VALUES (?,?,?,?,?)",
+                  (f"z{9 - i}", "t1", json.dumps(m), "{}", "2025-01-01 10:00:05"))
+    c.commit()
+    c.close()
+
+    async def go():
+        db = LocalDBClient(str(path))
+        await db.initialize()
+        got = await db.get_thread_messages("t1")
+        assert [m.content for m in got] == ["first", "second", "multi\npart", "fourth"]
+        from kafka_llm_service_amd.llm.types import Message
+        await db.add_message("t1", Message(role="user", content="fifth"))
+        assert (await db.get_thread_messages("t1"))[-1].content == "fifth"
+        await db.close()
+    asyncio.run(go())
