@@ -11,6 +11,7 @@ blocks on the GPU (SURVEY.md §2.4 "Engine step loop must not run on the API eve
 from __future__ import annotations
 
 import logging
+import os
 import time
 from dataclasses import dataclass, field, replace
 
@@ -48,6 +49,9 @@ class EngineConfig:
     target_wgs: int = 256               # tile-kernel workgroups per pass (8-wave WGs, one per CU)
     prefill_kv_chunk: int = 1024        # key-range split for long-context prefill tiles
     use_graphs: bool = False
+    # decode GEMMs: "stream" = weight-streaming MFMA kernel on wave-tiled weight copies (csrc/wstream_gemm.hip),
+    # "blas" = hipBLASLt only; "auto" = stream on GPU (env KAFKA_DECODE_GEMM overrides)
+    decode_gemm: str = "auto"
     async_scheduling: bool = True       # plan step n+1 on the host while step n runs on the GPU
     eos_token_ids: list[int] = field(default_factory=list)
 
@@ -95,6 +99,11 @@ class LLMEngine:
         self.model = model or build_model(mc, self.device, tp=cfg.tp, tp_rank=cfg.tp_rank, seed=cfg.seed,
                                           weights=cfg.weights, max_positions=min(cfg.max_model_len,
                                                                                  mc.max_position_embeddings))
+        mode = os.environ.get("KAFKA_DECODE_GEMM", cfg.decode_gemm)
+        if mode == "auto":
+            mode = "stream" if self.device.type == "cuda" else "blas"
+        if mode == "stream" and not self.model.stream:
+            self.model.enable_stream_weights()  # before the KV pool is sized from the free memory
         self.load_s = time.perf_counter() - t0
         self.eos = set(cfg.eos_token_ids or mc.eos_token_ids)
         hkv, D, L = self.model.hkv, self.model.D, mc.num_layers
@@ -153,6 +162,10 @@ class LLMEngine:
             # a sequence that can never fit the KV pool would stall the scheduler; refuse it like an over-long prompt
             raise ValueError(f"This model's maximum context length is {pool_tokens} tokens on this replica (KV "
                              f"pool). However, your messages resulted in {len(prompt_ids)} tokens.")
+        V = self.model_cfg.vocab_size
+        if prompt_ids and (min(prompt_ids) < 0 or max(prompt_ids) >= V):
+            # an out-of-range id would read past the embedding table on the GPU (a device fault, not an exception)
+            raise ValueError(f"prompt token ids must lie in [0, {V}); got [{min(prompt_ids)}, {max(prompt_ids)}]")
         if params.tool_grammar is not None and params.allowed_tokens_fn is None:
             from kafka_llm_service_amd.engine.constrained import ToolCallConstraint
             from kafka_llm_service_amd.engine.tokenizer import tokenizer_for_model

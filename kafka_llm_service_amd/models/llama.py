@@ -35,7 +35,9 @@ class StepInput:
 
 
 class LayerWeights:
-    __slots__ = ("input_norm", "post_norm", "qkv", "o", "gate_up", "down", "router", "w13", "w2", "expert_ids")
+    __slots__ = ("input_norm", "post_norm", "qkv", "o", "gate_up", "down", "router", "w13", "w2", "expert_ids",
+                 "qkv_t", "o_t", "gate_up_t", "down_t")
+    STREAMED = ("qkv", "o", "gate_up", "down")  # projections with a wave-tiled copy for the decode GEMM
 
     def __init__(self):
         for s in self.__slots__:
@@ -66,10 +68,39 @@ class TransformerLM:
         self.cos_sin = ops.rope_cos_sin(maxp, self.D, cfg.rope_theta, cfg.rope_scaling, device=self.device)
         self.scale = self.D ** -0.5
         self.moe = None
+        self.lm_head_t = None
+        self.stream = False  # decode GEMMs on the weight-streaming kernel (enable_stream_weights)
 
     # ------------------------------------------------------------------------------------------------------------
+    def enable_stream_weights(self) -> int:
+        """Keep a wave-tiled copy of every dense projection and of the lm_head (ops.tile_weight) so decode-sized
+        steps (T <= ops.STREAM_MAX_M) run the weight-streaming MFMA GEMM (csrc/wstream_gemm.hip) instead of
+        hipBLASLt; prefill-sized steps keep the row-major weights. Costs one more copy of those weights (16 GB for
+        Llama-3-8B: the HBM of an MI355X has room, and the KV pool is sized after this). Returns the added bytes."""
+        added = 0
+        for lw in self.layers:
+            for name in LayerWeights.STREAMED:
+                w = getattr(lw, name)
+                if w is not None and ops.stream_plan(1, w.shape[0], w.shape[1]) is not None:
+                    setattr(lw, name + "_t", ops.tile_weight(w))
+                    added += w.numel() * w.element_size()
+        if ops.stream_plan(1, self.lm_head.shape[0], self.lm_head.shape[1]) is not None:
+            self.lm_head_t = ops.tile_weight(self.lm_head)
+            added += self.lm_head.numel() * self.lm_head.element_size()
+        self.stream = True
+        return added
+
+    def _linear(self, x: torch.Tensor, w: torch.Tensor, wt: torch.Tensor | None, max_splits: int = 8):
+        """x @ w^T: the weight-streaming kernel for decode-sized x (bf16 or a split-K slab out), else hipBLASLt."""
+        if self.stream and wt is not None and 0 < x.shape[0] <= ops.STREAM_MAX_M:
+            return ops.linear_stream(x, wt, max_splits)
+        return F.linear(x, w)
+
     def forward(self, inp: StepInput, k_caches: list[torch.Tensor], v_caches: list[torch.Tensor]) -> torch.Tensor:
-        """Returns logits [n, V] (bf16) for ``inp.logit_rows``."""
+        """Returns logits [n, V] (bf16) for ``inp.logit_rows``.
+
+        On decode-sized steps the projections return split-K slabs (fp32 [S, T, n], see ops.linear_stream) which
+        rope_kv_write / silu_mul / fused_add_rmsnorm consume directly; a TP all-reduce needs the bf16 sum first."""
         cfg = self.cfg
         T = inp.tokens.shape[0]
         h = self._embed(inp.tokens)
@@ -85,25 +116,27 @@ class TransformerLM:
                 residual = h.clone()
             else:
                 ops.fused_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x)
-            qkv = F.linear(x, lw.qkv)
+            qkv = self._linear(x, lw.qkv, lw.qkv_t)
             ops.rope_kv_write(qkv, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i], inp.slot_mapping,
                               self.hq, self.hkv)
             paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out)
-            o = F.linear(attn_out.view(T, -1), lw.o)
-            o = pstate.tp_all_reduce(o)
+            o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t)
+            if self.tp > 1:
+                o = pstate.tp_all_reduce(ops.slab_reduce(o))
             ops.fused_add_rmsnorm(o, residual, lw.post_norm, eps, out=x)
             if lw.router is not None:
                 delta = self.moe(x, lw)
             else:
-                gu = F.linear(x, lw.gate_up)
+                gu = self._linear(x, lw.gate_up, lw.gate_up_t)
                 a = ops.silu_mul(gu)
-                delta = F.linear(a, lw.down)
-                delta = pstate.tp_all_reduce(delta)
+                delta = self._linear(a, lw.down, lw.down_t)
+                if self.tp > 1:
+                    delta = pstate.tp_all_reduce(ops.slab_reduce(delta))
         rows = inp.logit_rows
-        d_sel = delta.index_select(0, rows)
+        d_sel = delta.index_select(1 if ops.is_slab(delta) else 0, rows)
         r_sel = residual.index_select(0, rows)
         hf = ops.fused_add_rmsnorm(d_sel, r_sel, self.final_norm, eps)
-        logits = F.linear(hf, self.lm_head)
+        logits = self._linear(hf, self.lm_head, self.lm_head_t, max_splits=1)
         if self.tp > 1:
             logits = pstate.tp_all_gather_lastdim(logits)
         return logits[:, :cfg.vocab_size]
@@ -130,6 +163,6 @@ class TransformerLM:
         for i, lw in enumerate(self.layers):
             for s in LayerWeights.__slots__:
                 t = getattr(lw, s)
-                if isinstance(t, torch.Tensor):
+                if isinstance(t, torch.Tensor) and not s.endswith("_t"):
                     out[f"layers.{i}.{s}"] = t
         return {k: v for k, v in out.items() if v is not None}

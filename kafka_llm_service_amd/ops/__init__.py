@@ -23,6 +23,16 @@ def _gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+def is_slab(t: torch.Tensor) -> bool:
+    """Split-K partial sums of the decode GEMM: fp32 [S, T, n] (``linear_stream``). The slab-aware ops below
+    (fused_add_rmsnorm, silu_mul, rope_kv_write) sum them while loading; ``slab_reduce`` gives the bf16 tensor."""
+    return t.dtype == torch.float32 and t.dim() == 3
+
+
+def rows_of(t: torch.Tensor) -> int:
+    return t.shape[1] if is_slab(t) else t.shape[0]
+
+
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | None = None) -> torch.Tensor:
     if out is None:
         out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
@@ -35,35 +45,42 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | No
 
 def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
                       out: torch.Tensor | None = None) -> torch.Tensor:
-    """residual <- x + residual (in place); returns rmsnorm(residual) * w (into ``out`` or a new tensor)."""
+    """residual <- x + residual (in place); returns rmsnorm(residual) * w (into ``out`` or a new tensor).
+    ``x`` may be a split-K slab [S, T, d] (summed in fp32 before the add)."""
+    slab = is_slab(x)
     if out is None:
-        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+        out = torch.empty(residual.shape, dtype=residual.dtype, device=x.device)
     if _gpu(x):
-        ext().fused_add_rmsnorm(out.view(-1, x.shape[-1]), x.reshape(-1, x.shape[-1]),
-                                residual.view(-1, x.shape[-1]), w, float(eps))
+        xa = x if slab else x.reshape(-1, x.shape[-1])
+        ext().fused_add_rmsnorm(out.view(-1, x.shape[-1]), xa, residual.view(-1, x.shape[-1]), w, float(eps))
     else:
-        y, s = ref.fused_add_rmsnorm(x, residual, w, eps)
+        y, s = ref.fused_add_rmsnorm(x.sum(0) if slab else x, residual, w, eps)
         residual.copy_(s)
         out.copy_(y)
     return out
 
 
 def silu_mul(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """silu(x[..., :F]) * x[..., F:] (bf16 out); ``x`` may be a split-K slab [S, T, 2F]."""
     F = x.shape[-1] // 2
+    slab = is_slab(x)
     if out is None:
-        out = torch.empty(*x.shape[:-1], F, dtype=x.dtype, device=x.device)
+        lead = (x.shape[1],) if slab else x.shape[:-1]
+        out = torch.empty(*lead, F, dtype=torch.bfloat16 if slab else x.dtype, device=x.device)
     if _gpu(x):
-        ext().silu_mul(out.view(-1, F), x.reshape(-1, 2 * F))
+        ext().silu_mul(out.view(-1, F), x if slab else x.reshape(-1, 2 * F))
     else:
-        out.copy_(ref.silu_mul(x))
+        out.copy_(ref.silu_mul(x.sum(0) if slab else x))
     return out
 
 
 def rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq: int, Hkv: int) -> None:
+    """RoPE on q/k + paged KV write; ``qkv`` is bf16 [T, W] or a split-K slab [S, T, W]."""
     if _gpu(qkv):
         ext().rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, int(Hq), int(Hkv))
     else:
-        ref.rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq, Hkv)
+        ref.rope_kv_write(qkv.sum(0) if is_slab(qkv) else qkv, positions, cos_sin, q_out, k_cache, v_cache,
+                          slot_mapping, Hq, Hkv)
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part, lse_part, num_splits: int,
@@ -130,6 +147,75 @@ def skinny_gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = Non
         ext().skinny_gemm(x, w, out, int(U))
     else:
         out.copy_((x.float() @ w.float().t()).to(x.dtype))
+    return out
+
+
+def tile_weight(w: torch.Tensor) -> torch.Tensor:
+    """Row-major weight [N, K] -> the wave-tiled layout [N/32, K/16, 64, 8] read by the weight-streaming decode GEMM
+    (csrc/wstream_gemm.hip): lane l = (r = l % 32, h = l // 32) of tile (nb, kb) holds W[32 nb + r, 16 kb + 8 h : +8]."""
+    N, K = w.shape
+    return w.reshape(N // 32, 32, K // 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous().view(N // 32, K // 16, 64, 8)
+
+
+def untile_weight(wt: torch.Tensor) -> torch.Tensor:
+    nb, kb = wt.shape[0], wt.shape[1]
+    return wt.view(nb, kb, 2, 32, 8).permute(0, 3, 1, 2, 4).reshape(nb * 32, kb * 16)
+
+
+STREAM_MAX_M = 128
+
+
+def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, int] | None:
+    """(row tiles, K chunk, splits) of the decode GEMM for a shape, None if unsupported (same rule as
+    kafka_wstream_plan in csrc/wstream_gemm.hip, mirrored so CPU runs take the same split decisions)."""
+    if M < 1 or M > STREAM_MAX_M or N % 32 or N <= 0:
+        return None
+    mt = 1 if M <= 32 else (2 if M <= 64 else 4)
+    kc = 128 if mt == 4 else 256
+    if K % kc or K <= 0:
+        return None
+    nx, chunks, s = (N + 127) // 128, K // kc, 1
+    while s * 2 <= max_splits and s * 2 <= 8 and chunks % (s * 2) == 0 and nx * s < 256:
+        s *= 2
+    return mt, kc, s
+
+
+def linear_stream(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, nt: bool = True) -> torch.Tensor:
+    """y = x @ W^T for decode-sized M (<= 128) from the wave-tiled weight ``wt``: the weight-streaming MFMA kernel.
+    Returns bf16 [M, N] when the plan has one split, else the fp32 split-K slabs [S, M, N] (a slab; the consumer
+    kernels sum it while loading)."""
+    M, K = x.shape
+    N = wt.shape[0] * 32
+    plan = stream_plan(M, N, K, max_splits)
+    if plan is None:
+        raise ValueError(f"linear_stream: unsupported shape M={M} N={N} K={K}")
+    S = plan[2]
+    if _gpu(x):
+        if S == 1:
+            y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+            ext().wstream_gemm(x, wt, y, None, int(max_splits), bool(nt))
+            return y
+        p = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+        ext().wstream_gemm(x, wt, None, p, int(max_splits), bool(nt))
+        return p
+    w = untile_weight(wt).float()
+    xf = x.float()
+    if S == 1:
+        return (xf @ w.t()).to(x.dtype)
+    ks = K // S
+    return torch.stack([xf[:, s * ks:(s + 1) * ks] @ w[:, s * ks:(s + 1) * ks].t() for s in range(S)])
+
+
+def slab_reduce(p: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """bf16 [M, N] = sum of the split-K slabs [S, M, N] (bf16 inputs pass through)."""
+    if not is_slab(p):
+        return p
+    if out is None:
+        out = torch.empty(p.shape[1], p.shape[2], dtype=torch.bfloat16, device=p.device)
+    if _gpu(p):
+        ext().slab_reduce(p, out)
+    else:
+        out.copy_(p.sum(0))
     return out
 
 

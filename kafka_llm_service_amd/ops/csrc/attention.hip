@@ -1,7 +1,8 @@
 // Paged attention for gfx950 on v_mfma_f32_32x32x16_bf16.
 //
 // KV page layout (page = 16 tokens, one layer):
-//   K: [num_blocks, Hkv, 16, D]   key-major, 256 B per key row (D = 128)
+//   K: [num_blocks, Hkv, 16, D]   stored as D/8 chunk planes [16][16 keys][8]: (key o, d) at ((d>>3)*16 + o)*8 + (d&7)
+//                                 (see rope_kv.hip): a wave's K fragment load is two contiguous 512-B runs
 //   V: [num_blocks, Hkv, D, 16]   V^T per page, key offset o stored at swap_bits_2_3(o)   (see rope_kv.hip)
 //
 // One wave processes 32 query rows x 32 keys per step, entirely in registers:
@@ -61,9 +62,10 @@ __device__ __forceinline__ void load_kv(KVFrag<D>& f, const bf16* __restrict__ k
                                         int lane) {
   const int r = lane & 31, h = lane >> 5;
   const int kp = (r >> 4) ? page1 : page0;
-  const bf16* kptr = k_cache + ((int64_t)kp * Hkv + kvh) * (PAGE * D) + (r & 15) * D + 8 * h;
+  // chunk plane 2kk + h, key r & 15
+  const bf16* kptr = k_cache + ((int64_t)kp * Hkv + kvh) * (PAGE * D) + (r & 15) * 8 + h * (PAGE * 8);
 #pragma unroll
-  for (int kk = 0; kk < D / 16; ++kk) f.k[kk] = load_bf16x8(kptr + 16 * kk);
+  for (int kk = 0; kk < D / 16; ++kk) f.k[kk] = load_bf16x8(kptr + kk * (2 * PAGE * 8));
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
     const int vp = s2 ? page1 : page0;
@@ -302,9 +304,9 @@ __device__ __forceinline__ void stage_load(StageRegs<NT>& sr, const bf16* __rest
 #pragma unroll
   for (int i = 0; i < 512 / NT; ++i) {
     const int qd = tid + NT * i;
-    const int key = qd >> 4, c = qd & 15;
-    const int page = key < 16 ? p0 : p1;
-    sr.k[i] = asm_load16(k_cache + ((int64_t)page * Hkv + kvh) * (PAGE * D) + (key & 15) * D + c * 8);
+    // K: 16-B piece qd & 255 of page qd >> 8 (= chunk plane (qd >> 4) & 15, key qd & 15): contiguous per wave
+    const int page = (qd >> 8) ? p1 : p0;
+    sr.k[i] = asm_load16(k_cache + ((int64_t)page * Hkv + kvh) * (PAGE * D) + (qd & 255) * 8);
     const int vp = (qd >> 8) ? p1 : p0;
     sr.v[i] = asm_load16(v_cache + ((int64_t)vp * Hkv + kvh) * (D * PAGE) + (qd & 255) * 8);
   }
@@ -320,7 +322,7 @@ __device__ __forceinline__ void stage_store(const StageRegs<NT>& sr, char* lds, 
 #pragma unroll
   for (int i = 0; i < 512 / NT; ++i) {
     const int qd = tid + NT * i;
-    const int key = qd >> 4, c = qd & 15;
+    const int key = ((qd >> 8) << 4) | (qd & 15), c = (qd >> 4) & 15;
     *reinterpret_cast<bf16x8*>(lds + key * 256 + 16 * (c ^ (key & 15))) = sr.k[i];
     const int vq = qd & 255, d = vq >> 1, half = vq & 1;
     *reinterpret_cast<bf16x8*>(lds + KT_BYTES + (qd >> 8) * 4096 + d * 32 + 16 * (half ^ ((d >> 3) & 1))) =

@@ -12,10 +12,14 @@ hipError_t kafka_launch_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs
                           hipStream_t st);
 hipError_t kafka_launch_fused_add_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs, bf16* resid, int64_t rs,
                                     const bf16* w, int T, int d, float eps, hipStream_t st);
+hipError_t kafka_launch_fused_add_rmsnorm_slab(bf16* out, int64_t os, const float* xp, int S, int64_t ps, bf16* resid,
+                                               int64_t rs, const bf16* w, int T, int d, float eps, hipStream_t st);
 hipError_t kafka_launch_silu_mul(bf16* out, const bf16* x, int64_t xs, int T, int F, hipStream_t st);
-hipError_t kafka_launch_rope_kv(const bf16* qkv, int64_t qkv_stride, const int64_t* positions, const float* cos_sin,
-                          bf16* q_out, int64_t q_stride, bf16* k_cache, bf16* v_cache, const int64_t* slot_mapping,
-                          int T, int Hq, int Hkv, int D, int block_size, hipStream_t st);
+hipError_t kafka_launch_silu_mul_slab(bf16* out, const float* xp, int S, int64_t ps, int T, int F, hipStream_t st);
+hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int S, int64_t ps, int64_t qkv_stride,
+                                const int64_t* positions, const float* cos_sin, bf16* q_out, int64_t q_stride,
+                                bf16* k_cache, bf16* v_cache, const int64_t* slot_mapping, int T, int Hq, int Hkv,
+                                int D, int block_size, hipStream_t st);
 hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const bf16* k_cache, const bf16* v_cache, int B,
                               int Hkv, int G, int D, const int* block_tables, int bt_stride, const int* seq_lens,
                               const int* kv_start, float* out_part, float* lse_part, int S, int S_total,
@@ -33,6 +37,10 @@ int kafka_skinny_gemm_plan(int M, int N, int K, int U, int* splitk, int* k_per_w
 hipError_t kafka_launch_skinny_gemm(const bf16* X, int64_t ldx, const bf16* W, int64_t ldw, bf16* Y, int64_t ldy,
                                     float* slab, int M, int N, int K, int U, int splitk, int k_per_wave,
                                     hipStream_t st);
+int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits);
+hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt, int kc,
+                                     int splits, int nt, bf16* Y, int64_t ldy, float* P, hipStream_t st);
+hipError_t kafka_launch_slab_reduce(const float* P, int S, int M, int N, bf16* Y, int64_t ldy, hipStream_t st);
 hipError_t kafka_launch_moe_route(const bf16* logits, int64_t ld, int T, int E, int K, int BM, float* topk_w,
                                   int* topk_e, int* perm_tok, float* perm_w, int* expert_off, int* tile_off,
                                   hipStream_t st);
@@ -73,31 +81,57 @@ static void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
                                   cur_stream()));
 }
 
-static void fused_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor residual, at::Tensor w, double eps) {
-  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(residual, at::kBFloat16); CHECK_DT(w, at::kBFloat16);
-  CHECK_DT(out, at::kBFloat16);
-  CHECK_LASTDIM(x); CHECK_LASTDIM(out); CHECK_LASTDIM(residual);
-  TORCH_CHECK(x.dim() == 2 && residual.dim() == 2 && out.dim() == 2, "fused_add_rmsnorm: 2-D tensors expected");
-  const int d = x.size(1);
-  TORCH_CHECK(d % 8 == 0 && d <= 16384 && w.numel() == d && residual.size(0) == x.size(0) &&
-                  residual.size(1) == d && out.size(0) == x.size(0) && out.size(1) == d,
-              "fused_add_rmsnorm: bad shapes");
-  CHECK_HIP(kafka_launch_fused_add_rmsnorm(bptr(out), out.stride(0), bptr(x), x.stride(0), bptr(residual),
-                                            residual.stride(0), bptr(w), x.size(0), d, eps, cur_stream()));
+// A split-K slab is an fp32 contiguous [S, T, n] tensor (wstream_gemm output); kernels that accept one sum it on load.
+static bool is_slab(const at::Tensor& x) { return x.scalar_type() == at::kFloat && x.dim() == 3; }
+static void check_slab(const at::Tensor& x) {
+  TORCH_CHECK(x.is_contiguous() && x.size(0) >= 1 && x.size(2) % 8 == 0, "slab must be contiguous fp32 [S, T, n]");
 }
 
+// x: bf16 [T, d] or slab [S, T, d]
+static void fused_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor residual, at::Tensor w, double eps) {
+  CHECK_CUDA(x); CHECK_DT(residual, at::kBFloat16); CHECK_DT(w, at::kBFloat16);
+  CHECK_DT(out, at::kBFloat16);
+  CHECK_LASTDIM(x); CHECK_LASTDIM(out); CHECK_LASTDIM(residual);
+  const bool slab = is_slab(x);
+  if (slab) check_slab(x); else CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK((slab || x.dim() == 2) && residual.dim() == 2 && out.dim() == 2,
+              "fused_add_rmsnorm: 2-D tensors (or a 3-D fp32 slab) expected");
+  const int64_t T = x.size(slab ? 1 : 0);
+  const int d = x.size(slab ? 2 : 1);
+  TORCH_CHECK(d % 8 == 0 && d <= 16384 && w.numel() == d && residual.size(0) == T &&
+                  residual.size(1) == d && out.size(0) == T && out.size(1) == d,
+              "fused_add_rmsnorm: bad shapes");
+  if (slab)
+    CHECK_HIP(kafka_launch_fused_add_rmsnorm_slab(bptr(out), out.stride(0), x.data_ptr<float>(), x.size(0),
+                                                  T * d, bptr(residual), residual.stride(0), bptr(w), T, d, eps,
+                                                  cur_stream()));
+  else
+    CHECK_HIP(kafka_launch_fused_add_rmsnorm(bptr(out), out.stride(0), bptr(x), x.stride(0), bptr(residual),
+                                              residual.stride(0), bptr(w), T, d, eps, cur_stream()));
+}
+
+// x: bf16 [T, 2F] or slab [S, T, 2F]
 static void silu_mul(at::Tensor out, at::Tensor x) {
-  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(out, at::kBFloat16);
-  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && out.is_contiguous() && x.stride(1) == 1, "silu_mul: 2-D");
+  CHECK_CUDA(x); CHECK_DT(out, at::kBFloat16);
+  const bool slab = is_slab(x);
+  if (slab) check_slab(x); else CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK((slab || (x.dim() == 2 && x.stride(1) == 1)) && out.dim() == 2 && out.is_contiguous(),
+              "silu_mul: 2-D (or slab)");
   const int F = out.size(1);
-  TORCH_CHECK(x.size(1) == 2 * F && F % 8 == 0 && out.size(0) == x.size(0), "silu_mul: bad shapes");
-  CHECK_HIP(kafka_launch_silu_mul(bptr(out), bptr(x), x.stride(0), x.size(0), F, cur_stream()));
+  const int64_t T = x.size(slab ? 1 : 0);
+  TORCH_CHECK(x.size(slab ? 2 : 1) == 2 * F && F % 8 == 0 && out.size(0) == T, "silu_mul: bad shapes");
+  if (slab)
+    CHECK_HIP(kafka_launch_silu_mul_slab(bptr(out), x.data_ptr<float>(), x.size(0), T * 2 * F, T, F, cur_stream()));
+  else
+    CHECK_HIP(kafka_launch_silu_mul(bptr(out), bptr(x), x.stride(0), T, F, cur_stream()));
 }
 
 static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin, at::Tensor q_out,
                           at::Tensor k_cache, at::Tensor v_cache, c10::optional<at::Tensor> slot_mapping, int64_t Hq,
                           int64_t Hkv) {
-  CHECK_CUDA(qkv); CHECK_DT(qkv, at::kBFloat16); CHECK_DT(q_out, at::kBFloat16);
+  CHECK_CUDA(qkv); CHECK_DT(q_out, at::kBFloat16);
+  const bool slab = is_slab(qkv);
+  if (slab) check_slab(qkv); else CHECK_DT(qkv, at::kBFloat16);
   CHECK_DT(positions, at::kLong); CHECK_DT(cos_sin, at::kFloat);
   CHECK_DT(k_cache, at::kBFloat16); CHECK_DT(v_cache, at::kBFloat16);
   TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && cos_sin.is_contiguous() &&
@@ -109,8 +143,9 @@ static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_s
                   v_cache.size(0) == k_cache.size(0), "rope_kv_write: cache shape mismatch");
   TORCH_CHECK(bs == 16, "page size must be 16");
   TORCH_CHECK(D == 128 || D == 64, "head dim must be 64 or 128");
-  const int T = qkv.size(0);
-  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv shape");
+  const int T = qkv.size(slab ? 1 : 0);
+  const int64_t W = (Hq + 2 * Hkv) * D;
+  TORCH_CHECK(slab ? qkv.size(2) == W : (qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) == W), "qkv shape");
   TORCH_CHECK(positions.numel() == T && cos_sin.dim() == 2 && cos_sin.size(1) == D, "positions/cos_sin shape");
   TORCH_CHECK(q_out.dim() == 3 && q_out.size(0) == T && q_out.size(1) == Hq && q_out.size(2) == D &&
                   q_out.stride(2) == 1 && q_out.stride(1) == D, "q_out shape");
@@ -120,8 +155,10 @@ static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_s
     TORCH_CHECK(slot_mapping->numel() == T && slot_mapping->is_contiguous(), "slot_mapping shape");
     sm = slot_mapping->data_ptr<int64_t>();
   }
-  CHECK_HIP(kafka_launch_rope_kv(bptr(qkv), qkv.stride(0), positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
-                                  bptr(q_out), q_out.stride(0), bptr(k_cache), bptr(v_cache), sm, T, Hq, Hkv, D, bs,
+  CHECK_HIP(kafka_launch_rope_kv(slab ? nullptr : bptr(qkv), slab ? qkv.data_ptr<float>() : nullptr,
+                                  slab ? qkv.size(0) : 0, slab ? (int64_t)T * W : 0, slab ? W : qkv.stride(0),
+                                  positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), bptr(q_out),
+                                  q_out.stride(0), bptr(k_cache), bptr(v_cache), sm, T, Hq, Hkv, D, bs,
                                   cur_stream()));
 }
 
@@ -273,6 +310,55 @@ static void skinny_gemm(at::Tensor x, at::Tensor w, at::Tensor out, int64_t U) {
                                      K, (int)U, splitk, kpw, cur_stream()));
 }
 
+// (mt, kc, splits) of the weight-streaming decode GEMM for a shape, or (0, 0, 0) if unsupported
+static std::vector<int64_t> wstream_plan(int64_t M, int64_t N, int64_t K, int64_t max_splits) {
+  int mt = 0, kc = 0, s = 0;
+  if (kafka_wstream_plan((int)M, (int)N, (int)K, (int)max_splits, &mt, &kc, &s) != 0) return {0, 0, 0};
+  return {mt, kc, s};
+}
+
+// x [M, K] bf16 . W^T with W given wave-tiled as wt [N/32, K/16, 64, 8] (ops.tile_weight). Writes bf16 y [M, N]
+// (splits == 1) or fp32 slabs p [splits, M, N].
+static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y, c10::optional<at::Tensor> p,
+                         int64_t max_splits, bool nt) {
+  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
+  TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0, "wstream_gemm: x must be [M, K] with 16-B rows");
+  TORCH_CHECK(wt.dim() == 4 && wt.is_contiguous() && wt.size(2) == 64 && wt.size(3) == 8,
+              "wstream_gemm: wt must be contiguous [N/32, K/16, 64, 8]");
+  const int M = x.size(0), K = x.size(1), N = wt.size(0) * 32;
+  TORCH_CHECK(wt.size(1) * 16 == K, "wstream_gemm: K mismatch");
+  int mt = 0, kc = 0, s = 0;
+  TORCH_CHECK(kafka_wstream_plan(M, N, K, (int)max_splits, &mt, &kc, &s) == 0, "wstream_gemm: unsupported shape");
+  bf16* yp = nullptr;
+  int64_t ldy = 0;
+  float* pp = nullptr;
+  if (s == 1) {
+    TORCH_CHECK(y.has_value(), "wstream_gemm: y required for a single split");
+    CHECK_DT(y.value(), at::kBFloat16); CHECK_LASTDIM(y.value());
+    TORCH_CHECK(y->dim() == 2 && y->size(0) == M && y->size(1) == N, "wstream_gemm: y shape");
+    yp = bptr(y.value());
+    ldy = y->stride(0);
+  } else {
+    TORCH_CHECK(p.has_value(), "wstream_gemm: slab output required");
+    CHECK_DT(p.value(), at::kFloat);
+    TORCH_CHECK(p->is_contiguous() && p->dim() == 3 && p->size(0) == s && p->size(1) == M && p->size(2) == N,
+                "wstream_gemm: slab shape must be [splits, M, N]");
+    pp = p->data_ptr<float>();
+  }
+  CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, nt ? 1 : 0, yp, ldy, pp,
+                                      cur_stream()));
+}
+
+// y [M, N] bf16 = sum over the slabs p [S, M, N]
+static void slab_reduce(at::Tensor p, at::Tensor y) {
+  CHECK_CUDA(p); CHECK_DT(p, at::kFloat); CHECK_DT(y, at::kBFloat16); CHECK_LASTDIM(y);
+  check_slab(p);
+  TORCH_CHECK(y.dim() == 2 && y.size(0) == p.size(1) && y.size(1) == p.size(2) && y.stride(0) % 8 == 0,
+              "slab_reduce: y must be [M, N]");
+  CHECK_HIP(kafka_launch_slab_reduce(p.data_ptr<float>(), p.size(0), p.size(1), p.size(2), bptr(y), y.stride(0),
+                                     cur_stream()));
+}
+
 // softmax -> top-k -> renormalise + stable expert sort (one kernel, no host sync)
 static void moe_route(at::Tensor logits, int64_t k, int64_t bm, at::Tensor topk_w, at::Tensor topk_e,
                       at::Tensor perm_tok, at::Tensor perm_w, at::Tensor expert_off, at::Tensor tile_off) {
@@ -381,6 +467,9 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("sample", &sample);
   m.def("skinny_supported", &skinny_supported);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("wstream_plan", &wstream_plan);
+  m.def("wstream_gemm", &wstream_gemm);
+  m.def("slab_reduce", &slab_reduce);
   m.def("moe_route", &moe_route);
   m.def("car_alloc", &car_alloc);
   m.def("car_ipc_handle", &car_ipc_handle);

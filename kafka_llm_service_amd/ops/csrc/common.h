@@ -64,6 +64,30 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 __device__ __forceinline__ bf16x8 load_bf16x8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 __device__ __forceinline__ void store_bf16x8(bf16* p, bf16x8 v) { *reinterpret_cast<bf16x8*>(p) = v; }
 
+// 8 consecutive fp32 values at element offset `off` of a bf16 tensor x, or — when xp is set — the sum of S fp32
+// split-K slabs (slab stride ps elements, same element offset): the decode GEMM (wstream_gemm.hip) leaves its output
+// as slabs and the consuming kernel combines them while loading.
+__device__ __forceinline__ void load_in8(float (&v)[8], const bf16* __restrict__ x, const float* __restrict__ xp,
+                                         int S, int64_t ps, int64_t off) {
+  if (xp) {
+    f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+    const float* p = xp + off;
+    for (int s = 0; s < S; ++s) {
+      a += *reinterpret_cast<const f32x4*>(p + s * ps);
+      b += *reinterpret_cast<const f32x4*>(p + s * ps + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = a[j];
+      v[4 + j] = b[j];
+    }
+  } else {
+    const bf16x8 a = load_bf16x8(x + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)a[j];
+  }
+}
+
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }

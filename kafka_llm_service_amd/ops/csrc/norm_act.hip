@@ -4,6 +4,10 @@
 // row kept in registers between the reduction and the scale pass (one HBM read + one write per element),
 // fp32 accumulation. The residual add is fused into the norm so the decoder layer reads the residual
 // stream once per sub-block instead of three times.
+//
+// Split-K slab inputs: the decode GEMM (wstream_gemm.hip) leaves its output as S fp32 partial slabs
+// P[S][T][n]; every kernel here can take such a slab instead of a bf16 input and sums the S partials while
+// loading (load_in8 in common.h), so the split-K combine costs no launch of its own.
 #include "common.h"
 
 namespace kafka {
@@ -12,7 +16,8 @@ namespace kafka {
 // If RESID: r = x + r (rounded to bf16, written back to r), y = norm(r) * w.
 template <int NV, bool RESID>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(bf16* __restrict__ out, int64_t out_stride,
-                                                       const bf16* __restrict__ x, int64_t x_stride,
+                                                       const bf16* __restrict__ x, const float* __restrict__ xp,
+                                                       int S, int64_t ps, int64_t x_stride,
                                                        bf16* __restrict__ resid, int64_t r_stride,
                                                        const bf16* __restrict__ w, int d, float eps) {
   __shared__ float red[4];
@@ -24,20 +29,19 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(bf16* __restrict__ out, in
   for (int i = 0; i < NV; ++i) {
     const int vi = threadIdx.x + i * 256;
     if (vi < nvec) {
-      bf16x8 a = load_bf16x8(x + row * x_stride + vi * 8);
+      load_in8(v[i], x, xp, S, ps, row * x_stride + vi * 8);
       if constexpr (RESID) {
-        bf16x8 b = load_bf16x8(resid + row * r_stride + vi * 8);
+        const bf16x8 b = load_bf16x8(resid + row * r_stride + vi * 8);
         bf16x8 s;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s[j] = (bf16)((float)a[j] + (float)b[j]);
+        for (int j = 0; j < 8; ++j) {
+          s[j] = (bf16)(v[i][j] + (float)b[j]);
+          v[i][j] = (float)s[j];
+        }
         store_bf16x8(resid + row * r_stride + vi * 8, s);
-        a = s;
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[i][j] = (float)a[j];
-        ss += v[i][j] * v[i][j];
-      }
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
     }
   }
   ss = block_sum<256>(ss, red);
@@ -55,50 +59,56 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(bf16* __restrict__ out, in
   }
 }
 
-// out[t, :] = silu(x[t, :F]) * x[t, F:]   (x: [T, 2F] row stride xs, out: [T, F] contiguous)
+// out[t, :] = silu(x[t, :F]) * x[t, F:]   (x: [T, 2F] row stride xs (bf16 or slabs), out: [T, F] contiguous)
 __global__ __launch_bounds__(256) void silu_mul_kernel(bf16* __restrict__ out, const bf16* __restrict__ x,
+                                                        const float* __restrict__ xp, int S, int64_t ps,
                                                         int64_t xs, int F) {
   const int64_t row = blockIdx.y;
   const int nvec = F >> 3;
   for (int vi = blockIdx.x * 256 + threadIdx.x; vi < nvec; vi += gridDim.x * 256) {
-    bf16x8 g = load_bf16x8(x + row * xs + vi * 8);
-    bf16x8 u = load_bf16x8(x + row * xs + F + vi * 8);
+    float g[8], u[8];
+    load_in8(g, x, xp, S, ps, row * xs + vi * 8);
+    load_in8(u, x, xp, S, ps, row * xs + F + vi * 8);
     bf16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float gf = (float)g[j];
-      float s = gf / (1.0f + __expf(-gf));
-      o[j] = (bf16)(s * (float)u[j]);
-    }
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)(g[j] / (1.0f + __expf(-g[j])) * u[j]);
     store_bf16x8(out + row * (int64_t)F + vi * 8, o);
   }
 }
 
 template <bool RESID>
-static hipError_t launch_rmsnorm_t(bf16* out, int64_t os, const bf16* x, int64_t xs, bf16* r, int64_t rs,
-                                   const bf16* w, int T, int d, float eps, hipStream_t st) {
+static hipError_t launch_rmsnorm_t(bf16* out, int64_t os, const bf16* x, const float* xp, int S, int64_t ps,
+                                   int64_t xs, bf16* r, int64_t rs, const bf16* w, int T, int d, float eps,
+                                   hipStream_t st) {
   const int nvec = d / 8;
   const int nv = (nvec + 255) / 256;
   dim3 grid(T), block(256);
   if (T == 0) return hipSuccess;
   switch (nv) {
-    case 1: rmsnorm_kernel<1, RESID><<<grid, block, 0, st>>>(out, os, x, xs, r, rs, w, d, eps); break;
-    case 2: rmsnorm_kernel<2, RESID><<<grid, block, 0, st>>>(out, os, x, xs, r, rs, w, d, eps); break;
+    case 1: rmsnorm_kernel<1, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
+    case 2: rmsnorm_kernel<2, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
     case 3:
-    case 4: rmsnorm_kernel<4, RESID><<<grid, block, 0, st>>>(out, os, x, xs, r, rs, w, d, eps); break;
-    default: rmsnorm_kernel<8, RESID><<<grid, block, 0, st>>>(out, os, x, xs, r, rs, w, d, eps); break;
+    case 4: rmsnorm_kernel<4, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
+    default: rmsnorm_kernel<8, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
   }
   return hipGetLastError();
 }
 
 extern "C" hipError_t kafka_launch_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs, const bf16* w, int T, int d,
                           float eps, hipStream_t st) {
-  return launch_rmsnorm_t<false>(out, os, x, xs, nullptr, 0, w, T, d, eps, st);
+  return launch_rmsnorm_t<false>(out, os, x, nullptr, 0, 0, xs, nullptr, 0, w, T, d, eps, st);
 }
 
 extern "C" hipError_t kafka_launch_fused_add_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs, bf16* resid, int64_t rs,
                                     const bf16* w, int T, int d, float eps, hipStream_t st) {
-  return launch_rmsnorm_t<true>(out, os, x, xs, resid, rs, w, T, d, eps, st);
+  return launch_rmsnorm_t<true>(out, os, x, nullptr, 0, 0, xs, resid, rs, w, T, d, eps, st);
+}
+
+// fused add + RMSNorm whose x input is S fp32 split-K slabs [S][T][d] (row stride d, slab stride ps)
+extern "C" hipError_t kafka_launch_fused_add_rmsnorm_slab(bf16* out, int64_t os, const float* xp, int S, int64_t ps,
+                                                         bf16* resid, int64_t rs, const bf16* w, int T, int d,
+                                                         float eps, hipStream_t st) {
+  return launch_rmsnorm_t<true>(out, os, nullptr, xp, S, ps, d, resid, rs, w, T, d, eps, st);
 }
 
 extern "C" hipError_t kafka_launch_silu_mul(bf16* out, const bf16* x, int64_t xs, int T, int F, hipStream_t st) {
@@ -106,7 +116,18 @@ extern "C" hipError_t kafka_launch_silu_mul(bf16* out, const bf16* x, int64_t xs
   const int nvec = F / 8;
   int gx = (nvec + 255) / 256;
   if (gx > 64) gx = 64;
-  silu_mul_kernel<<<dim3(gx, T), dim3(256), 0, st>>>(out, x, xs, F);
+  silu_mul_kernel<<<dim3(gx, T), dim3(256), 0, st>>>(out, x, nullptr, 0, 0, xs, F);
+  return hipGetLastError();
+}
+
+// SwiGLU over S fp32 split-K slabs [S][T][2F]
+extern "C" hipError_t kafka_launch_silu_mul_slab(bf16* out, const float* xp, int S, int64_t ps, int T, int F,
+                                                hipStream_t st) {
+  if (T == 0) return hipSuccess;
+  const int nvec = F / 8;
+  int gx = (nvec + 255) / 256;
+  if (gx > 64) gx = 64;
+  silu_mul_kernel<<<dim3(gx, T), dim3(256), 0, st>>>(out, nullptr, xp, S, ps, 2 * (int64_t)F, F);
   return hipGetLastError();
 }
 

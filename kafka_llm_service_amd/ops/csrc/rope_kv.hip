@@ -1,8 +1,12 @@
 // Rotary embedding on Q/K fused with the paged KV-cache write (gfx950).
 //
-// Input is the fused QKV projection output [T, (Hq + 2*Hkv) * D]. One workgroup per token:
+// Input is the fused QKV projection output [T, (Hq + 2*Hkv) * D] — bf16, or S fp32 split-K slabs of the decode
+// GEMM (wstream_gemm.hip) summed while loading. One workgroup per token:
 //   * Q heads: rotate-half RoPE -> q_out[T, Hq, D]
-//   * K heads: rotate-half RoPE -> k_cache page  [num_blocks, Hkv, 16, D]   (key-major rows, 256 B per key)
+//   * K heads: rotate-half RoPE -> k_cache page  [num_blocks, Hkv, 16, D]   as D/8 chunk planes [D/8][16 keys][8]:
+//              element (key o, d) at ((d >> 3) * 16 + o) * 8 + (d & 7). The MFMA A fragment of a 16-key page for
+//              k-step kk (lanes: 16 keys x 2 halves of 8 d) is then ONE contiguous 512-B run (chunks 2kk, 2kk+1),
+//              where a key-major page gives 16 rows x 32 B per wave-instruction.
 //   * V heads: copy            -> v_cache page  [num_blocks, Hkv, D, 16]   (d-major: V^T per page)
 // The V^T page stores key offset o at position swap_bits_2_3(o). With that permutation the PV step of the
 // attention kernels (O^T = V^T . P, P taken straight from the S^T accumulator registers of
@@ -18,7 +22,8 @@ namespace kafka {
 __device__ __forceinline__ int vt_pos(int o) { return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1); }
 
 template <int D>
-__global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ qkv, int64_t qkv_stride,
+__global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ qkv, const float* __restrict__ qp,
+                                                       int S, int64_t ps, int64_t qkv_stride,
                                                        const int64_t* __restrict__ positions,
                                                        const float* __restrict__ cos_sin,
                                                        bf16* __restrict__ q_out, int64_t q_stride,
@@ -31,7 +36,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
   const int64_t t = blockIdx.x;
   const int64_t pos = positions[t];
   const int64_t slot = slot_mapping ? slot_mapping[t] : -1;
-  const bf16* row = qkv + t * qkv_stride;
+  const int64_t row = t * qkv_stride;
   const float* cs = cos_sin + pos * D;
   const int n_rope = (Hq + Hkv) * RU;
   const int n_total = n_rope + Hkv * VU;
@@ -41,9 +46,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
     if (u < n_rope) {
       const int head = u / RU;
       const int c = (u % RU) * 8;
-      const bf16* src = row + head * D;
-      bf16x8 x1 = load_bf16x8(src + c);
-      bf16x8 x2 = load_bf16x8(src + HALF + c);
+      float x1[8], x2[8];
+      load_in8(x1, qkv, qp, S, ps, row + head * D + c);
+      load_in8(x2, qkv, qp, S, ps, row + head * D + HALF + c);
       f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + c);
       f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + c + 4);
       f32x4 s0 = *reinterpret_cast<const f32x4*>(cs + HALF + c);
@@ -53,7 +58,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
       bf16x8 o1, o2;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float a = (float)x1[j], b = (float)x2[j];
+        const float a = x1[j], b = x2[j];
         o1[j] = (bf16)(a * cv[j] - b * sv[j]);
         o2[j] = (bf16)(b * cv[j] + a * sv[j]);
       }
@@ -63,33 +68,37 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
         store_bf16x8(dst + HALF + c, o2);
       } else if (slot >= 0) {
         const int kh = head - Hq;
-        bf16* dst = k_cache + ((blk * Hkv + kh) * block_size + off) * D;
-        store_bf16x8(dst + c, o1);
-        store_bf16x8(dst + HALF + c, o2);
+        bf16* dst = k_cache + (blk * Hkv + kh) * (int64_t)block_size * D + off * 8;
+        store_bf16x8(dst + (c >> 3) * block_size * 8, o1);
+        store_bf16x8(dst + ((HALF + c) >> 3) * block_size * 8, o2);
       }
     } else if (slot >= 0) {
       const int v = u - n_rope;
       const int vh = v / VU;
       const int c = (v % VU) * 8;
-      bf16x8 x = load_bf16x8(row + (Hq + Hkv + vh) * D + c);
+      float x[8];
+      load_in8(x, qkv, qp, S, ps, row + (Hq + Hkv + vh) * D + c);
       bf16* dst = v_cache + (blk * Hkv + vh) * (int64_t)D * block_size + vt_pos(off);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dst[(int64_t)(c + j) * block_size] = x[j];
+      for (int j = 0; j < 8; ++j) dst[(int64_t)(c + j) * block_size] = (bf16)x[j];
     }
   }
 }
 
-extern "C" hipError_t kafka_launch_rope_kv(const bf16* qkv, int64_t qkv_stride, const int64_t* positions, const float* cos_sin,
-                          bf16* q_out, int64_t q_stride, bf16* k_cache, bf16* v_cache, const int64_t* slot_mapping,
-                          int T, int Hq, int Hkv, int D, int block_size, hipStream_t st) {
+// qp != nullptr: the input is S fp32 slabs [S][T][(Hq + 2 Hkv) D] (slab stride ps) instead of bf16 qkv
+extern "C" hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int S, int64_t ps, int64_t qkv_stride,
+                                          const int64_t* positions, const float* cos_sin, bf16* q_out,
+                                          int64_t q_stride, bf16* k_cache, bf16* v_cache,
+                                          const int64_t* slot_mapping, int T, int Hq, int Hkv, int D,
+                                          int block_size, hipStream_t st) {
   if (T == 0) return hipSuccess;
   if (D != 128 && D != 64) return hipErrorInvalidValue;
   if (D == 128)
-    rope_kv_kernel<128><<<T, 256, 0, st>>>(qkv, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache, v_cache,
-                                           slot_mapping, Hq, Hkv, block_size);
+    rope_kv_kernel<128><<<T, 256, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
+                                           v_cache, slot_mapping, Hq, Hkv, block_size);
   else
-    rope_kv_kernel<64><<<T, 256, 0, st>>>(qkv, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache, v_cache,
-                                          slot_mapping, Hq, Hkv, block_size);
+    rope_kv_kernel<64><<<T, 256, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
+                                          v_cache, slot_mapping, Hq, Hkv, block_size);
   return hipGetLastError();
 }
 

@@ -1,0 +1,213 @@
+// Weight-streaming decode GEMM on pre-tiled weights (gfx950):   Y[M, N] = X[M, K] . W[N, K]^T,  M <= 128.
+//
+// At decode the weights are read exactly once per step and M (running sequences) is small, so this GEMM is an HBM
+// stream of W with just enough MFMA work riding on it. Two layout decisions make the stream full-rate:
+//
+//   * W is stored "wave-tiled" (done once at load time, ops.tile_weight):  Wt[N/32][K/16][64 lanes][8] bf16 with
+//     lane l = (r = l & 31, h = l >> 5) holding W[32 nb + r][16 kb + 8 h + j]. That is exactly the B fragment of
+//     v_mfma_f32_32x32x16_bf16 for a 32-column tile, so every wave-instruction of the stream is ONE contiguous 1 KB
+//     read (16 B per lane, non-temporal: each byte is used once), and one wave's whole K slice is a single
+//     contiguous run. (A row-major [N, K] weight read as MFMA fragments touches 32 rows x 32 B per instruction.)
+//   * X (the activations, <= 128 x K bf16, L2-resident) is staged per 128/256-deep K chunk into LDS with full-line
+//     coalesced loads and read back as A fragments with ds_read_b128 from an XOR-swizzled image (chunk c of row m
+//     at c ^ (m & 15): the 16 lanes of one LDS cycle hit 16 different bank groups). The 4 waves of a workgroup own 4
+//     different 32-column tiles and share each X chunk, so X costs 1/4 of the W traffic on-chip and nothing in HBM.
+//
+// Work decomposition: workgroup = 4 waves = 128 output columns x one K split; grid (ceil(N / 128), S). S (1..8)
+// is chosen on the host so the grid has >= 256 workgroups when N is small. S == 1 writes bf16 Y directly; S > 1
+// writes fp32 partial slabs P[S][M][N] that the NEXT kernel sums while reading its input (rope_kv, fused
+// add+RMSNorm, SwiGLU all accept slabs), so split-K costs no extra launch and no extra bf16 round trip.
+// Pipelining: X chunk c+1 and the W fragments of chunk c+1 are issued before the MFMAs of chunk c; the LDS image of
+// chunk c+1 is written after them (issue-early / write-late, one barrier per chunk).
+// C = X . W^T comes out with lanes along N (col = lane & 31), so every epilogue store instruction writes two
+// 128-B row segments.
+#include "common.h"
+
+namespace kafka {
+
+template <int MT, int KC, bool NT>
+__global__ __launch_bounds__(256) void wstream_gemm_kernel(const bf16* __restrict__ X, int64_t ldx,
+                                                            const bf16x8* __restrict__ Wt, int M, int N, int K,
+                                                            int ks, bf16* __restrict__ Y, int64_t ldy,
+                                                            float* __restrict__ P) {
+  constexpr int ROWS = 32 * MT;
+  constexpr int CPR = KC / 8;             // 16-B chunks per X row of one K chunk
+  constexpr int XL = ROWS * CPR / 256;    // X chunks staged per thread
+  constexpr int KSTEP = KC / 16;          // MFMA k-steps per K chunk
+  static_assert(CPR >= 16 && XL >= 1, "chunk too small for the swizzle");
+  __shared__ __attribute__((aligned(16))) bf16 xs[2][ROWS * KC];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int nb = blockIdx.x * 4 + w;
+  // wave-uniform: a tail wave past the last column tile streams a valid tile and skips only its stores — every
+  // load and MFMA stays unconditional, so hipcc's waitcnt pass sees straight-line code and keeps counted vmcnt
+  // waits (a divergent `if` around the loads collapses them to vmcnt(0..1) at the join)
+  const bool active = nb < (N >> 5);
+  const int k0 = blockIdx.y * ks;
+  const int nchunks = ks / KC;
+  const bf16x8* wp = Wt + ((int64_t)(active ? nb : (N >> 5) - 1) * (K >> 4) + (k0 >> 4)) * 64 + lane;
+
+  bf16x8 xr[XL];
+  auto load_x = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < XL; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / CPR, c = idx % CPR;
+      const int m = row < M ? row : M - 1;  // rows >= M compute garbage that is never stored
+      xr[i] = load_bf16x8(X + (int64_t)m * ldx + k0 + ch * KC + c * 8);
+    }
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < XL; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / CPR, c = idx % CPR;
+      *reinterpret_cast<bf16x8*>(&xs[buf][row * KC + 8 * (c ^ (row & 15))]) = xr[i];
+    }
+  };
+  auto load_w = [&](bf16x8(&wv)[KSTEP], int ch) {
+#pragma unroll
+    for (int t = 0; t < KSTEP; ++t) {
+      const bf16x8* p = wp + (int64_t)(ch * KSTEP + t) * 64;
+      wv[t] = NT ? __builtin_nontemporal_load(p) : *p;
+    }
+  };
+  f32x16 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
+  auto compute = [&](int buf, const bf16x8(&wv)[KSTEP]) {
+#pragma unroll
+    for (int t = 0; t < KSTEP; ++t) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = mt * 32 + r, c = 2 * t + h;
+        const bf16x8 xf = *reinterpret_cast<const bf16x8*>(&xs[buf][m * KC + 8 * (c ^ (m & 15))]);
+        acc[mt] = mfma32(xf, wv[t], acc[mt]);
+      }
+    }
+  };
+
+  bf16x8 wa[KSTEP], wb[KSTEP];
+  load_x(0);
+  load_w(wa, 0);
+  store_x(0);
+  __syncthreads();
+  // steady state: two chunks per trip, both prefetches in range (no conditional loads inside the trip)
+  int ch = 0;
+  for (; ch + 2 < nchunks; ch += 2) {
+    load_x(ch + 1);
+    load_w(wb, ch + 1);
+    compute(0, wa);
+    store_x(1);
+    __syncthreads();
+    load_x(ch + 2);
+    load_w(wa, ch + 2);
+    compute(1, wb);
+    store_x(0);
+    __syncthreads();
+  }
+  // tail: one or two chunks left (chunk ch is in buffer 0 / wa)
+  if (ch + 1 < nchunks) {
+    load_x(ch + 1);
+    load_w(wb, ch + 1);
+    compute(0, wa);
+    store_x(1);
+    __syncthreads();
+    compute(1, wb);
+  } else {
+    compute(0, wa);
+  }
+
+  if (!active) return;
+  const int n = nb * 32 + r;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (m < M) {
+        if (P)
+          P[((int64_t)blockIdx.y * M + m) * N + n] = acc[mt][i];
+        else
+          Y[(int64_t)m * ldy + n] = (bf16)acc[mt][i];
+      }
+    }
+}
+
+// Y[m, n] = sum_s P[s, m, n] (bf16), 8 columns per thread: the standalone combine for callers without a
+// slab-aware consumer (TP all-reduce inputs, tests).
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ P, int S, int M, int N,
+                                                          bf16* __restrict__ Y, int64_t ldy) {
+  const int64_t idx = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (idx >= (int64_t)M * N) return;
+  const int m = (int)(idx / N), n = (int)(idx % N);
+  const int64_t ps = (int64_t)M * N;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < S; ++s) {
+    const float* p = P + s * ps + idx;
+    a += *reinterpret_cast<const f32x4*>(p);
+    b += *reinterpret_cast<const f32x4*>(p + 4);
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = (bf16)a[j];
+    o[4 + j] = (bf16)b[j];
+  }
+  store_bf16x8(Y + (int64_t)m * ldy + n, o);
+}
+
+// Host plan: row tiles MT, K chunk KC and split count S for a shape; returns 0 if supported.
+//   max_splits caps S (1 forces a direct bf16 output).
+extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits) {
+  if (M < 1 || M > 128 || N % 32 != 0 || N <= 0) return 1;
+  const int MT = M <= 32 ? 1 : (M <= 64 ? 2 : 4);
+  const int KC = MT == 4 ? 128 : 256;
+  if (K % KC != 0 || K <= 0) return 2;
+  const int nx = (N + 127) / 128;
+  const int chunks = K / KC;
+  int s = 1;
+  while (s * 2 <= max_splits && s * 2 <= 8 && chunks % (s * 2) == 0 && nx * s < 256) s *= 2;
+  *mt = MT;
+  *kc = KC;
+  *splits = s;
+  return 0;
+}
+
+extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K,
+                                               int mt, int kc, int splits, int nt, bf16* Y, int64_t ldy, float* P,
+                                               hipStream_t st) {
+  if (M < 1) return hipSuccess;
+  if (K % (kc * splits) != 0 || (splits > 1 && P == nullptr) || (splits == 1 && P == nullptr && Y == nullptr))
+    return hipErrorInvalidValue;
+  const dim3 grid((N + 127) / 128, splits);
+  const int ks = K / splits;
+  const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
+  float* p = splits > 1 ? P : nullptr;
+#define KAFKA_WS(MT_, KC_, NT_) \
+  wstream_gemm_kernel<MT_, KC_, NT_><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p)
+  if (mt == 1 && kc == 256) {
+    if (nt) KAFKA_WS(1, 256, true); else KAFKA_WS(1, 256, false);
+  } else if (mt == 2 && kc == 256) {
+    if (nt) KAFKA_WS(2, 256, true); else KAFKA_WS(2, 256, false);
+  } else if (mt == 4 && kc == 128) {
+    if (nt) KAFKA_WS(4, 128, true); else KAFKA_WS(4, 128, false);
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef KAFKA_WS
+  return hipGetLastError();
+}
+
+extern "C" hipError_t kafka_launch_slab_reduce(const float* P, int S, int M, int N, bf16* Y, int64_t ldy,
+                                              hipStream_t st) {
+  if (M < 1) return hipSuccess;
+  if (N % 8 != 0) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)M * N / 8;
+  slab_reduce_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(P, S, M, N, Y, ldy);
+  return hipGetLastError();
+}
+
+}  // namespace kafka

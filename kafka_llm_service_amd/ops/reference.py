@@ -2,7 +2,8 @@
 
 They define the numerics the CDNA4 kernels are tested against, and they are the CPU execution path used by the
 unit tests (no GPU in CI). They use exactly the same tensor layouts as the kernels, including the paged KV layout
-  K page: [num_blocks, Hkv, 16, D]      V page: [num_blocks, Hkv, D, 16]  (V^T, key offset o at vt_pos(o)).
+  K page: [num_blocks, Hkv, 16, D] holding D/8 chunk planes [D/8][16 keys][8] (k_planes / k_natural below)
+  V page: [num_blocks, Hkv, D, 16]  (V^T, key offset o at vt_pos(o)).
 """
 from __future__ import annotations
 
@@ -24,6 +25,18 @@ def vt_pos(o: torch.Tensor | int):
 _VT_PERM = torch.tensor([vt_pos(o) for o in range(PAGE)], dtype=torch.long)
 
 
+def k_planes(k_cache: torch.Tensor) -> torch.Tensor:
+    """View of a K cache [nb, Hkv, 16, D] as its chunk planes [nb, Hkv, D/8, 16 keys, 8] (the memory layout)."""
+    nb, hkv, _, D = k_cache.shape
+    return k_cache.view(nb, hkv, D // 8, PAGE, 8)
+
+
+def k_natural(k_pages: torch.Tensor) -> torch.Tensor:
+    """K pages [n, Hkv, 16, D] as stored -> [n, Hkv, 16 keys, D] in natural (key, d) order."""
+    n, hkv, _, D = k_pages.shape
+    return k_pages.reshape(n, hkv, D // 8, PAGE, 8).permute(0, 1, 3, 2, 4).reshape(n, hkv, PAGE, D)
+
+
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
     xf = x.float()
     r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
@@ -31,7 +44,7 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
 
 
 def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float):
-    s = (x.float() + residual.float()).to(x.dtype)
+    s = (x.float() + residual.float()).to(residual.dtype)
     return rmsnorm(s, w, eps), s
 
 
@@ -61,7 +74,7 @@ def rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping
         if s < 0:
             continue
         blk, off = divmod(s, PAGE)
-        k_cache[blk, :, off, :] = k[t]
+        k_planes(k_cache)[blk, :, :, off, :] = k[t].reshape(Hkv, D // 8, 8)
         v_cache[blk, :, :, vt_pos(off)] = v[t]
 
 
@@ -69,7 +82,7 @@ def gather_kv(k_cache, v_cache, block_table, length: int):
     """Materialise [length, Hkv, D] K and V for one sequence from the paged caches (fp32)."""
     nb = (length + PAGE - 1) // PAGE
     ids = block_table[:nb].long()
-    k = k_cache[ids].float()  # [nb, Hkv, 16, D]
+    k = k_natural(k_cache[ids].float())  # [nb, Hkv, 16, D]
     v = v_cache[ids].float()  # [nb, Hkv, D, 16]
     v = v[..., _VT_PERM.to(v.device)]  # undo the page permutation -> [nb, Hkv, D, 16] natural key order
     k = k.permute(0, 2, 1, 3).reshape(nb * PAGE, k.shape[1], k.shape[3])[:length]

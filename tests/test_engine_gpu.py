@@ -18,10 +18,10 @@ def eng(cuda):
                                   cascade_min_prefix=64, prefill_kv_chunk=256))
 
 
-def _prompts(seed, shared, tails):
+def _prompts(seed, shared, tails, vocab=50000):
     g = torch.Generator().manual_seed(seed)
-    prefix = torch.randint(0, 50000, (shared,), generator=g).tolist()
-    return [prefix + torch.randint(0, 50000, (n,), generator=g).tolist() for n in tails]
+    prefix = torch.randint(0, vocab, (shared,), generator=g).tolist()
+    return [prefix + torch.randint(0, vocab, (n,), generator=g).tolist() for n in tails]
 
 
 def _oracle_ok(model, prompts, outs, tol=0.15):
@@ -61,7 +61,7 @@ def test_native_extension_loaded(eng):
 def test_mixtral_engine_matches_oracle(cuda):
     """Mixtral MoE through the HIP router + grouped GEMM kernels vs the dense oracle's per-expert loop."""
     e = LLMEngine(EngineConfig(model="tiny-mixtral", device="cuda:0", num_kv_blocks=1024, max_model_len=4096))
-    prompts = _prompts(3, 64, (5, 40, 130))
+    prompts = _prompts(3, 64, (5, 40, 130), vocab=e.model_cfg.vocab_size)
     outs = e.generate(prompts, GREEDY)
     _oracle_ok(e.model, prompts, outs)
 

@@ -256,3 +256,55 @@ def test_grouped_gemm(cuda, T, d, N, E, e_lo, e_n):
     out_ref = torch.zeros(T, d)
     ref.grouped_gemm(h.cpu(), w2.cpu(), rc.perm_tok, rc.perm_w, rc.expert_off, e_lo, False, None, out_ref)
     _close(out, out_ref, atol=0.02, rtol=0.01, msg="combine")
+
+
+@pytest.mark.parametrize("M", [1, 7, 32, 33, 64, 65, 128])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1280, 8192), (16032, 1024), (96, 512)])
+def test_wstream_gemm(cuda, M, N, K):
+    """Weight-streaming decode GEMM on wave-tiled weights (bf16 direct and split-K slabs) vs fp32 matmul."""
+    torch.manual_seed(11)
+    x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+    wt = ops.tile_weight(w)
+    assert torch.equal(ops.untile_weight(wt), w)
+    ref_y = x.float() @ w.float().t()
+    for ms in (1, 8):
+        y = ops.linear_stream(x, wt, max_splits=ms)
+        plan = ops.stream_plan(M, N, K, ms)
+        if plan[2] == 1:
+            assert y.dtype == torch.bfloat16 and y.shape == (M, N)
+        else:
+            assert ops.is_slab(y) and y.shape == (plan[2], M, N)
+        _close(ops.slab_reduce(y), ref_y, atol=0.02, rtol=0.01, msg=f"wstream M={M} N={N} K={K} ms={ms}")
+        torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("T", [1, 37, 64])
+def test_slab_consumers(cuda, T):
+    """fused_add_rmsnorm / silu_mul / rope_kv_write fed with split-K slabs == the same ops on the summed input."""
+    torch.manual_seed(12)
+    S, d, F = 4, 4096, 2048
+    p = torch.randn(S, T, d, device=cuda)
+    r1 = torch.randn(T, d, device=cuda, dtype=torch.bfloat16)
+    r2 = r1.clone()
+    w = torch.randn(d, device=cuda, dtype=torch.bfloat16)
+    y = ops.fused_add_rmsnorm(p, r1, w, 1e-5)
+    y_ref, s_ref = ref.fused_add_rmsnorm(p.sum(0).cpu(), r2.cpu(), w.cpu(), 1e-5)
+    _close(r1, s_ref, atol=2e-2, rtol=1e-2, msg="slab residual")
+    _close(y, y_ref, atol=0.05, rtol=0.01, msg="slab norm")
+    g = torch.randn(S, T, 2 * F, device=cuda)
+    _close(ops.silu_mul(g), ref.silu_mul(g.sum(0).cpu()), atol=0.03, rtol=0.01, msg="slab silu")
+    Hq, Hkv, D, nb = 32, 8, 128, 8
+    qkv = torch.randn(S, T, (Hq + 2 * Hkv) * D, device=cuda)
+    pos = torch.randint(0, 4000, (T,), device=cuda, dtype=torch.long)
+    cs = ref.rope_cos_sin(8192, D, 500000.0, None, device=cuda)
+    slots = torch.randperm(nb * 16, device=cuda)[:T].long()
+    q = torch.empty(T, Hq, D, device=cuda, dtype=torch.bfloat16)
+    k, v = _make_cache(nb, Hkv, D, cuda)
+    ops.rope_kv_write(qkv, pos, cs, q, k, v, slots, Hq, Hkv)
+    q2 = torch.empty(T, Hq, D, dtype=torch.bfloat16)
+    k2, v2 = _make_cache(nb, Hkv, D)
+    ref.rope_kv_write(qkv.sum(0).cpu(), pos.cpu(), cs.cpu(), q2, k2, v2, slots.cpu(), Hq, Hkv)
+    _close(q, q2, atol=0.05, rtol=0.01, msg="slab q")
+    _close(k, k2, atol=0.05, rtol=0.01, msg="slab k")
+    _close(v, v2, atol=0.02, rtol=0.01, msg="slab v")

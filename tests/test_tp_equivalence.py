@@ -98,7 +98,7 @@ def _logits_main(rank: int, world: int, port: int, q, model: str) -> None:
         if st.is_tp_leader:
             lg = _capture_logits(eng, _prompts()[1])
             tp_worker.release_followers()
-            q.put(lg)
+            q.put(lg.float().numpy())  # numpy pickles by value: no fd hand-off that dies with this process
         else:
             tp_worker.follower_loop(eng)
     finally:
@@ -115,7 +115,7 @@ def test_tp2_logits_close_to_tp1(model):
     procs = [ctx.Process(target=_logits_main, args=(r, 2, port, q, model)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=240)
+    got = torch.from_numpy(q.get(timeout=240))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
