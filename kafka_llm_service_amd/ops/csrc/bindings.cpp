@@ -349,6 +349,25 @@ static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> 
                                       cur_stream()));
 }
 
+// explicit-configuration variant (microbenchmark sweeps): (mt, kc, splits) as given, no planning
+static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y, c10::optional<at::Tensor> p,
+                             int64_t mt, int64_t kc, int64_t s, bool nt) {
+  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
+  TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0 && wt.dim() == 4 && wt.is_contiguous(), "wstream_gemm_cfg: x/wt");
+  const int M = x.size(0), K = x.size(1), N = wt.size(0) * 32;
+  TORCH_CHECK(wt.size(1) * 16 == K && M >= 1 && M <= 32 * mt && K % (kc * s) == 0, "wstream_gemm_cfg: shape/config");
+  if (s == 1) {
+    TORCH_CHECK(y.has_value() && y->dim() == 2 && y->size(0) == M && y->size(1) == N, "wstream_gemm_cfg: y");
+    CHECK_DT(y.value(), at::kBFloat16); CHECK_LASTDIM(y.value());
+  } else {
+    TORCH_CHECK(p.has_value() && p->is_contiguous() && p->numel() == s * M * N, "wstream_gemm_cfg: p");
+    CHECK_DT(p.value(), at::kFloat);
+  }
+  CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, (int)mt, (int)kc, (int)s, nt ? 1 : 0,
+                                      s == 1 ? bptr(y.value()) : nullptr, s == 1 ? y->stride(0) : 0,
+                                      s == 1 ? nullptr : p->data_ptr<float>(), cur_stream()));
+}
+
 // y [M, N] bf16 = sum over the slabs p [S, M, N]
 static void slab_reduce(at::Tensor p, at::Tensor y) {
   CHECK_CUDA(p); CHECK_DT(p, at::kFloat); CHECK_DT(y, at::kBFloat16); CHECK_LASTDIM(y);
@@ -469,6 +488,7 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("skinny_gemm", &skinny_gemm);
   m.def("wstream_plan", &wstream_plan);
   m.def("wstream_gemm", &wstream_gemm);
+  m.def("wstream_gemm_cfg", &wstream_gemm_cfg);
   m.def("slab_reduce", &slab_reduce);
   m.def("moe_route", &moe_route);
   m.def("car_alloc", &car_alloc);

@@ -67,14 +67,37 @@ __device__ __forceinline__ void store_bf16x8(bf16* p, bf16x8 v) { *reinterpret_c
 // 8 consecutive fp32 values at element offset `off` of a bf16 tensor x, or — when xp is set — the sum of S fp32
 // split-K slabs (slab stride ps elements, same element offset): the decode GEMM (wstream_gemm.hip) leaves its output
 // as slabs and the consuming kernel combines them while loading.
+template <int S>
+__device__ __forceinline__ void sum_slabs8(f32x4& a, f32x4& b, const float* __restrict__ p, int64_t ps) {
+  f32x4 va[S], vb[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {  // every slab load in flight before the first add (one HBM latency, not S)
+    va[s] = *reinterpret_cast<const f32x4*>(p + s * ps);
+    vb[s] = *reinterpret_cast<const f32x4*>(p + s * ps + 4);
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    a += va[s];
+    b += vb[s];
+  }
+}
+
+// 8 consecutive inputs as fp32: from bf16 x, or summed over S fp32 split-K slabs xp (slab stride ps)
 __device__ __forceinline__ void load_in8(float (&v)[8], const bf16* __restrict__ x, const float* __restrict__ xp,
                                          int S, int64_t ps, int64_t off) {
   if (xp) {
     f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
     const float* p = xp + off;
-    for (int s = 0; s < S; ++s) {
-      a += *reinterpret_cast<const f32x4*>(p + s * ps);
-      b += *reinterpret_cast<const f32x4*>(p + s * ps + 4);
+    switch (S) {  // uniform branch; each case fully unrolled
+      case 1: sum_slabs8<1>(a, b, p, ps); break;
+      case 2: sum_slabs8<2>(a, b, p, ps); break;
+      case 4: sum_slabs8<4>(a, b, p, ps); break;
+      case 8: sum_slabs8<8>(a, b, p, ps); break;
+      default:
+        for (int s = 0; s < S; ++s) {
+          a += *reinterpret_cast<const f32x4*>(p + s * ps);
+          b += *reinterpret_cast<const f32x4*>(p + s * ps + 4);
+        }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

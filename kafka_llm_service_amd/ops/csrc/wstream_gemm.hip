@@ -144,18 +144,11 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   if (idx >= (int64_t)M * N) return;
   const int m = (int)(idx / N), n = (int)(idx % N);
   const int64_t ps = (int64_t)M * N;
-  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < S; ++s) {
-    const float* p = P + s * ps + idx;
-    a += *reinterpret_cast<const f32x4*>(p);
-    b += *reinterpret_cast<const f32x4*>(p + 4);
-  }
+  float v[8];
+  load_in8(v, nullptr, P, S, ps, idx);
   bf16x8 o;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    o[j] = (bf16)a[j];
-    o[4 + j] = (bf16)b[j];
-  }
+  for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
   store_bf16x8(Y + (int64_t)m * ldy + n, o);
 }
 
@@ -168,8 +161,12 @@ extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, 
   if (K % KC != 0 || K <= 0) return 2;
   const int nx = (N + 127) / 128;
   const int chunks = K / KC;
+  // split until the grid reaches ~192 (MT <= 2) / 256 (MT = 4) workgroups: measured on MI355X
+  // (benchmarks/wstream_sweep.py, profiles/wstream_sweep_r01.log) — every extra split adds 2 x M x N x 4 B of slab
+  // traffic, so e.g. gate_up (N = 28672) at M = 64 runs fastest unsplit and qkv (N = 6144) with S = 4
+  const int target = MT == 4 ? 256 : 192;
   int s = 1;
-  while (s * 2 <= max_splits && s * 2 <= 8 && chunks % (s * 2) == 0 && nx * s < 256) s *= 2;
+  while (s * 2 <= max_splits && s * 2 <= 8 && chunks % (s * 2) == 0 && nx * s < target) s *= 2;
   *mt = MT;
   *kc = KC;
   *splits = s;
@@ -190,6 +187,10 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   wstream_gemm_kernel<MT_, KC_, NT_><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p)
   if (mt == 1 && kc == 256) {
     if (nt) KAFKA_WS(1, 256, true); else KAFKA_WS(1, 256, false);
+  } else if (mt == 1 && kc == 512) {
+    if (nt) KAFKA_WS(1, 512, true); else KAFKA_WS(1, 512, false);
+  } else if (mt == 2 && kc == 128) {
+    if (nt) KAFKA_WS(2, 128, true); else KAFKA_WS(2, 128, false);
   } else if (mt == 2 && kc == 256) {
     if (nt) KAFKA_WS(2, 256, true); else KAFKA_WS(2, 256, false);
   } else if (mt == 4 && kc == 128) {
