@@ -163,6 +163,12 @@ def main():
     if dev.startswith("cuda"):
         torch.cuda.synchronize()
     _barrier(leaders)
+    prof = None
+    if os.environ.get("KAFKA_CPROFILE"):  # host-side profile of the timed steps only (scripts/gpu_cpu_prof.sh)
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     window[0] = t0
     for _ in range(args.steps):
@@ -170,6 +176,14 @@ def main():
     if dev.startswith("cuda"):
         torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if prof is not None:
+        import pstats
+
+        prof.disable()
+        with open(os.environ["KAFKA_CPROFILE"], "w") as f:
+            st = pstats.Stats(prof, stream=f)
+            st.sort_stats("tottime").print_stats(50)
+            st.sort_stats("cumtime").print_stats(60)
     _barrier(leaders)
     if tp > 1:
         tp_worker.release_followers()

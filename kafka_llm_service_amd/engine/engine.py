@@ -74,6 +74,14 @@ class _Plan:
     n_added: int
 
 
+@dataclass
+class _InFlight:
+    sampled: list           # sequences with a row in the step's sampler output
+    slots: list             # index of each one's PENDING placeholder in its output_ids
+    launched: object        # ModelRunner.Launched
+    t0: float
+
+
 def _agree_min(n: int) -> int:
     import torch.distributed as dist
 
@@ -142,7 +150,7 @@ class LLMEngine:
         self.requests: dict[str, Sequence] = {}
         self.stats = {"steps": 0, "prompt_tokens": 0, "cached_tokens": 0, "output_tokens": 0, "step_time": 0.0,
                       "replans": 0, "planned_ahead": 0}
-        self._plan: _Plan | None = None
+        self._inflight: _InFlight | None = None  # the step on the GPU that has not been collected yet
         self._n_added = 0
         self.stop_checker_factory = None  # set by the frontend: (request params) -> incremental stop-string checker
         log.info("engine ready: %s tp=%d kv pages=%d (%.1f GB) load %.1fs", mc.name, cfg.tp, nb,
@@ -184,6 +192,8 @@ class LLMEngine:
     def abort(self, request_id: str) -> None:
         seq = self.requests.pop(request_id, None)
         if seq is not None and not seq.finished:
+            while seq.output_ids and seq.output_ids[-1] == PENDING:  # tokens of in-flight steps are void now
+                seq.output_ids.pop()
             self.sched.finish(seq, "abort")
 
     def has_unfinished(self) -> bool:
@@ -201,32 +211,59 @@ class LLMEngine:
     def step(self) -> list[StepOutput]:
         """Run one engine iteration and return the tokens it produced.
 
-        With ``async_scheduling`` the host work of the NEXT iteration (scheduling, page allocation, block tables,
-        attention work items: ~1 ms of Python/C++ for 64 long-context threads) is done while the GPU runs this one:
-        the sequences sampled by the in-flight step carry a PENDING placeholder token, their decode rows are patched
-        with the real ids at launch. A plan is dropped (and redone after the step lands) when requests arrived or
-        sequences finished in between, so new turns are never delayed and no row is computed for a finished
-        sequence; sequences that will finish by length are left out of speculative plans up front."""
+        With ``async_scheduling`` the GPU always has the NEXT step queued behind the one being waited on: step n+1 is
+        planned on the host (scheduling, page allocation, block tables, attention work items) and LAUNCHED while step
+        n still runs, then step n is collected. Decode rows of n+1 whose input token is being sampled by n carry a
+        PENDING placeholder; the runner copies those ids device-side from n's sampler output, so the host never waits
+        for a token before enqueueing the next forward. Rows planned for sequences that then finish at n (EOS, stop
+        string, abort) compute one void token that is discarded; sequences that will finish by length are left out of
+        speculative plans up front. Steps whose sampling needs the landed tokens on the host (token-constrained tool
+        calls, penalties) and TP leaders (followers mirror host plans) launch after collecting n instead; a plan that
+        would have to preempt is redone synchronously."""
         if self.fi.active:
             self.fi.on_step()
-        plan = self._plan
-        self._plan = None
-        if plan is not None and (plan.n_added != self._n_added or any(s.finished for s in plan.seqs)):
-            plan = None
-            self.stats["replans"] += 1
-        if plan is None:
+        cut: list[StepOutput] = []
+        if self._inflight is None:
             with trace.span("schedule"):
                 batch = self.sched.schedule()
                 cut = self._cut_outputs(batch)
                 if batch.empty:
                     return cut
                 host, sampled = self.runner.build_host(batch)
-        else:
-            batch, host, sampled = plan.batch, plan.host, plan.sampled
+            self._inflight = self._launch(batch, host, sampled, None)
+        cur = self._inflight
+        self._inflight = None
+        plan = None
+        if self.cfg.async_scheduling:
+            with trace.span("plan_ahead"):
+                plan = self._speculate()
+        if plan is not None and self.runner.broadcast is None and not self._needs_landed(plan.sampled):
             self.stats["planned_ahead"] += 1
+            self._inflight = self._launch(plan.batch, plan.host, plan.sampled, cur)
+            plan = None
+        outs = cut + self._finish_step(cur)
+        if plan is not None:
+            if plan.n_added != self._n_added or any(s.finished for s in plan.seqs):
+                self.stats["replans"] += 1  # dropped: the next call plans again with the landed tokens
+            else:
+                self.stats["planned_ahead"] += 1
+                self._inflight = self._launch(plan.batch, plan.host, plan.sampled, None)
+        return outs
+
+    @staticmethod
+    def _needs_landed(sampled: list[Sequence]) -> bool:
+        """True if a row's sampling reads the sequence's previous tokens on the host while one is still PENDING."""
+        for s in sampled:
+            p = s.params
+            if (p.allowed_tokens_fn is not None or p.presence_penalty or p.frequency_penalty) and PENDING in \
+                    s.output_ids[-2:]:
+                return True
+        return False
+
+    def _launch(self, batch, host, sampled: list[Sequence], prev: "_InFlight | None") -> "_InFlight":
         t0 = time.perf_counter()
         with trace.span("launch", B=host.B, T=host.T):
-            launched = self.runner.launch(host, sampled)
+            launched = self.runner.launch(host, sampled, prev.launched if prev is not None else None)
         # advance computed counts + register completed pages in the prefix tree (the step's KV writes are ordered
         # before any later reader on the stream); the sampled tokens are pending until the step lands
         for s in batch.decode:
@@ -237,19 +274,23 @@ class LLMEngine:
             self.kvm.commit(s.seq_id, s.num_computed)
         for s, a, b in batch.prefill:
             self.kvm.commit(s.seq_id, s.num_computed)
+        slots = []
         for s in sampled:
+            slots.append(len(s.output_ids))
             s.output_ids.append(PENDING)
-        if self.cfg.async_scheduling:
-            with trace.span("plan_ahead"):
-                self._plan = self._speculate()
+        return _InFlight(sampled, slots, launched, t0)
+
+    def _finish_step(self, cur: "_InFlight") -> list[StepOutput]:
         with trace.span("collect"):
-            toks = self.runner.collect(launched)
+            toks = self.runner.collect(cur.launched)
         now = time.perf_counter()
-        self.stats["step_time"] += now - t0
+        self.stats["step_time"] += now - cur.t0
         self.stats["steps"] += 1
-        outs: list[StepOutput] = [] if plan is not None else cut
-        for s, t in zip(sampled, toks):
-            s.output_ids[-1] = t
+        outs: list[StepOutput] = []
+        for s, idx, t in zip(cur.sampled, cur.slots, toks):
+            if s.finished:  # ended (stop / abort) while this step was in flight: its row was void
+                continue
+            s.output_ids[idx] = t
             self.kvm.append_token(s.seq_id, t)
             if s.first_token_time is None:
                 s.first_token_time = now
@@ -257,13 +298,15 @@ class LLMEngine:
                 self.stats["cached_tokens"] += s.num_cached
             s.last_token_time = now
             self.stats["output_tokens"] += 1
-            reason = self._check_stop(s, t)
+            n_out = idx + 1
+            reason = self._check_stop(s, t, n_out)
             if reason:
+                del s.output_ids[n_out:]  # rows already planned past the end
                 self.sched.finish(s, reason)
                 self.requests.pop(s.request_id, None)
                 trace.request_span(s, now)
-            outs.append(StepOutput(s.request_id, [t], reason is not None, reason, len(s.prompt_ids),
-                                   len(s.output_ids), s.num_cached))
+            outs.append(StepOutput(s.request_id, [t], reason is not None, reason, len(s.prompt_ids), n_out,
+                                   s.num_cached))
         return outs
 
     def _cut_outputs(self, batch) -> list[StepOutput]:
@@ -285,7 +328,7 @@ class LLMEngine:
         seqs = list(batch.decode) + [s for s, _, _ in batch.prefill]
         return _Plan(batch, host, sampled, seqs, self._n_added)
 
-    def _check_stop(self, s: Sequence, t: int) -> str | None:
+    def _check_stop(self, s: Sequence, t: int, n_out: int) -> str | None:
         p = s.params
         if not p.ignore_eos and t in self.eos:
             return "stop"
@@ -293,9 +336,9 @@ class LLMEngine:
             return "stop"
         if s.stop_checker is not None and s.stop_checker(t):
             return "stop"
-        if len(s.output_ids) >= p.max_tokens:
+        if n_out >= p.max_tokens:
             return "length"
-        if s.total_len >= self.cfg.max_model_len:
+        if len(s.prompt_ids) + n_out >= self.cfg.max_model_len:
             return "length"
         return None
 

@@ -59,7 +59,7 @@ class DecodeGraphs:
     @staticmethod
     def key(h, sp) -> tuple:
         return (h.B, h.splits, h.prefix_splits, h.n_prefix_items, bool(h.cascade_prefix), h.i64.size, h.i32.size,
-                sp.greedy)
+                h.n_late, h.late_off, sp.greedy)
 
     def eligible(self, h, sp) -> bool:
         return (not self.disabled and h.B > 0 and h.T == h.B and h.n_items == 0 and not sp.procs
@@ -116,6 +116,7 @@ class DecodeGraphs:
             else:
                 toks = ops.sample(logits, e.f32[:n], e.f32[n:], e.topk, e.seeds)
             e.out.copy_(toks)
+            r.tok_buf[:n].copy_(toks)  # input ids of the next step's late rows (ModelRunner.views)
 
         self._load(e, h, sp)
         if self.backend == "fake":

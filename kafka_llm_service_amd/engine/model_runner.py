@@ -10,6 +10,7 @@ batches run eagerly.
 from __future__ import annotations
 
 import math
+from collections import deque
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -44,6 +45,10 @@ class HostStep:
     # (row, seq, position): decode inputs whose token was still being sampled at planning time, filled at launch
     patch: list = field(default_factory=list)
     stats: dict = field(default_factory=dict)
+    # rows filled on the device from ModelRunner.tok_buf: i64[late_off : +n_late] = destination token rows,
+    # i64[late_off + n_late : +n_late] = source rows of the previous step's sampler output
+    n_late: int = 0
+    late_off: int = 0
 
 
 @dataclass
@@ -60,6 +65,8 @@ class SampleParams:
 class Launched:
     tokens: torch.Tensor            # sampled ids (pinned host buffer on GPU, plain tensor on CPU)
     event: object = None            # completion event of the D2H copy
+    dev_tokens: torch.Tensor | None = None  # the sampler's device output (input ids of the next step's decode rows)
+    rows: dict | None = None        # seq_id -> row of dev_tokens
 
 
 def decode_splits(B: int, hkv: int, max_keys: int, target_wgs: int = 512, min_keys_per_split: int = 256) -> int:
@@ -92,8 +99,12 @@ class ModelRunner:
         self._bt = np.zeros((max_num_seqs * 2, max_blocks_per_seq), dtype=np.int32)
         self._pin = pin
         self.last_stats: dict = {}
+        self.recent_stats: deque = deque(maxlen=16)  # stats of the last launched steps (two can be in flight)
         self.broadcast = None  # set on a TP leader: callable(HostStep) (engine/tp_worker.py)
-        self._tok_host = None  # pinned landing buffer of the sampled ids
+        self._tok_host = None  # pinned landing buffers of the sampled ids
+        # every step's sampled ids also land here (fixed address, so hipGraphs can read it): the next step's decode
+        # rows whose token was still being sampled at launch gather their input ids from it on the stream
+        self.tok_buf = torch.zeros(max_num_seqs * 2 + 64, dtype=torch.int64, device=self.device)
         self.graphs = None  # engine/graphs.py DecodeGraphs when hipGraph decode is enabled
 
     # ------------------------------------------------------------------------------------------------------------
@@ -239,6 +250,9 @@ class ModelRunner:
                                                 device=self.device)
                 meta.prefill_lse = torch.full((Tp, Hq, h.prefill_splits), float("-inf"), dtype=torch.float32,
                                               device=self.device)
+        if h.n_late:
+            L, n = h.late_off, h.n_late
+            t_tokens.index_copy_(0, d64[L:L + n], self.tok_buf.index_select(0, d64[L + n:L + 2 * n]))
         return StepInput(t_tokens, t_pos, t_slots, meta, t_rows)
 
     def _host(self, a: np.ndarray) -> torch.Tensor:
@@ -326,14 +340,33 @@ class ModelRunner:
         return sample_seqs, self.collect(self.launch(host, sample_seqs))
 
     @torch.inference_mode()
-    def launch(self, host: HostStep, sample_seqs: list[Sequence]) -> "Launched":
+    def launch(self, host: HostStep, sample_seqs: list[Sequence], prev: Launched | None = None) -> Launched:
         """Enqueue one step on the GPU without waiting for it: (TP broadcast) -> H2D -> forward -> sample -> async
-        D2H of the sampled ids into pinned memory. ``collect`` waits for them."""
-        for row, s, pos in host.patch:  # decode inputs that were still being sampled when the step was planned
-            host.i64[row] = s.token_at(pos)
+        D2H of the sampled ids into pinned memory. ``collect`` waits for them.
+
+        Decode rows whose input token was PENDING at planning time are filled from the host if the token has landed
+        since, else device-side from ``prev`` (the in-flight step that samples it): one gather + scatter on the
+        stream, so the launch never waits for the previous step."""
+        late_dst, late_src = [], []
+        for row, s, pos in host.patch:
+            t = s.token_at(pos)
+            if t >= 0:
+                host.i64[row] = t
+            else:
+                if prev is None or prev.rows is None or s.seq_id not in prev.rows:
+                    raise RuntimeError(f"decode row {row}: token {pos} of seq {s.seq_id} is neither landed nor in "
+                                       "the in-flight step")
+                late_dst.append(row)
+                late_src.append(prev.rows[s.seq_id])
         host.patch = []
+        if late_dst:
+            host.late_off, host.n_late = host.i64.size, len(late_dst)
+            host.i64 = np.concatenate([host.i64, np.asarray(late_dst + late_src, dtype=np.int64)])
         self.last_stats = host.stats
+        self.recent_stats.append(host.stats)
         if self.broadcast is not None:  # TP leader: followers run the same step on their shards
+            if late_dst:
+                raise RuntimeError("TP steps must be launched with landed tokens")
             self.broadcast(host)
         sp = self.sample_params(sample_seqs)
         toks = None
@@ -343,16 +376,21 @@ class ModelRunner:
             inp = self.to_device(host)
             logits = self.model.forward(inp, self.k_caches, self.v_caches)
             toks = self.sample_device(logits, sp)
+            self.tok_buf[:toks.shape[0]].copy_(toks)
+        rows = {s.seq_id: i for i, s in enumerate(sample_seqs)}
         if self.device.type != "cuda":
-            return Launched(toks, None)
+            return Launched(toks.clone(), None, toks, rows)
         n = toks.shape[0]
-        if self._tok_host is None or self._tok_host.shape[0] < n or self._tok_host.dtype != toks.dtype:
-            self._tok_host = torch.empty(max(n, 256), dtype=toks.dtype, pin_memory=True)
-        out = self._tok_host[:n]
+        # a ring of pinned landing buffers: two steps can be in flight, each D2H needs its own
+        ring = self._tok_host
+        if ring is None or ring[0].shape[0] < n or ring[0].dtype != toks.dtype:
+            ring = self._tok_host = [torch.empty(max(n, 256), dtype=toks.dtype, pin_memory=True) for _ in range(3)]
+        self._tok_i = (getattr(self, "_tok_i", 0) + 1) % len(ring)
+        out = ring[self._tok_i][:n]
         out.copy_(toks, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        return Launched(out, ev)
+        return Launched(out, ev, toks, rows)
 
     def collect(self, h: "Launched") -> list[int]:
         if h.event is not None:

@@ -59,7 +59,7 @@ def test_cascade_equals_plain(base_engine):
     e2.generate([prompts[0][:96] + [7]], GREEDY)
     plain = e1.generate(prompts, GREEDY)
     casc = e2.generate(prompts, GREEDY)
-    assert e2.runner.last_stats["cascade_prefix"] >= 80
+    assert max(st["cascade_prefix"] for st in e2.runner.recent_stats) >= 80
     assert casc == plain
 
 
@@ -130,7 +130,7 @@ def test_split_kv_prefill_equals_plain(base_engine):
     e.generate([prompts[0][:290] + [3]], GREEDY)
     s = e.add_request("q", prompts[0], GREEDY)
     e.step()
-    assert e.runner.last_stats["prefill_splits"] >= 9
+    assert max(st["prefill_splits"] for st in e.runner.recent_stats) >= 9
     while not s.finished:
         e.step()
     assert s.output_ids == ref[0]
@@ -168,7 +168,37 @@ def test_async_scheduling_equals_sync(base_engine):
     sync_out, _ = run(False)
     async_out, st = run(True)
     assert async_out == sync_out
-    assert st["planned_ahead"] > 0 and st["replans"] > 0
+    assert st["planned_ahead"] > 0
+
+
+def test_overlapped_launch_stops_and_aborts(base_engine):
+    """Step n+1 is launched before step n lands (its decode inputs copied device-side from n's sampler output). A
+    sequence that stops on a token at n, or is aborted while both steps are in flight, gets no extra token; the
+    void row is discarded and every page is freed."""
+    prompts = _prompts(seed=13, shared=40, tails=(3, 17, 9))
+    ref = _engine(model=base_engine.model, async_scheduling=False)
+    free_run = ref.generate(prompts, SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True))
+    stop_tok = free_run[1][4]
+    sp = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True, stop_token_ids=[stop_tok])
+    want = ref.generate(prompts, sp)
+    eng = _engine(model=base_engine.model)
+    got = eng.generate(prompts, sp)
+    assert got == want and len(got[1]) <= 5 and got[1][-1] == stop_tok
+    seqs = [eng.add_request(f"a{i}", p, SamplingParams(temperature=0.0, max_tokens=30, ignore_eos=True))
+            for i, p in enumerate(prompts)]
+    for _ in range(4):
+        eng.step()
+    eng.abort("a1")
+    n_at_abort = len(seqs[1].output_ids)
+    while eng.has_unfinished():
+        eng.step()
+    eng.step()  # drain the last in-flight step
+    assert len(seqs[1].output_ids) == n_at_abort and seqs[1].finish_reason == "abort"
+    assert [s.output_ids for s in (seqs[0], seqs[2])] == [free_run[0] + s.output_ids[12:] for s in (seqs[0],)] + \
+        [free_run[2] + seqs[2].output_ids[12:]]
+    assert all(t >= 0 for s in seqs for t in s.output_ids)
+    eng.kvm.check_invariants()
+    assert eng.kv_stats()["sequences"] == 0
 
 
 def test_pinned_prefix_survives_eviction(base_engine):

@@ -45,8 +45,8 @@ def test_cascade_and_split_prefill(eng):
     saw_split = saw_cascade = False
     while any(not s.finished for s in seqs):
         eng.step()
-        saw_split |= eng.runner.last_stats["prefill_splits"] > 0
-        saw_cascade |= eng.runner.last_stats["cascade_prefix"] > 0
+        saw_split |= any(st["prefill_splits"] > 0 for st in eng.runner.recent_stats)
+        saw_cascade |= any(st["cascade_prefix"] > 0 for st in eng.runner.recent_stats)
     assert saw_split and saw_cascade
     _oracle_ok(eng.model, prompts, [s.output_ids for s in seqs])
 
