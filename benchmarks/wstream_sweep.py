@@ -15,12 +15,12 @@ from kafka_llm_service_amd.ops import _ext
 
 from wstream_bench import SHAPES, timeit  # noqa: E402
 
-VARIANTS = [(1, 256), (1, 512), (2, 128), (2, 256), (4, 128)]
+VARIANTS = [(1, 256, 1), (1, 256, 2), (2, 128, 1), (2, 128, 2), (2, 256, 1), (2, 256, 2), (4, 128, 1), (4, 128, 2)]
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--M", default="32,64,128")
+    ap.add_argument("--M", default="16,64,128")
     ap.add_argument("--shapes", default="8b.qkv,8b.o,8b.gate_up,8b.down,8b.lm_head")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -32,7 +32,8 @@ def main():
         wts = [ops.tile_weight((torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)) for _ in range(copies)]
         for M in [int(m) for m in args.M.split(",")]:
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
-            for mt, kc in VARIANTS:
+            ref = x.float() @ ops.untile_weight(wts[0]).float().t()
+            for mt, kc, kw in VARIANTS:
                 if M > 32 * mt:
                     continue
                 for s in (1, 2, 4, 8):
@@ -41,13 +42,17 @@ def main():
                     y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
                     p = torch.empty(s, M, N, device=dev) if s > 1 else None
 
-                    def run(wt, y=y, p=p, mt=mt, kc=kc, s=s):
-                        ext.wstream_gemm_cfg(x, wt, y if s == 1 else None, p, mt, kc, s, True)
+                    def run(wt, y=y, p=p, mt=mt, kc=kc, s=s, kw=kw):
+                        ext.wstream_gemm_cfg(x, wt, y if s == 1 else None, p, mt, kc, s, True, kw)
 
                     t = timeit([lambda wt=wt: run(wt) for wt in wts])
                     t_red = timeit([lambda: ext.slab_reduce(p, y)]) if s > 1 else 0.0
-                    print(json.dumps({"shape": name, "M": M, "mt": mt, "kc": kc, "S": s, "us": round(t, 1),
-                                      "TB/s": round(nbytes / t / 1e6, 2), "reduce_us": round(t_red, 1),
+                    run(wts[0])
+                    if s > 1:
+                        ext.slab_reduce(p, y)
+                    err = (y.float() - ref).abs().max().item()
+                    print(json.dumps({"shape": name, "M": M, "mt": mt, "kc": kc, "kw": kw, "S": s, "us": round(t, 1),
+                                      "TB/s": round(nbytes / t / 1e6, 2), "reduce_us": round(t_red, 1), "err": round(err, 4),
                                       "grid": ((N + 127) // 128) * s}), flush=True)
         del wts
         torch.cuda.empty_cache()

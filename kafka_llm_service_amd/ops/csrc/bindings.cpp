@@ -39,7 +39,7 @@ hipError_t kafka_launch_skinny_gemm(const bf16* X, int64_t ldx, const bf16* W, i
                                     hipStream_t st);
 int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits);
 hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt, int kc,
-                                     int splits, int nt, bf16* Y, int64_t ldy, float* P, hipStream_t st);
+                                     int splits, int nt, int kw, bf16* Y, int64_t ldy, float* P, hipStream_t st);
 hipError_t kafka_launch_slab_reduce(const float* P, int S, int M, int N, bf16* Y, int64_t ldy, hipStream_t st);
 hipError_t kafka_launch_moe_route(const bf16* logits, int64_t ld, int T, int E, int K, int BM, float* topk_w,
                                   int* topk_e, int* perm_tok, float* perm_w, int* expert_off, int* tile_off,
@@ -345,13 +345,13 @@ static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> 
                 "wstream_gemm: slab shape must be [splits, M, N]");
     pp = p->data_ptr<float>();
   }
-  CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, nt ? 1 : 0, yp, ldy, pp,
+  CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, nt ? 1 : 0, 1, yp, ldy, pp,
                                       cur_stream()));
 }
 
 // explicit-configuration variant (microbenchmark sweeps): (mt, kc, splits) as given, no planning
 static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y, c10::optional<at::Tensor> p,
-                             int64_t mt, int64_t kc, int64_t s, bool nt) {
+                             int64_t mt, int64_t kc, int64_t s, bool nt, int64_t kw) {
   CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0 && wt.dim() == 4 && wt.is_contiguous(), "wstream_gemm_cfg: x/wt");
   const int M = x.size(0), K = x.size(1), N = wt.size(0) * 32;
@@ -364,6 +364,7 @@ static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tens
     CHECK_DT(p.value(), at::kFloat);
   }
   CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, (int)mt, (int)kc, (int)s, nt ? 1 : 0,
+                                      (int)kw,
                                       s == 1 ? bptr(y.value()) : nullptr, s == 1 ? y->stride(0) : 0,
                                       s == 1 ? nullptr : p->data_ptr<float>(), cur_stream()));
 }

@@ -25,33 +25,38 @@
 
 namespace kafka {
 
-template <int MT, int KC, bool NT>
-__global__ __launch_bounds__(256) void wstream_gemm_kernel(const bf16* __restrict__ X, int64_t ldx,
-                                                            const bf16x8* __restrict__ Wt, int M, int N, int K,
-                                                            int ks, bf16* __restrict__ Y, int64_t ldy,
-                                                            float* __restrict__ P) {
+template <int MT, int KC, bool NT, int KW>
+__global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __restrict__ X, int64_t ldx,
+                                                                 const bf16x8* __restrict__ Wt, int M, int N, int K,
+                                                                 int ks, bf16* __restrict__ Y, int64_t ldy,
+                                                                 float* __restrict__ P) {
+  constexpr int NTH = 256 * KW;
   constexpr int ROWS = 32 * MT;
   constexpr int CPR = KC / 8;             // 16-B chunks per X row of one K chunk
-  constexpr int XL = ROWS * CPR / 256;    // X chunks staged per thread
+  constexpr int XL = ROWS * CPR / NTH;    // X chunks staged per thread
   constexpr int KSTEP = KC / 16;          // MFMA k-steps per K chunk
-  static_assert(CPR >= 16 && XL >= 1, "chunk too small for the swizzle");
+  constexpr int KSW = KSTEP / KW;         // k-steps of one wave (KW waves split each chunk along K)
+  static_assert(CPR >= 16 && XL >= 1 && KSW >= 1, "chunk too small");
+  static_assert(2 * ROWS * KC * 2 >= 4 * (KW - 1) * MT * 16 * 64 * 4, "LDS too small for the K-half reduction");
   __shared__ __attribute__((aligned(16))) bf16 xs[2][ROWS * KC];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ct = w & 3, kh = w >> 2;  // column tile of the workgroup, K part of the chunk
   const int r = lane & 31, h = lane >> 5;
-  const int nb = blockIdx.x * 4 + w;
+  const int nb = blockIdx.x * 4 + ct;
   // wave-uniform: a tail wave past the last column tile streams a valid tile and skips only its stores — every
   // load and MFMA stays unconditional, so hipcc's waitcnt pass sees straight-line code and keeps counted vmcnt
   // waits (a divergent `if` around the loads collapses them to vmcnt(0..1) at the join)
   const bool active = nb < (N >> 5);
   const int k0 = blockIdx.y * ks;
   const int nchunks = ks / KC;
-  const bf16x8* wp = Wt + ((int64_t)(active ? nb : (N >> 5) - 1) * (K >> 4) + (k0 >> 4)) * 64 + lane;
+  const bf16x8* wp =
+      Wt + ((int64_t)(active ? nb : (N >> 5) - 1) * (K >> 4) + (k0 >> 4) + kh * KSW) * 64 + lane;
 
   bf16x8 xr[XL];
   auto load_x = [&](int ch) {
 #pragma unroll
     for (int i = 0; i < XL; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NTH * i;
       const int row = idx / CPR, c = idx % CPR;
       const int m = row < M ? row : M - 1;  // rows >= M compute garbage that is never stored
       xr[i] = load_bf16x8(X + (int64_t)m * ldx + k0 + ch * KC + c * 8);
@@ -60,14 +65,14 @@ __global__ __launch_bounds__(256) void wstream_gemm_kernel(const bf16* __restric
   auto store_x = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < XL; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NTH * i;
       const int row = idx / CPR, c = idx % CPR;
       *reinterpret_cast<bf16x8*>(&xs[buf][row * KC + 8 * (c ^ (row & 15))]) = xr[i];
     }
   };
-  auto load_w = [&](bf16x8(&wv)[KSTEP], int ch) {
+  auto load_w = [&](bf16x8(&wv)[KSW], int ch) {
 #pragma unroll
-    for (int t = 0; t < KSTEP; ++t) {
+    for (int t = 0; t < KSW; ++t) {
       const bf16x8* p = wp + (int64_t)(ch * KSTEP + t) * 64;
       wv[t] = NT ? __builtin_nontemporal_load(p) : *p;
     }
@@ -77,19 +82,19 @@ __global__ __launch_bounds__(256) void wstream_gemm_kernel(const bf16* __restric
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
-  auto compute = [&](int buf, const bf16x8(&wv)[KSTEP]) {
+  auto compute = [&](int buf, const bf16x8(&wv)[KSW]) {
 #pragma unroll
-    for (int t = 0; t < KSTEP; ++t) {
+    for (int t = 0; t < KSW; ++t) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int m = mt * 32 + r, c = 2 * t + h;
+        const int m = mt * 32 + r, c = 2 * (kh * KSW + t) + h;
         const bf16x8 xf = *reinterpret_cast<const bf16x8*>(&xs[buf][m * KC + 8 * (c ^ (m & 15))]);
         acc[mt] = mfma32(xf, wv[t], acc[mt]);
       }
     }
   };
 
-  bf16x8 wa[KSTEP], wb[KSTEP];
+  bf16x8 wa[KSW], wb[KSW];
   load_x(0);
   load_w(wa, 0);
   store_x(0);
@@ -120,7 +125,28 @@ __global__ __launch_bounds__(256) void wstream_gemm_kernel(const bf16* __restric
     compute(0, wa);
   }
 
-  if (!active) return;
+  if constexpr (KW > 1) {
+    // the KW waves of a column tile hold partial sums over different k-steps: fold them through LDS (the X stage
+    // is dead now), every wave reaches both barriers
+    float* red = reinterpret_cast<float*>(&xs[0][0]);
+    __syncthreads();
+    if (kh > 0) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[((((kh - 1) * 4 + ct) * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
+    }
+    __syncthreads();
+    if (kh == 0) {
+#pragma unroll
+      for (int j = 1; j < KW; ++j)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[mt][i] += red[((((j - 1) * 4 + ct) * MT + mt) * 16 + i) * 64 + lane];
+    }
+  }
+  if (!active || kh != 0) return;
   const int n = nb * 32 + r;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -174,8 +200,8 @@ extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, 
 }
 
 extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K,
-                                               int mt, int kc, int splits, int nt, bf16* Y, int64_t ldy, float* P,
-                                               hipStream_t st) {
+                                               int mt, int kc, int splits, int nt, int kw, bf16* Y, int64_t ldy,
+                                               float* P, hipStream_t st) {
   if (M < 1) return hipSuccess;
   if (K % (kc * splits) != 0 || (splits > 1 && P == nullptr) || (splits == 1 && P == nullptr && Y == nullptr))
     return hipErrorInvalidValue;
@@ -183,21 +209,23 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   const int ks = K / splits;
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   float* p = splits > 1 ? P : nullptr;
-#define KAFKA_WS(MT_, KC_, NT_) \
-  wstream_gemm_kernel<MT_, KC_, NT_><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p)
-  if (mt == 1 && kc == 256) {
-    if (nt) KAFKA_WS(1, 256, true); else KAFKA_WS(1, 256, false);
-  } else if (mt == 1 && kc == 512) {
-    if (nt) KAFKA_WS(1, 512, true); else KAFKA_WS(1, 512, false);
-  } else if (mt == 2 && kc == 128) {
-    if (nt) KAFKA_WS(2, 128, true); else KAFKA_WS(2, 128, false);
-  } else if (mt == 2 && kc == 256) {
-    if (nt) KAFKA_WS(2, 256, true); else KAFKA_WS(2, 256, false);
-  } else if (mt == 4 && kc == 128) {
-    if (nt) KAFKA_WS(4, 128, true); else KAFKA_WS(4, 128, false);
-  } else {
-    return hipErrorInvalidValue;
-  }
+#define KAFKA_WS(MT_, KC_, KW_)                                                                             \
+  do {                                                                                                     \
+    if (nt)                                                                                                \
+      wstream_gemm_kernel<MT_, KC_, true, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p); \
+    else                                                                                                   \
+      wstream_gemm_kernel<MT_, KC_, false, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p); \
+  } while (0)
+  if (mt == 1 && kc == 256 && kw == 1) KAFKA_WS(1, 256, 1);
+  else if (mt == 1 && kc == 256 && kw == 2) KAFKA_WS(1, 256, 2);
+  else if (mt == 1 && kc == 512 && kw == 1) KAFKA_WS(1, 512, 1);
+  else if (mt == 2 && kc == 128 && kw == 1) KAFKA_WS(2, 128, 1);
+  else if (mt == 2 && kc == 128 && kw == 2) KAFKA_WS(2, 128, 2);
+  else if (mt == 2 && kc == 256 && kw == 1) KAFKA_WS(2, 256, 1);
+  else if (mt == 2 && kc == 256 && kw == 2) KAFKA_WS(2, 256, 2);
+  else if (mt == 4 && kc == 128 && kw == 1) KAFKA_WS(4, 128, 1);
+  else if (mt == 4 && kc == 128 && kw == 2) KAFKA_WS(4, 128, 2);
+  else return hipErrorInvalidValue;
 #undef KAFKA_WS
   return hipGetLastError();
 }
