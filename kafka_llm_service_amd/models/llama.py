@@ -36,7 +36,7 @@ class StepInput:
 
 class LayerWeights:
     __slots__ = ("input_norm", "post_norm", "qkv", "o", "gate_up", "down", "router", "w13", "w2", "expert_ids",
-                 "qkv_t", "o_t", "gate_up_t", "down_t")
+                 "qkv_t", "o_t", "gate_up_t", "down_t", "glu")
     STREAMED = ("qkv", "o", "gate_up", "down")  # projections with a wave-tiled copy for the decode GEMM
 
     def __init__(self):
@@ -82,7 +82,10 @@ class TransformerLM:
             for name in LayerWeights.STREAMED:
                 w = getattr(lw, name)
                 if w is not None and ops.stream_plan(1, w.shape[0], w.shape[1]) is not None:
-                    setattr(lw, name + "_t", ops.tile_weight(w))
+                    glu = name == "gate_up" and w.shape[0] % 64 == 0
+                    setattr(lw, name + "_t", ops.tile_weight(w, glu=glu))
+                    if name == "gate_up":
+                        lw.glu = glu
                     added += w.numel() * w.element_size()
         if ops.stream_plan(1, self.lm_head.shape[0], self.lm_head.shape[1]) is not None:
             self.lm_head_t = ops.tile_weight(self.lm_head)
@@ -127,8 +130,10 @@ class TransformerLM:
             if lw.router is not None:
                 delta = self.moe(x, lw)
             else:
-                gu = self._linear(x, lw.gate_up, lw.gate_up_t)
-                a = ops.silu_mul(gu)
+                if self.stream and lw.glu and 0 < T <= ops.STREAM_MAX_M:
+                    a = ops.linear_glu(x, lw.gate_up_t)  # SwiGLU in the GEMM epilogue (or on its slabs)
+                else:
+                    a = ops.silu_mul(F.linear(x, lw.gate_up))
                 delta = self._linear(a, lw.down, lw.down_t)
                 if self.tp > 1:
                     delta = pstate.tp_all_reduce(ops.slab_reduce(delta))

@@ -150,16 +150,23 @@ def skinny_gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = Non
     return out
 
 
-def tile_weight(w: torch.Tensor) -> torch.Tensor:
+def tile_weight(w: torch.Tensor, glu: bool = False) -> torch.Tensor:
     """Row-major weight [N, K] -> the wave-tiled layout [N/32, K/16, 64, 8] read by the weight-streaming decode GEMM
-    (csrc/wstream_gemm.hip): lane l = (r = l % 32, h = l // 32) of tile (nb, kb) holds W[32 nb + r, 16 kb + 8 h : +8]."""
+    (csrc/wstream_gemm.hip): lane l = (r = l % 32, h = l // 32) of tile (nb, kb) holds W[32 nb + r, 16 kb + 8 h : +8].
+    ``glu``: W = [gate; up] (N = 2F); the 32-row tiles are interleaved gate_0, up_0, gate_1, up_1, ... so one
+    workgroup holds matching gate/up columns and the GEMM can emit silu(gate) * up directly."""
     N, K = w.shape
-    return w.reshape(N // 32, 32, K // 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous().view(N // 32, K // 16, 64, 8)
+    t = w.reshape(N // 32, 32, K // 16, 2, 8).permute(0, 2, 3, 1, 4)
+    if glu:
+        t = t.reshape(2, N // 64, K // 16, 2, 32, 8).transpose(0, 1)
+    return t.contiguous().view(N // 32, K // 16, 64, 8)
 
 
-def untile_weight(wt: torch.Tensor) -> torch.Tensor:
+def untile_weight(wt: torch.Tensor, glu: bool = False) -> torch.Tensor:
     nb, kb = wt.shape[0], wt.shape[1]
-    return wt.view(nb, kb, 2, 32, 8).permute(0, 3, 1, 2, 4).reshape(nb * 32, kb * 16)
+    if glu:
+        wt = wt.view(nb // 2, 2, kb, 64, 8).transpose(0, 1).reshape(nb, kb, 64, 8)
+    return wt.reshape(nb, kb, 2, 32, 8).permute(0, 3, 1, 2, 4).reshape(nb * 32, kb * 16)
 
 
 STREAM_MAX_M = 128
@@ -181,10 +188,12 @@ def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, 
     return mt, kc, s
 
 
-def linear_stream(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, nt: bool = True) -> torch.Tensor:
+def linear_stream(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, nt: bool = True,
+                  glu: bool = False) -> torch.Tensor:
     """y = x @ W^T for decode-sized M (<= 128) from the wave-tiled weight ``wt``: the weight-streaming MFMA kernel.
     Returns bf16 [M, N] when the plan has one split, else the fp32 split-K slabs [S, M, N] (a slab; the consumer
-    kernels sum it while loading)."""
+    kernels sum it while loading). ``glu`` (wt tiled with glu=True): a one-split plan returns the ACTIVATED
+    silu(gate) * up [M, N/2] (fused epilogue); a split plan returns gate | up slabs as usual (see ``linear_glu``)."""
     M, K = x.shape
     N = wt.shape[0] * 32
     plan = stream_plan(M, N, K, max_splits)
@@ -193,18 +202,30 @@ def linear_stream(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, nt: bo
     S = plan[2]
     if _gpu(x):
         if S == 1:
-            y = torch.empty(M, N, dtype=x.dtype, device=x.device)
-            ext().wstream_gemm(x, wt, y, None, int(max_splits), bool(nt))
+            y = torch.empty(M, N // 2 if glu else N, dtype=x.dtype, device=x.device)
+            ext().wstream_gemm(x, wt, y, None, int(max_splits), bool(nt), bool(glu))
             return y
         p = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
-        ext().wstream_gemm(x, wt, None, p, int(max_splits), bool(nt))
+        ext().wstream_gemm(x, wt, None, p, int(max_splits), bool(nt), bool(glu))
         return p
-    w = untile_weight(wt).float()
+    w = untile_weight(wt, glu).float()
     xf = x.float()
     if S == 1:
-        return (xf @ w.t()).to(x.dtype)
+        y = xf @ w.t()
+        if glu:
+            return ref.silu_mul(y).to(x.dtype)
+        return y.to(x.dtype)
     ks = K // S
     return torch.stack([xf[:, s * ks:(s + 1) * ks] @ w[:, s * ks:(s + 1) * ks].t() for s in range(S)])
+
+
+def linear_glu(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8) -> torch.Tensor:
+    """silu(x @ Wg^T) * (x @ Wu^T) from GLU-tiled gate_up weights: fused into the GEMM epilogue when the plan has one
+    split, else the GEMM's slabs go through silu_mul."""
+    N = wt.shape[0] * 32
+    plan = stream_plan(x.shape[0], N, x.shape[1], max_splits)
+    y = linear_stream(x, wt, max_splits, glu=True)
+    return y if plan is not None and plan[2] == 1 else silu_mul(y)
 
 
 def slab_reduce(p: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

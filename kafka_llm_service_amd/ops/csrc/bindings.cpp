@@ -39,7 +39,8 @@ hipError_t kafka_launch_skinny_gemm(const bf16* X, int64_t ldx, const bf16* W, i
                                     hipStream_t st);
 int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits);
 hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt, int kc,
-                                     int splits, int nt, int kw, bf16* Y, int64_t ldy, float* P, hipStream_t st);
+                                     int splits, int nt, int kw, int glu, bf16* Y, int64_t ldy, float* P,
+                                     hipStream_t st);
 hipError_t kafka_launch_slab_reduce(const float* P, int S, int M, int N, bf16* Y, int64_t ldy, hipStream_t st);
 hipError_t kafka_launch_moe_route(const bf16* logits, int64_t ld, int T, int E, int K, int BM, float* topk_w,
                                   int* topk_e, int* perm_tok, float* perm_w, int* expert_off, int* tile_off,
@@ -320,22 +321,24 @@ static std::vector<int64_t> wstream_plan(int64_t M, int64_t N, int64_t K, int64_
 // x [M, K] bf16 . W^T with W given wave-tiled as wt [N/32, K/16, 64, 8] (ops.tile_weight). Writes bf16 y [M, N]
 // (splits == 1) or fp32 slabs p [splits, M, N].
 static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y, c10::optional<at::Tensor> p,
-                         int64_t max_splits, bool nt) {
+                         int64_t max_splits, bool nt, bool glu) {
   CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0, "wstream_gemm: x must be [M, K] with 16-B rows");
   TORCH_CHECK(wt.dim() == 4 && wt.is_contiguous() && wt.size(2) == 64 && wt.size(3) == 8,
               "wstream_gemm: wt must be contiguous [N/32, K/16, 64, 8]");
   const int M = x.size(0), K = x.size(1), N = wt.size(0) * 32;
   TORCH_CHECK(wt.size(1) * 16 == K, "wstream_gemm: K mismatch");
+  TORCH_CHECK(!glu || N % 64 == 0, "wstream_gemm: GLU weights need N % 64 == 0");
   int mt = 0, kc = 0, s = 0;
   TORCH_CHECK(kafka_wstream_plan(M, N, K, (int)max_splits, &mt, &kc, &s) == 0, "wstream_gemm: unsupported shape");
   bf16* yp = nullptr;
   int64_t ldy = 0;
   float* pp = nullptr;
   if (s == 1) {
+    // glu + one split: y is the activated [M, N/2]; otherwise [M, N] in gate | up column order
     TORCH_CHECK(y.has_value(), "wstream_gemm: y required for a single split");
     CHECK_DT(y.value(), at::kBFloat16); CHECK_LASTDIM(y.value());
-    TORCH_CHECK(y->dim() == 2 && y->size(0) == M && y->size(1) == N, "wstream_gemm: y shape");
+    TORCH_CHECK(y->dim() == 2 && y->size(0) == M && y->size(1) == (glu ? N / 2 : N), "wstream_gemm: y shape");
     yp = bptr(y.value());
     ldy = y->stride(0);
   } else {
@@ -345,8 +348,8 @@ static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> 
                 "wstream_gemm: slab shape must be [splits, M, N]");
     pp = p->data_ptr<float>();
   }
-  CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, nt ? 1 : 0, 1, yp, ldy, pp,
-                                      cur_stream()));
+  CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, nt ? 1 : 0, 1, glu ? 1 : 0,
+                                      yp, ldy, pp, cur_stream()));
 }
 
 // explicit-configuration variant (microbenchmark sweeps): (mt, kc, splits) as given, no planning
@@ -364,7 +367,7 @@ static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tens
     CHECK_DT(p.value(), at::kFloat);
   }
   CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, (int)mt, (int)kc, (int)s, nt ? 1 : 0,
-                                      (int)kw,
+                                      (int)kw, 0,
                                       s == 1 ? bptr(y.value()) : nullptr, s == 1 ? y->stride(0) : 0,
                                       s == 1 ? nullptr : p->data_ptr<float>(), cur_stream()));
 }

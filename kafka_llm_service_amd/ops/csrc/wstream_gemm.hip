@@ -29,7 +29,7 @@ template <int MT, int KC, bool NT, int KW>
 __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                                  const bf16x8* __restrict__ Wt, int M, int N, int K,
                                                                  int ks, bf16* __restrict__ Y, int64_t ldy,
-                                                                 float* __restrict__ P) {
+                                                                 float* __restrict__ P, int glu) {
   constexpr int NTH = 256 * KW;
   constexpr int ROWS = 32 * MT;
   constexpr int CPR = KC / 8;             // 16-B chunks per X row of one K chunk
@@ -146,8 +146,36 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
           for (int i = 0; i < 16; ++i) acc[mt][i] += red[((((j - 1) * 4 + ct) * MT + mt) * 16 + i) * 64 + lane];
     }
   }
+  if (glu && P == nullptr) {
+    // fused SwiGLU epilogue (weight tiles GLU-interleaved: tile 2j = gate rows [32j, 32j+32), tile 2j+1 = the
+    // matching up rows): odd waves hand their up tile to the even wave of the pair through LDS, which writes
+    // silu(gate) * up straight from the fp32 accumulators into Y [M, N/2]
+    float* red = reinterpret_cast<float*>(&xs[0][0]);
+    __syncthreads();
+    if (kh == 0 && (ct & 1)) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[(((ct >> 1) * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
+    }
+    __syncthreads();
+    if (!active || kh != 0 || (ct & 1)) return;
+    const int n = (nb >> 1) * 32 + r;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (m < M) {
+          const float g = acc[mt][i], u = red[(((ct >> 1) * MT + mt) * 16 + i) * 64 + lane];
+          Y[(int64_t)m * ldy + n] = (bf16)(g / (1.0f + __expf(-g)) * u);
+        }
+      }
+    return;
+  }
   if (!active || kh != 0) return;
-  const int n = nb * 32 + r;
+  // GLU-interleaved tiles written un-split: tile 2j -> gate columns [32j, +32), tile 2j+1 -> up columns N/2 + 32j
+  const int n = glu ? ((nb & 1) ? (N >> 1) : 0) + (nb >> 1) * 32 + r : nb * 32 + r;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -200,9 +228,10 @@ extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, 
 }
 
 extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K,
-                                               int mt, int kc, int splits, int nt, int kw, bf16* Y, int64_t ldy,
-                                               float* P, hipStream_t st) {
+                                               int mt, int kc, int splits, int nt, int kw, int glu, bf16* Y,
+                                               int64_t ldy, float* P, hipStream_t st) {
   if (M < 1) return hipSuccess;
+  if (glu && (N % 64 != 0 || kw != 1)) return hipErrorInvalidValue;
   if (K % (kc * splits) != 0 || (splits > 1 && P == nullptr) || (splits == 1 && P == nullptr && Y == nullptr))
     return hipErrorInvalidValue;
   const dim3 grid((N + 127) / 128, splits);
@@ -212,9 +241,9 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
 #define KAFKA_WS(MT_, KC_, KW_)                                                                             \
   do {                                                                                                     \
     if (nt)                                                                                                \
-      wstream_gemm_kernel<MT_, KC_, true, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p); \
+      wstream_gemm_kernel<MT_, KC_, true, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu); \
     else                                                                                                   \
-      wstream_gemm_kernel<MT_, KC_, false, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p); \
+      wstream_gemm_kernel<MT_, KC_, false, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu); \
   } while (0)
   if (mt == 1 && kc == 256 && kw == 1) KAFKA_WS(1, 256, 1);
   else if (mt == 1 && kc == 256 && kw == 2) KAFKA_WS(1, 256, 2);

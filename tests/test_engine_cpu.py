@@ -242,6 +242,7 @@ def test_stream_decode_gemm_matches_oracle():
     m = eng.model
     assert m.stream and m.layers[0].qkv_t is not None and m.lm_head_t is not None
     assert torch.equal(ops.untile_weight(m.layers[0].down_t), m.layers[0].down)
+    assert m.layers[0].glu and torch.equal(ops.untile_weight(m.layers[0].gate_up_t, glu=True), m.layers[0].gate_up)
     # tiny-llama decode shapes take split-K plans, so the slab consumers are exercised
     assert ops.stream_plan(3, m.layers[0].o.shape[0], m.layers[0].o.shape[1])[2] > 1
     prompts = _prompts(seed=9)

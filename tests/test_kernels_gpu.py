@@ -279,6 +279,26 @@ def test_wstream_gemm(cuda, M, N, K):
         torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("M", [1, 40, 64, 100])
+@pytest.mark.parametrize("N,K", [(28672, 4096), (7168, 8192), (2048, 1024)])
+def test_wstream_glu(cuda, M, N, K):
+    """GLU-tiled gate_up: fused silu(gate) * up epilogue (one split) and de-interleaved gate | up slabs (split plans)
+    vs the fp32 reference."""
+    torch.manual_seed(13)
+    x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+    wt = ops.tile_weight(w, glu=True)
+    assert torch.equal(ops.untile_weight(wt, glu=True), w)
+    y_ref = x.float() @ w.float().t()
+    a = ops.linear_glu(x, wt)
+    _close(a, ref.silu_mul(y_ref.cpu()), atol=0.03, rtol=0.02, msg=f"glu M={M} N={N} K={K}")
+    for ms in (1, 8):
+        y = ops.linear_stream(x, wt, max_splits=ms, glu=True)
+        if ops.is_slab(y):
+            _close(ops.slab_reduce(y), y_ref, atol=0.02, rtol=0.01, msg=f"glu slab M={M} N={N} ms={ms}")
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("T", [1, 37, 64])
 def test_slab_consumers(cuda, T):
     """fused_add_rmsnorm / silu_mul / rope_kv_write fed with split-K slabs == the same ops on the summed input."""
