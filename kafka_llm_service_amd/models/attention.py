@@ -85,11 +85,15 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         elif meta.prefix_items is not None:
             ops.attn_prefill(meta.prefix_items, qd, k_cache, v_cache, meta.block_tables, meta.q_limit,
                              meta.scale, out_part=meta.part, lse_part=meta.lse)
+        # one split per sequence (the usual case at 64+ sequences): the decode kernel merges the prefix partials
+        # itself and writes the final rows; else partials + merge kernel
+        fused = meta.num_splits == 1 and meta.num_prefix_splits <= 63 and not overlap
         ops.attn_decode(qd, k_cache, v_cache, meta.block_tables, meta.seq_lens, meta.kv_start, meta.part,
-                        meta.lse, meta.num_splits, meta.num_prefix_splits, meta.scale)
+                        meta.lse, meta.num_splits, meta.num_prefix_splits, meta.scale, out=out[:B] if fused else None)
         if overlap:
             main.wait_stream(side)
-        ops.attn_merge(meta.part, meta.lse, out[:B])
+        if not fused:
+            ops.attn_merge(meta.part, meta.lse, out[:B])
     if meta.prefill_items is not None and meta.num_tokens > B:
         if meta.prefill_splits:
             ops.attn_prefill(meta.prefill_items, q[B:], k_cache, v_cache, meta.block_tables, meta.q_limit[B:],

@@ -84,13 +84,16 @@ def rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part, lse_part, num_splits: int,
-                split_offset: int, scale: float) -> None:
+                split_offset: int, scale: float, out=None) -> None:
     """Split-K paged decode attention writing (O, lse2) partials [B, Hq, S_total, D] at splits
-    [split_offset, split_offset + num_splits)."""
+    [split_offset, split_offset + num_splits). With ``out`` (needs num_splits == 1) the kernel instead merges its
+    result with the partials [0, split_offset) already present (cascade prefix) and writes final bf16 rows."""
     if _gpu(q):
         ext().attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part, lse_part,
-                          int(num_splits), int(split_offset), float(scale))
+                          int(num_splits), int(split_offset), float(scale), out)
         return
+    if out is not None and num_splits != 1:
+        raise ValueError("fused-merge decode needs num_splits == 1")
     o, l2 = ref.attn_decode_full(q, k_cache, v_cache, block_tables, seq_lens, scale, kv_start)
     B = q.shape[0]
     S_total = out_part.shape[2]
@@ -99,6 +102,9 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part,
     lp[:B, :, split_offset:split_offset + num_splits] = float("-inf")
     out_part[:B, :, split_offset] = o
     lp[:B, :, split_offset] = l2
+    if out is not None:
+        n = split_offset + 1
+        ref.attn_merge(out_part[:B, :, :n].contiguous(), lp[:B, :, :n].contiguous(), out[:B])
 
 
 def attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, scale: float, out=None, out_part=None,

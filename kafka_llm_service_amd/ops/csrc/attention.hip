@@ -203,7 +203,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16* __restrict
                                                            const int* __restrict__ seq_lens,
                                                            const int* __restrict__ kv_start,
                                                            float* __restrict__ out_part, float* __restrict__ lse_part,
-                                                           int S_total, int split_offset, float scale_log2) {
+                                                           int S_total, int split_offset, float scale_log2,
+                                                           bf16* __restrict__ out, int64_t out_stride) {
   __shared__ float sO[4][8][D];
   __shared__ float sM[4][8];
   __shared__ float sL[4][8];
@@ -244,6 +245,72 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16* __restrict
     }
   }
   __syncthreads();
+  if (out != nullptr) {
+    // Fused merge (one split per sequence): fold in the cascade-prefix partials [0, split_offset) written earlier
+    // on the stream and write the final bf16 rows — no merge kernel, no partial round trip of this split.
+    // Phase 1: wave w owns heads w, w + 4: lanes load the prefix lse values in parallel, wave-reduce the max and
+    // the weight sum, and publish per-split weights in LDS. Phase 2: thread (g, 4 dims) sums weight x partial over
+    // the splits with all loads of a group of 8 in flight.
+    __shared__ float sW[8][65];
+    __shared__ float sWt[8];
+    for (int g = w; g < G; g += 4) {
+      float Ms = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Ms = fmaxf(Ms, sM[i][g]);
+      float Ls = 0.f;
+      if (Ms != -INFINITY) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ls += exp2f(sM[i][g] - Ms) * sL[i][g];
+      }
+      const float ls = Ls > 0.f ? Ms + log2f(Ls) : -INFINITY;
+      const int64_t pbase = ((int64_t)b * Hq + kvh * G + g) * S_total;
+      const float lv = lane < split_offset ? lse_part[pbase + lane] : (lane == split_offset ? ls : -INFINITY);
+      float mx = lv;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+      const float wv = mx == -INFINITY ? 0.f : exp2f(lv - mx);
+      float ws = wv;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) ws += __shfl_xor(ws, o, 64);
+      if (lane <= split_offset) sW[g][lane] = wv;
+      if (lane == 0) sWt[g] = ws;
+    }
+    __syncthreads();
+    const int g = threadIdx.x >> 5, c = (threadIdx.x & 31) * 4;
+    if (g < G) {
+      // this workgroup's own (normalised) result for dims c..c+3
+      float Ms = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Ms = fmaxf(Ms, sM[i][g]);
+      f32x4 os = {0.f, 0.f, 0.f, 0.f};
+      float Ls = 0.f;
+      if (Ms != -INFINITY) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float f = exp2f(sM[i][g] - Ms);
+          Ls += f * sL[i][g];
+          os += *reinterpret_cast<const f32x4*>(&sO[i][g][c]) * f;
+        }
+      }
+      f32x4 acc4 = Ls > 0.f ? os * (sW[g][split_offset] / Ls) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* pp = out_part + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
+      int s2 = 0;
+      for (; s2 + 8 <= split_offset; s2 += 8) {
+        f32x4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const f32x4*>(pp + (s2 + j) * D);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc4 += v[j] * sW[g][s2 + j];
+      }
+      for (; s2 < split_offset; ++s2) acc4 += *reinterpret_cast<const f32x4*>(pp + s2 * D) * sW[g][s2];
+      const float inv = sWt[g] > 0.f ? 1.f / sWt[g] : 0.f;
+      bf16x4 o4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc4[j] * inv);
+      *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
+    }
+    return;
+  }
   for (int idx = threadIdx.x; idx < G * D; idx += 256) {
     const int g = idx / D, d = idx % D;
     float M = -INFINITY;
@@ -556,13 +623,15 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(const float* __restrict
 extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const bf16* k_cache, const bf16* v_cache, int B,
                               int Hkv, int G, int D, const int* block_tables, int bt_stride, const int* seq_lens,
                               const int* kv_start, float* out_part, float* lse_part, int S, int S_total,
-                              int split_offset, float scale, hipStream_t st) {
+                              int split_offset, float scale, bf16* out, int64_t out_stride, hipStream_t st) {
   if (B == 0) return hipSuccess;
   if (D != 128 || G > 8 || G < 1) return hipErrorInvalidValue;
+  // the fused merge needs one split per sequence and at most 63 prefix partials (one wave lane each + its own)
+  if (out != nullptr && (S != 1 || split_offset > 63)) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
   attn_decode_kernel<128><<<dim3(S, Hkv, B), 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables,
                                                            bt_stride, seq_lens, kv_start, out_part, lse_part, S_total,
-                                                           split_offset, scale_log2);
+                                                           split_offset, scale_log2, out, out_stride);
   return hipGetLastError();
 }
 

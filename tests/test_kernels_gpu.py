@@ -112,6 +112,48 @@ def test_attn_decode(cuda, Hq, Hkv, lens, S):
     _close(lse_o, l_ref, atol=0.02, msg="decode lse")
 
 
+@pytest.mark.parametrize("n_pre", [0, 1, 3, 6])
+def test_attn_decode_fused_merge(cuda, n_pre):
+    """One split per sequence: the decode kernel merges the cascade-prefix partials itself and writes bf16 rows."""
+    torch.manual_seed(6)
+    Hq, Hkv, D = 32, 8, 128
+    P = 16 * 12
+    suffix = [1, 29, 300, 64]
+    B = len(suffix)
+    lens = [P + s for s in suffix]
+    n_pref = P // 16
+    nb_total = n_pref + sum((s + 15) // 16 + 1 for s in suffix) + 2
+    g = torch.Generator().manual_seed(7)
+    k = torch.randn(nb_total, Hkv, 16, D, generator=g).to(torch.bfloat16).to(cuda)
+    v = torch.randn(nb_total, Hkv, D, 16, generator=g).to(torch.bfloat16).to(cuda)
+    bt = torch.zeros(B, 64, dtype=torch.int32)
+    c = n_pref
+    for b in range(B):
+        bt[b, :n_pref] = torch.arange(n_pref)
+        n = (lens[b] + 15) // 16 - n_pref
+        bt[b, n_pref:n_pref + n] = torch.arange(c, c + n)
+        c += n
+    bt = bt.to(cuda)
+    q = torch.randn(B, Hq, D, device=cuda, dtype=torch.bfloat16)
+    sl = torch.tensor(lens, dtype=torch.int32, device=cuda)
+    scale = 1 / math.sqrt(D)
+    part = torch.empty(B, Hq, n_pre + 1, D, device=cuda)
+    lse = torch.empty(B, Hq, n_pre + 1, device=cuda)
+    if n_pre:
+        bounds = [round(P * i / n_pre / 32) * 32 for i in range(n_pre)] + [P]
+        items = torch.tensor([[0, B, 0, bounds[i], bounds[i + 1], i, 0, 0] for i in range(n_pre)],
+                             dtype=torch.int32, device=cuda)
+        q_limit = torch.full((B,), 1 << 30, dtype=torch.int32, device=cuda)
+        ops.attn_prefill(items, q, k, v, bt, q_limit, scale, out_part=part, lse_part=lse)
+        ks = torch.full((B,), P, dtype=torch.int32, device=cuda)
+    else:
+        ks = None
+    out = torch.empty(B, Hq, D, device=cuda, dtype=torch.bfloat16)
+    ops.attn_decode(q, k, v, bt, sl, ks, part, lse, 1, n_pre, scale, out=out)
+    o_ref, _ = ref.attn_decode_full(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), sl.cpu(), scale)
+    _close(out, o_ref, atol=0.02, msg=f"fused merge n_pre={n_pre}")
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2])
 def test_attn_decode_kv_start_cascade(cuda, variant):
     """Cascade: prefix partial from attn_prefill (rows = decode seqs) + suffix partial from attn_decode == full."""
