@@ -26,6 +26,8 @@
 //    1 = 4 waves / 128 rows, LDS; 2 = 4 waves / 128 rows, per-wave register loads. ops.tile_rows(variant).)
 #include "common.h"
 
+#include <type_traits>
+
 namespace kafka {
 
 constexpr int PAGE = 16;
@@ -344,7 +346,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16* __restrict
 constexpr int KT_BYTES = 32 * 128 * 2;
 constexpr int VT_BYTES = 2 * 128 * 16 * 2;
 constexpr int STAGE_BYTES = KT_BYTES + VT_BYTES;
-constexpr int MAX_STAGED_PAGES = 2048;  // keys [base, base + 32k) have their page ids staged in LDS
+constexpr int MAX_STAGED_PAGES = 2048;
+#ifndef ATTN_PREFETCH
+#define ATTN_PREFETCH 2  // K/V blocks in flight per workgroup (4 measured no faster: not latency-bound)
+#endif  // keys [base, base + 32k) have their page ids staged in LDS
 
 // NT threads stage one block: K 512 chunks + V 512 chunks of 16 B -> 1024 / NT chunks of each per thread.
 template <int NT>
@@ -382,6 +387,17 @@ __device__ __forceinline__ void stage_load(StageRegs<NT>& sr, const bf16* __rest
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// s_waitcnt vmcnt(n * L) for a wave-uniform runtime n in [0, MAXN] (the count must be an immediate)
+template <int L, int MAXN>
+__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
+  if constexpr (MAXN >= 5) if (n >= 5) { wait_vmcnt<5 * L>(); return; }
+  if constexpr (MAXN >= 4) if (n == 4) { wait_vmcnt<4 * L>(); return; }
+  if constexpr (MAXN >= 3) if (n == 3) { wait_vmcnt<3 * L>(); return; }
+  if constexpr (MAXN >= 2) if (n == 2) { wait_vmcnt<2 * L>(); return; }
+  if constexpr (MAXN >= 1) if (n == 1) { wait_vmcnt<1 * L>(); return; }
+  wait_vmcnt<0>();
 }
 
 template <int NT>
@@ -501,44 +517,51 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkIte
         b2 = (key0 + 16 < hi_wg) ? s_pages[i0 + 1] : a;
       };
       if (!fits) acc.m = acc.l = __builtin_nanf("");
-      // two register stages in flight (A: odd blocks, B: even blocks >= 2): the load of block b+3 is issued right
-      // after block b's MFMAs and written to LDS two blocks later, so HBM latency has two compute phases of cover.
-      StageRegs<NW * 64> ra, rb;
+      // PF register stages in flight: block j is loaded into stage j % PF, PF blocks ahead of the one being
+      // computed, and written to LDS (double buffer) right before it is needed. (PF = 4 measured the same as 2 on
+      // the cascade pass, profiles/README.md: the kernel is not waiting on HBM latency.)
+      constexpr int PF = ATTN_PREFETCH;
+      StageRegs<NW * 64> rs[PF];
       int p0, p1;
       pages_of(base, p0, p1);
-      stage_load<NW * 64>(ra, k_cache, v_cache, Hkv, kvh, p0, p1, tid);
+      stage_load<NW * 64>(rs[0], k_cache, v_cache, Hkv, kvh, p0, p1, tid);
       wait_vmcnt<0>();
-      stage_store<NW * 64>(ra, lds, tid);
-      if (nblk > 1) {
-        pages_of(base + 32, p0, p1);
-        stage_load<NW * 64>(ra, k_cache, v_cache, Hkv, kvh, p0, p1, tid);
-      }
-      if (nblk > 2) {
-        pages_of(base + 64, p0, p1);
-        stage_load<NW * 64>(rb, k_cache, v_cache, Hkv, kvh, p0, p1, tid);
+      stage_store<NW * 64>(rs[0], lds, tid);
+#pragma unroll
+      for (int j = 1; j <= PF; ++j) {
+        if (j < nblk) {
+          pages_of(base + 32 * j, p0, p1);
+          stage_load<NW * 64>(rs[j % PF], k_cache, v_cache, Hkv, kvh, p0, p1, tid);
+        }
       }
       __syncthreads();
-      auto body = [&](int b, StageRegs<NW * 64>& regs) {
+      // J = b % PF (compile time, so the stage registers are statically indexed)
+      auto body = [&](auto Jc, int b) {
+        constexpr int J = decltype(Jc)::value;
         const int key0 = base + 32 * b;
         if (key0 < hi) {  // wave-uniform: skip blocks past this wave's causal limit
           const bool masked = (key0 < lo) | (key0 + 32 > hi) | (key0 + 31 > wmin);
           attn_compute_lds<D>(lds + (b & 1) * STAGE_BYTES, key0, lo, hi, limit, qf, scale_log2, acc, lane, masked);
         }
         if (b + 1 < nblk) {
-          // regs hold block b+1; the other stage (block b+2) may still be in flight
-          if (b + 2 < nblk) wait_vmcnt<LOADS>();
-          else wait_vmcnt<0>();
-          stage_store<NW * 64>(regs, lds + ((b + 1) & 1) * STAGE_BYTES, tid);
-        }
-        if (b + 3 < nblk) {
-          pages_of(key0 + 96, p0, p1);
-          stage_load<NW * 64>(regs, k_cache, v_cache, Hkv, kvh, p0, p1, tid);
+          // stage (J+1) % PF holds block b+1; blocks b+2 .. min(b+PF, nblk-1) may still be in flight behind it
+          const int younger = min(PF - 1, nblk - 2 - b);
+          wait_vmcnt_dyn<LOADS, PF - 1>(younger);
+          stage_store<NW * 64>(rs[(J + 1) % PF], lds + ((b + 1) & 1) * STAGE_BYTES, tid);
+          if (b + 1 + PF < nblk) {
+            pages_of(key0 + 32 * (1 + PF), p0, p1);
+            stage_load<NW * 64>(rs[(J + 1) % PF], k_cache, v_cache, Hkv, kvh, p0, p1, tid);
+          }
         }
         __syncthreads();
       };
-      for (int b = 0; b < (fits ? nblk : 0); b += 2) {
-        body(b, ra);
-        if (b + 1 < nblk) body(b + 1, rb);
+      for (int b = 0; b < (fits ? nblk : 0); b += PF) {
+        body(std::integral_constant<int, 0>{}, b);
+        if constexpr (PF > 1) if (b + 1 < nblk) body(std::integral_constant<int, 1 % PF>{}, b + 1);
+        if constexpr (PF > 2) if (b + 2 < nblk) body(std::integral_constant<int, 2 % PF>{}, b + 2);
+        if constexpr (PF > 3) if (b + 3 < nblk) body(std::integral_constant<int, 3 % PF>{}, b + 3);
+        if constexpr (PF > 4) if (b + 4 < nblk) body(std::integral_constant<int, 4 % PF>{}, b + 4);
+        if constexpr (PF > 5) if (b + 5 < nblk) body(std::integral_constant<int, 5 % PF>{}, b + 5);
       }
     }
   }
