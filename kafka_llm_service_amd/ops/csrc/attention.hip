@@ -198,7 +198,7 @@ __device__ __forceinline__ void init_acc(WaveAcc<D>& acc) {
 // ------------------------------------------------------------------------------------------------------------------
 // Decode: grid (S, Hkv, B), 256 threads. Requires G <= 8.
 template <int D>
-__global__ __launch_bounds__(256) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
+__global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
                                                            const bf16* __restrict__ k_cache,
                                                            const bf16* __restrict__ v_cache, int Hkv, int G,
                                                            const int* __restrict__ block_tables, int bt_stride,
