@@ -85,12 +85,12 @@ class DecodeGraphs:
 
     def _load(self, e: _Entry, h, sp) -> None:
         r = self.runner
-        e.s64.copy_(r._host(h.i64), non_blocking=True)
-        e.s32.copy_(r._host(h.i32), non_blocking=True)
+        e.s64.copy_(r._h2d(h.i64))
+        e.s32.copy_(r._h2d(h.i32))
         if not sp.greedy:
-            e.f32.copy_(r._host(np.concatenate([sp.temp, sp.topp])), non_blocking=True)
-            e.topk.copy_(r._host(sp.topk), non_blocking=True)
-            e.seeds.copy_(r._host(sp.seeds), non_blocking=True)
+            e.f32.copy_(r._h2d(np.concatenate([sp.temp, sp.topp])))
+            e.topk.copy_(r._h2d(sp.topk))
+            e.seeds.copy_(r._h2d(sp.seeds))
 
     def _capture(self, k: tuple, h, sp) -> _Entry:
         r = self.runner

@@ -78,6 +78,45 @@ def decode_splits(B: int, hkv: int, max_keys: int, target_wgs: int = 512, min_ke
     return s
 
 
+_NP2TORCH = {np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32, np.dtype(np.float32): torch.float32}
+
+
+class _Stager:
+    """Per-step host->device uploads through a ring of pinned staging arenas (one arena per launch, bump-allocated):
+    no pinned allocation and no pageable copy on the step path, so every upload is a plain async DMA in stream
+    order. An arena is reused ``depth`` launches later, when at most two steps can be in flight — its copies have
+    executed by then."""
+
+    def __init__(self, device: torch.device, nbytes: int = 8 << 20, depth: int = 4):
+        self.device = device
+        self.nbytes = nbytes
+        self.bufs: list[torch.Tensor | None] = [None] * depth
+        self.i = 0
+        self.off = 0
+
+    def begin(self) -> None:
+        self.i = (self.i + 1) % len(self.bufs)
+        self.off = 0
+
+    def upload(self, a: np.ndarray) -> torch.Tensor:
+        a = np.ascontiguousarray(a)
+        if self.device.type != "cuda":
+            return torch.from_numpy(a)
+        nb = a.nbytes
+        off = (self.off + 255) & ~255
+        buf = self.bufs[self.i]
+        if buf is None or off + nb > buf.numel():
+            # (a replaced arena goes back to torch's pinned cache, which waits for its recorded copies)
+            self.bufs[self.i] = buf = torch.empty(max(self.nbytes, 2 * (off + nb)), dtype=torch.uint8,
+                                                  pin_memory=True)
+        stage = buf[off:off + nb]
+        stage.numpy()[:] = a.reshape(-1).view(np.uint8)
+        self.off = off + nb
+        dev = torch.empty(a.size, dtype=_NP2TORCH[a.dtype], device=self.device)
+        dev.view(torch.uint8).copy_(stage, non_blocking=True)
+        return dev.view(a.shape)
+
+
 class ModelRunner:
     def __init__(self, model: TransformerLM, k_caches, v_caches, kvm, max_num_seqs: int, max_blocks_per_seq: int,
                  cascade_min_prefix: int = 512, use_cascade: bool = True, target_wgs: int = 256,
@@ -102,6 +141,7 @@ class ModelRunner:
         self.recent_stats: deque = deque(maxlen=16)  # stats of the last launched steps (two can be in flight)
         self.broadcast = None  # set on a TP leader: callable(HostStep) (engine/tp_worker.py)
         self._tok_host = None  # pinned landing buffers of the sampled ids
+        self.stager = _Stager(self.device)
         # every step's sampled ids also land here (fixed address, so hipGraphs can read it): the next step's decode
         # rows whose token was still being sampled at launch gather their input ids from it on the stream
         self.tok_buf = torch.zeros(max_num_seqs * 2 + 64, dtype=torch.int64, device=self.device)
@@ -261,10 +301,7 @@ class ModelRunner:
         return t.pin_memory() if self.device.type == "cuda" else t
 
     def _h2d(self, a: np.ndarray) -> torch.Tensor:
-        t = torch.from_numpy(a)
-        if self.device.type == "cuda":
-            return t.pin_memory().to(self.device, non_blocking=True)
-        return t.to(self.device)
+        return self.stager.upload(a)
 
     # ------------------------------------------------------------------------------------------------------------
     def sample(self, logits: torch.Tensor, seqs: list[Sequence]) -> torch.Tensor:
@@ -296,9 +333,8 @@ class ModelRunner:
         dev = logits.device
         if sp.greedy:
             return ops.sample(logits, torch.zeros(n, device=dev))
-        f32 = torch.from_numpy(np.concatenate([sp.temp, sp.topp])).to(dev, non_blocking=True)
-        return ops.sample(logits, f32[:n], f32[n:], torch.from_numpy(sp.topk).to(dev, non_blocking=True),
-                          torch.from_numpy(sp.seeds).to(dev, non_blocking=True))
+        f32 = self._h2d(np.concatenate([sp.temp, sp.topp]))
+        return ops.sample(logits, f32[:n], f32[n:], self._h2d(sp.topk), self._h2d(sp.seeds))
 
     def _mask_tensor(self, m) -> torch.Tensor:
         """Device copy of a constrained.Mask's base vocab mask (cached by key) with its extra ids allowed."""
@@ -364,6 +400,7 @@ class ModelRunner:
             host.i64 = np.concatenate([host.i64, np.asarray(late_dst + late_src, dtype=np.int64)])
         self.last_stats = host.stats
         self.recent_stats.append(host.stats)
+        self.stager.begin()
         if self.broadcast is not None:  # TP leader: followers run the same step on their shards
             if late_dst:
                 raise RuntimeError("TP steps must be launched with landed tokens")

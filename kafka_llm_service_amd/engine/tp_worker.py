@@ -66,6 +66,7 @@ def follower_loop(engine) -> int:
         host = box[0]
         if host is None:
             return n
+        runner.stager.begin()
         inp = runner.to_device(host)
         runner.model.forward(inp, runner.k_caches, runner.v_caches)
         n += 1
