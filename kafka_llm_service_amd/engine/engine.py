@@ -111,7 +111,13 @@ class LLMEngine:
         if mode == "auto":
             mode = "stream" if self.device.type == "cuda" else "blas"
         if mode == "stream" and not self.model.stream:
-            self.model.enable_stream_weights()  # before the KV pool is sized from the free memory
+            need = self.model.stream_weight_bytes()
+            free = torch.cuda.mem_get_info(self.device)[0] if self.device.type == "cuda" else need * 4
+            if need <= 0.5 * free:
+                self.model.enable_stream_weights()  # before the KV pool is sized from the free memory
+            else:  # e.g. Llama-3-70B on one GPU: a second copy of 140 GB would starve the KV pool
+                log.warning("decode GEMMs on hipBLASLt: the wave-tiled weight copy (%.1f GB) does not fit next to "
+                            "the KV pool (%.1f GB free)", need / 1e9, free / 1e9)
         self.load_s = time.perf_counter() - t0
         self.eos = set(cfg.eos_token_ids or mc.eos_token_ids)
         hkv, D, L = self.model.hkv, self.model.D, mc.num_layers

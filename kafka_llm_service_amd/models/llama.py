@@ -72,6 +72,18 @@ class TransformerLM:
         self.stream = False  # decode GEMMs on the weight-streaming kernel (enable_stream_weights)
 
     # ------------------------------------------------------------------------------------------------------------
+    def stream_weight_bytes(self) -> int:
+        """Bytes enable_stream_weights would add (the wave-tiled copies)."""
+        n = 0
+        for lw in self.layers:
+            for name in LayerWeights.STREAMED:
+                w = getattr(lw, name)
+                if w is not None and ops.stream_plan(1, w.shape[0], w.shape[1]) is not None:
+                    n += w.numel() * w.element_size()
+        if ops.stream_plan(1, self.lm_head.shape[0], self.lm_head.shape[1]) is not None:
+            n += self.lm_head.numel() * self.lm_head.element_size()
+        return n
+
     def enable_stream_weights(self) -> int:
         """Keep a wave-tiled copy of every dense projection and of the lm_head (ops.tile_weight) so decode-sized
         steps (T <= ops.STREAM_MAX_M) run the weight-streaming MFMA GEMM (csrc/wstream_gemm.hip) instead of
