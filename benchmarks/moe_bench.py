@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Mixtral-8x7B MoE layer microbenchmark on one MI355X: router (HIP) + grouped gate_up GEMM + SiLU*mul + grouped
 down GEMM with the fused weighted combine, at decode-like token counts (BASELINE config 5: 128 threads) and a
-prefill chunk. Reports us/layer and the expert-weight streaming rate (every expert with >= 1 token is read once).
+prefill chunk. Reports us/layer and the expert-weight streaming rate (every expert with >= 1 token is read once) for
+the LDS-tiled grouped GEMM and, at decode sizes (T <= 128), for the grouped weight-streaming kernel.
 
   python benchmarks/moe_bench.py            # T = 1, 16, 64, 128, 512, 2048
 """
@@ -39,6 +40,7 @@ def main():
     router = (torch.randn(E, d, device=dev) * d ** -0.5).to(torch.bfloat16)
     w13 = (torch.randn(E, 2 * F, d, device=dev) * d ** -0.5).to(torch.bfloat16)
     w2 = (torch.randn(E, d, F, device=dev) * F ** -0.5).to(torch.bfloat16)
+    w13t, w2t = ops.tile_experts(w13, glu=True), ops.tile_experts(w2)  # grouped weight-streaming layout
     for T in Ts:
         x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
 
@@ -50,13 +52,23 @@ def main():
             ops.grouped_gemm(a, w2, r, gather=False, combine_out=out)
             return out
 
+        def layer_stream():
+            r = ops.moe_route(torch.nn.functional.linear(x, router), K)
+            a = ops.grouped_stream_glu(x, w13t, r)
+            out = torch.zeros(T, d, dtype=torch.float32, device=dev)
+            ops.grouped_stream_combine(a, w2t, r, T, out)
+            return out
+
         us = timeit(layer)
+        us_s = timeit(layer_stream) if T <= ops.STREAM_MAX_M else None
         r = ops.moe_route(torch.nn.functional.linear(x, router), K)
         used = int((r.expert_off[1:] - r.expert_off[:-1] > 0).sum().item())
         bytes_w = used * (2 * F * d + d * F) * 2
         print(json.dumps({"T": T, "experts_used": used, "us_per_layer": round(us, 1),
                           "weight_TB/s": round(bytes_w / us / 1e6, 2),
-                          "TFLOP/s": round(2 * T * K * 3 * F * d / us / 1e6, 1)}), flush=True)
+                          "TFLOP/s": round(2 * T * K * 3 * F * d / us / 1e6, 1),
+                          "stream_us_per_layer": round(us_s, 1) if us_s else None,
+                          "stream_weight_TB/s": round(bytes_w / us_s / 1e6, 2) if us_s else None}), flush=True)
 
 
 if __name__ == "__main__":

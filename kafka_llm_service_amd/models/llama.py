@@ -5,8 +5,10 @@ Per layer (SURVEY.md §3.2 "Target equivalent"):
     -> paged attention (decode / cascade / chunked prefill, HIP MFMA) -> O GEMM (row-parallel) -> [TP all-reduce]
     -> fused_add_rmsnorm -> gate_up GEMM (column-parallel) -> silu_mul (HIP) -> down GEMM (row-parallel)
     -> [TP all-reduce]                                     (Mixtral: router -> expert MLPs, models/moe.py)
-Dense GEMMs are hipBLASLt through ``torch.nn.functional.linear`` (bf16, fp32 accumulate). The elementwise / norm /
-attention / sampling work runs in the hand-written kernels of ``ops/csrc``.
+Decode-sized steps (T <= 128) run every projection on the weight-streaming MFMA kernel (``ops/csrc/wstream_gemm.hip``,
+wave-tiled weight copies, SwiGLU fused into gate_up; the grouped variant for Mixtral's experts); prefill-sized steps
+use hipBLASLt through ``torch.nn.functional.linear`` (bf16, fp32 accumulate). Norm / RoPE / attention / sampling run
+in the hand-written kernels of ``ops/csrc``.
 
 Weights are stored HF-style ``[out, in]`` so safetensors checkpoints load without transposes; random init (seeded,
 synthetic benchmarks — no checkpoints are downloadable here) is the default.
@@ -36,7 +38,7 @@ class StepInput:
 
 class LayerWeights:
     __slots__ = ("input_norm", "post_norm", "qkv", "o", "gate_up", "down", "router", "w13", "w2", "expert_ids",
-                 "qkv_t", "o_t", "gate_up_t", "down_t", "glu")
+                 "qkv_t", "o_t", "gate_up_t", "down_t", "glu", "w13_t", "w2_t")
     STREAMED = ("qkv", "o", "gate_up", "down")  # projections with a wave-tiled copy for the decode GEMM
 
     def __init__(self):
@@ -80,6 +82,10 @@ class TransformerLM:
                 w = getattr(lw, name)
                 if w is not None and ops.stream_plan(1, w.shape[0], w.shape[1]) is not None:
                     n += w.numel() * w.element_size()
+            for name in ("w13", "w2"):
+                w = getattr(lw, name)
+                if w is not None and ops.stream_moe_supported(w.shape[1], w.shape[2]):
+                    n += w.numel() * w.element_size()
         if ops.stream_plan(1, self.lm_head.shape[0], self.lm_head.shape[1]) is not None:
             n += self.lm_head.numel() * self.lm_head.element_size()
         return n
@@ -99,6 +105,11 @@ class TransformerLM:
                     if name == "gate_up":
                         lw.glu = glu
                     added += w.numel() * w.element_size()
+            if lw.w13 is not None and ops.stream_moe_supported(lw.w13.shape[1], lw.w13.shape[2]) and \
+                    ops.stream_moe_supported(lw.w2.shape[1], lw.w2.shape[2]):
+                lw.w13_t = ops.tile_experts(lw.w13, glu=True)  # expert MLPs: grouped streaming kernel
+                lw.w2_t = ops.tile_experts(lw.w2)
+                added += (lw.w13.numel() + lw.w2.numel()) * lw.w13.element_size()
         if ops.stream_plan(1, self.lm_head.shape[0], self.lm_head.shape[1]) is not None:
             self.lm_head_t = ops.tile_weight(self.lm_head)
             added += self.lm_head.numel() * self.lm_head.element_size()

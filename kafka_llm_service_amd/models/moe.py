@@ -30,6 +30,7 @@ def route(logits: torch.Tensor, k: int):
 
 class MoEBlock:
     def __init__(self, model):
+        self.model = model
         cfg = model.cfg
         self.E = cfg.num_experts
         self.k = cfg.num_experts_per_tok
@@ -43,6 +44,14 @@ class MoEBlock:
         T, d = x.shape
         logits = F.linear(x, lw.router)
         r = ops.moe_route(logits, self.k)
+        if self.model.stream and lw.w13_t is not None and T <= ops.STREAM_MAX_M:
+            # decode-sized steps: expert weights streamed from their wave-tiled copies, SwiGLU fused into the gate_up
+            # epilogue, weighted combine fused into the down epilogue (csrc/wstream_gemm.hip, grouped variant)
+            a = ops.grouped_stream_glu(x, lw.w13_t, r, e_lo=self.e0)
+            out = torch.zeros(T, d, dtype=torch.float32, device=x.device)
+            ops.grouped_stream_combine(a, lw.w2_t, r, T, out, e_lo=self.e0)
+            out = out.to(x.dtype)
+            return pstate.tp_all_reduce(out) if self.ep > 1 else out
         # gate_up for every (token, expert) entry routed to a local expert, rows gathered from x by the kernel
         h = ops.grouped_gemm(x, lw.w13, r, gather=True, e_lo=self.e0)
         a = ops.silu_mul(h)

@@ -234,6 +234,54 @@ def linear_glu(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8) -> torch.
     return y if plan is not None and plan[2] == 1 else silu_mul(y)
 
 
+def tile_experts(w: torch.Tensor, glu: bool = False) -> torch.Tensor:
+    """Expert weights [E, N, K] -> wave-tiled [E, N/32, K/16, 64, 8] (``tile_weight`` per expert)."""
+    E, N, K = w.shape
+    out = torch.empty(E, N // 32, K // 16, 64, 8, dtype=w.dtype, device=w.device)
+    for e in range(E):
+        out[e].copy_(tile_weight(w[e], glu))
+    return out
+
+
+def untile_experts(wt: torch.Tensor, glu: bool = False) -> torch.Tensor:
+    return torch.stack([untile_weight(wt[e], glu) for e in range(wt.shape[0])])
+
+
+def stream_moe_supported(N: int, K: int) -> bool:
+    return N % 64 == 0 and K % 256 == 0
+
+
+def grouped_stream_glu(x: torch.Tensor, wt: torch.Tensor, r: "MoERouting", e_lo: int = 0) -> torch.Tensor:
+    """silu(gate) * up for every routed (token, local expert) entry, rows in expert-sorted order [n_ent, F]: the
+    weight-streaming grouped kernel on GLU-tiled expert weights (``tile_experts(w13, glu=True)``)."""
+    T = x.shape[0]
+    n_ent = r.perm_tok.numel()
+    F = wt.shape[1] * 16
+    y = torch.empty(n_ent, F, dtype=x.dtype, device=x.device)
+    if _gpu(x):
+        ext().wstream_grouped(x, wt, r.perm_tok, r.perm_w, r.expert_off, int(e_lo), int(T), True, y, None)
+        return y
+    h = ref_grouped(x, untile_experts(wt, glu=True), r, e_lo, gather=True)
+    y.copy_(ref.silu_mul(h))
+    return y
+
+
+def grouped_stream_combine(a: torch.Tensor, wt: torch.Tensor, r: "MoERouting", T: int, out: torch.Tensor,
+                           e_lo: int = 0) -> torch.Tensor:
+    """out[token] += w * (a[entry] @ W_e^T) over the local experts' entries (out f32 [T, N], zeroed by the caller)."""
+    if _gpu(a):
+        ext().wstream_grouped(a, wt, r.perm_tok, r.perm_w, r.expert_off, int(e_lo), int(T), False, None, out)
+        return out
+    ref.grouped_gemm(a, untile_experts(wt), r.perm_tok, r.perm_w, r.expert_off, e_lo, False, None, out)
+    return out
+
+
+def ref_grouped(x, w, r, e_lo, gather):
+    y = torch.zeros(r.perm_tok.numel(), w.shape[1], dtype=x.dtype)
+    ref.grouped_gemm(x, w, r.perm_tok, r.perm_w, r.expert_off, e_lo, gather, y, None)
+    return y
+
+
 def slab_reduce(p: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """bf16 [M, N] = sum of the split-K slabs [S, M, N] (bf16 inputs pass through)."""
     if not is_slab(p):

@@ -42,6 +42,10 @@ hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt,
                                      int splits, int nt, int kw, int glu, bf16* Y, int64_t ldy, float* P,
                                      hipStream_t st);
 hipError_t kafka_launch_slab_reduce(const float* P, int S, int M, int N, bf16* Y, int64_t ldy, hipStream_t st);
+hipError_t kafka_launch_wstream_grouped(const bf16* X, int64_t ldx, const bf16* Wt, int e_local, int N, int K,
+                                        const int* perm_tok, const float* perm_w, const int* expert_off, int e_lo,
+                                        int max_rows, int gather, bf16* Y, int64_t ldy, float* out, int64_t ldo,
+                                        hipStream_t st);
 hipError_t kafka_launch_moe_route(const bf16* logits, int64_t ld, int T, int E, int K, int BM, float* topk_w,
                                   int* topk_e, int* perm_tok, float* perm_w, int* expert_off, int* tile_off,
                                   hipStream_t st);
@@ -383,6 +387,47 @@ static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tens
                                       s == 1 ? nullptr : p->data_ptr<float>(), cur_stream()));
 }
 
+// Expert MLP halves on wave-tiled expert weights wt [E_local, N/32, K/16, 64, 8] (ops.tile_experts). glu: gate_up
+// with fused SwiGLU into y [n_ent, N/2]; else down with the weighted combine into out f32 [T, N]. max_rows = T
+// bounds every expert segment (a token picks an expert at most once).
+static void wstream_grouped(at::Tensor x, at::Tensor wt, at::Tensor perm_tok, at::Tensor perm_w, at::Tensor expert_off,
+                            int64_t e_lo, int64_t max_rows, bool gather, c10::optional<at::Tensor> y,
+                            c10::optional<at::Tensor> out) {
+  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
+  CHECK_DT(perm_tok, at::kInt); CHECK_DT(perm_w, at::kFloat); CHECK_DT(expert_off, at::kInt);
+  TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0, "wstream_grouped: x must be [rows, K] with 16-B rows");
+  TORCH_CHECK(wt.dim() == 5 && wt.is_contiguous() && wt.size(3) == 64 && wt.size(4) == 8,
+              "wstream_grouped: wt must be contiguous [E_local, N/32, K/16, 64, 8]");
+  const int E_local = wt.size(0), N = wt.size(1) * 32, K = wt.size(2) * 16;
+  TORCH_CHECK(x.size(1) == K && K % 256 == 0 && N % 64 == 0, "wstream_grouped: K / N");
+  const int64_t n_ent = perm_tok.numel();
+  TORCH_CHECK(perm_w.numel() == n_ent && perm_tok.is_contiguous() && perm_w.is_contiguous(), "wstream_grouped: perm");
+  TORCH_CHECK(expert_off.is_contiguous() && e_lo >= 0 && expert_off.numel() >= e_lo + E_local + 1,
+              "wstream_grouped: expert_off too short for the local experts");
+  TORCH_CHECK(max_rows >= 1 && (gather ? x.size(0) == max_rows : x.size(0) >= n_ent),
+              "wstream_grouped: x rows (tokens when gathering, entries otherwise)");
+  bf16* yp = nullptr;
+  int64_t ldy = 0;
+  float* op = nullptr;
+  int64_t ldo = 0;
+  if (y.has_value()) {
+    CHECK_DT(y.value(), at::kBFloat16); CHECK_LASTDIM(y.value());
+    TORCH_CHECK(!out.has_value() && y->dim() == 2 && y->size(0) >= n_ent && y->size(1) == N / 2,
+                "wstream_grouped: y must be [n_ent, N/2]");
+    yp = bptr(y.value());
+    ldy = y->stride(0);
+  } else {
+    TORCH_CHECK(out.has_value(), "wstream_grouped: y or out required");
+    CHECK_DT(out.value(), at::kFloat); CHECK_LASTDIM(out.value());
+    TORCH_CHECK(out->dim() == 2 && out->size(0) == max_rows && out->size(1) == N, "wstream_grouped: out [T, N]");
+    op = out->data_ptr<float>();
+    ldo = out->stride(0);
+  }
+  CHECK_HIP(kafka_launch_wstream_grouped(bptr(x), x.stride(0), bptr(wt), E_local, N, K, perm_tok.data_ptr<int>(),
+                                         perm_w.data_ptr<float>(), expert_off.data_ptr<int>(), (int)e_lo,
+                                         (int)max_rows, gather ? 1 : 0, yp, ldy, op, ldo, cur_stream()));
+}
+
 // y [M, N] bf16 = sum over the slabs p [S, M, N]
 static void slab_reduce(at::Tensor p, at::Tensor y) {
   CHECK_CUDA(p); CHECK_DT(p, at::kFloat); CHECK_DT(y, at::kBFloat16); CHECK_LASTDIM(y);
@@ -505,6 +550,7 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("wstream_gemm", &wstream_gemm);
   m.def("wstream_gemm_cfg", &wstream_gemm_cfg);
   m.def("slab_reduce", &slab_reduce);
+  m.def("wstream_grouped", &wstream_grouped);
   m.def("moe_route", &moe_route);
   m.def("car_alloc", &car_alloc);
   m.def("car_ipc_handle", &car_ipc_handle);

@@ -190,6 +190,154 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
     }
 }
 
+// Grouped (MoE) variant: one weight stream per expert over wave-tiled expert weights Wt[E_local][N/32][K/16][64][8].
+// Grid (ceil(N / 128), E_local, row tiles of 32 * MT); expert e's rows are the routing segment
+// [expert_off[e], expert_off[e + 1]) read on the device (no host sync after the router); workgroups past the end
+// of their expert's segment exit at once, and row tiles past it skip their MFMAs (wave-uniform).
+//   GATHER: A row = X[perm_tok[entry]] (token activations), else X[entry] (expert-sorted intermediate).
+//   Epilogue GLU (GLU-interleaved tiles): Y[entry, :N/2] = silu(gate) * up, bf16 — the SwiGLU of the expert MLP.
+//   Epilogue COMBINE: out_f32[perm_tok[entry], n] += perm_w[entry] * y (a token gets exactly k contributions).
+template <int MT, int KC, bool GATHER, bool COMBINE>
+__global__ __launch_bounds__(256) void wstream_grouped_kernel(const bf16* __restrict__ X, int64_t ldx,
+                                                               const bf16x8* __restrict__ Wt, int N, int K,
+                                                               const int* __restrict__ perm_tok,
+                                                               const float* __restrict__ perm_w,
+                                                               const int* __restrict__ expert_off, int e_lo,
+                                                               bf16* __restrict__ Y, int64_t ldy,
+                                                               float* __restrict__ out, int64_t ldo) {
+  constexpr int ROWS = 32 * MT;
+  constexpr int CPR = KC / 8;
+  constexpr int XL = ROWS * CPR / 256;
+  constexpr int KSTEP = KC / 16;
+  static_assert(CPR >= 16 && XL >= 1, "chunk too small");
+  __shared__ __attribute__((aligned(16))) bf16 xs[2][ROWS * KC];
+  const int el = blockIdx.y, e = e_lo + el;
+  const int seg0 = expert_off[e];
+  const int cnt = expert_off[e + 1] - seg0;
+  const int row0 = blockIdx.z * ROWS;
+  if (row0 >= cnt) return;  // workgroup-uniform
+  const int rows = min(ROWS, cnt - row0);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int nb = blockIdx.x * 4 + w;
+  const bool active = nb < (N >> 5);
+  const bf16x8* wp = Wt + ((int64_t)el * (N >> 5) + (active ? nb : (N >> 5) - 1)) * (K >> 4) * 64 + lane;
+  const int nchunks = K / KC;
+
+  // A-row sources of this thread's staged chunks (fixed over K)
+  const bf16* xsrc[XL];
+#pragma unroll
+  for (int i = 0; i < XL; ++i) {
+    const int idx = tid + 256 * i;
+    const int row = idx / CPR, c = idx % CPR;
+    const int ent = seg0 + row0 + min(row, rows - 1);  // rows past the segment reload a valid row, never stored
+    const int64_t src = GATHER ? (int64_t)perm_tok[ent] : (int64_t)ent;
+    xsrc[i] = X + src * ldx + c * 8;
+  }
+  bf16x8 xr[XL];
+  auto load_x = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < XL; ++i) xr[i] = load_bf16x8(xsrc[i] + ch * KC);
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < XL; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / CPR, c = idx % CPR;
+      *reinterpret_cast<bf16x8*>(&xs[buf][row * KC + 8 * (c ^ (row & 15))]) = xr[i];
+    }
+  };
+  auto load_w = [&](bf16x8(&wv)[KSTEP], int ch) {
+#pragma unroll
+    for (int t = 0; t < KSTEP; ++t) wv[t] = __builtin_nontemporal_load(wp + (int64_t)(ch * KSTEP + t) * 64);
+  };
+  const int mt_used = (rows + 31) >> 5;  // row tiles with live rows (uniform)
+  f32x16 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
+  auto compute = [&](int buf, const bf16x8(&wv)[KSTEP]) {
+#pragma unroll
+    for (int t = 0; t < KSTEP; ++t) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        if (mt < mt_used) {
+          const int m = mt * 32 + r, c = 2 * t + h;
+          const bf16x8 xf = *reinterpret_cast<const bf16x8*>(&xs[buf][m * KC + 8 * (c ^ (m & 15))]);
+          acc[mt] = mfma32(xf, wv[t], acc[mt]);
+        }
+      }
+    }
+  };
+  bf16x8 wa[KSTEP], wb[KSTEP];
+  load_x(0);
+  load_w(wa, 0);
+  store_x(0);
+  __syncthreads();
+  int ch = 0;
+  for (; ch + 2 < nchunks; ch += 2) {
+    load_x(ch + 1);
+    load_w(wb, ch + 1);
+    compute(0, wa);
+    store_x(1);
+    __syncthreads();
+    load_x(ch + 2);
+    load_w(wa, ch + 2);
+    compute(1, wb);
+    store_x(0);
+    __syncthreads();
+  }
+  if (ch + 1 < nchunks) {
+    load_x(ch + 1);
+    load_w(wb, ch + 1);
+    compute(0, wa);
+    store_x(1);
+    __syncthreads();
+    compute(1, wb);
+  } else {
+    compute(0, wa);
+  }
+
+  if constexpr (!COMBINE) {
+    // SwiGLU epilogue: odd waves hand their up tile to the even wave of the pair through LDS
+    float* red = reinterpret_cast<float*>(&xs[0][0]);
+    __syncthreads();
+    if (w & 1) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[(((w >> 1) * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
+    }
+    __syncthreads();
+    if (!active || (w & 1)) return;
+    const int n = (nb >> 1) * 32 + r;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (m < rows) {
+          const float g = acc[mt][i], u = red[(((w >> 1) * MT + mt) * 16 + i) * 64 + lane];
+          Y[(int64_t)(seg0 + row0 + m) * ldy + n] = (bf16)(g / (1.0f + __expf(-g)) * u);
+        }
+      }
+  } else {
+    if (!active) return;
+    const int n = nb * 32 + r;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (m < rows) {
+          const int ent = seg0 + row0 + m;
+          atomicAdd(out + (int64_t)perm_tok[ent] * ldo + n, perm_w[ent] * acc[mt][i]);
+        }
+      }
+  }
+}
+
 // Y[m, n] = sum_s P[s, m, n] (bf16), 8 columns per thread: the standalone combine for callers without a
 // slab-aware consumer (TP all-reduce inputs, tests).
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ P, int S, int M, int N,
@@ -268,4 +416,33 @@ extern "C" hipError_t kafka_launch_slab_reduce(const float* P, int S, int M, int
   return hipGetLastError();
 }
 
+}  // namespace kafka
+
+namespace kafka {
+// Grouped streaming GEMM for the expert MLP (see wstream_grouped_kernel). max_rows bounds any expert's segment
+// (the token count T: a token picks an expert at most once); glu: gate_up with fused SwiGLU into Y [n_ent, N/2];
+// else combine into out_f32 [T, N].
+extern "C" hipError_t kafka_launch_wstream_grouped(const bf16* X, int64_t ldx, const bf16* Wt, int e_local, int N,
+                                                  int K, const int* perm_tok, const float* perm_w,
+                                                  const int* expert_off, int e_lo, int max_rows, int gather,
+                                                  bf16* Y, int64_t ldy, float* out, int64_t ldo, hipStream_t st) {
+  if (max_rows < 1 || e_local < 1) return hipSuccess;
+  if (N % 64 != 0 || K % 256 != 0 || (out == nullptr) == (Y == nullptr)) return hipErrorInvalidValue;
+  const int MT = max_rows <= 32 ? 1 : 2;
+  const dim3 grid((N + 127) / 128, e_local, (max_rows + 32 * MT - 1) / (32 * MT));
+  const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
+#define KAFKA_WG(MT_, G_, C_)                                                                              \
+  wstream_grouped_kernel<MT_, 256, G_, C_><<<grid, 256, 0, st>>>(X, ldx, wt, N, K, perm_tok, perm_w, expert_off, \
+                                                                 e_lo, Y, ldy, out, ldo)
+  const bool comb = out != nullptr;
+  if (MT == 1) {
+    if (gather) { if (comb) KAFKA_WG(1, true, true); else KAFKA_WG(1, true, false); }
+    else { if (comb) KAFKA_WG(1, false, true); else KAFKA_WG(1, false, false); }
+  } else {
+    if (gather) { if (comb) KAFKA_WG(2, true, true); else KAFKA_WG(2, true, false); }
+    else { if (comb) KAFKA_WG(2, false, true); else KAFKA_WG(2, false, false); }
+  }
+#undef KAFKA_WG
+  return hipGetLastError();
+}
 }  // namespace kafka

@@ -300,6 +300,36 @@ def test_grouped_gemm(cuda, T, d, N, E, e_lo, e_n):
     _close(out, out_ref, atol=0.02, rtol=0.01, msg="combine")
 
 
+@pytest.mark.parametrize("T,d,F,E,e_lo,e_n", [(1, 512, 512, 8, 0, 8), (37, 1024, 768, 8, 0, 8),
+                                              (64, 4096, 1792, 8, 0, 8), (128, 512, 1024, 8, 2, 4),
+                                              (100, 768, 256, 8, 4, 4)])
+def test_wstream_grouped(cuda, T, d, F, E, e_lo, e_n):
+    """Expert MLP on the grouped weight-streaming kernel (GLU-tiled w13 with fused SwiGLU, w2 with the fused weighted
+    combine) vs the fp32 reference of the same routing, including an expert-parallel subset of experts."""
+    torch.manual_seed(9)
+    x = torch.randn(T, d, device=cuda, dtype=torch.bfloat16)
+    w13 = (torch.randn(e_n, 2 * F, d, device=cuda) * d ** -0.5).to(torch.bfloat16)
+    w2 = (torch.randn(e_n, d, F, device=cuda) * F ** -0.5).to(torch.bfloat16)
+    r = ops.moe_route(torch.randn(T, E, device=cuda).to(torch.bfloat16), 2)
+    rc = ops.MoERouting(*(t.cpu() for t in (r.topk_w, r.topk_e, r.perm_tok, r.perm_w, r.expert_off, r.tile_off)),
+                        E)
+    w13t, w2t = ops.tile_experts(w13, glu=True), ops.tile_experts(w2)
+    assert torch.equal(ops.untile_experts(w13t, glu=True), w13)
+    a = ops.grouped_stream_glu(x, w13t, r, e_lo=e_lo)
+    h_ref = torch.zeros(T * 2, 2 * F)
+    ref.grouped_gemm(x.cpu().float(), w13.cpu().float(), rc.perm_tok, rc.perm_w, rc.expert_off, e_lo, True, h_ref,
+                     None)
+    eo = rc.expert_off.tolist()
+    lo, hi = eo[e_lo], eo[e_lo + e_n]
+    _close(a[lo:hi], ref.silu_mul(h_ref[lo:hi]), atol=0.03, rtol=0.02, msg="grouped glu")
+    out = torch.zeros(T, d, device=cuda)
+    ops.grouped_stream_combine(a, w2t, r, T, out, e_lo=e_lo)
+    out_ref = torch.zeros(T, d)
+    ref.grouped_gemm(a.cpu(), w2.cpu(), rc.perm_tok, rc.perm_w, rc.expert_off, e_lo, False, None, out_ref)
+    _close(out, out_ref, atol=0.02, rtol=0.01, msg="grouped combine")
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("M", [1, 7, 32, 33, 64, 65, 128])
 @pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1280, 8192), (16032, 1024), (96, 512)])
 def test_wstream_gemm(cuda, M, N, K):
