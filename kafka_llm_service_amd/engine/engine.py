@@ -135,8 +135,11 @@ class LLMEngine:
         if cfg.tp > 1:
             nb = _agree_min(nb)  # every rank of the TP group indexes the same page ids
         self.num_blocks = nb
-        self.k_cache = torch.empty(L, nb, hkv, 16, D, dtype=torch.bfloat16, device=self.device)
-        self.v_cache = torch.empty(L, nb, hkv, D, 16, dtype=torch.bfloat16, device=self.device)
+        # zeroed once: attention tiles read whole 16-key pages and 32-key blocks, and a masked key still multiplies
+        # its V row by p = 0 — finite leftovers of other sequences are harmless, NaN bit patterns in never-written
+        # memory are not (0 * NaN = NaN; tests/test_engine_gpu.py poisons the allocator to keep this honest)
+        self.k_cache = torch.zeros(L, nb, hkv, 16, D, dtype=torch.bfloat16, device=self.device)
+        self.v_cache = torch.zeros(L, nb, hkv, D, 16, dtype=torch.bfloat16, device=self.device)
         self.kvm = KVManager(nb, 16, cfg.enable_prefix_cache)
         max_blocks = (cfg.max_model_len + 15) // 16
         self.sched = Scheduler(SchedulerConfig(max_num_seqs=cfg.max_num_seqs,

@@ -80,3 +80,24 @@ def test_hipgraph_decode_matches_eager(eng):
     assert not g.runner.graphs.disabled, "hipGraph capture failed (see log)"
     assert st["captures"] >= 1 and st["replays"] >= 1
     assert graphed == eager
+
+
+@pytest.mark.parametrize("model", ["tiny-mixtral", "small-llama"])
+def test_engine_on_poisoned_memory(cuda, model):
+    """Every buffer the engine allocates comes from NaN-filled memory: no kernel may read an uninitialised value into
+    a result (regression: never-written KV pool pages reached the PV product as 0 * NaN)."""
+    junk = [torch.full((1 << 27,), float("nan"), device=cuda) for _ in range(4)]
+    del junk
+    e = LLMEngine(EngineConfig(model=model, device="cuda:0", num_kv_blocks=1024, max_model_len=4096))
+    seen = []
+    orig = e.runner.sample_device
+
+    def chk(logits, sp):
+        seen.append(bool(torch.isfinite(logits.float()).all().item()))
+        return orig(logits, sp)
+
+    e.runner.sample_device = chk
+    prompts = _prompts(7, 64, (5, 40, 130), vocab=e.model_cfg.vocab_size)
+    outs = e.generate(prompts, GREEDY)
+    assert seen and all(seen)
+    _oracle_ok(e.model, prompts, outs)
