@@ -67,13 +67,13 @@ __device__ __forceinline__ void load_kv(KVFrag<D>& f, const bf16* __restrict__ k
   // chunk plane 2kk + h, key r & 15
   const bf16* kptr = k_cache + ((int64_t)kp * Hkv + kvh) * (PAGE * D) + (r & 15) * 8 + h * (PAGE * 8);
 #pragma unroll
-  for (int kk = 0; kk < D / 16; ++kk) f.k[kk] = load_bf16x8(kptr + kk * (2 * PAGE * 8));
+  for (int kk = 0; kk < D / 16; ++kk) f.k[kk] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kptr + kk * (2 * PAGE * 8)));
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
     const int vp = s2 ? page1 : page0;
     const bf16* vptr = v_cache + ((int64_t)vp * Hkv + kvh) * (D * PAGE) + r * PAGE + 8 * h;
 #pragma unroll
-    for (int t = 0; t < D / 32; ++t) f.v[s2][t] = load_bf16x8(vptr + 32 * t * PAGE);
+    for (int t = 0; t < D / 32; ++t) f.v[s2][t] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(vptr + 32 * t * PAGE));
   }
 }
 
