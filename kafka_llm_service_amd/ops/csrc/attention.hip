@@ -364,7 +364,7 @@ struct StageRegs {
 __device__ __forceinline__ bf16x8 asm_load16(const bf16* p) {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   i32x4 r;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r) : "v"(p) : "memory");
   return __builtin_bit_cast(bf16x8, r);
 }
 
