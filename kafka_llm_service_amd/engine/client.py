@@ -461,6 +461,6 @@ async def make_engine_client(server_cfg):
     ecfg = EngineConfig(model=server_cfg.model, weights=server_cfg.weights, max_model_len=server_cfg.max_model_len,
                         **server_cfg.engine_kwargs)
     n = max(1, server_cfg.dp)
-    if n == 1 and server_cfg.tp == 1:
+    if n == 1 and server_cfg.tp == 1 and not getattr(server_cfg, "engine_process", False):
         return await asyncio.to_thread(InProcessClient, ecfg)
     return await asyncio.to_thread(DPClient, ecfg, n, 900.0, max(1, server_cfg.tp))

@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import asyncio
 import json
+import os
 import logging
 import time
 import uuid
@@ -112,11 +113,25 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
 
     @asynccontextmanager
     async def lifespan(app: FastAPI):
+        prof = None
+        if os.environ.get("KAFKA_CPROFILE_SERVER"):  # host profile of the API process, dumped at shutdown
+            import cProfile
+
+            prof = cProfile.Profile()
+            prof.enable()
         await st.start()
         try:
             yield
         finally:
             await st.stop()
+            if prof is not None:
+                import pstats
+
+                prof.disable()
+                with open(os.environ["KAFKA_CPROFILE_SERVER"], "w") as f:
+                    ps = pstats.Stats(prof, stream=f)
+                    ps.sort_stats("tottime").print_stats(45)
+                    ps.sort_stats("cumtime").print_stats(60)
 
     app = FastAPI(title="kafka-llm-service-amd", lifespan=lifespan)
     app.state.kafka = st
