@@ -31,6 +31,10 @@ SPILL_FACTOR = float(os.environ.get("KAFKA_DP_SPILL_FACTOR", "2.0"))
 SPILL_MIN = int(os.environ.get("KAFKA_DP_SPILL_MIN", "48"))
 
 
+class EngineUnavailable(RuntimeError):
+    """No live engine can take the request (replica died / restarting / collective timeout): HTTP 503."""
+
+
 def route(key: str | None, n: int, loads: list[int], alive: list[bool] | None = None,
           spill_factor: float = SPILL_FACTOR, spill_min: int = SPILL_MIN) -> int:
     """Replica for a request: the thread's home replica (stable hash of the thread id, so its KV prefix is reused);
@@ -327,7 +331,7 @@ class DPClient:
                 self._streams.pop(rid, None)
             self._loads[r] = 0
         for rid, (loop, q, _) in dead:
-            loop.call_soon_threadsafe(q.put_nowait, RuntimeError(f"engine replica {r} died"))
+            loop.call_soon_threadsafe(q.put_nowait, EngineUnavailable(f"engine replica {r} died"))
 
     async def generate(self, request_id: str, prompt_ids: list[int], params: SamplingParams,
                        routing_key: str | None = None) -> AsyncIterator[StepOutput]:
@@ -336,7 +340,7 @@ class DPClient:
         with self._lock:
             r = route(routing_key, self.n_replicas, self._loads, self._alive)
             if r < 0:
-                raise RuntimeError("no engine replica available (all replicas are restarting)")
+                raise EngineUnavailable("no engine replica available (all replicas are restarting)")
             self._streams[request_id] = (loop, q, r)
             self._loads[r] += 1
         pd = {k: v for k, v in params.__dict__.items() if k != "allowed_tokens_fn"}
@@ -345,7 +349,7 @@ class DPClient:
         except (OSError, BrokenPipeError):
             with self._lock:
                 self._streams.pop(request_id, None)
-            raise RuntimeError(f"engine replica {r} is down")
+            raise EngineUnavailable(f"engine replica {r} is down")
         done = False
         try:
             while True:

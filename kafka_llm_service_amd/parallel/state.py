@@ -5,8 +5,11 @@ Layout of a node of ``world`` ranks:
   * the remaining factor ``dp = world // tp`` are independent engine replicas (DP) — each replica owns its own KV
     cache and its own threads (thread-affinity routing, ``engine/dp_router.py``); replicas never communicate on the
     hot path.
-  * ``ep`` (Mixtral) re-uses the TP group: experts are partitioned over its ranks and tokens are exchanged with
-    all-to-all (``parallel/moe_ep.py``).
+  * ``ep`` (Mixtral) re-uses the TP group: experts are partitioned over its ranks; activations are already
+    replicated after the attention all-reduce, so each rank gathers its experts' tokens locally and one all-reduce
+    combines the partial outputs (``models/moe.py``; README "Expert parallelism").
+  * every collective has a timeout (``KAFKA_COLLECTIVE_TIMEOUT_S``, default 300 s): a hung peer fails the replica's
+    process instead of blocking it forever; the DP client then marks it down (HTTP 503 / error frames) and respawns.
 
 The reference service has no collectives at all; this module is new.
 """
@@ -14,6 +17,7 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
@@ -67,13 +71,13 @@ def init(tp: int = 1, backend: str | None = None, device: str | None = None) -> 
             if backend == "nccl":
                 torch.cuda.set_device(local_rank)
                 kw["device_id"] = torch.device("cuda", local_rank)
-            dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+            dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=_timeout(), **kw)
         st.backend = backend
         if tp > 1:
             for g in range(world // tp):
                 ranks = list(range(g * tp, (g + 1) * tp))
-                pg = dist.new_group(ranks, backend=backend)
-                cpg = dist.new_group(ranks, backend="gloo") if backend != "gloo" else pg
+                pg = dist.new_group(ranks, backend=backend, timeout=_timeout())
+                cpg = dist.new_group(ranks, backend="gloo", timeout=_timeout()) if backend != "gloo" else pg
                 if rank in ranks:
                     st.tp_group, st.cpu_group = pg, cpg
             if backend == "nccl" and os.environ.get("KAFKA_CUSTOM_AR", "0") == "1":
@@ -83,6 +87,10 @@ def init(tp: int = 1, backend: str | None = None, device: str | None = None) -> 
                 comm.register_custom(st.tp_group, CustomAllReduce(st.cpu_group, st.tp_rank, tp))
     _STATE = st
     return st
+
+
+def _timeout() -> timedelta:
+    return timedelta(seconds=float(os.environ.get("KAFKA_COLLECTIVE_TIMEOUT_S", "300")))
 
 
 def set_state(st: ParallelState) -> None:

@@ -314,4 +314,12 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
     async def _value_error(request: Request, exc: ValueError):
         return JSONResponse({"detail": str(exc)}, status_code=400)
 
+    from kafka_llm_service_amd.engine.client import EngineUnavailable
+
+    @app.exception_handler(EngineUnavailable)
+    async def _engine_unavailable(request: Request, exc: EngineUnavailable):
+        # a dead / restarting replica (or an RCCL collective timeout that took its TP group down) is a transient
+        # server condition: 503 so clients retry, the stream path reports it as an error frame
+        return JSONResponse({"detail": str(exc)}, status_code=503)
+
     return app

@@ -186,3 +186,27 @@ def test_engine_context_length_error(engine_client):
     f = frames(c.post("/v1/chat/completions", json=body).text)
     err = [x for x in f if isinstance(x, dict) and "error" in x]
     assert err and "maximum context length" in err[0]["error"]["message"] and f[-1] == "[DONE]"
+
+
+def test_engine_unavailable_is_503():
+    """A dead / restarting engine replica surfaces as HTTP 503 on non-stream requests (retryable) and as an error
+    frame on streams."""
+    from kafka_llm_service_amd.engine.client import EngineUnavailable
+    from kafka_llm_service_amd.llm.base import LLMProvider
+
+    class Down(LLMProvider):
+        async def stream_completion(self, messages, **kw):
+            raise EngineUnavailable("engine replica 0 is down")
+            yield  # pragma: no cover
+
+        async def completion(self, messages, **kw):
+            raise EngineUnavailable("engine replica 0 is down")
+
+    st = ServerState(ServerConfig(backend="stub", sandbox="none"), llm_provider=Down(), db=MemoryDBClient())
+    with TestClient(create_app(state=st), raise_server_exceptions=False) as c:
+        body = {"model": "kafka", "messages": [{"role": "user", "content": "hi"}]}
+        r = c.post("/v1/chat/completions", json=body)
+        assert r.status_code == 503 and "down" in r.json()["detail"]
+        r = c.post("/v1/chat/completions", json=dict(body, stream=True))
+        fr = frames(r.text)
+        assert fr[-1] == "[DONE]" and "error" in fr[-2]
