@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Decode-shaped GEMMs of Llama-3-8B (y = x W^T, bf16): hipBLASLt vs rocBLAS vs the in-tree skinny GEMM.
+"""Decode-shaped GEMMs of Llama-3-8B (y = x W^T, bf16): hipBLASLt vs rocBLAS vs bmm split-K vs the in-tree weight-streaming GEMM (csrc/wstream_gemm.hip).
 
 Reports us/call and the weight-streaming bandwidth (weights are read once per call; x is tiny)."""
 from __future__ import annotations
@@ -39,7 +39,7 @@ def main():
     try:
         from kafka_llm_service_amd import ops
 
-        have_custom = hasattr(ops, "skinny_gemm")
+        have_custom = hasattr(ops, "linear_stream")
     except Exception:
         pass
     for name, (N, K) in SHAPES.items():
@@ -66,16 +66,14 @@ def main():
                 err = (f(0).float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
                 row[f"bmm_splitk{S}_us"] = round(timeit(f), 1)
                 row[f"bmm_splitk{S}_err"] = round(err, 4)
-            if have_custom and M <= 64 and not libs_only:
+            if have_custom and ops.stream_plan(M, N, K) is not None and not libs_only:
                 ref = F.linear(x, w).float()
-                for U in (4, 8):
-                    if not ops.skinny_supported(M, N, K, U):
-                        continue
-                    y = ops.skinny_gemm(x, w, U=U)
-                    err = (y.float() - ref).abs().max().item()
-                    us = timeit(lambda i: ops.skinny_gemm(x, ws[i % nrot], U=U))
-                    row[f"skinny{U}_us"] = round(us, 1)
-                    row[f"skinny{U}_err"] = round(err / (ref.abs().max().item() + 1e-6), 4)
+                wts = [ops.tile_weight(wi) for wi in ws]
+                y = ops.slab_reduce(ops.linear_stream(x, wts[0]))
+                err = (y.float() - ref).abs().max().item()
+                row["wstream_us"] = round(timeit(lambda i: ops.linear_stream(x, wts[i % nrot])), 1)
+                row["wstream_err"] = round(err / (ref.abs().max().item() + 1e-6), 4)
+                del wts
             best = min(v for k, v in row.items() if k.endswith("_us"))
             row["best_TB/s"] = round(N * K * 2 / best / 1e6, 2)
             print(json.dumps(row), flush=True)

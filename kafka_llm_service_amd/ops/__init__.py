@@ -141,21 +141,6 @@ def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, step=No
     return out
 
 
-def skinny_supported(M: int, N: int, K: int, U: int = 4) -> bool:
-    return ext().skinny_supported(int(M), int(N), int(K), int(U))
-
-
-def skinny_gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, U: int = 4) -> torch.Tensor:
-    """y = x @ w.T for decode-sized M (<= 64): the weight-streaming MFMA kernel (csrc/skinny_gemm.hip)."""
-    if out is None:
-        out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-    if _gpu(x):
-        ext().skinny_gemm(x, w, out, int(U))
-    else:
-        out.copy_((x.float() @ w.float().t()).to(x.dtype))
-    return out
-
-
 def tile_weight(w: torch.Tensor, glu: bool = False) -> torch.Tensor:
     """Row-major weight [N, K] -> the wave-tiled layout [N/32, K/16, 64, 8] read by the weight-streaming decode GEMM
     (csrc/wstream_gemm.hip): lane l = (r = l % 32, h = l // 32) of tile (nb, kb) holds W[32 nb + r, 16 kb + 8 h : +8].

@@ -33,10 +33,6 @@ hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows
 hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
                          const float* top_p, const int* top_k, const int64_t* seeds, const int64_t* step,
                          int64_t* out_tokens, hipStream_t st);
-int kafka_skinny_gemm_plan(int M, int N, int K, int U, int* splitk, int* k_per_wave);
-hipError_t kafka_launch_skinny_gemm(const bf16* X, int64_t ldx, const bf16* W, int64_t ldw, bf16* Y, int64_t ldy,
-                                    float* slab, int M, int N, int K, int U, int splitk, int k_per_wave,
-                                    hipStream_t st);
 int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits);
 hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt, int kc,
                                      int splits, int nt, int kw, int glu, bf16* Y, int64_t ldy, float* P,
@@ -301,31 +297,6 @@ static void sample(at::Tensor logits, c10::optional<at::Tensor> temperature, c10
                                  (const int64_t*)st, out.data_ptr<int64_t>(), cur_stream()));
 }
 
-static bool skinny_supported(int64_t M, int64_t N, int64_t K, int64_t U) {
-  int s, kpw;
-  return kafka_skinny_gemm_plan((int)M, (int)N, (int)K, (int)U, &s, &kpw) == 0;
-}
-
-// y[M, N] = x[M, K] . w[N, K]^T for decode-sized M (<= 64), weights streamed once
-static void skinny_gemm(at::Tensor x, at::Tensor w, at::Tensor out, int64_t U) {
-  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(w, at::kBFloat16); CHECK_DT(out, at::kBFloat16);
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_gemm: 2-D tensors");
-  TORCH_CHECK(x.stride(1) == 1 && w.stride(1) == 1 && out.stride(1) == 1, "skinny_gemm: unit inner stride");
-  const int M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N, "skinny_gemm: shape mismatch");
-  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "skinny_gemm: 16-B rows");
-  int splitk = 1, kpw = 0;
-  TORCH_CHECK(kafka_skinny_gemm_plan(M, N, K, (int)U, &splitk, &kpw) == 0, "skinny_gemm: unsupported shape");
-  at::Tensor slab;
-  float* sp = nullptr;
-  if (splitk > 1) {
-    slab = at::empty({(int64_t)splitk * M * N}, x.options().dtype(at::kFloat));
-    sp = slab.data_ptr<float>();
-  }
-  CHECK_HIP(kafka_launch_skinny_gemm(bptr(x), x.stride(0), bptr(w), w.stride(0), bptr(out), out.stride(0), sp, M, N,
-                                     K, (int)U, splitk, kpw, cur_stream()));
-}
-
 // (mt, kc, splits) of the weight-streaming decode GEMM for a shape, or (0, 0, 0) if unsupported
 static std::vector<int64_t> wstream_plan(int64_t M, int64_t N, int64_t K, int64_t max_splits) {
   int mt = 0, kc = 0, s = 0;
@@ -544,8 +515,6 @@ PYBIND11_MODULE(_kafka_ops, m) {
         py::arg("scale"), py::arg("variant") = 0);
   m.def("attn_merge", &attn_merge);
   m.def("sample", &sample);
-  m.def("skinny_supported", &skinny_supported);
-  m.def("skinny_gemm", &skinny_gemm);
   m.def("wstream_plan", &wstream_plan);
   m.def("wstream_gemm", &wstream_gemm);
   m.def("wstream_gemm_cfg", &wstream_gemm_cfg);
