@@ -29,6 +29,7 @@ import time
 
 import torch
 
+METRIC = "output tok/s + p50 TTFT, Llama-3-8B, 64 concurrent threads, 1/2/4/8 MI355X"  # BASELINE.json
 BASELINE_TOKS = 22300.0  # stub chunks/s, 64 threads, stream (reference plumbing ceiling)
 
 
@@ -230,7 +231,8 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
     p99 = ttfts[min(len(ttfts) - 1, int(len(ttfts) * 0.99))] * 1e3 if ttfts else None
     kv = eng.kv_stats()
     res = {
-        "metric": "output tok/s + p50 TTFT, Llama-3-8B, 64 concurrent threads",
+        "metric": METRIC if (args.model, args.threads) == ("llama3-8b", 64) else
+        f"output tok/s + p50 TTFT, {args.model}, {args.threads} concurrent threads per replica",
         "value": round(value, 1), "unit": "tok/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": round(value / BASELINE_TOKS, 3), "dtype": "bf16",

@@ -13,6 +13,8 @@ expert sort, no host sync) -> ``ops.grouped_gemm`` gate_up (HIP MFMA, A rows gat
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -31,6 +33,8 @@ def route(logits: torch.Tensor, k: int):
 class MoEBlock:
     def __init__(self, model):
         self.model = model
+        # expert all-to-all dispatch/combine instead of the all-reduce combine (opt-in, see _a2a)
+        self.a2a = os.environ.get("KAFKA_MOE_A2A", "0") == "1"
         cfg = model.cfg
         self.E = cfg.num_experts
         self.k = cfg.num_experts_per_tok
@@ -44,6 +48,8 @@ class MoEBlock:
         T, d = x.shape
         logits = F.linear(x, lw.router)
         r = ops.moe_route(logits, self.k)
+        if self.ep > 1 and self.a2a:
+            return self._a2a(x, lw, r)
         if self.model.stream and lw.w13_t is not None and T <= ops.STREAM_MAX_M:
             # decode-sized steps: expert weights streamed from their wave-tiled copies, SwiGLU fused into the gate_up
             # epilogue, weighted combine fused into the down epilogue (csrc/wstream_gemm.hip, grouped variant)
@@ -62,3 +68,71 @@ class MoEBlock:
         if self.ep > 1:
             out = pstate.tp_all_reduce(out)
         return out
+
+
+    # ------------------------------------------------------------------------------------------------------------
+    def _a2a(self, x: torch.Tensor, lw, r) -> torch.Tensor:
+        """Expert parallelism with an all-to-all dispatch and combine (``KAFKA_MOE_A2A=1``; BASELINE config 5's
+        "expert all-to-all").
+
+        Every rank holds all T tokens (replicated after the attention all-reduce) and computes the same routing.
+        Rank q OWNS tokens [q Tl, (q+1) Tl): it packs each owned (token, expert) pair into the bucket of the rank
+        that holds the expert (``all_to_all_single`` with equal splits: a capacity of Tl*k rows per destination, so
+        no host round trip for split sizes), the expert ranks run their local experts on what they received (the
+        same grouped-GEMM kernels over a k=1 routing of the received rows), the outputs travel back with a second
+        all-to-all, the owner applies the routing weights and the owners' rows are all-gathered into the replicated
+        [T, d] the next layer expects. With tensor-parallel attention this moves more bytes than the default
+        all-reduce combine (capacity padding + the all-gather), so it is not the default; it is the building block
+        for data-parallel attention, where tokens are not replicated."""
+        import torch.distributed as dist
+
+        T, d = x.shape
+        ep, q, k, El = self.ep, self.r, self.k, self.e_local
+        grp = pstate.get().tp_group
+        dev = x.device
+        Tl = (T + ep - 1) // ep
+        lo, hi = min(T, q * Tl), min(T, (q + 1) * Tl)
+        n_own = hi - lo
+        C = Tl * k  # rows per destination bucket (worst case: every owned pair goes to one rank)
+        te = r.topk_e[lo:hi].long().reshape(-1)                  # [n_own*k] global expert ids
+        tw = r.topk_w[lo:hi].float().reshape(-1)
+        tok = torch.arange(lo, hi, device=dev).repeat_interleave(k)
+        dest = te // El
+        # stable position of each pair inside its destination bucket
+        onehot = F.one_hot(dest, ep).to(torch.int32)
+        pos = ((torch.cumsum(onehot, 0) - 1) * onehot).sum(1)
+        send = torch.zeros(ep, C, d, dtype=x.dtype, device=dev)
+        meta = torch.full((ep, C), -1, dtype=torch.int32, device=dev)
+        if n_own:
+            send[dest, pos] = x[tok]
+            meta[dest, pos] = (te - dest * El).to(torch.int32)
+        recv = torch.empty_like(send)
+        rmeta = torch.empty_like(meta)
+        dist.all_to_all_single(recv, send, group=grp)
+        dist.all_to_all_single(rmeta, meta, group=grp)
+        # local expert MLP over the received rows (k = 1 routing; empty slots carry expert -1 and are skipped)
+        rows = recv.view(ep * C, d)
+        re = rmeta.view(-1).long()
+        valid = re >= 0
+        key = torch.where(valid, re, torch.full_like(re, El))     # empty slots sort past the last expert
+        perm = torch.argsort(key, stable=True)
+        counts = torch.bincount(key, minlength=El + 1)[:El]
+        eo = torch.zeros(El + 1, dtype=torch.int32, device=dev)
+        eo[1:] = torch.cumsum(counts, 0)
+        to = torch.zeros(El + 1, dtype=torch.int32, device=dev)
+        to[1:] = torch.cumsum((counts + ops.GG_BM - 1) // ops.GG_BM, 0)
+        n_valid = int(ep * C)  # perm covers every slot; segments stop at eo[El]
+        rr = ops.MoERouting(torch.ones(ep * C, 1, device=dev), re.to(torch.int32).view(-1, 1),
+                            perm.to(torch.int32), torch.ones(n_valid, device=dev), eo, to, El)
+        h = ops.grouped_gemm(rows, lw.w13, rr, gather=True, e_lo=0)
+        a = ops.silu_mul(h)
+        y = torch.zeros(ep * C, d, dtype=torch.float32, device=dev)
+        ops.grouped_gemm(a, lw.w2, rr, gather=False, e_lo=0, combine_out=y)
+        back = torch.empty_like(send)
+        dist.all_to_all_single(back, y.to(x.dtype).view(ep, C, d), group=grp)
+        own = torch.zeros(Tl, d, dtype=torch.float32, device=dev)
+        if n_own:
+            own.index_add_(0, tok - lo, back[dest, pos].float() * tw[:, None])
+        full = torch.empty(ep * Tl, d, dtype=x.dtype, device=dev)
+        dist.all_gather_into_tensor(full, own.to(x.dtype), group=grp)
+        return full[:T]

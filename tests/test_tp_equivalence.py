@@ -90,6 +90,9 @@ def _capture_logits(eng, prompt):
 def _logits_main(rank: int, world: int, port: int, q, model: str) -> None:
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(world),
                        "RANK": str(rank), "LOCAL_RANK": str(rank)})
+    if model.endswith("+a2a"):  # expert all-to-all dispatch/combine instead of the all-reduce combine
+        os.environ["KAFKA_MOE_A2A"] = "1"
+        model = model[:-4]
     from kafka_llm_service_amd.engine import tp_worker
     from kafka_llm_service_amd.parallel import state as pstate
 
@@ -106,9 +109,10 @@ def _logits_main(rank: int, world: int, port: int, q, model: str) -> None:
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("model", ["tiny-llama", "tiny-mixtral"])
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-mixtral", "tiny-mixtral+a2a"])
 def test_tp2_logits_close_to_tp1(model):
-    """Dense: Megatron TP=2. Mixtral: attention TP=2 + expert parallel EP=2 over the same group."""
+    """Dense: Megatron TP=2. Mixtral: attention TP=2 + expert parallel EP=2 over the same group, with the
+    all-reduce combine or the all-to-all dispatch/combine (+a2a)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
@@ -119,7 +123,7 @@ def test_tp2_logits_close_to_tp1(model):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    want = _capture_logits(LLMEngine(EngineConfig(**dict(CFG, model=model))), _prompts()[1])
+    want = _capture_logits(LLMEngine(EngineConfig(**dict(CFG, model=model.replace("+a2a", "")))), _prompts()[1])
     assert got.shape == want.shape
     assert torch.allclose(got, want, atol=3e-2, rtol=0), (got - want).abs().max()
 
