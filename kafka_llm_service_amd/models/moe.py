@@ -56,18 +56,22 @@ class MoEBlock:
             a = ops.grouped_stream_glu(x, lw.w13_t, r, e_lo=self.e0)
             out = torch.zeros(T, d, dtype=torch.float32, device=x.device)
             ops.grouped_stream_combine(a, lw.w2_t, r, T, out, e_lo=self.e0)
-            out = out.to(x.dtype)
-            return pstate.tp_all_reduce(out) if self.ep > 1 else out
+            return self._finish(out, x.dtype)
         # gate_up for every (token, expert) entry routed to a local expert, rows gathered from x by the kernel
         h = ops.grouped_gemm(x, lw.w13, r, gather=True, e_lo=self.e0)
         a = ops.silu_mul(h)
         # down projection with the routing-weighted scatter-combine fused into the epilogue
         out = torch.zeros(T, d, dtype=torch.float32, device=x.device)
         ops.grouped_gemm(a, lw.w2, r, gather=False, e_lo=self.e0, combine_out=out)
-        out = out.to(x.dtype)
+        return self._finish(out, x.dtype)
+
+    def _finish(self, out: torch.Tensor, dtype) -> torch.Tensor:
+        """The fp32 combine buffer [T, d] as the layer's delta: on one rank it is handed on as a one-split slab
+        [1, T, d] (the next add + RMSNorm sums slabs while loading — no separate fp32 -> bf16 pass); expert-parallel
+        ranks all-reduce the bf16 partial outputs."""
         if self.ep > 1:
-            out = pstate.tp_all_reduce(out)
-        return out
+            return pstate.tp_all_reduce(out.to(dtype))
+        return out.unsqueeze(0)
 
 
     # ------------------------------------------------------------------------------------------------------------
