@@ -1,7 +1,7 @@
 // Rotary embedding on Q/K fused with the paged KV-cache write (gfx950).
 //
 // Input is the fused QKV projection output [T, (Hq + 2*Hkv) * D] — bf16, or S fp32 split-K slabs of the decode
-// GEMM (wstream_gemm.hip) summed while loading. One workgroup per token:
+// GEMM (wstream_gemm.hip) summed while loading. One workgroup per token, one thread per 8-element unit:
 //   * Q heads: rotate-half RoPE -> q_out[T, Hq, D]
 //   * K heads: rotate-half RoPE -> k_cache page  [num_blocks, Hkv, 16, D]   as D/8 chunk planes [D/8][16 keys][8]:
 //              element (key o, d) at ((d >> 3) * 16 + o) * 8 + (d & 7). The MFMA A fragment of a 16-key page for
@@ -22,7 +22,7 @@ namespace kafka {
 __device__ __forceinline__ int vt_pos(int o) { return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1); }
 
 template <int D>
-__global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ qkv, const float* __restrict__ qp,
+__global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ qkv, const float* __restrict__ qp,
                                                        int S, int64_t ps, int64_t qkv_stride,
                                                        const int64_t* __restrict__ positions,
                                                        const float* __restrict__ cos_sin,
@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
   const int n_total = n_rope + Hkv * VU;
   const int64_t blk = slot >= 0 ? slot / block_size : 0;
   const int off = slot >= 0 ? (int)(slot % block_size) : 0;
-  for (int u = threadIdx.x; u < n_total; u += 256) {
+  for (int u = threadIdx.x; u < n_total; u += blockDim.x) {
     if (u < n_rope) {
       const int head = u / RU;
       const int c = (u % RU) * 8;
@@ -93,12 +93,16 @@ extern "C" hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int
                                           int block_size, hipStream_t st) {
   if (T == 0) return hipSuccess;
   if (D != 128 && D != 64) return hipErrorInvalidValue;
+  // one thread per work unit (8 rotation pairs of a Q/K head, or 8 V elements), so a token's whole row is one
+  // round of loads instead of a strided loop paying the HBM latency twice (448 units for Llama-3-8B)
+  const int units = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
+  const int nt = units <= 256 ? 256 : (units <= 512 ? 512 : 1024);
   if (D == 128)
-    rope_kv_kernel<128><<<T, 256, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
-                                           v_cache, slot_mapping, Hq, Hkv, block_size);
-  else
-    rope_kv_kernel<64><<<T, 256, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
+    rope_kv_kernel<128><<<T, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
                                           v_cache, slot_mapping, Hq, Hkv, block_size);
+  else
+    rope_kv_kernel<64><<<T, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
+                                         v_cache, slot_mapping, Hq, Hkv, block_size);
   return hipGetLastError();
 }
 
