@@ -42,6 +42,18 @@ struct AttnWorkItem {
   int pad0, pad1;
 };
 
+// Reductions with the partner lane l ^ 32 on gfx950's v_permlane32_swap (one VALU op, no LDS crossbar round trip
+// through ds_bpermute — which also queued behind the K/V fragment reads): swapping a register with itself leaves
+// x[l] in one result and x[l ^ 32] in the other, so a symmetric op of the two is the xor-32 reduction on every lane.
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 template <int D>
 struct WaveAcc {
   f32x16 o[D / 32];
@@ -104,7 +116,7 @@ __device__ __forceinline__ void softmax_pv(f32x16& s, bool masked, int key0, int
   float mx = s[0];
 #pragma unroll
   for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[i]);
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx = xor32_max(mx);
   const float m_new = fmaxf(acc.m, mx * scale_log2);
   const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
   if (!__all(m_new == acc.m)) {
@@ -121,7 +133,7 @@ __device__ __forceinline__ void softmax_pv(f32x16& s, bool masked, int key0, int
     s[i] = p;
     psum += p;
   }
-  psum += __shfl_xor(psum, 32, 64);
+  psum = xor32_sum(psum);
   acc.l += psum;
   bf16x8 pf[2];
 #pragma unroll
