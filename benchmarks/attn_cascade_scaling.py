@@ -4,6 +4,7 @@
 per-workgroup cost a (launch, Q / page-table loads, pipeline fill, partial write-out) from the per-32-key-block cost b."""
 import json
 import math
+import os
 import statistics
 
 import torch
@@ -27,22 +28,29 @@ for P in (4608, 9216, 18432, 36864, 73728):
     part = torch.empty(B, Hq, nc, D, device=dev)
     lse = torch.empty(B, Hq, nc, device=dev)
 
-    def run():
-        ops.attn_prefill(items, q, k, v, bt, ql, D ** -0.5, out_part=part, lse_part=lse)
+    ref_part, ref_lse = None, None
+    for variant in [int(x) for x in os.environ.get("VARIANTS", "0").split(",")]:
+      def run():
+        ops.attn_prefill(items, q, k, v, bt, ql, D ** -0.5, out_part=part, lse_part=lse, variant=variant)
 
-    ts = []
-    for _ in range(5):
-        run()
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(20):
-            run()
-        e.record()
-        torch.cuda.synchronize()
-        ts.append(s.elapsed_time(e) * 1e3 / 20)
-    us = statistics.median(ts)
-    flops = 4 * B * Hq * P * D
-    print(json.dumps({"prefix": P, "blocks_per_wg": chunk // 32, "us": round(us, 1),
-                      "TF/s": round(flops / us / 1e6, 1)}), flush=True)
+      ts = []
+      for _ in range(5):
+          run()
+          torch.cuda.synchronize()
+          s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+          s.record()
+          for _ in range(20):
+              run()
+          e.record()
+          torch.cuda.synchronize()
+          ts.append(s.elapsed_time(e) * 1e3 / 20)
+      us = statistics.median(ts)
+      if ref_part is None:
+          ref_part, ref_lse = part.clone(), lse.clone()
+          err = 0.0
+      else:
+          err = max((part - ref_part).abs().max().item(), (lse - ref_lse).abs().max().item())
+      flops = 4 * B * Hq * P * D
+      print(json.dumps({"prefix": P, "blocks_per_wg": chunk // 32, "us": round(us, 1),
+                        "TF/s": round(flops / us / 1e6, 1), "variant": variant, "max_err": err}), flush=True)
     del k, v
