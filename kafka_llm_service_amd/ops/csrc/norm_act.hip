@@ -25,6 +25,13 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(bf16* __restrict__ out, in
   const int nvec = d >> 3;
   float v[NV][8];
   float ss = 0.f;
+  // the weight loads go out with the row loads (not after the reduction: one HBM round trip instead of two)
+  bf16x8 wv[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = threadIdx.x + i * 256;
+    if (vi < nvec) wv[i] = load_bf16x8(w + vi * 8);
+  }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int vi = threadIdx.x + i * 256;
@@ -50,10 +57,9 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(bf16* __restrict__ out, in
   for (int i = 0; i < NV; ++i) {
     const int vi = threadIdx.x + i * 256;
     if (vi < nvec) {
-      bf16x8 wv = load_bf16x8(w + vi * 8);
       bf16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[i][j] * r * (float)wv[j]);
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[i][j] * r * (float)wv[i][j]);
       store_bf16x8(out + row * out_stride + vi * 8, o);
     }
   }
