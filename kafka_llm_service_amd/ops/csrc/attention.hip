@@ -473,6 +473,21 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkIte
   const bool valid = tok < it.q_count;
   const int token = it.q_start + tok;
   const int limit = valid ? q_limit[token] : -1;
+  const int* bt = block_tables + (int64_t)it.bt_row * bt_stride;
+  // LDS variant: the Q fragments and the page ids of the item's key range are requested here, together with
+  // q_limit, so the prologue pays one memory round trip for all three instead of one each
+  __shared__ __attribute__((aligned(16))) char lds[LDS ? 2 * STAGE_BYTES : 16];
+  __shared__ int s_hi[NW];
+  __shared__ int s_pages[LDS ? MAX_STAGED_PAGES : 1];
+  bf16x8 qf[D / 16];
+  if constexpr (LDS) {
+    load_q_frags<D>(qf, q + (int64_t)token * q_stride + (int64_t)(kvh * G + g) * D, valid, h);
+    // (the host never builds an LDS-variant item spanning more than MAX_STAGED_PAGES pages: model_runner splits
+    // longer key ranges; a violating item produces NaN instead of reading out of bounds)
+    const int pg0 = (it.kv_lo & ~31) >> 4;
+    const int npg = min(((it.kv_hi + 15) >> 4) - pg0, MAX_STAGED_PAGES);
+    for (int i = threadIdx.x; i < npg; i += NW * 64) s_pages[i] = bt[pg0 + i];
+  }
   // wave-uniform key range
   int wmax = limit;
 #pragma unroll
@@ -482,30 +497,23 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkIte
   for (int o = 32; o > 0; o >>= 1) wmin = min(wmin, __shfl_xor(wmin, o, 64));
   const int lo = it.kv_lo;
   const int hi = min(it.kv_hi, wmax + 1);
-  const int* bt = block_tables + (int64_t)it.bt_row * bt_stride;
 
   WaveAcc<D> acc;
   init_acc<D>(acc);
   if constexpr (!LDS) {
     if (hi > lo) {
-      bf16x8 qf[D / 16];
       load_q_frags<D>(qf, q + (int64_t)token * q_stride + (int64_t)(kvh * G + g) * D, valid, h);
       const int base = lo & ~31;
       attn_blocks<D>(k_cache, v_cache, Hkv, kvh, bt, base, 0, (hi - base + 31) >> 5, 1, hi, lo, hi, limit, qf,
                      scale_log2, acc, lane);
     }
   } else {
-    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE_BYTES];
-    __shared__ int s_hi[NW];
-    __shared__ int s_pages[MAX_STAGED_PAGES];
     if (lane == 0) s_hi[w] = hi;
     __syncthreads();
     int hi_wg = s_hi[0];
 #pragma unroll
     for (int i = 1; i < NW; ++i) hi_wg = max(hi_wg, s_hi[i]);
     if (hi_wg > lo) {  // workgroup-uniform
-      bf16x8 qf[D / 16];
-      load_q_frags<D>(qf, q + (int64_t)token * q_stride + (int64_t)(kvh * G + g) * D, valid, h);
       // retire the Q loads here: otherwise hipcc keeps a vmcnt(0) for them inside the loop, which would also
       // drain the (compiler-invisible) staging loads every block
 #pragma unroll
@@ -514,15 +522,11 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkIte
       const int nblk = (hi_wg - base + 31) >> 5;
       const int tid = threadIdx.x;
       constexpr int LOADS = 2 * (512 / (NW * 64));  // asm loads per register stage per thread
-      // page indices of the item's key range staged in LDS once: no scalar global load (and no lgkmcnt(0) on it)
-      // inside the block loop
-      // (the host never builds an LDS-variant item spanning more than MAX_STAGED_PAGES pages: model_runner splits
-      // longer key ranges; a violating item produces NaN instead of reading out of bounds)
+      // page indices of the item's key range were staged in LDS in the prologue (published by the s_hi barrier):
+      // no scalar global load (and no lgkmcnt(0) on it) inside the block loop
       const int pg0 = base >> 4;
       const int npg = ((hi_wg + 15) >> 4) - pg0;
       const bool fits = npg <= MAX_STAGED_PAGES;
-      for (int i = tid; i < npg && i < MAX_STAGED_PAGES; i += NW * 64) s_pages[i] = bt[pg0 + i];
-      __syncthreads();
       auto pages_of = [&](int key0, int& a, int& b2) {
         const int i0 = min((key0 >> 4) - pg0, MAX_STAGED_PAGES - 2);
         a = s_pages[i0];
