@@ -85,9 +85,9 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         elif meta.prefix_items is not None:
             ops.attn_prefill(meta.prefix_items, qd, k_cache, v_cache, meta.block_tables, meta.q_limit,
                              meta.scale, out_part=meta.part, lse_part=meta.lse)
-        # one split per sequence (the usual case at 64+ sequences): the decode kernel merges the prefix partials
-        # itself and writes the final rows; else partials + merge kernel
-        fused = meta.num_splits == 1 and meta.num_prefix_splits <= 63 and not overlap
+        # the decode kernel merges the prefix partials itself and writes the final rows (one split per sequence —
+        # the usual case at 64+ sequences — directly, several through its ticket counters); else merge kernel
+        fused = meta.num_splits + meta.num_prefix_splits <= 64 and not overlap
         ops.attn_decode(qd, k_cache, v_cache, meta.block_tables, meta.seq_lens, meta.kv_start, meta.part,
                         meta.lse, meta.num_splits, meta.num_prefix_splits, meta.scale, out=out[:B] if fused else None)
         if overlap:

@@ -83,17 +83,31 @@ def rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping
                           slot_mapping, Hq, Hkv)
 
 
+_TICKETS: dict = {}
+
+
+def _tickets(dev: torch.device, n: int) -> torch.Tensor:
+    """Zeroed int32 counters for the decode kernel's ticket merge (re-armed by the kernel itself, so one buffer per
+    device serves every layer and step; allocated once, large, so graph capture never allocates)."""
+    t = _TICKETS.get(dev)
+    if t is None or t.numel() < n:
+        t = _TICKETS[dev] = torch.zeros(max(n, 1 << 16), dtype=torch.int32, device=dev)
+    return t
+
+
 def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part, lse_part, num_splits: int,
                 split_offset: int, scale: float, out=None) -> None:
     """Split-K paged decode attention writing (O, lse2) partials [B, Hq, S_total, D] at splits
-    [split_offset, split_offset + num_splits). With ``out`` (needs num_splits == 1) the kernel instead merges its
-    result with the partials [0, split_offset) already present (cascade prefix) and writes final bf16 rows."""
+    [split_offset, split_offset + num_splits). With ``out`` (at most 64 partials in total) the kernel instead merges
+    the result with the partials [0, split_offset) already present (cascade prefix) and writes final bf16 rows: with
+    one split per sequence directly, with several through ticket counters (the last split of a sequence merges)."""
     if _gpu(q):
+        tk = _tickets(q.device, q.shape[0] * k_cache.shape[1]) if out is not None and num_splits > 1 else None
         ext().attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part, lse_part,
-                          int(num_splits), int(split_offset), float(scale), out)
+                          int(num_splits), int(split_offset), float(scale), out, tk)
         return
-    if out is not None and num_splits != 1:
-        raise ValueError("fused-merge decode needs num_splits == 1")
+    if out is not None and split_offset + num_splits > 64:
+        raise ValueError("fused-merge decode needs <= 64 partials")
     o, l2 = ref.attn_decode_full(q, k_cache, v_cache, block_tables, seq_lens, scale, kv_start)
     B = q.shape[0]
     S_total = out_part.shape[2]
@@ -103,7 +117,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part,
     out_part[:B, :, split_offset] = o
     lp[:B, :, split_offset] = l2
     if out is not None:
-        n = split_offset + 1
+        n = split_offset + num_splits
         ref.attn_merge(out_part[:B, :, :n].contiguous(), lp[:B, :, :n].contiguous(), out[:B])
 
 

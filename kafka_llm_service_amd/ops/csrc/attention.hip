@@ -218,7 +218,8 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
                                                            const int* __restrict__ kv_start,
                                                            float* __restrict__ out_part, float* __restrict__ lse_part,
                                                            int S_total, int split_offset, float scale_log2,
-                                                           bf16* __restrict__ out, int64_t out_stride) {
+                                                           bf16* __restrict__ out, int64_t out_stride,
+                                                           int* __restrict__ tickets) {
   __shared__ float sO[4][8][D];
   __shared__ float sM[4][8];
   __shared__ float sL[4][8];
@@ -259,14 +260,14 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
     }
   }
   __syncthreads();
-  if (out != nullptr) {
+  __shared__ float sW[8][65];
+  __shared__ float sWt[8];
+  if (out != nullptr && S == 1) {
     // Fused merge (one split per sequence): fold in the cascade-prefix partials [0, split_offset) written earlier
     // on the stream and write the final bf16 rows — no merge kernel, no partial round trip of this split.
     // Phase 1: wave w owns heads w, w + 4: lanes load the prefix lse values in parallel, wave-reduce the max and
     // the weight sum, and publish per-split weights in LDS. Phase 2: thread (g, 4 dims) sums weight x partial over
     // the splits with all loads of a group of 8 in flight.
-    __shared__ float sW[8][65];
-    __shared__ float sWt[8];
     for (int g = w; g < G; g += 4) {
       float Ms = -INFINITY;
 #pragma unroll
@@ -340,8 +341,67 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
       }
     }
     const int64_t pidx = ((int64_t)b * Hq + kvh * G + g) * S_total + split_offset + split;
-    out_part[pidx * D + d] = L > 0.f ? O / L : 0.f;
-    if (d == 0) lse_part[pidx] = L > 0.f ? M + log2f(L) : -INFINITY;
+    const float ov = L > 0.f ? O / L : 0.f, lv = L > 0.f ? M + log2f(L) : -INFINITY;
+    if (out == nullptr) {
+      out_part[pidx * D + d] = ov;
+      if (d == 0) lse_part[pidx] = lv;
+    } else {  // ticket merge: write-through (agent-coherent) stores, no L2-wide write-back fence needed
+      __hip_atomic_store(out_part + pidx * D + d, ov, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == 0) __hip_atomic_store(lse_part + pidx, lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (out == nullptr) return;
+  // Ticket merge (S > 1, e.g. one long sequence spread over many workgroups): every split publishes its partial
+  // with agent-coherent write-through stores (another XCD's workgroup may read it; a __threadfence release here
+  // would write back the whole L2 from every workgroup), waits for them, takes a ticket, and the LAST of the S
+  // workgroups of (b, kvh) merges all split_offset + S partials (agent-coherent loads) and writes the bf16 rows —
+  // no merge kernel launch. The last one also re-arms the counter for the next launch.
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* tk = tickets + b * Hkv + kvh;
+    const int t = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t == S - 1;
+    if (t == S - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto ld4 = [&](const float* p) { return f32x4{ld(p), ld(p + 1), ld(p + 2), ld(p + 3)}; };
+  const int n = split_offset + S;  // <= 64 (host-checked)
+  for (int g = w; g < G; g += 4) {
+    const int64_t pbase = ((int64_t)b * Hq + kvh * G + g) * S_total;
+    const float lv = lane < n ? ld(lse_part + pbase + lane) : -INFINITY;
+    float mx = lv;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    const float wv = mx == -INFINITY ? 0.f : exp2f(lv - mx);
+    float ws = wv;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ws += __shfl_xor(ws, o, 64);
+    if (lane < n) sW[g][lane] = wv;
+    if (lane == 0) sWt[g] = ws;
+  }
+  __syncthreads();
+  const int g = threadIdx.x >> 5, c = (threadIdx.x & 31) * 4;
+  if (g < G) {
+    f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
+    const float* pp = out_part + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
+    int s2 = 0;
+    for (; s2 + 8 <= n; s2 += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ld4(pp + (s2 + j) * D);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc4 += v[j] * sW[g][s2 + j];
+    }
+    for (; s2 < n; ++s2) acc4 += ld4(pp + s2 * D) * sW[g][s2];
+    const float inv = sWt[g] > 0.f ? 1.f / sWt[g] : 0.f;
+    bf16x4 o4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc4[j] * inv);
+    *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
   }
 }
 
@@ -662,15 +722,17 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(const float* __restrict
 extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const bf16* k_cache, const bf16* v_cache, int B,
                               int Hkv, int G, int D, const int* block_tables, int bt_stride, const int* seq_lens,
                               const int* kv_start, float* out_part, float* lse_part, int S, int S_total,
-                              int split_offset, float scale, bf16* out, int64_t out_stride, hipStream_t st) {
+                              int split_offset, float scale, bf16* out, int64_t out_stride, int* tickets,
+                              hipStream_t st) {
   if (B == 0) return hipSuccess;
   if (D != 128 || G > 8 || G < 1) return hipErrorInvalidValue;
-  // the fused merge needs one split per sequence and at most 63 prefix partials (one wave lane each + its own)
-  if (out != nullptr && (S != 1 || split_offset > 63)) return hipErrorInvalidValue;
+  // fused merge: one wave lane per partial -> at most 64 (S == 1: 63 prefix partials + its own); S > 1 merges
+  // through the ticket counters ([B * Hkv] int32, zero, re-armed by the kernel)
+  if (out != nullptr && (split_offset + S > 64 || (S > 1 && tickets == nullptr))) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
   attn_decode_kernel<128><<<dim3(S, Hkv, B), 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables,
                                                            bt_stride, seq_lens, kv_start, out_part, lse_part, S_total,
-                                                           split_offset, scale_log2, out, out_stride);
+                                                           split_offset, scale_log2, out, out_stride, tickets);
   return hipGetLastError();
 }
 

@@ -23,7 +23,8 @@ hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int S, int64_t
 hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const bf16* k_cache, const bf16* v_cache, int B,
                               int Hkv, int G, int D, const int* block_tables, int bt_stride, const int* seq_lens,
                               const int* kv_start, float* out_part, float* lse_part, int S, int S_total,
-                              int split_offset, float scale, bf16* out, int64_t out_stride, hipStream_t st);
+                              int split_offset, float scale, bf16* out, int64_t out_stride, int* tickets,
+                              hipStream_t st);
 hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride, const bf16* k_cache,
                                const bf16* v_cache, int Hkv, int G, int D, const int* block_tables, int bt_stride,
                                const int* q_limit, bf16* out, int64_t out_stride, float* out_part, float* lse_part,
@@ -175,7 +176,7 @@ static void check_cache_pair(const at::Tensor& k_cache, const at::Tensor& v_cach
 static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
                         at::Tensor seq_lens, c10::optional<at::Tensor> kv_start, at::Tensor out_part,
                         at::Tensor lse_part, int64_t num_splits, int64_t split_offset, double scale,
-                        c10::optional<at::Tensor> out) {
+                        c10::optional<at::Tensor> out, c10::optional<at::Tensor> tickets) {
   CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
   CHECK_DT(block_tables, at::kInt); CHECK_DT(seq_lens, at::kInt); CHECK_DT(out_part, at::kFloat);
   CHECK_DT(lse_part, at::kFloat);
@@ -191,13 +192,20 @@ static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at
   TORCH_CHECK(lse_part.is_contiguous() && lse_part.numel() >= (int64_t)B * Hq * S_total, "lse_part");
   bf16* op = nullptr;
   int64_t ostride = 0;
-  if (out.has_value()) {  // fused merge: final bf16 rows [B, Hq, 128] (one split per sequence)
+  int* tp = nullptr;
+  if (out.has_value()) {  // fused merge: final bf16 rows [B, Hq, 128]
     CHECK_DT(out.value(), at::kBFloat16);
-    TORCH_CHECK(num_splits == 1 && split_offset <= 63 && out->dim() == 3 && out->size(0) >= B && out->size(1) == Hq &&
+    TORCH_CHECK(split_offset + num_splits <= 64 && out->dim() == 3 && out->size(0) >= B && out->size(1) == Hq &&
                     out->size(2) == 128 && out->stride(2) == 1 && out->stride(1) == 128,
-                "attn_decode: fused-merge out must be [B, Hq, 128], num_splits == 1, <= 63 prefix splits");
+                "attn_decode: fused-merge out must be [B, Hq, 128] with <= 64 partials in total");
     op = bptr(out.value());
     ostride = out->stride(0);
+    if (num_splits > 1) {
+      TORCH_CHECK(tickets.has_value() && tickets->is_cuda() && tickets->scalar_type() == at::kInt &&
+                      tickets->numel() >= (int64_t)B * Hkv,
+                  "attn_decode: num_splits > 1 with out needs an int32 ticket buffer of >= B * Hkv zeros");
+      tp = tickets->data_ptr<int>();
+    }
   }
   const int* ks = nullptr;
   if (kv_start.has_value()) {
@@ -208,7 +216,7 @@ static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at
   CHECK_HIP(kafka_launch_attn_decode(bptr(q), q.stride(0), bptr(k_cache), bptr(v_cache), B, Hkv, Hq / Hkv, 128,
                                       block_tables.data_ptr<int>(), block_tables.stride(0), seq_lens.data_ptr<int>(),
                                       ks, out_part.data_ptr<float>(), lse_part.data_ptr<float>(), num_splits,
-                                      S_total, split_offset, scale, op, ostride, cur_stream()));
+                                      S_total, split_offset, scale, op, ostride, tp, cur_stream()));
 }
 
 static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,

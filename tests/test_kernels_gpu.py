@@ -112,9 +112,11 @@ def test_attn_decode(cuda, Hq, Hkv, lens, S):
     _close(lse_o, l_ref, atol=0.02, msg="decode lse")
 
 
-@pytest.mark.parametrize("n_pre", [0, 1, 3, 6])
-def test_attn_decode_fused_merge(cuda, n_pre):
-    """One split per sequence: the decode kernel merges the cascade-prefix partials itself and writes bf16 rows."""
+@pytest.mark.parametrize("n_pre,S", [(0, 1), (1, 1), (3, 1), (6, 1), (0, 4), (3, 5), (0, 32)])
+def test_attn_decode_fused_merge(cuda, n_pre, S):
+    """The decode kernel merges the cascade-prefix partials itself and writes bf16 rows: directly with one split per
+    sequence, through ticket counters (last split merges) with several. Three launches back to back check that the
+    counters re-arm."""
     torch.manual_seed(6)
     Hq, Hkv, D = 32, 8, 128
     P = 16 * 12
@@ -137,8 +139,8 @@ def test_attn_decode_fused_merge(cuda, n_pre):
     q = torch.randn(B, Hq, D, device=cuda, dtype=torch.bfloat16)
     sl = torch.tensor(lens, dtype=torch.int32, device=cuda)
     scale = 1 / math.sqrt(D)
-    part = torch.empty(B, Hq, n_pre + 1, D, device=cuda)
-    lse = torch.empty(B, Hq, n_pre + 1, device=cuda)
+    part = torch.empty(B, Hq, n_pre + S, D, device=cuda)
+    lse = torch.empty(B, Hq, n_pre + S, device=cuda)
     if n_pre:
         bounds = [round(P * i / n_pre / 32) * 32 for i in range(n_pre)] + [P]
         items = torch.tensor([[0, B, 0, bounds[i], bounds[i + 1], i, 0, 0] for i in range(n_pre)],
@@ -148,10 +150,11 @@ def test_attn_decode_fused_merge(cuda, n_pre):
         ks = torch.full((B,), P, dtype=torch.int32, device=cuda)
     else:
         ks = None
-    out = torch.empty(B, Hq, D, device=cuda, dtype=torch.bfloat16)
-    ops.attn_decode(q, k, v, bt, sl, ks, part, lse, 1, n_pre, scale, out=out)
     o_ref, _ = ref.attn_decode_full(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), sl.cpu(), scale)
-    _close(out, o_ref, atol=0.02, msg=f"fused merge n_pre={n_pre}")
+    for it in range(3):
+        out = torch.full((B, Hq, D), float("nan"), device=cuda, dtype=torch.bfloat16)
+        ops.attn_decode(q, k, v, bt, sl, ks, part, lse, S, n_pre, scale, out=out)
+        _close(out, o_ref, atol=0.02, msg=f"fused merge n_pre={n_pre} S={S} launch {it}")
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2])
