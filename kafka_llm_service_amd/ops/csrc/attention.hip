@@ -368,7 +368,13 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
   __syncthreads();
   if (!s_last) return;
   auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  auto ld4 = [&](const float* p) { return f32x4{ld(p), ld(p + 1), ld(p + 2), ld(p + 3)}; };
+  // 16-B agent-coherent loads (sc1: not served from this XCD's possibly stale L2); inline asm, so the group below
+  // waits for them itself
+  auto ld4 = [](const float* p) {
+    f32x4 r;
+    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
+    return r;
+  };
   const int n = split_offset + S;  // <= 64 (host-checked)
   for (int g = w; g < G; g += 4) {
     const int64_t pbase = ((int64_t)b * Hq + kvh * G + g) * S_total;
@@ -388,15 +394,16 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
   if (g < G) {
     f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
     const float* pp = out_part + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
-    int s2 = 0;
-    for (; s2 + 8 <= n; s2 += 8) {
-      f32x4 v[8];
+    // groups of 16 partials with all loads in flight (the tail of the kernel: latency, not bandwidth)
+    for (int s2 = 0; s2 < n; s2 += 16) {
+      f32x4 v[16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = ld4(pp + (s2 + j) * D);
+      for (int j = 0; j < 16; ++j) v[j] = ld4(pp + min(s2 + j, n - 1) * D);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc4 += v[j] * sW[g][s2 + j];
+      for (int j = 0; j < 16; ++j)
+        if (s2 + j < n) acc4 += v[j] * sW[g][s2 + j];
     }
-    for (; s2 < n; ++s2) acc4 += ld4(pp + s2 * D) * sW[g][s2];
     const float inv = sWt[g] > 0.f ? 1.f / sWt[g] : 0.f;
     bf16x4 o4;
 #pragma unroll
