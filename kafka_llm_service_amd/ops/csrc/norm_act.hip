@@ -14,13 +14,13 @@ namespace kafka {
 
 // y = x * rsqrt(mean(x^2) + eps) * w     (x: [T, d] with row stride, out: [T, d] contiguous)
 // If RESID: r = x + r (rounded to bf16, written back to r), y = norm(r) * w.
-template <int NV, bool RESID>
-__global__ __launch_bounds__(256) void rmsnorm_kernel(bf16* __restrict__ out, int64_t out_stride,
+template <int NV, bool RESID, int NT = 256>
+__global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int64_t out_stride,
                                                        const bf16* __restrict__ x, const float* __restrict__ xp,
                                                        int S, int64_t ps, int64_t x_stride,
                                                        bf16* __restrict__ resid, int64_t r_stride,
                                                        const bf16* __restrict__ w, int d, float eps) {
-  __shared__ float red[4];
+  __shared__ float red[NT / 64];
   const int64_t row = blockIdx.x;
   const int nvec = d >> 3;
   float v[NV][8];
@@ -29,12 +29,12 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(bf16* __restrict__ out, in
   bf16x8 wv[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int vi = threadIdx.x + i * 256;
+    const int vi = threadIdx.x + i * NT;
     if (vi < nvec) wv[i] = load_bf16x8(w + vi * 8);
   }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int vi = threadIdx.x + i * 256;
+    const int vi = threadIdx.x + i * NT;
     if (vi < nvec) {
       load_in8(v[i], x, xp, S, ps, row * x_stride + vi * 8);
       if constexpr (RESID) {
@@ -51,11 +51,11 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(bf16* __restrict__ out, in
       for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
     }
   }
-  ss = block_sum<256>(ss, red);
+  ss = block_sum<NT>(ss, red);
   const float r = rsqrtf(ss / (float)d + eps);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int vi = threadIdx.x + i * 256;
+    const int vi = threadIdx.x + i * NT;
     if (vi < nvec) {
       bf16x8 o;
 #pragma unroll
@@ -90,6 +90,10 @@ static hipError_t launch_rmsnorm_t(bf16* out, int64_t os, const bf16* x, const f
   const int nv = (nvec + 255) / 256;
   dim3 grid(T), block(256);
   if (T == 0) return hipSuccess;
+  if (nvec <= 512 && nvec > 256) {  // e.g. d = 4096: one 16-B vector per thread, twice the loads in flight per row
+    rmsnorm_kernel<1, RESID, 512><<<grid, 512, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps);
+    return hipGetLastError();
+  }
   switch (nv) {
     case 1: rmsnorm_kernel<1, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
     case 2: rmsnorm_kernel<2, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
