@@ -51,7 +51,7 @@ class EngineConfig:
     use_graphs: bool = False
     # decode GEMMs: "stream" = weight-streaming MFMA kernel on wave-tiled weight copies (csrc/wstream_gemm.hip),
     # "blas" = hipBLASLt only; "auto" = stream on GPU (env KAFKA_DECODE_GEMM overrides)
-    decode_gemm: str = "auto"
+    decode_gemm: str = "auto"           # auto | stream | stream_only (tiled weights only) | blas
     async_scheduling: bool = True       # plan step n+1 on the host while step n runs on the GPU
     eos_token_ids: list[int] = field(default_factory=list)
 
@@ -116,8 +116,11 @@ class LLMEngine:
             if need <= 0.5 * free:
                 self.model.enable_stream_weights()  # before the KV pool is sized from the free memory
             else:  # e.g. Llama-3-70B on one GPU: a second copy of 140 GB would starve the KV pool
-                log.warning("decode GEMMs on hipBLASLt: the wave-tiled weight copy (%.1f GB) does not fit next to "
-                            "the KV pool (%.1f GB free)", need / 1e9, free / 1e9)
+                log.warning("wave-tiled weight copy (%.1f GB) does not fit next to the KV pool (%.1f GB free): "
+                            "keeping tiled weights only (prefill untiles per projection)", need / 1e9, free / 1e9)
+                self.model.enable_stream_weights(tiled_only=True)
+        elif mode == "stream_only" and not self.model.stream:
+            self.model.enable_stream_weights(tiled_only=True)
         self.load_s = time.perf_counter() - t0
         self.eos = set(cfg.eos_token_ids or mc.eos_token_ids)
         hkv, D, L = self.model.hkv, self.model.D, mc.num_layers

@@ -72,6 +72,7 @@ class TransformerLM:
         self.moe = None
         self.lm_head_t = None
         self.stream = False  # decode GEMMs on the weight-streaming kernel (enable_stream_weights)
+        self.tiled_only = False  # row-major dense weights dropped (enable_stream_weights(tiled_only=True))
 
     # ------------------------------------------------------------------------------------------------------------
     def stream_weight_bytes(self) -> int:
@@ -90,11 +91,15 @@ class TransformerLM:
             n += self.lm_head.numel() * self.lm_head.element_size()
         return n
 
-    def enable_stream_weights(self) -> int:
+    def enable_stream_weights(self, tiled_only: bool = False) -> int:
         """Keep a wave-tiled copy of every dense projection and of the lm_head (ops.tile_weight) so decode-sized
         steps (T <= ops.STREAM_MAX_M) run the weight-streaming MFMA GEMM (csrc/wstream_gemm.hip) instead of
         hipBLASLt; prefill-sized steps keep the row-major weights. Costs one more copy of those weights (16 GB for
-        Llama-3-8B: the HBM of an MI355X has room, and the KV pool is sized after this). Returns the added bytes."""
+        Llama-3-8B: the HBM of an MI355X has room, and the KV pool is sized after this). Returns the added bytes.
+
+        ``tiled_only``: when the second copy does not fit (Llama-3-70B on one GPU), the row-major dense projections are
+        dropped after tiling (no extra memory) and prefill-sized steps untile one weight at a time into a transient
+        buffer for hipBLASLt (``_dense``)."""
         added = 0
         for lw in self.layers:
             for name in LayerWeights.STREAMED:
@@ -104,7 +109,11 @@ class TransformerLM:
                     setattr(lw, name + "_t", ops.tile_weight(w, glu=glu))
                     if name == "gate_up":
                         lw.glu = glu
-                    added += w.numel() * w.element_size()
+                    if tiled_only:
+                        setattr(lw, name, None)
+                        del w
+                    else:
+                        added += w.numel() * w.element_size()
             if lw.w13 is not None and ops.stream_moe_supported(lw.w13.shape[1], lw.w13.shape[2]) and \
                     ops.stream_moe_supported(lw.w2.shape[1], lw.w2.shape[2]):
                 lw.w13_t = ops.tile_experts(lw.w13, glu=True)  # expert MLPs: grouped streaming kernel
@@ -114,13 +123,21 @@ class TransformerLM:
             self.lm_head_t = ops.tile_weight(self.lm_head)
             added += self.lm_head.numel() * self.lm_head.element_size()
         self.stream = True
+        self.tiled_only = tiled_only
+        if tiled_only and self.device.type == "cuda":
+            torch.cuda.empty_cache()
         return added
 
     def _linear(self, x: torch.Tensor, w: torch.Tensor, wt: torch.Tensor | None, max_splits: int = 8):
         """x @ w^T: the weight-streaming kernel for decode-sized x (bf16 or a split-K slab out), else hipBLASLt."""
         if self.stream and wt is not None and 0 < x.shape[0] <= ops.STREAM_MAX_M:
             return ops.linear_stream(x, wt, max_splits)
-        return F.linear(x, w)
+        return F.linear(x, self._dense(w, wt))
+
+    @staticmethod
+    def _dense(w: torch.Tensor | None, wt: torch.Tensor | None, glu: bool = False) -> torch.Tensor:
+        """The row-major weight for hipBLASLt: the stored one, or (tiled-only mode) a transient untiled copy."""
+        return w if w is not None else ops.untile_weight(wt, glu=glu)
 
     def forward(self, inp: StepInput, k_caches: list[torch.Tensor], v_caches: list[torch.Tensor]) -> torch.Tensor:
         """Returns logits [n, V] (bf16) for ``inp.logit_rows``.
@@ -156,7 +173,7 @@ class TransformerLM:
                 if self.stream and lw.glu and 0 < T <= ops.STREAM_MAX_M:
                     a = ops.linear_glu(x, lw.gate_up_t)  # SwiGLU in the GEMM epilogue (or on its slabs)
                 else:
-                    a = ops.silu_mul(F.linear(x, lw.gate_up))
+                    a = ops.silu_mul(F.linear(x, self._dense(lw.gate_up, lw.gate_up_t, bool(lw.glu))))
                 delta = self._linear(a, lw.down, lw.down_t)
                 if self.tp > 1:
                     delta = pstate.tp_all_reduce(ops.slab_reduce(delta))

@@ -250,6 +250,19 @@ def test_stream_decode_gemm_matches_oracle():
     _check_against_oracle(m, prompts, outs)
 
 
+def test_tiled_only_weights_match_stream():
+    """Tiled-only mode (the row-major dense weights dropped after tiling, prefill untiles per projection — what a
+    model whose second weight copy does not fit gets) generates exactly what the two-copy stream mode does."""
+    ref_eng = _engine(decode_gemm="stream")
+    eng = _engine(decode_gemm="stream_only")
+    m = eng.model
+    assert m.tiled_only and m.layers[0].qkv is None and m.layers[0].gate_up is None and m.layers[0].qkv_t is not None
+    prompts = _prompts(seed=9)
+    a = ref_eng.generate(prompts, GREEDY)
+    b = eng.generate(prompts, GREEDY)
+    assert a == b and all(len(x) for x in a)
+
+
 def test_out_of_vocab_prompt_rejected(base_engine):
     """Token ids outside the vocabulary are refused at admission (on the GPU they would read past the embedding)."""
     V = base_engine.model_cfg.vocab_size
