@@ -4,19 +4,41 @@
 BASELINE.json metric: "output tok/s + p50 TTFT, Llama-3-8B, 64 concurrent threads, 1/2/4/8 MI355X"
 (configs 2-3: Llama-3 8B bf16 TP=1, 64 concurrent threads with 4-turn history, per-thread prefix-KV reuse).
 
+Launch: ``python bench.py --gpus N`` runs N ranks. Under ``torch.distributed.run`` (the driver's N > 1 launch) every
+process is one rank; without a launcher and N > 1 this process becomes a parent that never touches the GPU and
+starts N child ranks itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env), relays rank 0's JSON line and
+exits with the worst child exit code. ``--gpus`` must equal the number of ranks (checked).
+
 Workload (synthetic data, random-init Llama-3-8B weights — no checkpoints/datasets are reachable offline):
   * every thread's prompt = the shared Kafka system prefix (default 18,000 tokens: the reference's ~70k-char system
-    prompt + ~6.6k chars of tool schemas) + its own 4-turn history (~1.3k tokens: 4 x (64 user +
-    256 assistant)) + a new 64-token user message;
-  * each thread loops forever: submit the next turn, stream max_tokens in [128, 384] (ignore_eos, T=0.7), append the
-    reply to its history, submit the next turn immediately — so the engine sees continuous batching with prefix hits
-    on the shared prefix AND on each thread's own history, the way /v1/threads/{id}/chat/completions traffic does;
-  * DP: one engine replica per GPU (one process per GPU under torchrun), 64 threads per replica (weak scaling).
+    prompt + ~6.6k chars of tool schemas, SURVEY.md §0) + its own history + a new user message (32-96 tokens);
+  * a thread slot runs conversations of 2H+1 turns (H = --history-turns = 4), so the history in front of a new
+    turn holds 0..2H earlier turns — 4 on average, ~1.3k tokens — and each reply streams
+    max_tokens in [128, 384] (ignore_eos, T = 0.7). When a conversation ends the slot starts a new one (a new
+    thread: only the shared prefix is cached);
+  * STEADY STATE FROM THE FIRST STEP: at setup every slot is put at a random point of its life — a random turn of
+    its conversation and, inside the in-flight reply, a random number of already-generated tokens (reply length
+    drawn length-biased, position uniform: the stationary distribution of this renewal process). Completions and
+    new-turn admissions (prefix-cache hits on the shared prefix and on the thread's own history, then a short
+    prefill) therefore happen at the steady rate in every window; a 20-step window measures the same thing a
+    300-step one does;
+  * ``--mixed-prefix F``: a fraction F of the slots use a different system prompt (threads created with their own
+    system message, quirk Q4 of SURVEY.md §2.9) — the multi-group cascade case;
+  * DP: one engine replica per GPU (one process per GPU), 64 threads per replica (weak scaling).
 
 A "step" is one engine iteration (one continuous-batching forward over the mixed decode/prefill batch, sampling
 included). W untimed warmup steps, then exactly K timed steps between barrier + synchronize; value = total output
-tokens of all ranks / max rank time. vs_baseline divides by the reference's own 64-thread streaming ceiling
-(22.3k chunks/s with an instant stub LLM).
+tokens of all ranks / max rank time.
+
+TTFT (first token of a new turn, engine-level: request arrival -> sampled token on the host; the first content
+frame of /root/reference/server.py:338-356) is sampled from every new turn that ARRIVES at or after the start of
+the timed window; completions are ~threads/mean(reply) per step (~0.25 at 64 threads), so after the K timed steps
+the engine keeps stepping under the same load (untimed, not counted in ``value``) until ``--ttft-samples`` turns
+have their first token (``ttft_extra_steps`` reports how many steps that took).
+
+vs_baseline: the reference publishes no number for this metric; the ratio is to the derived
+MI355X bound for exactly this workload (~17k tok/s on one GPU with cascade attention, BASELINE.md §3 /
+SURVEY.md §6.4), per GPU.
 """
 from __future__ import annotations
 
@@ -24,69 +46,139 @@ import argparse
 import json
 import os
 import random
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-
 METRIC = "output tok/s + p50 TTFT, Llama-3-8B, 64 concurrent threads, 1/2/4/8 MI355X"  # BASELINE.json
-BASELINE_TOKS = 22300.0  # stub chunks/s, 64 threads, stream (reference plumbing ceiling)
+BOUND_TOKS_PER_GPU = 17000.0  # derived 1-GPU bound with cascade attention on the ~18k prefix
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="number of ranks (one per GPU)")
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel size per replica (e.g. 8 for llama3-70b)")
-    ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=60)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--threads", type=int, default=64, help="concurrent threads per GPU")
+    ap.add_argument("--threads", type=int, default=64, help="concurrent threads per replica")
     ap.add_argument("--prefix-tokens", type=int, default=18000, help="shared system prefix (0 = short prompt)")
-    ap.add_argument("--history-turns", type=int, default=4)
-    ap.add_argument("--user-tokens", type=int, default=64)
-    ap.add_argument("--reply-tokens", type=int, default=256)
+    ap.add_argument("--mixed-prefix", type=float, default=0.0,
+                    help="fraction of threads on a second system prompt (multi-group cascade)")
+    ap.add_argument("--history-turns", type=int, default=4, help="mean earlier turns in front of a new turn")
+    ap.add_argument("--user-tokens", type=int, default=64, help="mean user-message tokens")
     ap.add_argument("--min-out", type=int, default=128)
     ap.add_argument("--max-out", type=int, default=384)
     ap.add_argument("--temperature", type=float, default=0.7)
+    ap.add_argument("--ttft-samples", type=int, default=64, help="new turns whose TTFT is sampled")
+    ap.add_argument("--ttft-max-steps", type=int, default=4000)
     ap.add_argument("--no-cascade", action="store_true")
     ap.add_argument("--graphs", action="store_true")
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
+# ---------------------------------------------------------------------------------------------------------------
+# parent: N child ranks without a launcher (never initialises the GPU itself)
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        out = None if r == 0 else subprocess.DEVNULL
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      stdout=out))
+    rc = 0
+    try:
+        for p in procs:
+            c = p.wait()
+            rc = rc or c
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+# ---------------------------------------------------------------------------------------------------------------
 class ThreadSim:
-    """One chat thread: history token ids + the turn currently in flight."""
+    """One thread slot: the conversation's history token ids, its system prefix and the turn in flight."""
 
     def __init__(self, tid: int, prefix: list[int], rng: random.Random, args, vocab: int):
         self.tid = tid
         self.rng = rng
         self.args = args
         self.vocab = vocab
-        self.history: list[int] = []
-        for _ in range(args.history_turns):
-            self.history += self._rand(args.user_tokens) + self._rand(args.reply_tokens)
         self.prefix = prefix
-        self.turn = 0
-        self.inflight = None
+        self.turns_total = 2 * args.history_turns + 1
+        self.conv = 0
+        self._new_conversation(rng.randrange(self.turns_total))
+        self.resumed: list[int] = []
+        self.pending_user: list[int] = []
 
     def _rand(self, n):
         return [self.rng.randrange(1000, min(self.vocab, 120000)) for _ in range(n)]
 
-    def next_prompt(self) -> list[int]:
-        self.pending_user = self._rand(self.args.user_tokens)
-        return self.prefix + self.history + self.pending_user
+    def _user_len(self) -> int:
+        u = self.args.user_tokens
+        return self.rng.randint(max(1, u // 2), max(1, u + u // 2))
+
+    def _reply_len(self) -> int:
+        return self.rng.randint(self.args.min_out, self.args.max_out)
+
+    def _new_conversation(self, turn: int) -> None:
+        self.conv += 1
+        self.turn = turn
+        self.history = []
+        for _ in range(turn):
+            self.history += self._rand(self._user_len()) + self._rand(self._reply_len())
+
+    def reply_budget(self, stationary: bool) -> tuple[int, int]:
+        """(reply length, tokens of it already generated). ``stationary``: a turn observed at a random instant —
+        length-biased length, uniform position (the renewal process's stationary state)."""
+        lo, hi = self.args.min_out, self.args.max_out
+        if not stationary:
+            return self._reply_len(), 0
+        while True:
+            n = self.rng.randint(lo, hi)
+            if self.rng.random() * hi < n:
+                return n, self.rng.randrange(n)
+
+    def next_prompt(self, done: int = 0) -> list[int]:
+        self.pending_user = self._rand(self._user_len())
+        self.resumed = self._rand(done)
+        return self.prefix + self.history + self.pending_user + self.resumed
 
     def complete(self, out_ids: list[int]) -> None:
-        self.history += self.pending_user + out_ids
+        self.history += self.pending_user + self.resumed + out_ids
         self.turn += 1
+        if self.turn >= self.turns_total:
+            self._new_conversation(0)
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus)
+    import torch
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks")
+    if world % args.tp:
+        raise SystemExit(f"bench.py: {world} ranks not divisible by --tp {args.tp}")
     from kafka_llm_service_amd.parallel import state as pstate
 
     dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
@@ -97,7 +189,7 @@ def main():
     from kafka_llm_service_amd.engine.sequence import SamplingParams
 
     cfg = EngineConfig(model=args.model, device=dev, seed=args.seed, max_num_seqs=max(256, 2 * args.threads),
-                       max_num_batched_tokens=8192, use_cascade=not args.no_cascade, use_graphs=args.graphs,
+                       use_cascade=not args.no_cascade, use_graphs=args.graphs, kv_dtype=args.kv_dtype,
                        max_model_len=131072 if args.prefix_tokens > 6000 else 8192, tp=tp, tp_rank=st.tp_rank)
     eng = LLMEngine(cfg)
     leaders = None
@@ -108,56 +200,60 @@ def main():
         leaders = dist.new_group(list(range(0, world, tp)), backend="gloo")
         if not st.is_tp_leader:
             tp_worker.follower_loop(eng)
-            return _report(args, world, rank, dev, eng, {"out_tokens": 0, "ttft": []}, 0.0, 0.0)
+            return _report(args, world, rank, dev, eng, {"out_tokens": 0, "ttft": [], "extra": 0}, 0.0, 0.0)
         tp_worker.attach_leader(eng)
     V = eng.model_cfg.vocab_size
     rng = random.Random(args.seed * 7919 + rank)
     prefix = [rng.randrange(1000, min(V, 120000)) for _ in range(args.prefix_tokens)]
-    threads = [ThreadSim(i, prefix, random.Random(args.seed * 1000 + rank * 100003 + i), args, V)
+    prefix_b = [rng.randrange(1000, min(V, 120000)) for _ in range(args.prefix_tokens)]
+    n_b = int(round(args.mixed_prefix * args.threads))
+    threads = [ThreadSim(i, prefix_b if i < n_b else prefix,
+                         random.Random(args.seed * 1000 + rank * 100003 + i), args, V)
                for i in range(args.threads)]
 
-    # ---- setup (untimed): populate the prefix cache with the shared prefix and each thread's history
+    # ---- setup (untimed): every slot at a random point of its life (see the module docstring); the shared
+    # prefix(es), each thread's history and its in-flight reply's already-generated tokens go into the prefix cache
     t_setup = time.perf_counter()
-    if prefix:
-        eng.generate([prefix + [5]], SamplingParams(temperature=0, max_tokens=1, ignore_eos=True))
-    eng.generate([t.prefix + t.history for t in threads], SamplingParams(temperature=0, max_tokens=1,
-                                                                            ignore_eos=True))
+    budgets = [th.reply_budget(stationary=True) for th in threads]
+    prompts = [th.next_prompt(done) for th, (_, done) in zip(threads, budgets)]
+    warm = SamplingParams(temperature=0, max_tokens=1, ignore_eos=True)
+    for p in {tuple(t.prefix) for t in threads if t.prefix}:
+        eng.generate([list(p) + [5]], warm)
+    eng.generate(prompts, warm)
     if dev.startswith("cuda"):
         torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
 
     req_thread = {}
-    counter = [0]
 
-    def submit(th: ThreadSim):
-        rid = f"t{th.tid}-turn{th.turn}"
-        n_out = th.rng.randint(args.min_out, args.max_out)
-        sp = SamplingParams(temperature=args.temperature, max_tokens=n_out, ignore_eos=True,
-                            seed=th.tid * 1000 + th.turn)
-        seq = eng.add_request(rid, th.next_prompt(), sp)
-        req_thread[rid] = (th, seq)
-        counter[0] += 1
+    def submit(th: ThreadSim, prompt: list[int] | None = None, n_left: int | None = None, resumed=False):
+        rid = f"t{th.tid}-c{th.conv}-turn{th.turn}"
+        if prompt is None:
+            n_left, _ = th.reply_budget(stationary=False)
+            prompt = th.next_prompt(0)
+        sp = SamplingParams(temperature=args.temperature, max_tokens=n_left, ignore_eos=True,
+                            seed=th.tid * 1000003 + th.conv * 1009 + th.turn)
+        seq = eng.add_request(rid, prompt, sp)
+        req_thread[rid] = (th, seq, resumed)
 
-    for th in threads:
-        submit(th)
+    for th, p, (n, done) in zip(threads, prompts, budgets):
+        submit(th, p, n - done, resumed=True)
 
-    timing = {"out_tokens": 0, "ttft": []}
-    window = [None]
+    timing = {"out_tokens": 0, "ttft": [], "extra": 0}
+    window = [float("inf")]
 
     def run_step(record: bool):
         outs = eng.step()
-        now = time.perf_counter()
         for o in outs:
-            th, seq = req_thread[o.request_id]
+            th, seq, resumed = req_thread[o.request_id]
             if record:
                 timing["out_tokens"] += len(o.new_token_ids)
-                if o.num_output_tokens == 1 and seq.arrival >= window[0]:
-                    timing["ttft"].append(seq.first_token_time - seq.arrival)
+            if o.num_output_tokens == 1 and not resumed and seq.arrival >= window[0]:
+                timing["ttft"].append(seq.first_token_time - seq.arrival)
             if o.finished:
                 del req_thread[o.request_id]
                 th.complete(seq.output_ids)
                 submit(th)
-        return now
 
     for _ in range(args.warmup):
         run_step(False)
@@ -182,9 +278,14 @@ def main():
 
         prof.disable()
         with open(os.environ["KAFKA_CPROFILE"], "w") as f:
-            st = pstats.Stats(prof, stream=f)
-            st.sort_stats("tottime").print_stats(50)
-            st.sort_stats("cumtime").print_stats(60)
+            ps = pstats.Stats(prof, stream=f)
+            ps.sort_stats("tottime").print_stats(50)
+            ps.sort_stats("cumtime").print_stats(60)
+    _barrier(leaders)
+    # ---- TTFT: keep the same load running (untimed) until enough new turns have produced their first token
+    while len(timing["ttft"]) < args.ttft_samples and timing["extra"] < args.ttft_max_steps:
+        run_step(False)
+        timing["extra"] += 1
     _barrier(leaders)
     if tp > 1:
         tp_worker.release_followers()
@@ -199,52 +300,56 @@ def _barrier(group) -> None:
 
 
 def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
+    import torch
+
     from kafka_llm_service_amd.parallel import state as pstate
 
-    local_stats = torch.tensor([timing["out_tokens"], elapsed], dtype=torch.float64)
     ttfts = sorted(timing["ttft"])
+    extra = timing["extra"]
     if world > 1:
         import torch.distributed as dist
 
-        dev_t = local_stats.to(dev)
-        toks = dev_t[:1].clone()
-        dist.all_reduce(toks)
-        tmax = dev_t[1:].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        total_tokens, elapsed = float(toks.item()), float(tmax.item())
-        # gather TTFT samples for the global p50
-        n = torch.tensor([len(ttfts)], device=dev)
-        sizes = [torch.zeros_like(n) for _ in range(world)]
-        dist.all_gather(sizes, n)
-        m = int(max(s.item() for s in sizes)) or 1
-        buf = torch.full((m,), float("nan"), dtype=torch.float64, device=dev)
-        if ttfts:
-            buf[:len(ttfts)] = torch.tensor(ttfts, dtype=torch.float64, device=dev)
-        bufs = [torch.empty_like(buf) for _ in range(world)]
-        dist.all_gather(bufs, buf)
-        allt = torch.cat(bufs).cpu()
-        ttfts = sorted(allt[~torch.isnan(allt)].tolist())
+        # gloo over the host: the result exchange needs no device collective
+        g = dist.new_group(list(range(world)), backend="gloo")
+        stats = torch.tensor([timing["out_tokens"], elapsed, extra], dtype=torch.float64)
+        toks = stats[:1].clone()
+        dist.all_reduce(toks, group=g)
+        tmax = stats[1:].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX, group=g)
+        total_tokens, elapsed, extra = float(toks.item()), float(tmax[0].item()), int(tmax[1].item())
+        allt = [None] * world
+        dist.all_gather_object(allt, ttfts, group=g)
+        ttfts = sorted(t for part in allt for t in part)
     else:
         total_tokens = float(timing["out_tokens"])
-    value = total_tokens / elapsed
+    value = total_tokens / elapsed if elapsed > 0 else 0.0
     p50 = ttfts[len(ttfts) // 2] * 1e3 if ttfts else None
     p99 = ttfts[min(len(ttfts) - 1, int(len(ttfts) * 0.99))] * 1e3 if ttfts else None
     kv = eng.kv_stats()
+    dp = world // args.tp
+    headline = (args.model, args.threads, args.prefix_tokens, args.tp) == ("llama3-8b", 64, 18000, 1)
     res = {
-        "metric": METRIC if (args.model, args.threads) == ("llama3-8b", 64) else
+        "metric": METRIC if headline else
         f"output tok/s + p50 TTFT, {args.model}, {args.threads} concurrent threads per replica",
         "value": round(value, 1), "unit": "tok/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": round(value / BASELINE_TOKS, 3), "dtype": "bf16",
+        "vs_baseline": round(value / (BOUND_TOKS_PER_GPU * world), 3) if headline else None,
+        "dtype": "bf16",
         "data": "synthetic (random-init weights, random token ids)",
-        "config": {"model": args.model, "global_batch": args.threads * (world // args.tp), "seq_len": args.prefix_tokens
-                   + args.history_turns * (args.user_tokens + args.reply_tokens) + args.user_tokens,
-                   "parallelism": f"dp{world // args.tp}" + (f"-tp{args.tp}" if args.tp > 1 else ""), "threads_per_gpu": args.threads,
+        "config": {"model": args.model, "global_batch": args.threads * dp,
+                   "seq_len": args.prefix_tokens + args.history_turns * (args.user_tokens + (args.min_out +
+                                                                                         args.max_out) // 2)
+                   + args.user_tokens,
+                   "parallelism": f"dp{dp}" + (f"-tp{args.tp}" if args.tp > 1 else ""),
+                   "threads_per_gpu": args.threads * dp // world,
                    "shared_prefix_tokens": args.prefix_tokens, "history_turns": args.history_turns,
-                   "max_out": [args.min_out, args.max_out], "temperature": args.temperature,
-                   "cascade": not args.no_cascade, "graphs": args.graphs},
+                   "mixed_prefix": args.mixed_prefix, "max_out": [args.min_out, args.max_out],
+                   "temperature": args.temperature, "cascade": not args.no_cascade, "graphs": args.graphs,
+                   "kv_dtype": args.kv_dtype},
         "ttft_p50_ms": round(p50, 2) if p50 else None, "ttft_p99_ms": round(p99, 2) if p99 else None,
-        "ttft_samples": len(ttfts), "setup_s": round(setup_s, 2),
+        "ttft_samples": len(ttfts), "ttft_extra_steps": extra,
+        "vs_baseline_basis": "derived 1-GPU bound 17k tok/s/GPU (BASELINE.md §3); reference publishes none",
+        "setup_s": round(setup_s, 2),
         "prefix_hit_rate": round(kv["hit_tokens"] / max(1, kv["query_tokens"]), 4),
         "preemptions": eng.sched.num_preemptions,
     }
@@ -255,6 +360,7 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     pstate.destroy()
+    return 0
 
 
 if __name__ == "__main__":

@@ -49,6 +49,7 @@ class EngineConfig:
     target_wgs: int = 256               # tile-kernel workgroups per pass (8-wave WGs, one per CU)
     prefill_kv_chunk: int = 1024        # key-range split for long-context prefill tiles
     use_graphs: bool = False
+    kv_dtype: str = "bf16"              # bf16 | fp8 (e4m3 KV pages with per-(page, head) scales)
     # decode GEMMs: "stream" = weight-streaming MFMA kernel on wave-tiled weight copies (csrc/wstream_gemm.hip),
     # "blas" = hipBLASLt only; "auto" = stream on GPU (env KAFKA_DECODE_GEMM overrides)
     decode_gemm: str = "auto"           # auto | stream | stream_only (tiled weights only) | blas

@@ -21,7 +21,7 @@ def _run(extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4",
            "--warmup", "2", "--model", "tiny-llama", "--prefix-tokens", "200", "--threads", "4", "--min-out", "4",
-           "--max-out", "8", "--reply-tokens", "16", "--user-tokens", "8", *extra]
+           "--max-out", "8", "--user-tokens", "8", "--ttft-samples", "4", *extra]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=500)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -47,3 +47,50 @@ def test_bench_tp2_json_line():
     d = _run(["--tp", "2"])
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["config"]["parallelism"] == "dp1-tp2" and d["config"]["global_batch"] == 4
+
+
+@pytest.mark.timeout(600)
+def test_bench_spawns_ranks_without_launcher():
+    """``python bench.py --gpus 2`` with no torchrun: the parent starts the 2 ranks itself (no exec), relays rank 0's
+    single JSON line, and the window contains new turns (staggered steady state) so TTFT is always sampled."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+           "--model", "tiny-llama", "--prefix-tokens", "200", "--threads", "4", "--min-out", "4", "--max-out", "8",
+           "--user-tokens", "8", "--ttft-samples", "4"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "2"
+    p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=500)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["ttft_samples"] >= 4 and d["ttft_p50_ms"] is not None
+
+
+def test_bench_rejects_rank_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "tiny-llama"],
+                       cwd="/tmp", env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr
+
+
+def test_stationary_reply_budget():
+    """Setup puts each slot at a random point of a length-biased reply: the remaining-token distribution has the
+    stationary mean (E[n^2]/(2 E[n]) for uniform lengths in [lo, hi])."""
+    import random
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    args = bench.parse(["--min-out", "128", "--max-out", "384"])
+    th = bench.ThreadSim(0, [], random.Random(0), args, 128256)
+    rem = []
+    for _ in range(20000):
+        n, done = th.reply_budget(stationary=True)
+        assert 0 <= done < n
+        rem.append(n - done)
+    lo, hi = 128, 384
+    ns = range(lo, hi + 1)
+    expect = sum(n * n for n in ns) / sum(ns) / 2
+    assert abs(sum(rem) / len(rem) - expect) < 0.03 * expect
