@@ -19,7 +19,7 @@ rc=$?; fault gpurun_out/smoke.log
 [[ $rc == 0 ]] || { echo "smoke failed"; tail -30 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log | cut -c1-300
 fi
-for W in ${WINDOWS:-"20:5 200:20"}; do
+for W in ${WINDOWS:-20:5 200:20}; do
   K=${W%%:*}; WU=${W##*:}
   step "bench $K/$WU $BENCH_EXTRA"
   timeout -k 10 400 python bench.py --steps $K --warmup $WU $BENCH_EXTRA > gpurun_out/bench_${K}_${WU}.log 2>&1
@@ -27,4 +27,14 @@ for W in ${WINDOWS:-"20:5 200:20"}; do
   [[ $rc == 0 ]] || { echo "bench failed rc=$rc"; tail -30 gpurun_out/bench_${K}_${WU}.log; exit 1; }
   tail -1 gpurun_out/bench_${K}_${WU}.log
 done
+if [[ -n $PROF ]]; then
+  step "rocprofv3 bench $PROF_ARGS"
+  (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 80 --warmup 20 --ttft-samples 0 $PROF_ARGS > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1)
+  rc=$?; fault gpurun_out/prof.log
+  [[ $rc == 0 ]] || { echo "prof failed rc=$rc"; tail -30 gpurun_out/prof.log; exit 1; }
+  tail -1 gpurun_out/prof.log | cut -c1-200
+  TR=$(find gpurun_out/prof -name "*kernel_trace.csv" | head -1)
+  python scripts/ktrace_mix.py "$TR" 80 > gpurun_out/prof_breakdown.txt && cat gpurun_out/prof_breakdown.txt | head -70
+  rm -f "$TR"
+fi
 echo "== done $(date +%T)"
