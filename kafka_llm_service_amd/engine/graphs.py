@@ -7,7 +7,7 @@ write / cascade + split-K paged attention / merge, final norm, lm_head, sampler)
 cost drops from ~2 ms to ~20 us, which is what lets the host keep up with short decode steps (small batches, TP
 shards) and leaves the CPU free for the API loop.
 
-Layout key: (B, decode split-K factor, cascade prefix chunks, prefix work items, cascade on/off, packed-buffer sizes,
+Layout key: (B, decode work items (padded to a power of two), partial slots, prefix work items, cascade on/off, packed-buffer sizes,
 greedy). Everything that changes from step to step — token ids, positions, KV slots, block tables, sequence lengths,
 cascade work items, sampling parameters and seeds — lives in STATIC device buffers that are refreshed (one async
 H2D each) before the replay; intermediates (activations, attention partials, logits) come from a graph memory pool
@@ -58,7 +58,7 @@ class DecodeGraphs:
 
     @staticmethod
     def key(h, sp) -> tuple:
-        return (h.B, h.splits, h.prefix_splits, h.n_prefix_items, bool(h.cascade_prefix), h.i64.size, h.i32.size,
+        return (h.B, h.n_dec_items, h.s_total, h.n_prefix_items, bool(h.cascade_prefix), h.i64.size, h.i32.size,
                 h.n_late, h.late_off, sp.greedy)
 
     def eligible(self, h, sp) -> bool:

@@ -1,7 +1,7 @@
 """Turns a ScheduledBatch into device tensors, runs the model and samples (one engine step on one GPU/TP rank).
 
 Host->device traffic per step is two packed pinned buffers (one int64: tokens / positions / slots / logit rows;
-one int32: block tables / seq lens / kv_start / work items / causal limits) copied with one async H2D each; the only
+one int32: block tables / causal limits / decode, cascade and prefill work items) copied with one async H2D each; the only
 device->host traffic is the sampled token ids (SURVEY.md §3.2 "device→host: sampled token ids only").
 
 Decode-only batches can be replayed from hipGraphs captured per batch-size bucket (``engine/graphs.py``); mixed
@@ -10,6 +10,7 @@ batches run eagerly.
 from __future__ import annotations
 
 import math
+import os
 from collections import deque
 from dataclasses import dataclass, field
 
@@ -29,15 +30,16 @@ MAX_ITEM_KEYS = 32000  # key range of one attention work item (page ids of an it
 @dataclass
 class HostStep:
     """Host-side plan of one step: packed int64 (tokens | positions | slots | logit rows) and int32 (block tables |
-    causal limits | decode seq lens | cascade kv_start + prefix items | prefill items) buffers plus their layout."""
+    causal limits | decode items | cascade prefix items | prefill items) buffers plus their layout."""
     B: int = 0
     T: int = 0
     nbt: int = 1
+    bt_w: int = 1           # block-table columns (pages of the longest row of the step)
     n_rows: int = 0
-    splits: int = 1
-    prefix_splits: int = 0
+    s_total: int = 1        # partial slots per decode row (cascade prefix chunks + suffix pieces)
+    n_dec_items: int = 0
     n_prefix_items: int = 0
-    cascade_prefix: int = 0
+    cascade_prefix: int = 0  # longest cascade prefix of the step (tokens; 0 = no cascade)
     n_items: int = 0
     prefill_splits: int = 0
     i64: np.ndarray | None = None
@@ -69,13 +71,85 @@ class Launched:
     rows: dict | None = None        # seq_id -> row of dev_tokens
 
 
-def decode_splits(B: int, hkv: int, max_keys: int, target_wgs: int = 512, min_keys_per_split: int = 256) -> int:
-    """Split-K factor for the decode kernel: enough workgroups to fill 256 CUs, >= min_keys_per_split keys each."""
-    if B <= 0:
-        return 1
-    s = max(1, math.ceil(target_wgs / (B * hkv)))
-    s = min(s, max(1, max_keys // min_keys_per_split), 32)
-    return s
+MIN_DECODE_KEYS = 256      # smallest key range of one decode work item
+# decode workgroups per launch (items x Hkv) the suffix pieces are sized for; 0 = one item per row (no split
+# unless a row alone would leave most CUs idle)
+DECODE_TARGET_ITEMS = int(os.environ.get("KAFKA_DECODE_TARGET", "768"))  # A/B: profiles/r02/decode_items_ab.jsonl
+MAX_PARTIALS = 64           # partial slots per row that the decode kernel's fused merge reads (one lane each)
+MAX_PREFIX_CHUNKS = 32
+
+
+def prefix_groups(bt: np.ndarray, nfull: np.ndarray, min_blocks: int) -> tuple[list[int], list[tuple[int, int]]]:
+    """Cascade groups of decode rows: rows whose block tables start with the same pages share that KV prefix.
+
+    ``bt`` int32 [B, W] block tables, ``nfull[b]`` = pages of row b that may belong to a shared prefix (full pages
+    before the one holding the current token). Returns (order, groups): a permutation of the rows that makes every
+    group contiguous, and (row_count, prefix_pages) per group in that order (groups first, then ungrouped rows).
+    A set of rows is split by the first page where it disagrees when its common prefix is shorter than
+    ``min_blocks`` — e.g. threads on the Kafka system prompt vs threads created with their own system message
+    (quirk Q4 of SURVEY.md §2.9) vs stateless /chat/completions traffic each get their own group."""
+    groups: list[tuple[list[int], int]] = []
+    loose: list[int] = []
+
+    def rec(rows: np.ndarray, d: int) -> None:
+        while True:
+            if len(rows) < 2:
+                loose.extend(rows.tolist())
+                return
+            lim = int(nfull[rows].min())
+            sub = bt[rows, d:lim]
+            if sub.shape[1]:
+                eq = (sub == sub[0]).all(0)
+                j = d + (int(np.argmin(eq)) if not eq.all() else sub.shape[1])
+            else:
+                j = d
+            if j >= min_blocks:
+                groups.append((rows.tolist(), j))
+                return
+            short = nfull[rows] <= j  # rows without a page j: cannot share anything longer
+            if short.any():
+                loose.extend(rows[short].tolist())
+                rows = rows[~short]
+                d = j
+                continue
+            col = bt[rows, j]
+            for v in np.unique(col):
+                rec(rows[col == v], j + 1)
+            return
+
+    rec(np.arange(bt.shape[0]), 0)
+    order = [r for rows, _ in groups for r in rows] + loose
+    return order, [(len(rows), p) for rows, p in groups]
+
+
+def decode_items(seq_lens: np.ndarray, kv_start: np.ndarray, npre: np.ndarray, hkv: int,
+                 target: int = DECODE_TARGET_ITEMS, min_keys: int = MIN_DECODE_KEYS) -> np.ndarray:
+    """Work items (b, lo, hi, split, nsplit, npre, 0, 0) of the decode kernel: every row's keys [kv_start, len) in
+    32-key-aligned pieces of about ``ch`` keys, ``ch`` chosen so the launch has ~``target`` workgroups (x Hkv) of
+    about equal bytes (long histories are split, short ones stay whole); at most MAX_PARTIALS - npre pieces."""
+    B = seq_lens.shape[0]
+    suffix = np.maximum(seq_lens - kv_start, 1).astype(np.int64)
+    # fewer rows than it takes to fill the GPU (B x Hkv < 512 workgroups): split so the launch still has ~512
+    target = max(target, 512) if B * hkv < 512 else target
+    if target <= 0:
+        ch = int(suffix.max())
+    else:
+        ch = max(min_keys, -(-int(suffix.sum()) * hkv // (target * 32)) * 32)
+    a0 = kv_start - kv_start % 32
+    nb = (seq_lens - a0 + 31) // 32
+    ns = np.minimum(np.maximum(1, -(-suffix // ch)), MAX_PARTIALS - npre)
+    bps = -(-nb // ns)
+    ns = -(-nb // bps)  # no empty trailing piece
+    rows = np.repeat(np.arange(B), ns)
+    first = np.cumsum(ns) - ns
+    split = np.arange(rows.shape[0]) - np.repeat(first, ns)
+    lo = np.maximum(kv_start[rows], a0[rows] + split * bps[rows] * 32)
+    hi = np.minimum(seq_lens[rows], a0[rows] + (split + 1) * bps[rows] * 32)
+    z = np.zeros_like(rows)
+    it = np.stack([rows, lo, hi, split, ns[rows], npre[rows], z, z], 1).astype(np.int32)
+    if ns.max() > 1:  # longest pieces first: they start while the dispatcher fills the GPU, short ones fill the tail
+        it = it[np.argsort(it[:, 1] - it[:, 2], kind="stable")]
+    return it
 
 
 _NP2TORCH = {np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32, np.dtype(np.float32): torch.float32}
@@ -135,7 +209,6 @@ class ModelRunner:
         self.use_cascade = use_cascade
         self.vocab = model.cfg.vocab_size
         pin = self.device.type == "cuda"
-        self._bt = np.zeros((max_num_seqs * 2, max_blocks_per_seq), dtype=np.int32)
         self._pin = pin
         self.last_stats: dict = {}
         self.recent_stats: deque = deque(maxlen=16)  # stats of the last launched steps (two can be in flight)
@@ -154,13 +227,33 @@ class ModelRunner:
 
     def build_host(self, batch: ScheduledBatch) -> tuple[HostStep, list[Sequence]]:
         """All host-side work of a step: token/slot/page-table packing and attention work-item planning. The result
-        is a few numpy arrays + scalars — what a TP leader broadcasts to its followers (``engine/tp_worker.py``)."""
-        dec = batch.decode
+        is a few numpy arrays + scalars — what a TP leader broadcasts to its followers (``engine/tp_worker.py``).
+
+        Decode rows are reordered so that every cascade group (rows sharing a KV prefix of at least
+        ``cascade_min_prefix`` tokens, ``prefix_groups``) is contiguous: each group's prefix is attended once for all
+        its rows by the tile kernel, the per-row suffixes by the decode kernel in pieces of about equal size."""
+        dec = list(batch.decode)
         B = len(dec)
         pre = batch.prefill
         T = B + sum(e - s for _, s, e in pre)
         rows = B + len(pre)
         nbt = max(1, rows)
+        need = max([-(-s.total_len // PAGE) for s in dec] + [-(-b // PAGE) for _, _, b in pre] + [1])
+        bt_w = self.max_blocks if self.graphs is not None else min(self.max_blocks, -(-need // 16) * 16)
+        bt = np.zeros((nbt, bt_w), dtype=np.int32)
+        groups: list[tuple[int, int]] = []
+        seq_lens = np.fromiter((s.total_len for s in dec), dtype=np.int64, count=B)
+        if B:
+            self.kvm.fill_block_tables([s.seq_id for s in dec], bt)
+            if self.use_cascade and B >= 2:
+                nfull = (seq_lens - 1) // PAGE
+                order, groups = prefix_groups(bt[:B], nfull, -(-self.cascade_min_prefix // PAGE))
+                if groups and order != list(range(B)):
+                    dec = [dec[i] for i in order]
+                    bt[:B] = bt[:B][order]
+                    seq_lens = seq_lens[order]
+        if pre:
+            self.kvm.fill_block_tables([s.seq_id for s, _, _ in pre], bt[B:])
         # ---- int64 pack: tokens | positions | slots | logit_rows
         tokens = np.empty(T, dtype=np.int64)
         positions = np.empty(T, dtype=np.int64)
@@ -168,7 +261,6 @@ class ModelRunner:
         q_limit = np.empty(T, dtype=np.int32)
         sample_seqs: list[Sequence] = []
         logit_rows: list[int] = []
-        seq_ids = []
         patch = []
         for i, s in enumerate(dec):
             p = s.total_len - 1
@@ -181,7 +273,6 @@ class ModelRunner:
             self.kvm.fill_slots(s.seq_id, p, p + 1, slots, i)
             sample_seqs.append(s)
             logit_rows.append(i)
-            seq_ids.append(s.seq_id)
         items = []
         r = B
         for j, (s, a, b) in enumerate(pre):
@@ -196,38 +287,46 @@ class ModelRunner:
             if b == s.total_len:
                 sample_seqs.append(s)
                 logit_rows.append(r + n - 1)
-            seq_ids.append(s.seq_id)
             r += n
-        bt = self._bt[:nbt]
-        self.kvm.fill_block_tables(seq_ids, bt)
-        # ---- decode metadata (+ cascade over the shared prefix)
-        h = HostStep(B=B, T=T, nbt=nbt, n_rows=len(logit_rows), patch=patch)
+        # ---- decode metadata (+ cascade over each group's shared prefix)
+        h = HostStep(B=B, T=T, nbt=nbt, bt_w=bt_w, n_rows=len(logit_rows), patch=patch)
         i32_parts = [bt.reshape(-1), q_limit]
         if B:
-            seq_lens = np.fromiter((s.total_len for s in dec), dtype=np.int32, count=B)
-            P = 0
-            if self.use_cascade and B >= 2:
-                P = self.kvm.common_prefix_blocks([s.seq_id for s in dec]) * PAGE
-                P = min(P, (int(seq_lens.min()) - 1) // PAGE * PAGE)
-                if P < self.cascade_min_prefix:
-                    P = 0
-            max_suffix = int(seq_lens.max()) - P
-            h.splits = decode_splits(B, self.model.hkv, max_suffix)
-            i32_parts += [seq_lens]
-            if P:
-                # key chunks sized so the prefix pass alone launches ~target_wgs workgroups
-                groups = math.ceil(B / self.tile)
-                want = max(1, self.target_wgs // (groups * self.model.hkv))
-                chunk = min(MAX_ITEM_KEYS, max(256, math.ceil(P / want / 32) * 32))
-                nc = math.ceil(P / chunk)
-                pit = []
-                for g0 in range(0, B, self.tile):
-                    for c in range(nc):
-                        pit.append((g0, min(self.tile, B - g0), 0, c * chunk, min(P, (c + 1) * chunk), c, 0, 0))
-                h.prefix_splits = nc
+            kv_start = np.zeros(B, dtype=np.int64)
+            npre = np.zeros(B, dtype=np.int64)
+            pit = []
+            if groups:
+                # key chunks sized so the prefix pass launches ~target_wgs workgroups over all groups together
+                work = sum(-(-n // self.tile) * p * PAGE for n, p in groups)
+                want = max(1, self.target_wgs // self.model.hkv)
+                chunk = min(MAX_ITEM_KEYS, max(256, -(-work // (want * 32)) * 32))
+                r0 = 0
+                for n, p in groups:
+                    P = p * PAGE
+                    nc = -(-P // chunk)
+                    ck = chunk
+                    if nc > MAX_PREFIX_CHUNKS:
+                        ck = -(-P // (MAX_PREFIX_CHUNKS * 32)) * 32
+                        nc = -(-P // ck)
+                    for g0 in range(r0, r0 + n, self.tile):
+                        for c in range(nc):
+                            pit.append((g0, min(self.tile, r0 + n - g0), r0, c * ck, min(P, (c + 1) * ck), c, 0, 0))
+                    kv_start[r0:r0 + n] = P
+                    npre[r0:r0 + n] = nc
+                    h.cascade_prefix = max(h.cascade_prefix, P)
+                    r0 += n
+            ditems = decode_items(seq_lens, kv_start, npre, self.model.hkv)
+            if self.graphs is not None:  # fixed-size item list per bucket (graph replay); pads are dropped
+                cap = max(64, 1 << (int(ditems.shape[0]) - 1).bit_length())
+                pad = np.zeros((cap - ditems.shape[0], 8), dtype=np.int32)
+                pad[:, 3] = -1
+                ditems = np.concatenate([ditems, pad])
+            h.n_dec_items = int(ditems.shape[0])
+            h.s_total = int((npre[ditems[:, 0]] + ditems[:, 4]).max()) if B else 1
+            i32_parts.append(ditems.reshape(-1))
+            if pit:
                 h.n_prefix_items = len(pit)
-                i32_parts += [np.full(B, P, dtype=np.int32), np.asarray(pit, dtype=np.int32).reshape(-1)]
-            h.cascade_prefix = P
+                i32_parts.append(np.asarray(pit, dtype=np.int32).reshape(-1))
         if items:
             # few query tiles against a long key range (a new turn of a thread with a ~20k-token cached context):
             # split every tile's key range so the pass fills the GPU, merge the partials afterwards
@@ -245,8 +344,9 @@ class ModelRunner:
             i32_parts.append(np.asarray(items, dtype=np.int32).reshape(-1))
         h.i64 = np.concatenate([tokens, positions, slots, np.asarray(logit_rows, dtype=np.int64)])
         h.i32 = np.concatenate(i32_parts)
-        h.stats = {"B": B, "T": T, "cascade_prefix": h.cascade_prefix, "splits": h.splits,
-                   "prefix_splits": h.prefix_splits, "prefill_splits": h.prefill_splits}
+        h.stats = {"B": B, "T": T, "cascade_prefix": h.cascade_prefix, "cascade_groups": len(groups),
+                   "decode_items": h.n_dec_items, "prefix_items": h.n_prefix_items, "s_total": h.s_total,
+                   "prefill_splits": h.prefill_splits}
         return h, sample_seqs
 
     def to_device(self, h: HostStep) -> StepInput:
@@ -261,24 +361,21 @@ class ModelRunner:
         t_rows = d64[3 * T:3 * T + h.n_rows]
         meta = AttnMeta(num_decode=B, num_tokens=T, scale=self.model.scale)
         o = 0
-        n_bt = nbt * self.max_blocks
-        meta.block_tables = d32[o:o + n_bt].view(nbt, self.max_blocks)
+        n_bt = nbt * h.bt_w
+        meta.block_tables = d32[o:o + n_bt].view(nbt, h.bt_w)
         o += n_bt
         meta.q_limit = d32[o:o + T]
         o += T
         Hq, D = self.model.hq, self.model.D
         if B:
-            meta.num_splits = h.splits
-            meta.num_prefix_splits = h.prefix_splits
-            meta.seq_lens = d32[o:o + B]
-            o += B
-            if h.cascade_prefix:
-                meta.kv_start = d32[o:o + B]
-                o += B
+            meta.decode_items = d32[o:o + h.n_dec_items * 8].view(-1, 8)
+            o += h.n_dec_items * 8
+            if h.n_prefix_items:
                 meta.prefix_items = d32[o:o + h.n_prefix_items * 8].view(-1, 8)
                 o += h.n_prefix_items * 8
-            meta.part = torch.empty(B, Hq, meta.s_total, D, dtype=torch.float32, device=self.device)
-            meta.lse = torch.empty(B, Hq, meta.s_total, dtype=torch.float32, device=self.device)
+            meta.s_total = h.s_total
+            meta.part = torch.empty(B, Hq, h.s_total, D, dtype=torch.float32, device=self.device)
+            meta.lse = torch.empty(B, Hq, h.s_total, dtype=torch.float32, device=self.device)
             meta.extra["cascade_prefix"] = h.cascade_prefix
         if h.n_items:
             meta.prefill_items = d32[o:o + h.n_items * 8].view(-1, 8)

@@ -95,30 +95,52 @@ def _tickets(dev: torch.device, n: int) -> torch.Tensor:
     return t
 
 
+DECODE_ITEM = 8  # int32 fields of a decode work item: (b, lo, hi, split, nsplit, npre, 0, 0)
+
+
+def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale: float, out=None) -> None:
+    """Paged decode attention over work items (int32 [n, 8]: row b, key range [lo, hi), piece ``split`` of
+    ``nsplit``, ``npre`` prefix partials in front). Each item writes its (O, lse2) partial to slot npre + split of
+    [B, Hq, S_total, D]; with ``out`` (npre + nsplit <= 64 per row) the rows are instead merged with their prefix
+    partials and written as final bf16 — a one-piece row directly, a split row by the last piece to finish (ticket
+    counters, no merge kernel)."""
+    if _gpu(q):
+        tk = _tickets(q.device, q.shape[0] * k_cache.shape[1]) if out is not None else None
+        ext().attn_decode(q, k_cache, v_cache, block_tables, items, out_part, lse_part, float(scale), out, tk)
+        return
+    ref.attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale, out)
+
+
+def uniform_decode_items(seq_lens: torch.Tensor, kv_start: torch.Tensor | None, num_splits: int,
+                         split_offset: int) -> torch.Tensor:
+    """Decode items splitting every row's keys [kv_start, seq_len) into ``num_splits`` 32-key-aligned pieces, with
+    partial slots from ``split_offset`` (built on the tensors' device, no host sync)."""
+    B, S = seq_lens.numel(), int(num_splits)
+    dev = seq_lens.device
+    L = seq_lens.long()
+    st = kv_start.long()[:B] if kv_start is not None else torch.zeros_like(L)
+    a0 = st - st % 32
+    nb = ((L - a0 + 31) // 32).clamp(min=0)
+    bps = (nb + S - 1) // S
+    b = torch.arange(B, device=dev).repeat_interleave(S)
+    s = torch.arange(S, device=dev).repeat(B)
+    blo = s * bps[b]
+    bhi = torch.minimum(nb[b], blo + bps[b])
+    lo = torch.maximum(st[b], a0[b] + blo * 32)
+    hi = torch.maximum(lo, torch.minimum(L[b], a0[b] + bhi * 32))
+    z = torch.zeros_like(b)
+    return torch.stack([b, lo, hi, s, z + S, z + int(split_offset), z, z], 1).to(torch.int32).contiguous()
+
+
 def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part, lse_part, num_splits: int,
                 split_offset: int, scale: float, out=None) -> None:
-    """Split-K paged decode attention writing (O, lse2) partials [B, Hq, S_total, D] at splits
-    [split_offset, split_offset + num_splits). With ``out`` (at most 64 partials in total) the kernel instead merges
-    the result with the partials [0, split_offset) already present (cascade prefix) and writes final bf16 rows: with
-    one split per sequence directly, with several through ticket counters (the last split of a sequence merges)."""
-    if _gpu(q):
-        tk = _tickets(q.device, q.shape[0] * k_cache.shape[1]) if out is not None and num_splits > 1 else None
-        ext().attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part, lse_part,
-                          int(num_splits), int(split_offset), float(scale), out, tk)
-        return
+    """Uniform split-K decode (every row's keys [kv_start, seq_len) in ``num_splits`` pieces) on the work-item
+    kernel: partials at slots [split_offset, split_offset + num_splits), or with ``out`` merged with the prefix
+    partials [0, split_offset) into final bf16 rows (see ``attn_decode_items``)."""
     if out is not None and split_offset + num_splits > 64:
         raise ValueError("fused-merge decode needs <= 64 partials")
-    o, l2 = ref.attn_decode_full(q, k_cache, v_cache, block_tables, seq_lens, scale, kv_start)
-    B = q.shape[0]
-    S_total = out_part.shape[2]
-    lp = lse_part.view(out_part.shape[0], out_part.shape[1], S_total)
-    out_part[:B, :, split_offset:split_offset + num_splits] = 0
-    lp[:B, :, split_offset:split_offset + num_splits] = float("-inf")
-    out_part[:B, :, split_offset] = o
-    lp[:B, :, split_offset] = l2
-    if out is not None:
-        n = split_offset + num_splits
-        ref.attn_merge(out_part[:B, :, :n].contiguous(), lp[:B, :, :n].contiguous(), out[:B])
+    items = uniform_decode_items(seq_lens[:q.shape[0]], kv_start, num_splits, split_offset)
+    attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale, out)
 
 
 def attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, scale: float, out=None, out_part=None,

@@ -26,6 +26,7 @@
 //    1 = 4 waves / 128 rows, LDS; 2 = 4 waves / 128 rows, per-wave register loads. ops.tile_rows(variant).)
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace kafka {
@@ -208,41 +209,51 @@ __device__ __forceinline__ void init_acc(WaveAcc<D>& acc) {
 }
 
 // ------------------------------------------------------------------------------------------------------------------
-// Decode: grid (S, Hkv, B), 256 threads. Requires G <= 8.
-template <int D>
+// Decode: grid (work items, Hkv), 256 threads. Requires G <= 8.
+// A work item is one decode row's key range [lo, hi) — the whole per-thread suffix, or one of `nsplit` pieces of a
+// long one (the host sizes pieces so every workgroup streams about the same bytes: one 3k-token history no longer
+// holds the whole launch while the short ones have finished). Row b's partials live at slots [0, npre) (cascade
+// prefix partials written by the tile kernel, for the row's prefix group) and npre + split (this piece).
+struct DecodeItem {
+  int b, lo, hi, split, nsplit, npre, pad0, pad1;
+};
+
+template <int D, bool HEADS_FAST>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
                                                            const bf16* __restrict__ k_cache,
                                                            const bf16* __restrict__ v_cache, int Hkv, int G,
                                                            const int* __restrict__ block_tables, int bt_stride,
-                                                           const int* __restrict__ seq_lens,
-                                                           const int* __restrict__ kv_start,
+                                                           const DecodeItem* __restrict__ items, int B,
                                                            float* __restrict__ out_part, float* __restrict__ lse_part,
-                                                           int S_total, int split_offset, float scale_log2,
+                                                           int S_total, float scale_log2,
                                                            bf16* __restrict__ out, int64_t out_stride,
                                                            int* __restrict__ tickets) {
   __shared__ float sO[4][8][D];
   __shared__ float sM[4][8];
   __shared__ float sL[4][8];
-  const int b = blockIdx.z, kvh = blockIdx.y, split = blockIdx.x, S = gridDim.x;
+  // HEADS_FAST: consecutive workgroups are the Hkv heads of one item (grid (Hkv, items)), else the items of one
+  // head (grid (items, Hkv)) — a placement choice only (which XCD's L2 sees which pages)
+  const DecodeItem it = items[HEADS_FAST ? blockIdx.y : blockIdx.x];
+  const int b = it.b, kvh = HEADS_FAST ? blockIdx.x : blockIdx.y, split = it.split, S = it.nsplit, split_offset = it.npre;
+  // a malformed item (host bug) is dropped instead of indexing out of bounds (workgroup-uniform)
+  if (b < 0 || b >= B || split < 0 || split >= S || split_offset < 0 || split_offset + S > S_total ||
+      (out != nullptr && split_offset + S > 64))
+    return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int Hq = Hkv * G;
-  const int len = seq_lens[b];
-  const int start = kv_start ? kv_start[b] : 0;
-  const int a0 = start & ~31;
-  const int nb = len > a0 ? (len - a0 + 31) >> 5 : 0;
-  const int bps = (nb + S - 1) / S;
-  const int blo = split * bps, bhi = min(nb, blo + bps);
-  const int lo = max(start, a0 + blo * 32), hi = min(len, a0 + bhi * 32);
+  const int lo = it.lo, hi = it.hi;
+  const int a0 = lo & ~31;
+  const int nb = hi > lo ? (hi - a0 + 31) >> 5 : 0;
   const int* bt = block_tables + (int64_t)b * bt_stride;
 
   WaveAcc<D> acc;
   init_acc<D>(acc);
-  if (blo + w < bhi) {
+  if (w < nb) {
     bf16x8 qf[D / 16];
     load_q_frags<D>(qf, q + (int64_t)b * q_stride + (int64_t)(kvh * G + r) * D, r < G, h);
-    attn_blocks<D>(k_cache, v_cache, Hkv, kvh, bt, a0, blo + w, bhi, 4, len, lo, hi, 0x7fffffff, qf, scale_log2,
-                   acc, lane);
+    attn_blocks<D>(k_cache, v_cache, Hkv, kvh, bt, a0, w, nb, 4, hi, lo, hi, 0x7fffffff, qf, scale_log2, acc,
+                   lane);
   }
   // cross-wave combine
   if (r < G) {
@@ -726,20 +737,30 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(const float* __restrict
 }
 
 // ------------------------------------------------------------------------------------------------------------------
-extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const bf16* k_cache, const bf16* v_cache, int B,
-                              int Hkv, int G, int D, const int* block_tables, int bt_stride, const int* seq_lens,
-                              const int* kv_start, float* out_part, float* lse_part, int S, int S_total,
-                              int split_offset, float scale, bf16* out, int64_t out_stride, int* tickets,
-                              hipStream_t st) {
-  if (B == 0) return hipSuccess;
+// items: int32 [n_items, 8] DecodeItem records (host-checked: npre + nsplit <= S_total, and <= 64 with `out` — the
+// fused merge gives one wave lane per partial; items with nsplit > 1 merge through the ticket counters
+// ([B * Hkv] int32, zero, re-armed by the kernel)).
+extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const bf16* k_cache, const bf16* v_cache,
+                              int n_items, int B, int Hkv, int G, int D, const int* block_tables, int bt_stride,
+                              const int* items, float* out_part, float* lse_part, int S_total, float scale,
+                              bf16* out, int64_t out_stride, int* tickets, hipStream_t st) {
+  if (n_items == 0) return hipSuccess;
   if (D != 128 || G > 8 || G < 1) return hipErrorInvalidValue;
-  // fused merge: one wave lane per partial -> at most 64 (S == 1: 63 prefix partials + its own); S > 1 merges
-  // through the ticket counters ([B * Hkv] int32, zero, re-armed by the kernel)
-  if (out != nullptr && (split_offset + S > 64 || (S > 1 && tickets == nullptr))) return hipErrorInvalidValue;
+  if (out != nullptr && tickets == nullptr) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
-  attn_decode_kernel<128><<<dim3(S, Hkv, B), 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables,
-                                                           bt_stride, seq_lens, kv_start, out_part, lse_part, S_total,
-                                                           split_offset, scale_log2, out, out_stride, tickets);
+  static const bool heads_fast = [] {
+    const char* e = getenv("KAFKA_DECODE_HEADS_FAST");
+    return e == nullptr || e[0] != '0';
+  }();
+  const auto* di = reinterpret_cast<const DecodeItem*>(items);
+  if (heads_fast)
+    attn_decode_kernel<128, true><<<dim3(Hkv, n_items), 256, 0, st>>>(
+        q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, di, B, out_part, lse_part, S_total,
+        scale_log2, out, out_stride, tickets);
+  else
+    attn_decode_kernel<128, false><<<dim3(n_items, Hkv), 256, 0, st>>>(
+        q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, di, B, out_part, lse_part, S_total,
+        scale_log2, out, out_stride, tickets);
   return hipGetLastError();
 }
 

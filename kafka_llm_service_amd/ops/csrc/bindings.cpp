@@ -20,11 +20,10 @@ hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int S, int64_t
                                 const int64_t* positions, const float* cos_sin, bf16* q_out, int64_t q_stride,
                                 bf16* k_cache, bf16* v_cache, const int64_t* slot_mapping, int T, int Hq, int Hkv,
                                 int D, int block_size, hipStream_t st);
-hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const bf16* k_cache, const bf16* v_cache, int B,
-                              int Hkv, int G, int D, const int* block_tables, int bt_stride, const int* seq_lens,
-                              const int* kv_start, float* out_part, float* lse_part, int S, int S_total,
-                              int split_offset, float scale, bf16* out, int64_t out_stride, int* tickets,
-                              hipStream_t st);
+hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const bf16* k_cache, const bf16* v_cache,
+                              int n_items, int B, int Hkv, int G, int D, const int* block_tables, int bt_stride,
+                              const int* items, float* out_part, float* lse_part, int S_total, float scale,
+                              bf16* out, int64_t out_stride, int* tickets, hipStream_t st);
 hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride, const bf16* k_cache,
                                const bf16* v_cache, int Hkv, int G, int D, const int* block_tables, int bt_stride,
                                const int* q_limit, bf16* out, int64_t out_stride, float* out_part, float* lse_part,
@@ -173,50 +172,43 @@ static void check_cache_pair(const at::Tensor& k_cache, const at::Tensor& v_cach
               "paged caches must be K[blocks,Hkv,16,128] / V[blocks,Hkv,128,16]");
 }
 
+// items: int32 [n, 8] decode work items (b, lo, hi, split, nsplit, npre, 0, 0) — see attention.hip DecodeItem.
+// Their values are device data; the kernel drops an item whose b / slots fall outside the checked buffer shapes.
 static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
-                        at::Tensor seq_lens, c10::optional<at::Tensor> kv_start, at::Tensor out_part,
-                        at::Tensor lse_part, int64_t num_splits, int64_t split_offset, double scale,
+                        at::Tensor items, at::Tensor out_part, at::Tensor lse_part, double scale,
                         c10::optional<at::Tensor> out, c10::optional<at::Tensor> tickets) {
   CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
-  CHECK_DT(block_tables, at::kInt); CHECK_DT(seq_lens, at::kInt); CHECK_DT(out_part, at::kFloat);
+  CHECK_DT(block_tables, at::kInt); CHECK_DT(items, at::kInt); CHECK_DT(out_part, at::kFloat);
   CHECK_DT(lse_part, at::kFloat);
   TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == 128 && q.size(2) == 128, "q must be [B, Hq, 128]");
   const int B = q.size(0), Hq = q.size(1), Hkv = k_cache.size(1);
   TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 8, "decode kernel needs Hq/Hkv <= 8");
   TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.stride(1) == 1, "block_tables");
-  TORCH_CHECK(seq_lens.numel() >= B && seq_lens.is_contiguous(), "seq_lens");
+  TORCH_CHECK(items.is_cuda() && items.is_contiguous() && items.dim() == 2 && items.size(1) == 8,
+              "items must be a device int32 [n, 8]");
   TORCH_CHECK(out_part.is_contiguous() && out_part.dim() == 4 && out_part.size(0) >= B && out_part.size(1) == Hq &&
                   out_part.size(3) == 128, "out_part must be [B, Hq, S_total, 128]");
   const int S_total = out_part.size(2);
-  TORCH_CHECK(split_offset >= 0 && num_splits >= 1 && split_offset + num_splits <= S_total, "split range");
   TORCH_CHECK(lse_part.is_contiguous() && lse_part.numel() >= (int64_t)B * Hq * S_total, "lse_part");
   bf16* op = nullptr;
   int64_t ostride = 0;
   int* tp = nullptr;
   if (out.has_value()) {  // fused merge: final bf16 rows [B, Hq, 128]
     CHECK_DT(out.value(), at::kBFloat16);
-    TORCH_CHECK(split_offset + num_splits <= 64 && out->dim() == 3 && out->size(0) >= B && out->size(1) == Hq &&
-                    out->size(2) == 128 && out->stride(2) == 1 && out->stride(1) == 128,
-                "attn_decode: fused-merge out must be [B, Hq, 128] with <= 64 partials in total");
+    TORCH_CHECK(out->dim() == 3 && out->size(0) >= B && out->size(1) == Hq && out->size(2) == 128 &&
+                    out->stride(2) == 1 && out->stride(1) == 128,
+                "attn_decode: fused-merge out must be [B, Hq, 128]");
     op = bptr(out.value());
     ostride = out->stride(0);
-    if (num_splits > 1) {
-      TORCH_CHECK(tickets.has_value() && tickets->is_cuda() && tickets->scalar_type() == at::kInt &&
-                      tickets->numel() >= (int64_t)B * Hkv,
-                  "attn_decode: num_splits > 1 with out needs an int32 ticket buffer of >= B * Hkv zeros");
-      tp = tickets->data_ptr<int>();
-    }
+    TORCH_CHECK(tickets.has_value() && tickets->is_cuda() && tickets->scalar_type() == at::kInt &&
+                    tickets->numel() >= (int64_t)B * Hkv,
+                "attn_decode: the fused merge needs an int32 ticket buffer of >= B * Hkv zeros");
+    tp = tickets->data_ptr<int>();
   }
-  const int* ks = nullptr;
-  if (kv_start.has_value()) {
-    CHECK_DT(kv_start.value(), at::kInt);
-    TORCH_CHECK(kv_start->numel() >= B && kv_start->is_contiguous(), "kv_start");
-    ks = kv_start->data_ptr<int>();
-  }
-  CHECK_HIP(kafka_launch_attn_decode(bptr(q), q.stride(0), bptr(k_cache), bptr(v_cache), B, Hkv, Hq / Hkv, 128,
-                                      block_tables.data_ptr<int>(), block_tables.stride(0), seq_lens.data_ptr<int>(),
-                                      ks, out_part.data_ptr<float>(), lse_part.data_ptr<float>(), num_splits,
-                                      S_total, split_offset, scale, op, ostride, tp, cur_stream()));
+  CHECK_HIP(kafka_launch_attn_decode(bptr(q), q.stride(0), bptr(k_cache), bptr(v_cache), items.size(0), B, Hkv,
+                                      Hq / Hkv, 128, block_tables.data_ptr<int>(), block_tables.stride(0),
+                                      items.data_ptr<int>(), out_part.data_ptr<float>(), lse_part.data_ptr<float>(),
+                                      S_total, scale, op, ostride, tp, cur_stream()));
 }
 
 static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,

@@ -127,6 +127,33 @@ def attn_decode_full(q, k_cache, v_cache, block_tables, seq_lens, scale, kv_star
     return out, lse
 
 
+def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale, out=None):
+    """Reference for the work-item decode kernel (ops/csrc/attention.hip attn_decode_kernel)."""
+    B, Hq, D = q.shape
+    Hkv = k_cache.shape[1]
+    G = Hq // Hkv
+    S_total = out_part.shape[2]
+    lp = lse_part.view(out_part.shape[0], Hq, S_total)
+    nparts = {}
+    for b, lo, hi, split, nsplit, npre in (it[:6] for it in items.tolist()):
+        nparts[b] = npre + nsplit
+        o = torch.zeros(Hq, D, dtype=torch.float32, device=q.device)
+        l2 = torch.full((Hq,), float("-inf"), dtype=torch.float32, device=q.device)
+        if hi > lo:
+            k, v = gather_kv(k_cache, v_cache, block_tables[b], hi)
+            mask = torch.zeros(1, hi, dtype=torch.bool, device=q.device)
+            mask[:, lo:hi] = True
+            for h in range(Hkv):
+                oh, lh = _attend(q[b, h * G:(h + 1) * G].float()[None], k[:, h], v[:, h], mask, scale)
+                o[h * G:(h + 1) * G] = oh[0]
+                l2[h * G:(h + 1) * G] = lh[0]
+        out_part[b, :, npre + split] = o
+        lp[b, :, npre + split] = l2
+    if out is not None:
+        for b, n in nparts.items():
+            attn_merge(out_part[b:b + 1, :, :n].contiguous(), lp[b:b + 1, :, :n].contiguous(), out[b:b + 1])
+
+
 def attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale, out=None, out_part=None,
                        lse_part=None):
     """Reference for the work-item prefill / cascade kernel (see ops/csrc/attention.hip)."""

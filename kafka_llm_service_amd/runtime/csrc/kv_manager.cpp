@@ -191,7 +191,9 @@ class KVManager {
   int64_t num_cached(int64_t sid) const { return get(sid)->n_cached; }
   std::vector<int32_t> tokens(int64_t sid) const { return get(sid)->tokens; }
 
-  // Fill an int32 [B, stride] block-table matrix for `sids` (rows beyond a sequence's table are left untouched).
+  // Fill an int32 [B, stride] block-table matrix for `sids` (columns beyond a sequence's table are left untouched).
+  // The matrix is sized per step to the pages the step's kernels can touch (model_runner: ceil(len / page) of the
+  // longest row), so a table with pages reserved further ahead is truncated to `stride` columns.
   void fill_block_tables(const std::vector<int64_t>& sids,
                          py::array_t<int32_t, py::array::c_style> out) {
     auto buf = out.mutable_unchecked<2>();
@@ -199,9 +201,9 @@ class KVManager {
     if ((int64_t)sids.size() > buf.shape(0)) throw std::runtime_error("block table buffer too small (rows)");
     for (size_t r = 0; r < sids.size(); ++r) {
       const Seq& s = *get(sids[r]);
-      if ((int64_t)s.blocks.size() > stride) throw std::runtime_error("block table buffer too small (cols)");
+      const int64_t n = std::min<int64_t>((int64_t)s.blocks.size(), stride);
       int32_t* row = buf.mutable_data(r, 0);
-      std::memcpy(row, s.blocks.data(), s.blocks.size() * sizeof(int32_t));
+      std::memcpy(row, s.blocks.data(), n * sizeof(int32_t));
     }
   }
 

@@ -271,3 +271,49 @@ def test_out_of_vocab_prompt_rejected(base_engine):
     with pytest.raises(ValueError, match="token ids"):
         base_engine.add_request("neg", [-1, 2], GREEDY)
     assert "oov" not in base_engine.requests
+
+
+def test_multi_group_cascade_equals_plain(base_engine):
+    """Three system prompts (Kafka prompt, a thread created with its own system message — quirk Q4 — and a second
+    custom prompt) plus a stateless row with no shared prefix: every group gets its own cascade pass and the
+    result equals plain per-row attention."""
+    groups = [_prompts(seed=10 + i, shared=96, tails=(3, 9, 30)) for i in range(3)]
+    loner = _prompts(seed=20, shared=0, tails=(50,))
+    prompts = [p for g in groups for p in g] + loner
+    e1 = _engine(model=base_engine.model, use_cascade=False)
+    e2 = _engine(model=base_engine.model, use_cascade=True, cascade_min_prefix=16)
+    for g in groups:
+        e2.generate([g[0][:96] + [7]], GREEDY)
+    plain = e1.generate(prompts, GREEDY)
+    casc = e2.generate(prompts, GREEDY)
+    assert max(st["cascade_groups"] for st in e2.runner.recent_stats) == 3
+    assert casc == plain
+
+
+def test_prefix_groups_and_decode_items():
+    import numpy as np
+
+    from kafka_llm_service_amd.engine.model_runner import MAX_PARTIALS, decode_items, prefix_groups
+
+    # rows 0,2,4 share pages [10, 11, 12, 13]; rows 1,3 share [10, 20, 21, 22] (same first page, then diverge);
+    # row 5 is alone
+    bt = np.array([[10, 11, 12, 13, 50], [10, 20, 21, 22, 51], [10, 11, 12, 13, 52], [10, 20, 21, 22, 53],
+                   [10, 11, 12, 13, 54], [90, 91, 92, 93, 94]], dtype=np.int32)
+    nfull = np.array([4, 4, 5, 4, 4, 4])
+    order, groups = prefix_groups(bt, nfull, min_blocks=3)
+    assert sorted(order) == list(range(6))
+    assert groups == [(3, 4), (2, 4)] and order[:3] == [0, 2, 4] and order[3:5] == [1, 3] and order[5] == 5
+    # below min_blocks nothing groups
+    assert prefix_groups(bt, nfull, min_blocks=5)[1] == []
+    # decode items: pieces cover [kv_start, len) exactly, 32-aligned inside, at most MAX_PARTIALS - npre per row
+    lens = np.array([5000, 40, 700, 19000])
+    ks = np.array([64, 0, 512, 0])
+    npre = np.array([3, 0, 3, 0])
+    it = decode_items(lens, ks, npre, hkv=8, target=64)
+    for b in range(4):
+        rows = it[it[:, 0] == b]
+        assert rows[0, 1] == ks[b] and rows[-1, 2] == lens[b]
+        assert (rows[1:, 1] == rows[:-1, 2]).all() and (rows[1:, 1] % 32 == 0).all()
+        assert (rows[:, 3] == np.arange(len(rows))).all() and (rows[:, 4] == len(rows)).all()
+        assert (rows[:, 5] == npre[b]).all() and len(rows) + npre[b] <= MAX_PARTIALS
+    assert (it[:, 0] == 3).sum() > (it[:, 0] == 1).sum() == 1  # the long row is split, the short one is not

@@ -157,6 +157,67 @@ def test_attn_decode_fused_merge(cuda, n_pre, S):
         _close(out, o_ref, atol=0.02, msg=f"fused merge n_pre={n_pre} S={S} launch {it}")
 
 
+def test_attn_decode_multi_group_cascade(cuda):
+    """Three prefix groups (different shared prefixes of 208 / 320 / 96 tokens) + two ungrouped rows, planned by the
+    engine's own planner (model_runner.prefix_groups / decode_items, long suffixes split into pieces), run as
+    prefix tile passes + the work-item decode kernel with its fused merge == dense attention per row."""
+    import numpy as np
+
+    from kafka_llm_service_amd.engine.model_runner import decode_items, prefix_groups
+
+    torch.manual_seed(8)
+    Hq, Hkv, D = 32, 8, 128
+    prefixes = [208, 320, 96]
+    members = [[0, 3, 5, 8], [1, 6], [2, 7, 9]]  # rows 4 and 10 stay ungrouped
+    suffix = [5, 700, 33, 1900, 450, 64, 17, 1, 300, 90, 2500]
+    B = len(suffix)
+    g = torch.Generator().manual_seed(9)
+    pages = iter(torch.randperm(4000, generator=g).tolist())
+    pre_pages = [[next(pages) for _ in range(P // 16)] for P in prefixes]
+    lens, rows = [], []
+    for b in range(B):
+        grp = [i for i, m in enumerate(members) if b in m]
+        base = pre_pages[grp[0]] if grp else []
+        L = len(base) * 16 + suffix[b]
+        rows.append(base + [next(pages) for _ in range((L + 15) // 16 - len(base))])
+        lens.append(L)
+    W = max(len(r) for r in rows)
+    bt_np = np.zeros((B, W), dtype=np.int32)
+    for b, r in enumerate(rows):
+        bt_np[b, :len(r)] = r
+    order, groups = prefix_groups(bt_np, (np.array(lens) - 1) // 16, min_blocks=4)
+    assert len(groups) == 3
+    bt_np, lens = bt_np[order], [lens[i] for i in order]
+    seq_lens = np.array(lens)
+    kv_start, npre = np.zeros(B, dtype=np.int64), np.zeros(B, dtype=np.int64)
+    pit, r0 = [], 0
+    for n, p in groups:
+        P, nc = p * 16, 3
+        ck = -(-P // (nc * 32)) * 32
+        nc = -(-P // ck)
+        pit += [(r0, n, r0, c * ck, min(P, (c + 1) * ck), c, 0, 0) for c in range(nc)]
+        kv_start[r0:r0 + n], npre[r0:r0 + n] = P, nc
+        r0 += n
+    dit = decode_items(seq_lens, kv_start, npre, Hkv, target=64)
+    assert (dit[:, 4] > 1).any()  # some suffix is split into pieces (ticket merge)
+    S_total = int((npre[dit[:, 0]] + dit[:, 4]).max())
+    k = torch.randn(4000, Hkv, 16, D, generator=g).to(torch.bfloat16).to(cuda)
+    v = torch.randn(4000, Hkv, D, 16, generator=g).to(torch.bfloat16).to(cuda)
+    bt = torch.from_numpy(bt_np).to(cuda)
+    q = torch.randn(B, Hq, D, device=cuda, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    part = torch.empty(B, Hq, S_total, D, device=cuda)
+    lse = torch.empty(B, Hq, S_total, device=cuda)
+    q_limit = torch.tensor(lens, dtype=torch.int32, device=cuda) - 1
+    o_ref, _ = ref.attn_decode_full(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), torch.tensor(lens), scale)
+    for launch in range(2):
+        ops.attn_prefill(torch.tensor(pit, dtype=torch.int32, device=cuda), q, k, v, bt, q_limit, scale,
+                         out_part=part, lse_part=lse)
+        out = torch.full((B, Hq, D), float("nan"), device=cuda, dtype=torch.bfloat16)
+        ops.attn_decode_items(q, k, v, bt, torch.from_numpy(dit).to(cuda), part, lse, scale, out=out)
+        _close(out, o_ref, atol=0.02, msg=f"multi-group cascade launch {launch}")
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2])
 def test_attn_decode_kv_start_cascade(cuda, variant):
     """Cascade: prefix partial from attn_prefill (rows = decode seqs) + suffix partial from attn_decode == full."""
