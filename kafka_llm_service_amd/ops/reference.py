@@ -136,6 +136,8 @@ def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_pa
     lp = lse_part.view(out_part.shape[0], Hq, S_total)
     nparts = {}
     for b, lo, hi, split, nsplit, npre in (it[:6] for it in items.tolist()):
+        if not (0 <= b < B and 0 <= split < nsplit and npre >= 0 and npre + nsplit <= S_total):
+            continue  # padding / malformed item: dropped, as by the kernel
         nparts[b] = npre + nsplit
         o = torch.zeros(Hq, D, dtype=torch.float32, device=q.device)
         l2 = torch.full((Hq,), float("-inf"), dtype=torch.float32, device=q.device)
