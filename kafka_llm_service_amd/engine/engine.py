@@ -156,7 +156,7 @@ class LLMEngine:
         self.runner = ModelRunner(self.model, kc, vc, self.kvm, cfg.max_num_seqs, max_blocks,
                                   cascade_min_prefix=cfg.cascade_min_prefix, use_cascade=cfg.use_cascade,
                                   target_wgs=cfg.target_wgs, prefill_kv_chunk=cfg.prefill_kv_chunk)
-        if cfg.use_graphs and cfg.tp == 1:
+        if cfg.use_graphs:
             from kafka_llm_service_amd.engine.graphs import DecodeGraphs
 
             self.runner.graphs = DecodeGraphs(self.runner)
@@ -231,8 +231,8 @@ class LLMEngine:
         for a token before enqueueing the next forward. Rows planned for sequences that then finish at n (EOS, stop
         string, abort) compute one void token that is discarded; sequences that will finish by length are left out of
         speculative plans up front. Steps whose sampling needs the landed tokens on the host (token-constrained tool
-        calls, penalties) and TP leaders (followers mirror host plans) launch after collecting n instead; a plan that
-        would have to preempt is redone synchronously."""
+        calls, penalties) launch after collecting n instead; a plan that would have to preempt is redone
+        synchronously. TP leaders plan ahead too: their followers sample the same ids on their own GPUs."""
         if self.fi.active:
             self.fi.on_step()
         cut: list[StepOutput] = []
@@ -250,7 +250,7 @@ class LLMEngine:
         if self.cfg.async_scheduling:
             with trace.span("plan_ahead"):
                 plan = self._speculate()
-        if plan is not None and self.runner.broadcast is None and not self._needs_landed(plan.sampled):
+        if plan is not None and not self._needs_landed(plan.sampled):
             self.stats["planned_ahead"] += 1
             self._inflight = self._launch(plan.batch, plan.host, plan.sampled, cur)
             plan = None

@@ -12,7 +12,9 @@ greedy). Everything that changes from step to step — token ids, positions, KV 
 cascade work items, sampling parameters and seeds — lives in STATIC device buffers that are refreshed (one async
 H2D each) before the replay; intermediates (activations, attention partials, logits) come from a graph memory pool
 shared by all captured layouts. Steps with prefill rows or host-side logits processing (penalties, tool grammars)
-run eagerly. Tensor parallelism keeps the eager path (the followers replay from the leader's broadcast plan).
+run eagerly. Under tensor parallelism every rank captures the same layouts from the same broadcast plans: the graph
+ends with this rank's vocab shard of the logits (the layer seams' custom xGMI all-reduces are inside it — their call
+counters live in device memory), and the logit all-gather + sampler run eagerly after the replay.
 
 ``backend="fake"`` re-runs the captured closure instead of a device graph: on CPU it checks the property a graph
 relies on — a replay reads ONLY the static buffers (tests/test_graphs.py).
@@ -43,7 +45,7 @@ class _FakeGraph:
 
 
 class _Entry:
-    __slots__ = ("graph", "s64", "s32", "f32", "topk", "seeds", "out", "layout")
+    __slots__ = ("graph", "s64", "s32", "f32", "topk", "seeds", "out", "layout", "local")
 
 
 class DecodeGraphs:
@@ -63,7 +65,7 @@ class DecodeGraphs:
 
     def eligible(self, h, sp) -> bool:
         return (not self.disabled and h.B > 0 and h.T == h.B and h.n_items == 0 and not sp.procs
-                and self.runner.broadcast is None)
+                and not sp.leader_tokens)
 
     # ------------------------------------------------------------------------------------------------------------
     def run(self, h, sp) -> torch.Tensor | None:
@@ -71,17 +73,30 @@ class DecodeGraphs:
         e = self.graphs.get(k)
         if e is None:
             try:
-                e = self._capture(k, h, sp)
+                e, local = self._capture(k, h, sp)
             except Exception:  # never let capture problems take the engine down: stay eager from here on
                 log.exception("hipGraph capture failed; decode steps run eagerly")
                 self.disabled = True
                 return None
-            return e.out  # the capture run computed this step
-        self.graphs.move_to_end(k)
-        self._load(e, h, sp)
-        e.graph.replay()
-        self.stats["replays"] += 1
-        return e.out
+        else:
+            self.graphs.move_to_end(k)
+            self._load(e, h, sp)
+            e.graph.replay()
+            self.stats["replays"] += 1
+            local = e.local
+        if self.runner.model.tp == 1:
+            return e.out  # sampled inside the graph
+        return self._finish_tp(local, h, sp)
+
+    def _finish_tp(self, local: torch.Tensor, h, sp) -> torch.Tensor:
+        """After a TP replay: all-gather the vocab shards, sample (every rank, same seeds), leave the ids in tok_buf."""
+        from kafka_llm_service_amd.parallel import state as pstate
+
+        r = self.runner
+        logits = pstate.tp_all_gather_lastdim(local)[:, :r.vocab]
+        toks = r.sample_device(logits, sp)
+        r.tok_buf[:toks.shape[0]].copy_(toks)
+        return toks
 
     def _load(self, e: _Entry, h, sp) -> None:
         r = self.runner
@@ -92,7 +107,7 @@ class DecodeGraphs:
             e.topk.copy_(r._h2d(sp.topk))
             e.seeds.copy_(r._h2d(sp.seeds))
 
-    def _capture(self, k: tuple, h, sp) -> _Entry:
+    def _capture(self, k: tuple, h, sp) -> tuple[_Entry, torch.Tensor | None]:
         r = self.runner
         dev = r.device
         n = h.n_rows
@@ -107,9 +122,13 @@ class DecodeGraphs:
         e.layout.i64 = e.layout.i32 = None
         e.layout.patch = []
         greedy = sp.greedy
+        tp = r.model.tp > 1
 
         def step():
             inp = r.views(e.s64, e.s32, e.layout)
+            if tp:  # the graph ends at this rank's logit shard (see the module docstring)
+                e.local = r.model.forward(inp, r.k_caches, r.v_caches, gather=False)
+                return
             logits = r.model.forward(inp, r.k_caches, r.v_caches)
             if greedy:
                 toks = ops.sample(logits, torch.zeros(n, device=dev))
@@ -119,8 +138,10 @@ class DecodeGraphs:
             r.tok_buf[:n].copy_(toks)  # input ids of the next step's late rows (ModelRunner.views)
 
         self._load(e, h, sp)
+        e.local = None
         if self.backend == "fake":
             e.graph = _FakeGraph(step)
+            warm = e.local
         else:
             # warm up on a side stream (library workspaces, lazy inits): this run computes THIS step (tokens and
             # its KV writes); the capture pass that follows records the kernels without executing them
@@ -129,6 +150,7 @@ class DecodeGraphs:
             with torch.cuda.stream(side):
                 step()
             torch.cuda.current_stream().wait_stream(side)
+            warm = e.local  # this step's logit shard (TP); the capture pass below only records
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.pool):
                 step()
@@ -137,4 +159,4 @@ class DecodeGraphs:
         self.stats["captures"] += 1
         while len(self.graphs) > self.max_graphs:
             self.graphs.popitem(last=False)
-        return e
+        return e, warm

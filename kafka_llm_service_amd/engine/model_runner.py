@@ -61,6 +61,54 @@ class SampleParams:
     seeds: np.ndarray
     procs: list          # rows that need host-side logits processing (penalties / token constraints)
     greedy: bool
+    # TP: the leader's step had host-processed rows, so every rank takes the leader's sampled ids (a device
+    # broadcast) instead of its own draw (followers cannot reproduce the host-side processing)
+    leader_tokens: bool = False
+
+
+_PLAN_SCALARS = ("B", "T", "nbt", "bt_w", "n_rows", "s_total", "n_dec_items", "n_prefix_items", "cascade_prefix",
+                 "n_items", "prefill_splits", "n_late", "late_off")
+PLAN_HDR = 32  # int64 header of a broadcast step plan
+
+
+def pack_plan(h: HostStep, sp: SampleParams) -> tuple[np.ndarray, np.ndarray]:
+    """A launched step as (int64 header [PLAN_HDR], uint8 payload): the fixed-layout wire format a TP leader sends its
+    followers (two gloo tensor broadcasts per step; no pickling). Everything a follower needs to run the SAME step:
+    the layout scalars, the packed int64 / int32 buffers and the sampling parameters (every rank samples the
+    all-gathered logits itself, so its device copy of the sampled ids — the next step's late decode inputs — is
+    identical to the leader's)."""
+    n = sp.temp.shape[0]
+    parts = [h.i64.astype(np.int64, copy=False), h.i32.astype(np.int32, copy=False),
+             sp.temp.astype(np.float32, copy=False), sp.topp.astype(np.float32, copy=False),
+             sp.topk.astype(np.int32, copy=False), sp.seeds.astype(np.int64, copy=False)]
+    payload = np.concatenate([np.ascontiguousarray(a).reshape(-1).view(np.uint8) for a in parts])
+    hdr = np.zeros(PLAN_HDR, dtype=np.int64)
+    hdr[0] = 1
+    k = len(_PLAN_SCALARS)
+    hdr[1:1 + k] = [getattr(h, f) for f in _PLAN_SCALARS]
+    hdr[1 + k:1 + k + 6] = [h.i64.size, h.i32.size, n, int(sp.greedy), int(bool(sp.procs) or sp.leader_tokens),
+                            payload.size]
+    return hdr, payload
+
+
+def unpack_plan(hdr: np.ndarray, payload: np.ndarray) -> tuple[HostStep, SampleParams]:
+    k = len(_PLAN_SCALARS)
+    h = HostStep(**{f: int(v) for f, v in zip(_PLAN_SCALARS, hdr[1:1 + k])})
+    n64, n32, n, greedy, lead, _ = (int(v) for v in hdr[1 + k:1 + k + 6])
+    o = 0
+
+    def take(dt, cnt):
+        nonlocal o
+        nb = np.dtype(dt).itemsize * cnt
+        a = payload[o:o + nb].view(dt)
+        o += nb
+        return a
+
+    h.i64 = take(np.int64, n64)
+    h.i32 = take(np.int32, n32)
+    sp = SampleParams(take(np.float32, n), take(np.float32, n), take(np.int32, n), take(np.int64, n), [],
+                      bool(greedy), bool(lead))
+    return h, sp
 
 
 @dataclass
@@ -165,12 +213,21 @@ class _Stager:
         self.device = device
         self.nbytes = nbytes
         self.bufs: list[torch.Tensor | None] = [None] * depth
+        self.events: list = [None] * depth  # copies of the arena's last launch (a TP follower is not throttled)
         self.i = 0
         self.off = 0
 
     def begin(self) -> None:
+        if self.device.type == "cuda":
+            ev = self.events[self.i]
+            if ev is None:
+                ev = self.events[self.i] = torch.cuda.Event()
+            ev.record()  # after every copy issued from the arena that is being left
         self.i = (self.i + 1) % len(self.bufs)
         self.off = 0
+        ev = self.events[self.i]
+        if ev is not None:
+            ev.synchronize()  # normally long done: the arena's copies ran len(bufs) launches ago
 
     def upload(self, a: np.ndarray) -> torch.Tensor:
         a = np.ascontiguousarray(a)
@@ -212,7 +269,7 @@ class ModelRunner:
         self._pin = pin
         self.last_stats: dict = {}
         self.recent_stats: deque = deque(maxlen=16)  # stats of the last launched steps (two can be in flight)
-        self.broadcast = None  # set on a TP leader: callable(HostStep) (engine/tp_worker.py)
+        self.broadcast = None  # set on a TP leader: callable(HostStep, SampleParams) (engine/tp_worker.py)
         self._tok_host = None  # pinned landing buffers of the sampled ids
         self.stager = _Stager(self.device)
         # every step's sampled ids also land here (fixed address, so hipGraphs can read it): the next step's decode
@@ -479,7 +536,8 @@ class ModelRunner:
 
         Decode rows whose input token was PENDING at planning time are filled from the host if the token has landed
         since, else device-side from ``prev`` (the in-flight step that samples it): one gather + scatter on the
-        stream, so the launch never waits for the previous step."""
+        stream, so the launch never waits for the previous step. Under TP the followers do the same from their own
+        copy of the sampled ids (every rank samples the all-gathered logits with the same parameters)."""
         late_dst, late_src = [], []
         for row, s, pos in host.patch:
             t = s.token_at(pos)
@@ -497,20 +555,11 @@ class ModelRunner:
             host.i64 = np.concatenate([host.i64, np.asarray(late_dst + late_src, dtype=np.int64)])
         self.last_stats = host.stats
         self.recent_stats.append(host.stats)
+        sp = self.sample_params(sample_seqs)
         self.stager.begin()
         if self.broadcast is not None:  # TP leader: followers run the same step on their shards
-            if late_dst:
-                raise RuntimeError("TP steps must be launched with landed tokens")
-            self.broadcast(host)
-        sp = self.sample_params(sample_seqs)
-        toks = None
-        if self.graphs is not None and self.graphs.eligible(host, sp):
-            toks = self.graphs.run(host, sp)
-        if toks is None:
-            inp = self.to_device(host)
-            logits = self.model.forward(inp, self.k_caches, self.v_caches)
-            toks = self.sample_device(logits, sp)
-            self.tok_buf[:toks.shape[0]].copy_(toks)
+            self.broadcast(host, sp)
+        toks = self._run(host, sp)
         rows = {s.seq_id: i for i, s in enumerate(sample_seqs)}
         if self.device.type != "cuda":
             return Launched(toks.clone(), None, toks, rows)
@@ -525,6 +574,33 @@ class ModelRunner:
         ev = torch.cuda.Event()
         ev.record()
         return Launched(out, ev, toks, rows)
+
+    @torch.inference_mode()
+    def follower_launch(self, host: HostStep, sp: SampleParams) -> None:
+        """A TP follower's copy of the leader's step (``tp_worker.follower_loop``): same forward on this rank's shard,
+        same collectives, same sampler — nothing comes back to the host."""
+        self.last_stats = host.stats
+        self.stager.begin()
+        self._run(host, sp)
+
+    def _run(self, host: HostStep, sp: SampleParams) -> torch.Tensor:
+        """Forward + sampling of one step (hipGraph replay for eligible decode steps): the sampled ids on the device,
+        also left in ``tok_buf`` for the next step's late decode rows."""
+        toks = None
+        if self.graphs is not None and self.graphs.eligible(host, sp):
+            toks = self.graphs.run(host, sp)
+        if toks is None:
+            inp = self.to_device(host)
+            logits = self.model.forward(inp, self.k_caches, self.v_caches)
+            toks = self.sample_device(logits, sp)
+            self.tok_buf[:toks.shape[0]].copy_(toks)
+        if sp.leader_tokens or (sp.procs and self.model.tp > 1):
+            # host-processed rows: the leader's draw is the truth; followers overwrite theirs (stream-ordered)
+            from kafka_llm_service_amd.parallel import state as pstate
+
+            pstate.tp_broadcast_from_leader(toks)
+            self.tok_buf[:toks.shape[0]].copy_(toks)
+        return toks
 
     def collect(self, h: "Launched") -> list[int]:
         if h.event is not None:

@@ -23,6 +23,7 @@ import os
 import torch
 import torch.distributed as dist
 
+from kafka_llm_service_amd.engine.model_runner import _PLAN_SCALARS, PLAN_HDR, pack_plan, unpack_plan
 from kafka_llm_service_amd.parallel import state as pstate
 
 log = logging.getLogger("kafka.tp")
@@ -35,14 +36,17 @@ def leader_src() -> int:
 
 
 def attach_leader(engine) -> None:
-    """Make ``engine`` (tp_rank 0) broadcast every step plan to its followers."""
+    """Make ``engine`` (tp_rank 0) broadcast every launched step to its followers: a fixed int64 header and one
+    uint8 payload (model_runner.pack_plan), two gloo tensor broadcasts — no pickling on the step path."""
     st = pstate.get()
     if st.tp == 1:
         return
     src, grp = leader_src(), st.cpu_group
 
-    def bcast(host):
-        dist.broadcast_object_list([host], src=src, group=grp)
+    def bcast(host, sp):
+        hdr, payload = pack_plan(host, sp)
+        dist.broadcast(torch.from_numpy(hdr), src=src, group=grp)
+        dist.broadcast(torch.from_numpy(payload), src=src, group=grp)
 
     engine.runner.broadcast = bcast
 
@@ -50,25 +54,27 @@ def attach_leader(engine) -> None:
 def release_followers() -> None:
     st = pstate.get()
     if st.tp > 1 and st.is_tp_leader:
-        dist.broadcast_object_list([None], src=leader_src(), group=st.cpu_group)
+        dist.broadcast(torch.zeros(PLAN_HDR, dtype=torch.int64), src=leader_src(), group=st.cpu_group)
 
 
 @torch.inference_mode()
 def follower_loop(engine) -> int:
-    """Mirror the leader's steps until it sends ``None``. Returns the number of steps run."""
+    """Mirror the leader's steps until it sends the exit header. Returns the number of steps run. The follower only
+    enqueues: its GPU runs each step when the collectives of that step meet the leader's (two steps can be in
+    flight, as on the leader)."""
     st = pstate.get()
     src, grp = leader_src(), st.cpu_group
     runner = engine.runner
     n = 0
+    hdr = torch.zeros(PLAN_HDR, dtype=torch.int64)
     while True:
-        box = [None]
-        dist.broadcast_object_list(box, src=src, group=grp)
-        host = box[0]
-        if host is None:
+        dist.broadcast(hdr, src=src, group=grp)
+        if int(hdr[0]) == 0:
             return n
-        runner.stager.begin()
-        inp = runner.to_device(host)
-        runner.model.forward(inp, runner.k_caches, runner.v_caches)
+        payload = torch.empty(int(hdr[1 + len(_PLAN_SCALARS) + 5]), dtype=torch.uint8)
+        dist.broadcast(payload, src=src, group=grp)
+        host, sp = unpack_plan(hdr.numpy(), payload.numpy())
+        runner.follower_launch(host, sp)
         n += 1
 
 

@@ -139,11 +139,15 @@ class TransformerLM:
         """The row-major weight for hipBLASLt: the stored one, or (tiled-only mode) a transient untiled copy."""
         return w if w is not None else ops.untile_weight(wt, glu=glu)
 
-    def forward(self, inp: StepInput, k_caches: list[torch.Tensor], v_caches: list[torch.Tensor]) -> torch.Tensor:
-        """Returns logits [n, V] (bf16) for ``inp.logit_rows``.
+    def forward(self, inp: StepInput, k_caches: list[torch.Tensor], v_caches: list[torch.Tensor],
+                gather: bool = True) -> torch.Tensor:
+        """Returns logits [n, V] (bf16) for ``inp.logit_rows`` — with ``gather=False`` this rank's vocab shard
+        [n, V_local] instead (the caller all-gathers: a captured decode graph ends before that collective).
 
         On decode-sized steps the projections return split-K slabs (fp32 [S, T, n], see ops.linear_stream) which
-        rope_kv_write / silu_mul / fused_add_rmsnorm consume directly; a TP all-reduce needs the bf16 sum first."""
+        rope_kv_write / silu_mul / fused_add_rmsnorm consume directly. Under TP every layer seam (O projection, MLP
+        down projection) is ONE call: all-reduce of the row-parallel partial sums + residual add + the next RMSNorm
+        (the custom xGMI all-reduce fuses all three when the message fits its buffer, parallel/comm.py)."""
         cfg = self.cfg
         T = inp.tokens.shape[0]
         h = self._embed(inp.tokens)
@@ -152,11 +156,14 @@ class TransformerLM:
         q = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
         attn_out = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
         eps = cfg.rms_norm_eps
-        delta = None
+        tp = self.tp > 1
+        delta, pending = None, False
         for i, lw in enumerate(self.layers):
             if delta is None:
                 ops.rmsnorm(h, lw.input_norm, eps, out=x)
                 residual = h.clone()
+            elif pending:
+                pstate.tp_all_reduce_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x)
             else:
                 ops.fused_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x)
             qkv = self._linear(x, lw.qkv, lw.qkv_t)
@@ -164,25 +171,30 @@ class TransformerLM:
                               self.hq, self.hkv)
             paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out)
             o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t)
-            if self.tp > 1:
-                o = pstate.tp_all_reduce(ops.slab_reduce(o))
-            ops.fused_add_rmsnorm(o, residual, lw.post_norm, eps, out=x)
+            if tp:
+                pstate.tp_all_reduce_add_rmsnorm(o, residual, lw.post_norm, eps, out=x)
+            else:
+                ops.fused_add_rmsnorm(o, residual, lw.post_norm, eps, out=x)
             if lw.router is not None:
                 delta = self.moe(x, lw)
+                pending = tp and not self.moe.reduced
             else:
                 if self.stream and lw.glu and 0 < T <= ops.STREAM_MAX_M:
                     a = ops.linear_glu(x, lw.gate_up_t)  # SwiGLU in the GEMM epilogue (or on its slabs)
                 else:
                     a = ops.silu_mul(F.linear(x, self._dense(lw.gate_up, lw.gate_up_t, bool(lw.glu))))
                 delta = self._linear(a, lw.down, lw.down_t)
-                if self.tp > 1:
-                    delta = pstate.tp_all_reduce(ops.slab_reduce(delta))
+                pending = tp
+        if pending:
+            delta = pstate.tp_all_reduce(delta)
         rows = inp.logit_rows
         d_sel = delta.index_select(1 if ops.is_slab(delta) else 0, rows)
         r_sel = residual.index_select(0, rows)
         hf = ops.fused_add_rmsnorm(d_sel, r_sel, self.final_norm, eps)
         logits = self._linear(hf, self.lm_head, self.lm_head_t, max_splits=1)
-        if self.tp > 1:
+        if not gather:
+            return logits
+        if tp:
             logits = pstate.tp_all_gather_lastdim(logits)
         return logits[:, :cfg.vocab_size]
 

@@ -66,12 +66,15 @@ class MoEBlock:
         return self._finish(out, x.dtype)
 
     def _finish(self, out: torch.Tensor, dtype) -> torch.Tensor:
-        """The fp32 combine buffer [T, d] as the layer's delta: on one rank it is handed on as a one-split slab
-        [1, T, d] (the next add + RMSNorm sums slabs while loading — no separate fp32 -> bf16 pass); expert-parallel
-        ranks all-reduce the bf16 partial outputs."""
-        if self.ep > 1:
-            return pstate.tp_all_reduce(out.to(dtype))
+        """The fp32 combine buffer [T, d] as the layer's delta, handed on as a one-split slab [1, T, d] (the next add +
+        RMSNorm sums slabs while loading — no separate fp32 -> bf16 pass). Expert-parallel ranks hold partial sums
+        over their own experts: the decoder's layer seam all-reduces them (``reduced`` is False)."""
         return out.unsqueeze(0)
+
+    @property
+    def reduced(self) -> bool:
+        """True if the layer output is already complete on every rank (the all-to-all path combines in place)."""
+        return self.ep == 1 or bool(self.a2a)
 
 
     # ------------------------------------------------------------------------------------------------------------

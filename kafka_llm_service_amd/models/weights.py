@@ -141,7 +141,9 @@ def random_init(model: TransformerLM, seed: int = 0, exact_tp: bool | None = Non
         if kind in ("input_norm", "post_norm", "final_norm"):
             t = torch.ones(shape, dtype=dt, device=dev)
         elif exact_tp:
-            full = _randn(shape, _seed(key, seed), torch.device("cpu") if tp > 1 else dev, dt)
+            # drawn on this rank's device with the device's generator, like the TP=1 model: the shards of a TP group
+            # are then exact slices of the TP=1 weights on the same kind of device
+            full = _randn(shape, _seed(key, seed), dev, dt)
             t = _shard_tensor(sh, key, full, eps).to(dev).contiguous()
         else:
             # same shapes as the shard, drawn directly on the device

@@ -1,32 +1,39 @@
 // One-shot all-reduce over xGMI for decode-sized TP messages (SURVEY.md §2.6 `custom_allreduce_oneshot`, §5.8).
 //
 // Every rank owns ONE fine-grained, uncached device allocation, IPC-mapped into every peer of its TP group:
-//     [ flags: MAX_RANKS x MAX_BLOCKS int32 | err: int32 | pad to 8 KB | data: 2 x max_bytes ]
-// A call with epoch e (host counter, +1 per call) uses data half (e & 1). Block b of every rank handles the same
-// slice b of the tensor:
-//   1. copy its slice of x into its OWN data half (uncached -> straight to HBM),
-//   2. publish: store e into flags[my_rank][b] of EVERY peer (system-scope release),
-//   3. wait until flags[p][b] >= e for every peer p in its own flag block (system-scope acquire, bounded spin:
-//      after ~2 s it sets err and proceeds, so a lost peer can never hang the GPU),
+//     [ flags: MAX_RANKS x MAX_BLOCKS int32 | err int32 | epochs: MAX_BLOCKS int32 | pad to 8 KB | data: 2 halves ]
+// Block b of every rank owns the same slice of the message and keeps its own call counter (epoch) in device memory
+// (epochs[b] of its rank's allocation: read + advanced by the block itself, so a captured hipGraph replays with
+// fresh epochs — nothing host-side is baked into the launch). A call with epoch e uses data half (e & 1):
+//   1. stage its slice of the input into its OWN data half: the input is bf16, or fp32 split-K slabs of the decode
+//      GEMM (summed while loading, rounded to bf16 once: half the xGMI bytes of fp32),
+//   2. publish: every staging wave waits for its stores, the block barriers, one wave releases system-wide and
+//      stores e into flags[my_rank][b] of EVERY peer,
+//   3. wait until flags[p][b] >= e for every peer p in its own flag block (relaxed polls, one system acquire;
+//      bounded: after ~2 s it sets err and proceeds, so a lost peer can never hang the GPU),
 //   4. read slice b from all peers' data halves at once (each MI355X reads its 7 peers over its 7 xGMI links in
-//      parallel: one hop, vs a ring's 2(N-1) hops), sum in fp32, write the result back into x.
+//      parallel: one hop, vs a ring's 2(N-1) hops) and sum in fp32 in a fixed rank order (bit-identical on every
+//      rank). Plain mode writes the bf16 sum; the fused mode (slices = whole rows) also adds the residual (updated in
+//      place, bf16) and writes rmsnorm(residual) * w — the all-reduce, the residual add and the next layer's
+//      RMSNorm in ONE launch (replaces slab-reduce + all-reduce + fused_add_rmsnorm).
 // Double-buffering by epoch parity makes a trailing barrier unnecessary: a peer can only still be reading half
-// (e & 1) of call e-2 before it signals call e-1, and this rank passed call e-1's barrier before starting call e.
-// Loads of peer data use sc0 sc1 (system-coherent) so no stale line from call e-2 can be returned.
+// (e & 1) during call e-2, and this block started call e only after every peer's block b had entered call e-1,
+// i.e. after every peer's launch of call e-2 had completed (stream order). Epochs advance together on all blocks
+// (every block takes part in every call, with or without rows), so e is the same for the whole call.
+// Loads of peer data use sc0 sc1 (system-coherent) so no stale line of an older call is returned.
 #include "common.h"
 
 namespace kafka {
 
 constexpr int AR_MAX_RANKS = 8;
 constexpr int AR_MAX_BLOCKS = 128;
-constexpr int AR_HEADER = 8192;  // flags (4 KB) + err, padded
+constexpr int AR_ERR_OFF = AR_MAX_RANKS * AR_MAX_BLOCKS * 4;  // 4096
+constexpr int AR_EPOCH_OFF = AR_ERR_OFF + 256;
+constexpr int AR_HEADER = 8192;
 
 struct ARPtrs {
   char* base[AR_MAX_RANKS];  // every rank's allocation, mapped into this process (base[rank] = own)
 };
-
-__device__ __forceinline__ f32x4 bf16x8_lo(bf16x8 v) { return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]}; }
-__device__ __forceinline__ f32x4 bf16x8_hi(bf16x8 v) { return f32x4{(float)v[4], (float)v[5], (float)v[6], (float)v[7]}; }
 
 typedef int ar_i32x4 __attribute__((ext_vector_type(4)));
 
@@ -37,56 +44,149 @@ __device__ __forceinline__ ar_i32x4 load_sys16_nowait(const bf16* p) {
   return r;
 }
 
-template <int NR>
-__global__ __launch_bounds__(256) void allreduce_oneshot_kernel(ARPtrs ptrs, int rank, int epoch, bf16* __restrict__ x,
-                                                                 int64_t n8, int64_t max_bytes) {
-  const int b = blockIdx.x, nb = gridDim.x;
-  const int64_t per = (n8 + nb - 1) / nb;  // 16-B chunks of this block's slice
-  const int64_t c0 = min(n8, (int64_t)b * per), c1 = min(n8, c0 + per);
-  const int64_t half = (int64_t)(epoch & 1) * max_bytes;
-  bf16* mine = reinterpret_cast<bf16*>(ptrs.base[rank] + AR_HEADER + half);
-  // 1. stage my slice
-  for (int64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) store_bf16x8(mine + c * 8, load_bf16x8(x + c * 8));
-  __threadfence_system();  // every thread's staging stores are visible system-wide before the flag goes out
+// This block's epoch for this call: its device counter + 1 (advanced here; one block per counter, stream-ordered
+// between launches). `s_e` is the block's broadcast slot in LDS.
+__device__ __forceinline__ int ar_epoch(const ARPtrs& ptrs, int rank, int* s_e) {
+  if (threadIdx.x == 0) {
+    int* ep = reinterpret_cast<int*>(ptrs.base[rank] + AR_EPOCH_OFF) + blockIdx.x;
+    // vector memory ops (atomic forms) on purpose: never the scalar cache for this read-modify-write
+    const int e = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    __hip_atomic_store(ep, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_e = e;
+  }
   __syncthreads();
-  // 2. publish to every peer, 3. wait for every peer
-  if (threadIdx.x < NR) {
-    const int p = threadIdx.x;
-    int* pf = reinterpret_cast<int*>(ptrs.base[p]) + rank * AR_MAX_BLOCKS + b;
-    __hip_atomic_store(pf, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    int* my = reinterpret_cast<int*>(ptrs.base[rank]) + p * AR_MAX_BLOCKS + b;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
-    while (__hip_atomic_load(my, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-      __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: report instead of hanging the queue
-        int* err = reinterpret_cast<int*>(ptrs.base[rank] + AR_MAX_RANKS * AR_MAX_BLOCKS * 4);
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
+  return *s_e;
+}
+
+// Steps 2 + 3: publish this block's staged slice to every peer and wait for theirs.
+template <int NR>
+__device__ __forceinline__ void ar_exchange(const ARPtrs& ptrs, int rank, int e) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's staging stores have completed
+  __syncthreads();                                    // ... and every other wave's
+  if (threadIdx.x < 64) {
+    __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x < NR) {
+      const int p = threadIdx.x;
+      int* pf = reinterpret_cast<int*>(ptrs.base[p]) + rank * AR_MAX_BLOCKS + blockIdx.x;
+      __hip_atomic_store(pf, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      int* my = reinterpret_cast<int*>(ptrs.base[rank]) + p * AR_MAX_BLOCKS + blockIdx.x;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
+      while (__hip_atomic_load(my, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: report instead of hanging the queue
+          int* err = reinterpret_cast<int*>(ptrs.base[rank] + AR_ERR_OFF);
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
       }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
   }
   __syncthreads();
-  // 4. reduce slice b over all ranks (fixed rank order: every rank computes bit-identical sums)
+}
+
+// Sum of chunk c (8 bf16) over all ranks' data halves, in rank order.
+template <int NR>
+__device__ __forceinline__ void ar_sum8(const ARPtrs& ptrs, int64_t half, int64_t c, float (&v)[8]) {
+  ar_i32x4 raw[NR];
+#pragma unroll
+  for (int p = 0; p < NR; ++p)  // all peers' loads in flight at once (one per xGMI link)
+    raw[p] = load_sys16_nowait(reinterpret_cast<const bf16*>(ptrs.base[p] + AR_HEADER + half) + c * 8);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = 0.f;
+#pragma unroll
+  for (int p = 0; p < NR; ++p) {
+    const bf16x8 b = __builtin_bit_cast(bf16x8, raw[p]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += (float)b[j];
+  }
+}
+
+__device__ __forceinline__ void stage8(bf16* mine, const bf16* x, const float* xp, int S, int64_t ps, int64_t c) {
+  float v[8];
+  load_in8(v, x, xp, S, ps, c * 8);
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+  store_bf16x8(mine + c * 8, o);
+}
+
+// Plain all-reduce of n8 16-B chunks: y = sum over ranks of (x or the slab sum), bf16. y may alias x.
+template <int NR>
+__global__ __launch_bounds__(256) void allreduce_oneshot_kernel(ARPtrs ptrs, int rank, const bf16* x,
+                                                                 const float* __restrict__ xp, int S, int64_t ps,
+                                                                 bf16* y, int64_t n8, int64_t max_bytes) {
+  __shared__ int s_e;
+  const int e = ar_epoch(ptrs, rank, &s_e);
+  const int b = blockIdx.x, nb = gridDim.x;
+  const int64_t per = (n8 + nb - 1) / nb;
+  const int64_t c0 = min(n8, (int64_t)b * per), c1 = min(n8, c0 + per);
+  const int64_t half = (int64_t)(e & 1) * max_bytes;
+  bf16* mine = reinterpret_cast<bf16*>(ptrs.base[rank] + AR_HEADER + half);
+  for (int64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) stage8(mine, x, xp, S, ps, c);
+  ar_exchange<NR>(ptrs, rank, e);
   for (int64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
-    ar_i32x4 raw[NR];
-#pragma unroll
-    for (int p = 0; p < NR; ++p)  // all peers' loads in flight at once (one per xGMI link)
-      raw[p] = load_sys16_nowait(reinterpret_cast<const bf16*>(ptrs.base[p] + AR_HEADER + half) + c * 8);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int p = 0; p < NR; ++p) {
-      const bf16x8 v = __builtin_bit_cast(bf16x8, raw[p]);
-      lo += bf16x8_lo(v);
-      hi += bf16x8_hi(v);
-    }
+    float v[8];
+    ar_sum8<NR>(ptrs, half, c, v);
     bf16x8 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      o[j] = (bf16)lo[j];
-      o[4 + j] = (bf16)hi[j];
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+    store_bf16x8(y + c * 8, o);
+  }
+}
+
+// Fused: rows r of [T, d] are owned by block r % nblocks (d <= 8 * 256 * CPT). Per row: s = bf16(allreduce(x) +
+// resid); resid = s; out = bf16(s * rsqrt(mean(s^2) + eps) * w) — the fused_add_rmsnorm of the same inputs.
+template <int NR, int CPT>
+__global__ __launch_bounds__(256) void allreduce_add_rmsnorm_kernel(ARPtrs ptrs, int rank, const bf16* x,
+                                                                     const float* __restrict__ xp, int S,
+                                                                     int64_t ps, int T, int d,
+                                                                     bf16* __restrict__ resid, int64_t rs,
+                                                                     const bf16* __restrict__ w, float eps,
+                                                                     bf16* __restrict__ out, int64_t os,
+                                                                     int64_t max_bytes) {
+  __shared__ int s_e;
+  __shared__ float red[4];
+  const int e = ar_epoch(ptrs, rank, &s_e);
+  const int64_t half = (int64_t)(e & 1) * max_bytes;
+  bf16* mine = reinterpret_cast<bf16*>(ptrs.base[rank] + AR_HEADER + half);
+  const int n8 = d >> 3;
+  for (int r = blockIdx.x; r < T; r += gridDim.x)
+    for (int c = threadIdx.x; c < n8; c += 256) stage8(mine, x, xp, S, ps, (int64_t)r * n8 + c);
+  ar_exchange<NR>(ptrs, rank, e);
+  for (int r = blockIdx.x; r < T; r += gridDim.x) {  // block-uniform
+    float v[CPT][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      if (c < n8) {
+        ar_sum8<NR>(ptrs, half, (int64_t)r * n8 + c, v[i]);
+        const bf16x8 rv = load_bf16x8(resid + (int64_t)r * rs + c * 8);
+        bf16x8 sv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sv[j] = (bf16)(v[i][j] + (float)rv[j]);
+          v[i][j] = (float)sv[j];
+          ss += v[i][j] * v[i][j];
+        }
+        store_bf16x8(resid + (int64_t)r * rs + c * 8, sv);
+      }
     }
-    store_bf16x8(x + c * 8, o);
+    const float inv = rsqrtf(block_sum<256>(ss, red) / (float)d + eps);
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      if (c < n8) {
+        const bf16x8 wv = load_bf16x8(w + c * 8);
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[i][j] * inv * (float)wv[j]);
+        store_bf16x8(out + (int64_t)r * os + c * 8, o);
+      }
+    }
   }
 }
 
@@ -108,18 +208,53 @@ extern "C" hipError_t kafka_car_close(void* p) { return hipIpcCloseMemHandle(p);
 
 extern "C" hipError_t kafka_car_free(void* p) { return hipFree(p); }
 
-extern "C" hipError_t kafka_launch_car_allreduce(char* const* bases, int nranks, int rank, int epoch, bf16* x,
-                                                int64_t n8, int64_t max_bytes, int nblocks, hipStream_t st) {
-  if (nranks < 2 || nranks > AR_MAX_RANKS || nblocks < 1 || nblocks > AR_MAX_BLOCKS || n8 * 16 > max_bytes)
+// x: bf16 input (or nullptr with xp = S fp32 slabs of stride ps elements); y: bf16 output (may alias x).
+// Every call of a group must use the same nblocks (the per-block epochs advance together).
+extern "C" hipError_t kafka_launch_car_allreduce(char* const* bases, int nranks, int rank, const bf16* x,
+                                                const float* xp, int S, int64_t ps, bf16* y, int64_t n8,
+                                                int64_t max_bytes, int nblocks, hipStream_t st) {
+  if (nranks < 2 || nranks > AR_MAX_RANKS || nblocks < 1 || nblocks > AR_MAX_BLOCKS || n8 * 16 > max_bytes ||
+      (x == nullptr) == (xp == nullptr))
     return hipErrorInvalidValue;
   ARPtrs p{};
   for (int i = 0; i < nranks; ++i) p.base[i] = bases[i];
   switch (nranks) {
-    case 2: allreduce_oneshot_kernel<2><<<nblocks, 256, 0, st>>>(p, rank, epoch, x, n8, max_bytes); break;
-    case 4: allreduce_oneshot_kernel<4><<<nblocks, 256, 0, st>>>(p, rank, epoch, x, n8, max_bytes); break;
-    case 8: allreduce_oneshot_kernel<8><<<nblocks, 256, 0, st>>>(p, rank, epoch, x, n8, max_bytes); break;
+    case 2: allreduce_oneshot_kernel<2><<<nblocks, 256, 0, st>>>(p, rank, x, xp, S, ps, y, n8, max_bytes); break;
+    case 4: allreduce_oneshot_kernel<4><<<nblocks, 256, 0, st>>>(p, rank, x, xp, S, ps, y, n8, max_bytes); break;
+    case 8: allreduce_oneshot_kernel<8><<<nblocks, 256, 0, st>>>(p, rank, x, xp, S, ps, y, n8, max_bytes); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t kafka_launch_car_allreduce_add_rmsnorm(char* const* bases, int nranks, int rank,
+                                                            const bf16* x, const float* xp, int S, int64_t ps,
+                                                            int T, int d, bf16* resid, int64_t rs, const bf16* w,
+                                                            float eps, bf16* out, int64_t os, int64_t max_bytes,
+                                                            int nblocks, hipStream_t st) {
+  if (nranks < 2 || nranks > AR_MAX_RANKS || nblocks < 1 || nblocks > AR_MAX_BLOCKS || d % 8 != 0 ||
+      (int64_t)T * d * 2 > max_bytes || (x == nullptr) == (xp == nullptr))
+    return hipErrorInvalidValue;
+  const int cpt = (d / 8 + 255) / 256;
+  ARPtrs p{};
+  for (int i = 0; i < nranks; ++i) p.base[i] = bases[i];
+#define KAFKA_CARN(NR_, CPT_)                                                                                    \
+  allreduce_add_rmsnorm_kernel<NR_, CPT_><<<nblocks, 256, 0, st>>>(p, rank, x, xp, S, ps, T, d, resid, rs, w, eps, \
+                                                                   out, os, max_bytes)
+#define KAFKA_CARN_R(CPT_)                          \
+  switch (nranks) {                                 \
+    case 2: KAFKA_CARN(2, CPT_); break;             \
+    case 4: KAFKA_CARN(4, CPT_); break;             \
+    case 8: KAFKA_CARN(8, CPT_); break;             \
+    default: return hipErrorInvalidValue;           \
+  }
+  if (cpt <= 1) { KAFKA_CARN_R(1) }
+  else if (cpt <= 2) { KAFKA_CARN_R(2) }
+  else if (cpt <= 4) { KAFKA_CARN_R(4) }
+  else if (cpt <= 8) { KAFKA_CARN_R(8) }
+  else return hipErrorInvalidValue;
+#undef KAFKA_CARN_R
+#undef KAFKA_CARN
   return hipGetLastError();
 }
 

@@ -55,8 +55,13 @@ hipError_t kafka_car_ipc_handle(void* p, hipIpcMemHandle_t* h);
 hipError_t kafka_car_open(const hipIpcMemHandle_t* h, void** out);
 hipError_t kafka_car_close(void* p);
 hipError_t kafka_car_free(void* p);
-hipError_t kafka_launch_car_allreduce(char* const* bases, int nranks, int rank, int epoch, bf16* x, int64_t n8,
-                                      int64_t max_bytes, int nblocks, hipStream_t st);
+hipError_t kafka_launch_car_allreduce(char* const* bases, int nranks, int rank, const bf16* x, const float* xp, int S,
+                                      int64_t ps, bf16* y, int64_t n8, int64_t max_bytes, int nblocks,
+                                      hipStream_t st);
+hipError_t kafka_launch_car_allreduce_add_rmsnorm(char* const* bases, int nranks, int rank, const bf16* x,
+                                                  const float* xp, int S, int64_t ps, int T, int d, bf16* resid,
+                                                  int64_t rs, const bf16* w, float eps, bf16* out, int64_t os,
+                                                  int64_t max_bytes, int nblocks, hipStream_t st);
 }  // extern "C"
 
 #define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
@@ -492,15 +497,51 @@ static int64_t car_error(int64_t own) {
   CHECK_HIP(hipMemcpy(&v, reinterpret_cast<char*>(own) + 8 * 128 * 4, sizeof(int), hipMemcpyDeviceToHost));
   return v;
 }
-static void car_all_reduce(at::Tensor x, std::vector<int64_t> bases, int64_t rank, int64_t epoch, int64_t max_bytes,
-                           int64_t nblocks) {
-  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16);
-  TORCH_CHECK(x.is_contiguous() && x.numel() % 8 == 0, "car_all_reduce: contiguous bf16, numel % 8 == 0");
-  TORCH_CHECK(x.numel() * 2 <= max_bytes, "car_all_reduce: message larger than the registered buffer");
+static std::vector<char*> car_bases(const std::vector<int64_t>& bases) {
   std::vector<char*> b(bases.size());
   for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<char*>(bases[i]);
-  CHECK_HIP(kafka_launch_car_allreduce(b.data(), (int)b.size(), (int)rank, (int)epoch, bptr(x), x.numel() / 8,
-                                       max_bytes, (int)nblocks, cur_stream()));
+  return b;
+}
+
+// x: bf16 [.., n] (in place when y is omitted) or an fp32 split-K slab [S, T, n] (then y is required)
+static void car_all_reduce(at::Tensor x, c10::optional<at::Tensor> y, std::vector<int64_t> bases, int64_t rank,
+                           int64_t max_bytes, int64_t nblocks) {
+  CHECK_CUDA(x);
+  const bool slab = is_slab(x);
+  if (slab) check_slab(x); else CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK(x.is_contiguous(), "car_all_reduce: contiguous input");
+  at::Tensor out = y.has_value() ? y.value() : x;
+  TORCH_CHECK(!slab || y.has_value(), "car_all_reduce: a slab input needs a bf16 output");
+  CHECK_DT(out, at::kBFloat16);
+  const int64_t n = slab ? x.size(1) * x.size(2) : x.numel();
+  TORCH_CHECK(out.is_contiguous() && out.numel() == n && n % 8 == 0, "car_all_reduce: output shape");
+  TORCH_CHECK(n * 2 <= max_bytes, "car_all_reduce: message larger than the registered buffer");
+  auto b = car_bases(bases);
+  CHECK_HIP(kafka_launch_car_allreduce(b.data(), (int)b.size(), (int)rank, slab ? nullptr : bptr(x),
+                                       slab ? x.data_ptr<float>() : nullptr, slab ? x.size(0) : 0,
+                                       slab ? x.size(1) * x.size(2) : 0, bptr(out), n / 8, max_bytes, (int)nblocks,
+                                       cur_stream()));
+}
+
+// residual <- allreduce(x) + residual; out = rmsnorm(residual) * w  (x: bf16 [T, d] or slab [S, T, d])
+static void car_all_reduce_add_rmsnorm(at::Tensor x, at::Tensor residual, at::Tensor w, double eps, at::Tensor out,
+                                       std::vector<int64_t> bases, int64_t rank, int64_t max_bytes,
+                                       int64_t nblocks) {
+  CHECK_CUDA(x); CHECK_DT(residual, at::kBFloat16); CHECK_DT(w, at::kBFloat16); CHECK_DT(out, at::kBFloat16);
+  const bool slab = is_slab(x);
+  if (slab) check_slab(x); else CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK(x.is_contiguous() && (slab || x.dim() == 2), "car_all_reduce_add_rmsnorm: x [T, d] or slab");
+  const int T = x.size(slab ? 1 : 0), d = x.size(slab ? 2 : 1);
+  TORCH_CHECK(residual.dim() == 2 && residual.size(0) == T && residual.size(1) == d && residual.stride(1) == 1 &&
+                  out.dim() == 2 && out.size(0) == T && out.size(1) == d && out.stride(1) == 1 &&
+                  w.is_contiguous() && w.numel() == d && d % 8 == 0 && d <= 16384,
+              "car_all_reduce_add_rmsnorm: shapes");
+  TORCH_CHECK((int64_t)T * d * 2 <= max_bytes, "car_all_reduce_add_rmsnorm: message larger than the buffer");
+  auto b = car_bases(bases);
+  CHECK_HIP(kafka_launch_car_allreduce_add_rmsnorm(
+      b.data(), (int)b.size(), (int)rank, slab ? nullptr : bptr(x), slab ? x.data_ptr<float>() : nullptr,
+      slab ? x.size(0) : 0, slab ? (int64_t)T * d : 0, T, d, bptr(residual), residual.stride(0), bptr(w), (float)eps,
+      bptr(out), out.stride(0), max_bytes, (int)nblocks, cur_stream()));
 }
 
 PYBIND11_MODULE(_kafka_ops, m) {
@@ -528,5 +569,6 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("car_free", &car_free);
   m.def("car_error", &car_error);
   m.def("car_all_reduce", &car_all_reduce);
+  m.def("car_all_reduce_add_rmsnorm", &car_all_reduce_add_rmsnorm);
   m.def("grouped_gemm", &grouped_gemm);
 }

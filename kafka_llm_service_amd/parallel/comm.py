@@ -24,12 +24,55 @@ def get_custom(group):
     return _CUSTOM.get(group)
 
 
+def _host_all_reduce(x: torch.Tensor, group) -> torch.Tensor:
+    """A device tensor over a gloo group (tests that put several ranks on one GPU, where RCCL refuses to run): the
+    sum goes through host memory."""
+    h = x.cpu()
+    dist.all_reduce(h, group=group)
+    x.copy_(h)
+    return x
+
+
+def _is_gloo(group) -> bool:
+    return dist.get_backend(group) == "gloo"
+
+
 def all_reduce(x: torch.Tensor, group) -> torch.Tensor:
+    """Sum of ``x`` over ``group``: bf16 in place, or — for fp32 split-K slabs [S, T, n] — into a new bf16 [T, n]."""
     impl = _CUSTOM.get(group)
     if impl is not None and impl.should_use(x):
         return impl.all_reduce(x)
+    from kafka_llm_service_amd import ops
+
+    x = ops.slab_reduce(x)
+    if x.is_cuda and _is_gloo(group):
+        return _host_all_reduce(x, group)
     dist.all_reduce(x, group=group)
     return x
+
+
+def all_reduce_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor,
+                           group) -> torch.Tensor:
+    """The TP layer seam: residual += allreduce(x); out = rmsnorm(residual) * w. One custom-all-reduce launch when
+    the message fits its buffer (the reduce, the residual add and the next RMSNorm fused), else RCCL + the fused
+    add+RMSNorm kernel."""
+    impl = _CUSTOM.get(group)
+    if impl is not None and impl.should_use(x) and residual.is_contiguous():
+        return impl.all_reduce_add_rmsnorm(x, residual, w, eps, out)
+    from kafka_llm_service_amd import ops
+
+    return ops.fused_add_rmsnorm(all_reduce(x, group), residual, w, eps, out=out)
+
+
+def all_gather_lastdim(x: torch.Tensor, world: int, group) -> torch.Tensor:
+    x = x.contiguous()
+    if x.is_cuda and _is_gloo(group):
+        parts = [torch.empty_like(x, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, x.cpu(), group=group)
+        return torch.cat(parts, dim=-1).to(x.device)
+    parts = [torch.empty_like(x) for _ in range(world)]
+    dist.all_gather(parts, x, group=group)
+    return torch.cat(parts, dim=-1)
 
 
 def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, out_splits: list[int], in_splits: list[int],

@@ -5,10 +5,15 @@ Llama-3-70B at TP=8 does 160 all-reduces of [B, 8192] bf16 (1 MiB at B = 64) per
 point-to-point links, so the one-shot algorithm — every rank reads all 7 peers' copies concurrently and reduces
 locally — moves the message in one hop at ~7 links' bandwidth (csrc/allreduce.hip).
 
-Setup: each rank allocates one fine-grained uncached buffer (flags + 2 x max_bytes data halves), the IPC handles are
-exchanged over the gloo control group, every rank maps every peer's buffer. Calls are stream-ordered and
-hipGraph-capturable (buffers are registered up front; the epoch is a kernel argument). Messages above ``max_bytes``
-(prefill chunks) go to RCCL. Enabled with ``KAFKA_CUSTOM_AR=1`` (``parallel/state.init``) — 2, 4 or 8 ranks.
+Setup: each rank allocates one fine-grained uncached buffer (flags + per-block epoch counters + 2 x max_bytes data
+halves), the IPC handles are exchanged over the gloo control group, every rank maps every peer's buffer. Calls are
+stream-ordered and hipGraph-capturable: the buffers are registered up front and the call counters live in device
+memory (each block advances its own), so a replayed graph runs fresh epochs. Every call uses the same ``nblocks``.
+
+``all_reduce_add_rmsnorm`` fuses the layer seam of a TP decoder: residual += allreduce(x); out = rmsnorm(residual)
+(x may be the fp32 split-K slabs of the decode GEMM). Messages above ``max_bytes`` (prefill chunks) go to RCCL.
+Enabled with ``KAFKA_CUSTOM_AR=1`` (``parallel/state.init``) — 2, 4 or 8 ranks, one GPU each; the same protocol
+runs between processes that share one GPU (tests/test_custom_allreduce_gpu.py on a 1-GPU box).
 """
 from __future__ import annotations
 
@@ -18,6 +23,10 @@ import torch.distributed as dist
 from kafka_llm_service_amd.ops._ext import ext
 
 
+def _is_slab(x: torch.Tensor) -> bool:
+    return x.dtype == torch.float32 and x.dim() == 3
+
+
 class CustomAllReduce:
     def __init__(self, cpu_group, rank: int, world: int, max_bytes: int = 8 << 20, nblocks: int = 64):
         if world not in (2, 4, 8):
@@ -25,7 +34,6 @@ class CustomAllReduce:
         self.rank, self.world = rank, world
         self.max_bytes = max_bytes
         self.nblocks = nblocks
-        self.epoch = 0
         e = ext()
         self.own = e.car_alloc(2 * max_bytes)
         handles = [None] * world
@@ -41,14 +49,25 @@ class CustomAllReduce:
                 self.bases.append(p)
         dist.barrier(group=cpu_group)
 
-    def should_use(self, x: torch.Tensor) -> bool:
-        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0
-                and x.numel() * 2 <= self.max_bytes)
+    def _fits(self, x: torch.Tensor) -> bool:
+        n = x.shape[1] * x.shape[2] if _is_slab(x) else x.numel()
+        return x.is_cuda and x.is_contiguous() and n % 8 == 0 and n * 2 <= self.max_bytes
 
-    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
-        self.epoch += 1
-        ext().car_all_reduce(x, self.bases, self.rank, self.epoch, self.max_bytes, self.nblocks)
-        return x
+    def should_use(self, x: torch.Tensor) -> bool:
+        return (x.dtype == torch.bfloat16 or _is_slab(x)) and self._fits(x)
+
+    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Sum over the group of x (bf16, in place unless ``out``) or of a split-K slab (into a new bf16 tensor)."""
+        if _is_slab(x) and out is None:
+            out = torch.empty(x.shape[1], x.shape[2], dtype=torch.bfloat16, device=x.device)
+        ext().car_all_reduce(x, out, self.bases, self.rank, self.max_bytes, self.nblocks)
+        return x if out is None else out
+
+    def all_reduce_add_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                               out: torch.Tensor) -> torch.Tensor:
+        ext().car_all_reduce_add_rmsnorm(x, residual, w, float(eps), out, self.bases, self.rank, self.max_bytes,
+                                         self.nblocks)
+        return out
 
     def check(self) -> None:
         """Raise if any wait timed out (a peer never arrived). Synchronises; for tests and health checks."""

@@ -62,6 +62,7 @@ def init(tp: int = 1, backend: str | None = None, device: str | None = None) -> 
     st = ParallelState(world=world, rank=rank, local_rank=local_rank, tp=tp, tp_rank=rank % tp, dp=world // tp,
                        dp_rank=rank // tp)
     if world > 1:
+        backend = backend or os.environ.get("KAFKA_TP_BACKEND") or None  # tests: "gloo" for ranks sharing one GPU
         if backend is None:
             backend = "nccl" if (device or "").startswith("cuda") or (device is None and torch.cuda.is_available()) \
                 else "gloo"
@@ -80,13 +81,25 @@ def init(tp: int = 1, backend: str | None = None, device: str | None = None) -> 
                 cpg = dist.new_group(ranks, backend="gloo", timeout=_timeout()) if backend != "gloo" else pg
                 if rank in ranks:
                     st.tp_group, st.cpu_group = pg, cpg
-            if backend == "nccl" and os.environ.get("KAFKA_CUSTOM_AR", "0") == "1":
-                from . import comm
-                from .custom_allreduce import CustomAllReduce
-
-                comm.register_custom(st.tp_group, CustomAllReduce(st.cpu_group, st.tp_rank, tp))
+            on_gpu = (device or "").startswith("cuda") or (device is None and torch.cuda.is_available())
+            if on_gpu and tp in (2, 4, 8) and os.environ.get("KAFKA_CUSTOM_AR", "1") == "1":
+                _register_custom_ar(st, tp)
     _STATE = st
     return st
+
+
+def _register_custom_ar(st: ParallelState, tp: int) -> None:
+    """The one-shot xGMI all-reduce for decode-sized messages (parallel/custom_allreduce.py); RCCL stays the path for
+    everything else, and for all of it when the IPC mapping cannot be set up (logged, not fatal)."""
+    import logging
+
+    from . import comm
+    from .custom_allreduce import CustomAllReduce
+
+    try:
+        comm.register_custom(st.tp_group, CustomAllReduce(st.cpu_group, st.tp_rank, tp))
+    except Exception:  # noqa: BLE001
+        logging.getLogger("kafka.parallel").exception("custom all-reduce unavailable; using RCCL for every message")
 
 
 def _timeout() -> timedelta:
@@ -99,6 +112,7 @@ def set_state(st: ParallelState) -> None:
 
 
 def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
+    """Sum over the TP group (bf16; fp32 split-K slabs come back as a bf16 sum)."""
     st = _STATE
     if st.tp == 1:
         return x
@@ -107,13 +121,36 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     return comm.all_reduce(x, st.tp_group)
 
 
+def tp_all_reduce_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                              out: torch.Tensor) -> torch.Tensor:
+    from . import comm
+
+    return comm.all_reduce_add_rmsnorm(x, residual, w, eps, out, _STATE.tp_group)
+
+
 def tp_all_gather_lastdim(x: torch.Tensor) -> torch.Tensor:
     st = _STATE
     if st.tp == 1:
         return x
-    parts = [torch.empty_like(x) for _ in range(st.tp)]
-    dist.all_gather(parts, x.contiguous(), group=st.tp_group)
-    return torch.cat(parts, dim=-1)
+    from . import comm
+
+    return comm.all_gather_lastdim(x, st.tp, st.tp_group)
+
+
+def tp_broadcast_from_leader(x: torch.Tensor) -> torch.Tensor:
+    """In place: every rank of the TP group gets the leader's ``x`` (device tensors over RCCL; over a gloo group —
+    several ranks on one GPU in tests — through host memory)."""
+    st = _STATE
+    if st.tp == 1:
+        return x
+    src = st.rank - st.tp_rank
+    if x.is_cuda and dist.get_backend(st.tp_group) == "gloo":
+        h = x.cpu()
+        dist.broadcast(h, src=src, group=st.tp_group)
+        x.copy_(h)
+        return x
+    dist.broadcast(x, src=src, group=st.tp_group)
+    return x
 
 
 def barrier() -> None:

@@ -29,39 +29,48 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
-def _group_main(rank: int, world: int, port: int, q) -> None:
+def _group_main(rank: int, world: int, port: int, q, extra: dict) -> None:
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(world),
                        "RANK": str(rank), "LOCAL_RANK": str(rank)})
     from kafka_llm_service_amd.engine import tp_worker
     from kafka_llm_service_amd.parallel import state as pstate
 
-    eng, st = tp_worker.build_tp_engine(dict(CFG), tp=world)
+    eng, st = tp_worker.build_tp_engine(dict(CFG, **extra), tp=world)
     try:
         if st.is_tp_leader:
             outs = eng.generate(_prompts(), GREEDY)
             tp_worker.release_followers()
-            q.put(("outs", outs, eng.num_blocks))
+            g = eng.runner.graphs
+            q.put(("outs", outs, eng.num_blocks, eng.stats["planned_ahead"], g.stats if g is not None else None))
         else:
             n = tp_worker.follower_loop(eng)
-            q.put(("follower_steps", n))
+            g = eng.runner.graphs
+            q.put(("follower_steps", n, g.stats if g is not None else None))
     finally:
         pstate.destroy()
 
 
 @pytest.mark.timeout(300)
-def test_tp2_generate_matches_tp1():
+@pytest.mark.parametrize("extra", [{}, {"use_graphs": True}], ids=["eager", "graphs"])
+def test_tp2_generate_matches_tp1(extra):
+    """Leader plans step n+1 while n runs (late decode inputs filled device-side on EVERY rank from its own sampler
+    output); with ``use_graphs`` every rank captures and replays the decode layouts (fake graph backend on CPU:
+    replays read only the static buffers) and samples after the logit all-gather."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_group_main, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_group_main, args=(r, 2, port, q, extra)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((m[0], m[1:]) for m in (q.get(timeout=240) for _ in range(2)))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    outs, nb = res["outs"]
+    outs, nb, ahead, gstats = res["outs"]
     assert res["follower_steps"][0] >= GREEDY.max_tokens and nb == 256
+    assert ahead > 0  # TP leaders plan ahead
+    if extra.get("use_graphs"):
+        assert gstats["replays"] >= 1 and res["follower_steps"][1]["replays"] == gstats["replays"]
     ref = LLMEngine(EngineConfig(**CFG))
     prompts = _prompts()
     # TP=2 reduces in a different order (bf16): tokens must be the TP=1 model's argmax up to a small logit margin
@@ -148,3 +157,25 @@ def test_dp_client_with_tp_groups():
 
     outs, h = asyncio.run(run())
     assert [len(o) for o in outs] == [5, 5] and h["replicas"] == 1
+
+
+def test_plan_wire_format_roundtrip():
+    import numpy as np
+
+    from kafka_llm_service_amd.engine.model_runner import HostStep, SampleParams, pack_plan, unpack_plan
+
+    h = HostStep(B=3, T=40, nbt=4, bt_w=32, n_rows=4, s_total=5, n_dec_items=6, n_prefix_items=2, cascade_prefix=512,
+                 n_items=1, prefill_splits=0, n_late=2, late_off=123)
+    h.i64 = np.arange(125, dtype=np.int64)
+    h.i32 = np.arange(4 * 32 + 77, dtype=np.int32)
+    sp = SampleParams(np.array([0.7, 0, 1, 2], np.float32), np.ones(4, np.float32), np.array([0, 5, 0, 1], np.int32),
+                      np.array([1, 2, 3, 1 << 40], np.int64), [], False)
+    hdr, payload = pack_plan(h, sp)
+    h2, sp2 = unpack_plan(hdr, payload)
+    for f in ("B", "T", "nbt", "bt_w", "n_rows", "s_total", "n_dec_items", "n_prefix_items", "cascade_prefix",
+              "n_items", "prefill_splits", "n_late", "late_off"):
+        assert getattr(h2, f) == getattr(h, f), f
+    assert (h2.i64 == h.i64).all() and (h2.i32 == h.i32).all()
+    for f in ("temp", "topp", "topk", "seeds"):
+        assert (getattr(sp2, f) == getattr(sp, f)).all()
+    assert sp2.greedy is False and sp2.leader_tokens is False
