@@ -17,6 +17,7 @@ from dataclasses import dataclass, field, replace
 
 import torch
 
+from kafka_llm_service_amd import ops
 from kafka_llm_service_amd.engine.model_runner import ModelRunner
 from kafka_llm_service_amd.engine.scheduler import NeedSync, Scheduler, SchedulerConfig
 from kafka_llm_service_amd.engine.sequence import PENDING, SamplingParams, Sequence, StepOutput
@@ -49,7 +50,6 @@ class EngineConfig:
     target_wgs: int = 256               # tile-kernel workgroups per pass (8-wave WGs, one per CU)
     prefill_kv_chunk: int = 1024        # key-range split for long-context prefill tiles
     use_graphs: bool = False
-    kv_dtype: str = "bf16"              # bf16 | fp8 (e4m3 KV pages with per-(page, head) scales)
     # decode GEMMs: "stream" = weight-streaming MFMA kernel on wave-tiled weight copies (csrc/wstream_gemm.hip),
     # "blas" = hipBLASLt only; "auto" = stream on GPU (env KAFKA_DECODE_GEMM overrides)
     decode_gemm: str = "auto"           # auto | stream | stream_only (tiled weights only) | blas
@@ -122,6 +122,10 @@ class LLMEngine:
                 self.model.enable_stream_weights(tiled_only=True)
         elif mode == "stream_only" and not self.model.stream:
             self.model.enable_stream_weights(tiled_only=True)
+        if self.model.tiled_only and cfg.max_num_seqs > ops.STREAM_MAX_M:
+            # decode batches beyond the streaming kernel's rows would untile every projection every step
+            log.info("tiled-only weights: max_num_seqs %d -> %d", cfg.max_num_seqs, ops.STREAM_MAX_M)
+            cfg.max_num_seqs = ops.STREAM_MAX_M
         self.load_s = time.perf_counter() - t0
         self.eos = set(cfg.eos_token_ids or mc.eos_token_ids)
         hkv, D, L = self.model.hkv, self.model.D, mc.num_layers

@@ -76,7 +76,7 @@ class TransformerLM:
 
     # ------------------------------------------------------------------------------------------------------------
     def stream_weight_bytes(self) -> int:
-        """Bytes enable_stream_weights would add (the wave-tiled copies)."""
+        """Bytes enable_stream_weights would add (the wave-tiled copies; 0 in tiled-only mode)."""
         n = 0
         for lw in self.layers:
             for name in LayerWeights.STREAMED:
@@ -87,7 +87,7 @@ class TransformerLM:
                 w = getattr(lw, name)
                 if w is not None and ops.stream_moe_supported(w.shape[1], w.shape[2]):
                     n += w.numel() * w.element_size()
-        if ops.stream_plan(1, self.lm_head.shape[0], self.lm_head.shape[1]) is not None:
+        if self.lm_head is not None and ops.stream_plan(1, self.lm_head.shape[0], self.lm_head.shape[1]) is not None:
             n += self.lm_head.numel() * self.lm_head.element_size()
         return n
 
@@ -97,9 +97,10 @@ class TransformerLM:
         hipBLASLt; prefill-sized steps keep the row-major weights. Costs one more copy of those weights (16 GB for
         Llama-3-8B: the HBM of an MI355X has room, and the KV pool is sized after this). Returns the added bytes.
 
-        ``tiled_only``: when the second copy does not fit (Llama-3-70B on one GPU), the row-major dense projections are
-        dropped after tiling (no extra memory) and prefill-sized steps untile one weight at a time into a transient
-        buffer for hipBLASLt (``_dense``)."""
+        ``tiled_only``: when the second copy does not fit (Llama-3-70B on one GPU), the row-major dense projections
+        and the lm_head are dropped after tiling (no extra memory) and prefill-sized steps untile one weight at a
+        time into a transient buffer for hipBLASLt (``_dense``); MoE experts keep their row-major layout only
+        (grouped GEMM at every step size — a tiled expert copy would be the 90 GB second copy this mode avoids)."""
         added = 0
         for lw in self.layers:
             for name in LayerWeights.STREAMED:
@@ -114,14 +115,18 @@ class TransformerLM:
                         del w
                     else:
                         added += w.numel() * w.element_size()
-            if lw.w13 is not None and ops.stream_moe_supported(lw.w13.shape[1], lw.w13.shape[2]) and \
+            if not tiled_only and lw.w13 is not None and \
+                    ops.stream_moe_supported(lw.w13.shape[1], lw.w13.shape[2]) and \
                     ops.stream_moe_supported(lw.w2.shape[1], lw.w2.shape[2]):
                 lw.w13_t = ops.tile_experts(lw.w13, glu=True)  # expert MLPs: grouped streaming kernel
                 lw.w2_t = ops.tile_experts(lw.w2)
                 added += (lw.w13.numel() + lw.w2.numel()) * lw.w13.element_size()
         if ops.stream_plan(1, self.lm_head.shape[0], self.lm_head.shape[1]) is not None:
             self.lm_head_t = ops.tile_weight(self.lm_head)
-            added += self.lm_head.numel() * self.lm_head.element_size()
+            if tiled_only:
+                self.lm_head = None
+            else:
+                added += self.lm_head_t.numel() * self.lm_head_t.element_size()
         self.stream = True
         self.tiled_only = tiled_only
         if tiled_only and self.device.type == "cuda":
@@ -210,10 +215,10 @@ class TransformerLM:
 
     # ------------------------------------------------------------------------------------------------------------
     def weight_bytes(self) -> int:
-        n = 0
-        for t in self.named_tensors().values():
-            n += t.numel() * t.element_size()
-        return n
+        """Device bytes of every weight tensor, wave-tiled copies included (so tiled-only models report fully)."""
+        ts = list(self.named_tensors().values()) + [self.lm_head_t]
+        ts += [getattr(lw, s) for lw in self.layers for s in LayerWeights.__slots__ if s.endswith("_t")]
+        return sum(t.numel() * t.element_size() for t in ts if isinstance(t, torch.Tensor))
 
     def named_tensors(self) -> dict[str, torch.Tensor]:
         out = {"embed": self.embed, "lm_head": self.lm_head, "final_norm": self.final_norm}

@@ -228,14 +228,23 @@ def save_safetensors(model: TransformerLM, path: str | Path) -> None:
     assert model.tp == 1
     D, F = cfg.head_dim, cfg.intermediate_size
     qn, kn = cfg.num_heads * D, cfg.num_kv_heads * D
-    out = {"model.embed_tokens.weight": model.embed, "lm_head.weight": model.lm_head,
+    from kafka_llm_service_amd import ops
+
+    def dense(lw, name):  # tiled-only models keep just the wave-tiled copy: untile it for export
+        w = getattr(lw, name)
+        return w if w is not None else ops.untile_weight(getattr(lw, name + "_t"), glu=bool(lw.glu) and
+                                                         name == "gate_up")
+
+    lm_head = model.lm_head if model.lm_head is not None else ops.untile_weight(model.lm_head_t)
+    out = {"model.embed_tokens.weight": model.embed, "lm_head.weight": lm_head,
            "model.norm.weight": model.final_norm}
     for i, lw in enumerate(model.layers):
+        qkv, o = dense(lw, "qkv"), dense(lw, "o")
         n = _hf_names(cfg, i)
         out[n["input_norm"]] = lw.input_norm
         out[n["post_norm"]] = lw.post_norm
-        out[n["q"]], out[n["k"]], out[n["v"]] = lw.qkv[:qn], lw.qkv[qn:qn + kn], lw.qkv[qn + kn:]
-        out[n["o"]] = lw.o
+        out[n["q"]], out[n["k"]], out[n["v"]] = qkv[:qn], qkv[qn:qn + kn], qkv[qn + kn:]
+        out[n["o"]] = o
         if cfg.num_experts:
             out[n["router"]] = lw.router
             for e in range(cfg.num_experts):
@@ -243,8 +252,9 @@ def save_safetensors(model: TransformerLM, path: str | Path) -> None:
                 out[n["expert"].format(e=e, w="w3")] = lw.w13[e, F:]
                 out[n["expert"].format(e=e, w="w2")] = lw.w2[e]
         else:
-            out[n["gate"]], out[n["up"]] = lw.gate_up[:F], lw.gate_up[F:]
-            out[n["down"]] = lw.down
+            gu = dense(lw, "gate_up")
+            out[n["gate"]], out[n["up"]] = gu[:F], gu[F:]
+            out[n["down"]] = dense(lw, "down")
     out = {k: v.detach().cpu().contiguous() for k, v in out.items()}
     Path(path).parent.mkdir(parents=True, exist_ok=True)
     save_file(out, str(path))

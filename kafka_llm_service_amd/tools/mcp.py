@@ -1,4 +1,5 @@
-"""Minimal Model Context Protocol client (JSON-RPC 2.0) — stdio and streamable-HTTP (with SSE responses).
+"""Minimal Model Context Protocol client (JSON-RPC 2.0) — stdio, streamable HTTP, and the legacy HTTP+SSE
+transport as the fallback for URL servers that do not speak streamable HTTP.
 
 The reference drives MCP servers through the ``mcp`` SDK (/root/reference/src/tools/agent.py:63-413: stdio or
 streamable-HTTP with SSE fallback, ``tools/list`` discovery, ``tools/call``, and a streaming side channel that tails
@@ -140,6 +141,97 @@ class _HttpTransport:
             await self.client.aclose()
 
 
+def _message_url(base: str, endpoint: str) -> str:
+    from urllib.parse import urljoin
+
+    return urljoin(base, endpoint)
+
+
+class _SseTransport:
+    """Legacy HTTP+SSE (MCP 2024-11-05): GET the server URL as an event stream; its first ``endpoint`` event names
+    the URL to POST JSON-RPC messages to; replies arrive as ``message`` events on the stream. A reader task routes
+    them to the waiting requests by id."""
+
+    def __init__(self, cfg: MCPServerConfig):
+        self.cfg = cfg
+        self.client = None
+        self.post_url: str | None = None
+        self.pending: dict[int, asyncio.Future] = {}
+        self.reader_task: asyncio.Task | None = None
+        self._endpoint: asyncio.Future | None = None
+
+    async def start(self, timeout: float = 30.0) -> None:
+        import httpx
+
+        self.client = httpx.AsyncClient(timeout=httpx.Timeout(timeout, read=None))
+        self._endpoint = asyncio.get_running_loop().create_future()
+        self.reader_task = asyncio.create_task(self._read_loop())
+        self.post_url = await asyncio.wait_for(self._endpoint, timeout)
+
+    async def _read_loop(self) -> None:
+        event, data = "message", []
+        try:
+            async with self.client.stream("GET", self.cfg.url, headers={"Accept": "text/event-stream"}) as r:
+                if r.status_code >= 400:
+                    raise MCPError(f"MCP SSE HTTP {r.status_code}")
+                async for line in r.aiter_lines():
+                    if line.startswith("event:"):
+                        event = line[6:].strip()
+                    elif line.startswith("data:"):
+                        data.append(line[5:].strip())
+                    elif not line:  # end of one event
+                        self._dispatch(event, "\n".join(data))
+                        event, data = "message", []
+        except Exception as e:  # noqa: BLE001 - surfaced to every waiter
+            err = e if isinstance(e, MCPError) else MCPError(f"MCP SSE stream failed: {e!r}")
+            if self._endpoint is not None and not self._endpoint.done():
+                self._endpoint.set_exception(err)
+            for fut in self.pending.values():
+                if not fut.done():
+                    fut.set_exception(err)
+            return
+        for fut in self.pending.values():
+            if not fut.done():
+                fut.set_exception(MCPError("MCP SSE stream closed"))
+
+    def _dispatch(self, event: str, data: str) -> None:
+        if event == "endpoint":
+            if not self._endpoint.done():
+                self._endpoint.set_result(_message_url(self.cfg.url, data))
+            return
+        try:
+            msg = json.loads(data)
+        except json.JSONDecodeError:
+            return
+        fut = self.pending.pop(msg.get("id"), None) if isinstance(msg, dict) else None
+        if fut is not None and not fut.done():
+            fut.set_result(msg)
+
+    async def request(self, msg: dict, timeout: float) -> dict | None:
+        fut = None
+        if "id" in msg:
+            fut = asyncio.get_running_loop().create_future()
+            self.pending[msg["id"]] = fut
+        r = await self.client.post(self.post_url, content=json.dumps(msg),
+                                   headers={"Content-Type": "application/json"}, timeout=timeout)
+        if r.status_code >= 400:
+            self.pending.pop(msg.get("id"), None)
+            raise MCPError(f"MCP SSE POST {r.status_code}: {r.text[:200]}")
+        if fut is None:
+            return None
+        return await asyncio.wait_for(fut, timeout)
+
+    async def close(self) -> None:
+        if self.reader_task:
+            self.reader_task.cancel()
+            try:
+                await self.reader_task
+            except (asyncio.CancelledError, Exception):  # noqa: BLE001
+                pass
+        if self.client:
+            await self.client.aclose()
+
+
 class MCPConnection:
     def __init__(self, config: MCPServerConfig, timeout: float = 60.0):
         self.config = config
@@ -150,19 +242,36 @@ class MCPConnection:
         self.connected = False
 
     async def connect(self) -> None:
+        """stdio for a command; for a URL streamable HTTP first and, if the server does not answer it, the legacy
+        HTTP+SSE transport (the fallback order of /root/reference/src/tools/agent.py:113-162)."""
         if self.config.command:
             self._t = _StdioTransport(self.config)
+            await self._t.start()
+            await self._handshake()
         elif self.config.url:
             self._t = _HttpTransport(self.config)
+            await self._t.start()
+            try:
+                await self._handshake()
+            except Exception as first:  # noqa: BLE001
+                await self._t.close()
+                self._t = _SseTransport(self.config)
+                try:
+                    await self._t.start(min(self.timeout, 30.0))
+                    await self._handshake()
+                except Exception as e:  # noqa: BLE001
+                    await self._t.close()
+                    raise MCPError(f"MCP {self.config.name!r}: streamable HTTP failed ({first}); SSE failed ({e})")
         else:
             raise MCPError(f"MCP server {self.config.name!r} has neither command nor url")
-        await self._t.start()
+        self.connected = True
+
+    async def _handshake(self) -> None:
         await self._rpc("initialize", {"protocolVersion": PROTOCOL_VERSION, "capabilities": {},
                                        "clientInfo": CLIENT_INFO})
         await self._t.request({"jsonrpc": "2.0", "method": "notifications/initialized"}, self.timeout)
         res = await self._rpc("tools/list", {})
         self.tools = [_mcp_tool_to_openai(t) for t in res.get("tools", [])]
-        self.connected = True
 
     async def _rpc(self, method: str, params: dict) -> dict:
         msg = {"jsonrpc": "2.0", "id": next(self._ids), "method": method, "params": params}

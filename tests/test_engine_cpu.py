@@ -317,3 +317,24 @@ def test_prefix_groups_and_decode_items():
         assert (rows[:, 3] == np.arange(len(rows))).all() and (rows[:, 4] == len(rows)).all()
         assert (rows[:, 5] == npre[b]).all() and len(rows) + npre[b] <= MAX_PARTIALS
     assert (it[:, 0] == 3).sum() > (it[:, 0] == 1).sum() == 1  # the long row is split, the short one is not
+
+
+def test_tiled_only_mixtral_and_export(tmp_path):
+    """Tiled-only mode on an MoE model: experts stay row-major (no second expert copy), the lm_head keeps only its
+    tiled copy, generation equals the two-copy stream mode, and safetensors export untiles what was dropped."""
+    from kafka_llm_service_amd.models.weights import build_model, save_safetensors
+
+    base = dict(model="tiny-mixtral", device="cpu", num_kv_blocks=256, max_model_len=2048)
+    ref_eng = LLMEngine(EngineConfig(**base, decode_gemm="stream"))
+    eng = LLMEngine(EngineConfig(**base, decode_gemm="stream_only"))
+    m = eng.model
+    assert m.tiled_only and m.lm_head is None and m.lm_head_t is not None
+    assert m.layers[0].w13 is not None and m.layers[0].w13_t is None  # experts: one (row-major) copy
+    assert eng.cfg.max_num_seqs <= 128
+    assert m.weight_bytes() >= ref_eng.model.weight_bytes() // 2
+    prompts = _prompts(seed=12)
+    assert eng.generate(prompts, GREEDY) == ref_eng.generate(prompts, GREEDY)
+    save_safetensors(m, tmp_path / "model.safetensors")
+    back = build_model(m.cfg, "cpu", weights=str(tmp_path))
+    assert torch.equal(back.lm_head, ref_eng.model.lm_head)
+    assert torch.equal(back.layers[1].qkv, ref_eng.model.layers[1].qkv)

@@ -140,3 +140,39 @@ def test_daytona_sandbox_interface_offline():
         raise AssertionError("expected SandboxError")
     except SandboxError as e:
         assert "daytona_sdk" in str(e)
+
+
+def test_mcp_http_falls_back_to_legacy_sse():
+    """A URL server that refuses streamable HTTP is reached over the legacy HTTP+SSE transport
+    (/root/reference/src/tools/agent.py:113-162)."""
+    import socket
+    import subprocess
+    import time
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    proc = subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "fixtures", "mcp_sse_server.py"),
+                             str(port)])
+    try:
+        import httpx
+
+        for _ in range(100):
+            try:
+                httpx.post(f"http://127.0.0.1:{port}/sse", timeout=1)
+                break
+            except httpx.HTTPError:
+                time.sleep(0.1)
+
+        async def main():
+            conn = MCPConnection(MCPServerConfig(name="legacy", url=f"http://127.0.0.1:{port}/sse"), timeout=20)
+            await conn.connect()
+            assert type(conn._t).__name__ == "_SseTransport"
+            assert [t["function"]["name"] for t in conn.tools] == ["echo", "add"]
+            assert await conn.call_tool("add", {"a": 4, "b": 5}) == "9"
+            assert await conn.call_tool("echo", {"text": "over sse"}) == "over sse"
+            await conn.disconnect()
+        asyncio.run(main())
+    finally:
+        proc.terminate()
+        proc.wait(timeout=10)
