@@ -105,6 +105,9 @@ def _system_message(chars: int) -> str | None:
 
 
 async def _thread(client, url, k, args, res):
+    if getattr(args, "stagger", 0) > 0 and k >= 0:
+        # steady-state arrivals: thread k starts at a deterministic point in [0, stagger) instead of all at once
+        await asyncio.sleep(args.stagger * ((k * 0.6180339887) % 1.0))
     body = {"system_message": _system_message(args.system_chars)} if args.system_chars > 0 else {}
     r = await client.post(f"{url}/v1/threads", json=body)
     tid = r.json()["thread_id"]
@@ -176,7 +179,8 @@ def run(url, args):
     return {
         "metric": "serve: p50 TTFT + output tok/s, /v1/threads/{id}/chat/completions",
         "backend": args.backend, "model": args.model, "threads": args.threads, "turns": args.turns,
-        "stream": not args.no_stream, "client_procs": P, "system_chars": args.system_chars, "requests": res["requests"], "wall_s": round(wall, 3),
+        "stream": not args.no_stream, "client_procs": P, "system_chars": args.system_chars,
+        "stagger_s": args.stagger, "requests": res["requests"], "wall_s": round(wall, 3),
         "client_cpu_s": round(res["client_cpu"], 3),
         "ttft_p50_ms": ms(_pct(res["ttft"], 0.5)), "ttft_p99_ms": ms(_pct(res["ttft"], 0.99)),
         "e2e_p50_ms": ms(_pct(res["e2e"], 0.5)), "e2e_p99_ms": ms(_pct(res["e2e"], 0.99)),
@@ -196,6 +200,8 @@ def main():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--threads", type=int, default=64)
     ap.add_argument("--turns", type=int, default=4)
+    ap.add_argument("--stagger", type=float, default=0.0,
+                    help="spread thread starts over this many seconds (0 = all threads start together, a burst)")
     ap.add_argument("--max-tokens", type=int, default=128)
     ap.add_argument("--temperature", type=float, default=0.7)
     ap.add_argument("--user-words", type=int, default=8)

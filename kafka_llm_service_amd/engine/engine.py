@@ -43,6 +43,7 @@ class EngineConfig:
     max_num_seqs: int = 256
     max_num_batched_tokens: int = 8192
     max_prefill_chunk: int = 8192
+    prefill_tokens_while_decoding: int = 512  # TPOT guard (engine/scheduler.py); 0 = off
     max_model_len: int = 131072
     enable_prefix_cache: bool = True
     use_cascade: bool = True
@@ -153,6 +154,7 @@ class LLMEngine:
         self.sched = Scheduler(SchedulerConfig(max_num_seqs=cfg.max_num_seqs,
                                                max_num_batched_tokens=cfg.max_num_batched_tokens,
                                                max_prefill_chunk=cfg.max_prefill_chunk,
+                                               prefill_tokens_while_decoding=cfg.prefill_tokens_while_decoding,
                                                max_model_len=cfg.max_model_len, max_blocks_per_seq=max_blocks),
                                self.kvm)
         kc = [self.k_cache[i] for i in range(L)]

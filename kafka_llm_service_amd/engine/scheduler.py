@@ -28,6 +28,11 @@ class SchedulerConfig:
     max_prefill_chunk: int = 8192
     max_model_len: int = 131072
     max_blocks_per_seq: int = 8192
+    # TPOT guard: while at least `tpot_guard_decodes` streams are decoding, a step takes at most this many prefill
+    # tokens (0 = no guard) — a cold 18k-token admission is spread over many steps instead of stalling every stream
+    # for one ~100 ms step; a new turn of a cached thread (tens of tokens) still fits in the next step
+    prefill_tokens_while_decoding: int = 512
+    tpot_guard_decodes: int = 16
 
 
 @dataclass
@@ -126,6 +131,8 @@ class Scheduler:
                 continue
             batch.decode.append(seq)
             budget -= 1
+        if cfg.prefill_tokens_while_decoding and len(batch.decode) >= cfg.tpot_guard_decodes:
+            budget = min(budget, cfg.prefill_tokens_while_decoding)
         # 2. running prefills
         for seq in list(self.running):
             if budget <= 0:

@@ -13,6 +13,7 @@ from typing import Any, AsyncGenerator
 
 from kafka_llm_service_amd.kafka.utils import sanitize_messages_for_openai
 from kafka_llm_service_amd.llm.types import Message
+from kafka_llm_service_amd.obs import trace
 
 
 class KafkaAgent(ABC):
@@ -63,15 +64,17 @@ class KafkaAgent(ABC):
         lock = db.thread_lock(tid) if (tid and db is not None and hasattr(db, "thread_lock")) else _async_null()
         async with lock:
             history: list[Message] = []
-            if tid and db is not None:
-                if not await db.thread_exists(tid):
-                    await db.create_thread(thread_id=tid)
-                history = await db.get_thread_messages(tid)
-            msgs = sanitize_messages_for_openai(history + list(new_messages))
+            with trace.span("api_db_load", "api", f"thr:{tid}"):
+                if tid and db is not None:
+                    if not await db.thread_exists(tid):
+                        await db.create_thread(thread_id=tid)
+                    history = await db.get_thread_messages(tid)
+                msgs = sanitize_messages_for_openai(history + list(new_messages))
             if save_to_thread and tid and db is not None:
                 new = [m for m in new_messages if m.role in ("user", "system")]
                 if new:
-                    await db.add_messages(tid, new)
+                    with trace.span("api_db_save", "api", f"thr:{tid}"):
+                        await db.add_messages(tid, new)
             async for ev in self.run(msgs, model=model, temperature=temperature, max_tokens=max_tokens,
                                      emit_messages=True, **kwargs):
                 if ev.get("type") == "_message":

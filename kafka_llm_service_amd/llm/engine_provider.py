@@ -13,6 +13,7 @@ token ids so the agent can store them with the message (thread token cache).
 """
 from __future__ import annotations
 
+import time
 import uuid
 from typing import Any, AsyncGenerator
 
@@ -23,6 +24,7 @@ from kafka_llm_service_amd.engine.sequence import SamplingParams
 from kafka_llm_service_amd.engine.tokenizer import IncrementalDetokenizer, tokenizer_for_model
 from kafka_llm_service_amd.llm.base import LLMProvider
 from kafka_llm_service_amd.llm.types import LLMProviderError, Message, StreamChunk, Usage
+from kafka_llm_service_amd.obs import trace
 
 
 class EngineLLMProvider(LLMProvider):
@@ -93,7 +95,8 @@ class EngineLLMProvider(LLMProvider):
         self.validate_messages(messages)
         if tools is None:
             tools = await self.get_tools()
-        prompt = self.render(messages, tools)
+        with trace.span("api_render", "api", f"thr:{routing_key}", messages=len(messages)):
+            prompt = self.render(messages, tools)
         limit = self.client.max_model_len
         if len(prompt) + 1 > limit:
             raise LLMProviderError(f"This model's maximum context length is {limit} tokens. However, your messages "
@@ -120,8 +123,13 @@ class EngineLLMProvider(LLMProvider):
         cached = 0
         n_out = 0
         stopped = False
+        tr = trace.tracer()
+        t_sub = time.perf_counter()
         async for out in self.client.generate(rid, prompt, params, routing_key):
             ids = out.new_token_ids
+            if tr is not None and n_out == 0:  # submit -> first engine output on this (API) loop
+                tr.complete("api_engine_first", "api", t_sub, time.perf_counter(), f"thr:{routing_key}",
+                            {"prompt_tokens": len(prompt), "cached": out.num_cached_tokens})
             all_ids.extend(ids)
             n_out = out.num_output_tokens
             cached = out.num_cached_tokens

@@ -27,6 +27,7 @@ class Tracer:
         self._f.write("[\n")
         self._lock = threading.Lock()
         self._pid = os.getpid()
+        self._last_flush = time.perf_counter()
 
     def complete(self, name: str, cat: str, start: float, end: float, tid: int | str | None = None,
                  args: dict | None = None) -> None:
@@ -39,6 +40,10 @@ class Tracer:
         line = json.dumps(ev) + ",\n"
         with self._lock:
             self._f.write(line)
+            now = time.perf_counter()
+            if now - self._last_flush > 0.5:  # a process killed without exit handlers keeps all but the last 0.5 s
+                self._f.flush()
+                self._last_flush = now
 
     def flush(self) -> None:
         with self._lock:

@@ -40,6 +40,7 @@ from fastapi import FastAPI, HTTPException, Request
 from fastapi.middleware.cors import CORSMiddleware
 from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 
+from kafka_llm_service_amd.obs import trace
 from kafka_llm_service_amd.kafka.types import (AgentRunRequest, ChatCompletionRequest, ChatMessage, Choice,
                                                ChatCompletionResponse, CreateThreadRequest, MessageContent, Usage)
 from kafka_llm_service_amd.kafka.utils import convert_to_internal_message
@@ -177,6 +178,9 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
                     if first:
                         t_first = time.perf_counter()
                         M.TTFT.observe(t_first - t0)
+                        tr = trace.tracer()
+                        if tr is not None:  # request in -> first content frame handed to the response
+                            tr.complete("api_http_ttft", "api", t0, t_first, f"thr:{thread_id}")
                         first = False
                     yield _chunk(cid, created, model, {"content": text}, None)
                 if ch[0].get("finish_reason") == "length":

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Per-request TTFT breakdown from KAFKA_TRACE_FILE traces of a serving run (Chrome trace JSON, one file per
+process): p50 / p99 / mean of every API-side span (DB load, template render, submit -> first engine output, request
+-> first SSE content frame) and of the engine's own arrival -> first-token span.
+
+    python scripts/ttft_breakdown.py gpurun_out/trace.*.json
+"""
+import glob
+import json
+import statistics
+import sys
+
+
+def load(paths):
+    evs = []
+    for p in paths:  # one event per line (a process killed before closing its file leaves no trailing "]")
+        for line in open(p):
+            line = line.strip().rstrip(",")
+            if line.startswith("{") and line.endswith("}") and line != "{}":
+                try:
+                    e = json.loads(line)
+                except json.JSONDecodeError:
+                    continue
+                if e.get("ph") == "X":
+                    evs.append(e)
+    return evs
+
+
+def main():
+    paths = [q for a in sys.argv[1:] for q in glob.glob(a)]
+    evs = load(paths)
+    names = ["api_http_ttft", "api_db_load", "api_db_save", "api_render", "api_engine_first", "first_token"]
+    print(f"{'span':20s} {'n':>6s} {'p50 ms':>9s} {'p99 ms':>9s} {'mean ms':>9s}")
+    for n in names:
+        d = sorted(e["dur"] / 1e3 for e in evs if e["name"] == n)
+        if not d:
+            continue
+        print(f"{n:20s} {len(d):6d} {d[len(d) // 2]:9.2f} {d[min(len(d) - 1, int(0.99 * len(d)))]:9.2f} "
+              f"{statistics.fmean(d):9.2f}")
+    steps = sorted(e["dur"] / 1e3 for e in evs if e["name"] == "launch")
+    if steps:
+        print(f"engine launch spans: {len(steps)}, p50 {steps[len(steps) // 2]:.2f} ms")
+
+
+if __name__ == "__main__":
+    main()

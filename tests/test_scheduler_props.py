@@ -84,3 +84,29 @@ def test_greedy_outputs_consistent_across_batching(seed):
     assert oracle_ok(base)
     assert oracle_ok(run(num_kv_blocks=14, max_prefill_chunk=16, max_num_batched_tokens=32))
     assert oracle_ok(run(num_kv_blocks=256, async_scheduling=False, enable_prefix_cache=False))
+
+
+def test_tpot_guard_caps_prefill_while_decoding():
+    """With >= tpot_guard_decodes streams decoding, a cold long prompt is admitted in chunks of at most
+    prefill_tokens_while_decoding tokens per step; without decodes it takes the full budget."""
+    from kafka_llm_service_amd.engine.scheduler import Scheduler, SchedulerConfig
+    from kafka_llm_service_amd.engine.sequence import SamplingParams, Sequence
+    from kafka_llm_service_amd.runtime import KVManager
+
+    kv = KVManager(4096, 16, True)
+    sch = Scheduler(SchedulerConfig(max_num_batched_tokens=8192, prefill_tokens_while_decoding=512,
+                                    tpot_guard_decodes=4), kv)
+    sp = SamplingParams(max_tokens=8, ignore_eos=True)
+    decs = [Sequence(f"d{i}", list(range(100 * i + 1, 100 * i + 33)), sp) for i in range(4)]
+    for d in decs:
+        sch.add(d)
+    b = sch.schedule()
+    assert sum(e - s for _, s, e in b.prefill) == 4 * 32  # no decodes yet: full budget
+    for d in decs:  # the prompts are computed; each now has one token to decode
+        d.num_computed = d.total_len
+        d.output_ids.append(7)
+        kv.append_token(d.seq_id, 7)
+    big = Sequence("cold", list(range(5000, 5000 + 18000)), sp)
+    sch.add(big)
+    b = sch.schedule()
+    assert len(b.decode) == 4 and sum(e - s for _, s, e in b.prefill) == 512
