@@ -13,7 +13,12 @@ Fixed vs the reference:
   * every message row keeps the engine token ids of generated assistant turns (``token_ids`` column): the chat
     template re-renders history from them exactly, which keeps the thread's KV prefix cache hot,
   * all SQLite work runs on one dedicated thread (sqlite3 connections are not thread-safe; aiosqlite is not
-    installed) so the API event loop never blocks on disk I/O (the reference's Supabase client blocked the loop).
+    installed) so the API event loop never blocks on disk I/O (the reference's Supabase client blocked the loop),
+  * a write-through cache of recent threads' histories (``LOCAL_DB_CACHE_THREADS``, default 4096; 0 = off) serves
+    the per-request history read without a trip through the SQLite thread, and ``add_messages(wait=False)`` queues
+    a write behind the ones before it (one FIFO writer: order and ``seq`` are kept) so the new user message's save
+    is off the time-to-first-token path; ``sync()`` waits for every queued write (the agent calls it before a
+    request ends). The cache assumes this process is the database's only writer (one server process per file).
 """
 from __future__ import annotations
 
@@ -23,7 +28,7 @@ import os
 import secrets
 import sqlite3
 import uuid
-from collections import defaultdict
+from collections import OrderedDict, defaultdict
 from concurrent.futures import ThreadPoolExecutor
 from datetime import datetime, timezone
 from typing import Any
@@ -100,6 +105,10 @@ class LocalDBClient:
         self._conn: sqlite3.Connection | None = None
         self._locks: dict[str, asyncio.Lock] = defaultdict(asyncio.Lock)
         self._initialized = False
+        self._cache_n = int(os.environ.get("LOCAL_DB_CACHE_THREADS", "4096"))
+        self._cache: OrderedDict[str, list[Message]] = OrderedDict()  # thread id -> full history, seq order
+        self._known: set[str] = set()
+        self._pending: set = set()  # write-behind futures not yet awaited
 
     # --- plumbing ---------------------------------------------------------------------------------------------
     def _connect(self) -> sqlite3.Connection:
@@ -117,6 +126,23 @@ class LocalDBClient:
 
     async def _run(self, fn, *args):
         return await asyncio.get_running_loop().run_in_executor(self._exec, fn, *args)
+
+    def _cache_put(self, thread_id: str, msgs: list[Message]) -> None:
+        if self._cache_n <= 0:
+            return
+        self._cache[thread_id] = msgs
+        self._cache.move_to_end(thread_id)
+        while len(self._cache) > self._cache_n:
+            self._cache.popitem(last=False)
+
+    async def sync(self) -> None:
+        """Wait until every queued write has reached SQLite (the writer is FIFO: a no-op behind them suffices)."""
+        if self._pending:
+            await self._run(lambda: None)
+            for f in list(self._pending):
+                if f.done():
+                    self._pending.discard(f)
+                    f.result()  # surface a failed write
 
     async def initialize(self) -> None:
         await self._run(self._connect)
@@ -146,14 +172,21 @@ class LocalDBClient:
                       "VALUES (?,?,?,?,?)", (tid, created, json.dumps(metadata or {}), user_id, kafka_profile_id))
             c.commit()
         await self._run(_do)
+        self._known.add(tid)
         if system_message:
             await self.add_message(tid, Message(role="system", content=system_message))
         return {"id": tid, "thread_id": tid, "created_at": created}
 
     async def thread_exists(self, thread_id: str) -> bool:
+        if thread_id in self._known:
+            return True
+
         def _do():
             return self._connect().execute("SELECT 1 FROM threads WHERE id=?", (thread_id,)).fetchone() is not None
-        return await self._run(_do)
+        ok = await self._run(_do)
+        if ok:
+            self._known.add(thread_id)
+        return ok
 
     async def get_thread_metadata(self, thread_id: str) -> dict[str, Any] | None:
         def _do():
@@ -168,6 +201,12 @@ class LocalDBClient:
     # --- messages ---------------------------------------------------------------------------------------------
     async def get_thread_messages(self, thread_id: str, limit: int | None = None,
                                   include_system: bool = True) -> list[Message]:
+        hit = self._cache.get(thread_id)
+        if hit is not None:
+            self._cache.move_to_end(thread_id)
+            out = [m.model_copy() for m in hit if include_system or m.role != "system"]  # callers may edit them
+            return out[:limit] if limit else out
+
         def _do():
             q = "SELECT message, token_ids FROM messages WHERE thread_id=? ORDER BY seq ASC"
             args: list[Any] = [thread_id]
@@ -184,10 +223,11 @@ class LocalDBClient:
             if r["token_ids"]:
                 d["token_ids"] = json.loads(r["token_ids"])
             out.append(Message.from_dict(d))
+        if not limit and include_system and not self._pending:  # no queued write this read could have missed
+            self._cache_put(thread_id, [m.model_copy() for m in out])
         return out
 
-    def _insert(self, c: sqlite3.Connection, thread_id: str, m: Message, metadata: dict | None) -> str:
-        mid = str(uuid.uuid4())
+    def _insert(self, c: sqlite3.Connection, thread_id: str, m: Message, metadata: dict | None, mid: str) -> str:
         c.execute("INSERT OR IGNORE INTO threads(id, created_at, metadata) VALUES (?,?,?)",
                   (thread_id, _now(), "{}"))
         seq = c.execute("UPDATE threads SET next_seq = next_seq + 1 WHERE id=? RETURNING next_seq - 1",
@@ -198,23 +238,37 @@ class LocalDBClient:
                    json.dumps(metadata or {}), _now()))
         return mid
 
-    async def add_message(self, thread_id: str, message: Message, metadata: dict | None = None) -> str:
-        def _do():
-            c = self._connect()
-            mid = self._insert(c, thread_id, message, metadata)
-            c.commit()
-            return mid
-        return await self._run(_do)
+    async def add_message(self, thread_id: str, message: Message, metadata: dict | None = None,
+                          wait: bool = True) -> str:
+        return (await self.add_messages(thread_id, [message], metadata, wait))[0]
 
-    async def add_messages(self, thread_id: str, messages: list[Message], metadata: dict | None = None) -> list[str]:
+    async def add_messages(self, thread_id: str, messages: list[Message], metadata: dict | None = None,
+                           wait: bool = True) -> list[str]:
+        """Append in order. ``wait=False``: queue the write behind the earlier ones and return at once (the cache
+        already shows the messages; ``sync()`` waits for the write)."""
+        ids = [str(uuid.uuid4()) for _ in messages]
+        msgs = list(messages)
+
         def _do():
             c = self._connect()
-            ids = [self._insert(c, thread_id, m, metadata) for m in messages]
+            for m, mid in zip(msgs, ids):
+                self._insert(c, thread_id, m, metadata, mid)
             c.commit()
             return ids
-        return await self._run(_do)
+        hit = self._cache.get(thread_id)
+        if hit is not None:
+            hit.extend(m.model_copy() for m in msgs)
+        self._known.add(thread_id)
+        fut = asyncio.get_running_loop().run_in_executor(self._exec, _do)
+        if wait:
+            return await fut
+        self._pending.add(fut)
+        fut.add_done_callback(lambda f: (self._pending.discard(f), f.exception()))
+        return ids
 
     async def delete_thread_messages(self, thread_id: str) -> int:
+        self._cache.pop(thread_id, None)
+
         def _do():
             c = self._connect()
             n = c.execute("DELETE FROM messages WHERE thread_id=?", (thread_id,)).rowcount

@@ -130,6 +130,10 @@ class AsyncEngine:
                 item = await q.get()
                 if isinstance(item, BaseException):
                     raise item
+                if not item.finished and not q.empty():
+                    item = _merge(item, q)  # the loop fell behind: hand on every landed token in one event
+                    if isinstance(item, BaseException):
+                        raise item
                 yield item
                 if item.finished:
                     finished = True
@@ -167,3 +171,20 @@ class AsyncEngine:
 def _put_all(items) -> None:
     for q, o in items:
         q.put_nowait(o)
+
+
+def _merge(first: StepOutput, q: asyncio.Queue):
+    """Fold the outputs already waiting in ``q`` into ``first`` (token ids concatenated, the last one's status): one
+    pass through the provider / agent / SSE layers per wakeup instead of one per token when the API loop is busy."""
+    ids = list(first.new_token_ids)
+    last = first
+    while not q.empty():
+        o = q.get_nowait()
+        if isinstance(o, BaseException):
+            return o
+        ids += o.new_token_ids
+        last = o
+        if o.finished:
+            break
+    return StepOutput(last.request_id, ids, last.finished, last.finish_reason, last.num_prompt_tokens,
+                      last.num_output_tokens, last.num_cached_tokens)

@@ -70,18 +70,29 @@ class KafkaAgent(ABC):
                         await db.create_thread(thread_id=tid)
                     history = await db.get_thread_messages(tid)
                 msgs = sanitize_messages_for_openai(history + list(new_messages))
+            behind = hasattr(db, "sync")  # a store with write-behind: saves leave the time-to-first-token path
             if save_to_thread and tid and db is not None:
                 new = [m for m in new_messages if m.role in ("user", "system")]
                 if new:
                     with trace.span("api_db_save", "api", f"thr:{tid}"):
-                        await db.add_messages(tid, new)
-            async for ev in self.run(msgs, model=model, temperature=temperature, max_tokens=max_tokens,
-                                     emit_messages=True, **kwargs):
-                if ev.get("type") == "_message":
-                    if save_to_thread and tid and db is not None:
-                        await db.add_message(tid, ev["message"])
-                    continue
-                yield ev
+                        if behind:
+                            await db.add_messages(tid, new, wait=False)
+                        else:
+                            await db.add_messages(tid, new)
+            try:
+                async for ev in self.run(msgs, model=model, temperature=temperature, max_tokens=max_tokens,
+                                         emit_messages=True, **kwargs):
+                    if ev.get("type") == "_message":
+                        if save_to_thread and tid and db is not None:
+                            if behind:
+                                await db.add_message(tid, ev["message"], wait=False)
+                            else:
+                                await db.add_message(tid, ev["message"])
+                        continue
+                    yield ev
+            finally:
+                if behind:
+                    await db.sync()  # every write of this request is in SQLite before the thread lock is released
 
     async def __aenter__(self) -> "KafkaAgent":
         await self.initialize()

@@ -113,3 +113,37 @@ def test_thread_config_join_playbooks_and_vm_key(db):
         assert (await db.get_thread_config("t1"))["vm_api_key"] == k1
         await db.close()
     asyncio.run(go())
+
+
+def test_local_db_cache_and_write_behind(tmp_path):
+    """The history cache answers reads without SQLite, write-behind saves keep their order (seq) and are durable
+    after sync(), and a fresh client on the same file sees exactly what the cached one served."""
+    import asyncio
+
+    from kafka_llm_service_amd.db.local import LocalDBClient
+    from kafka_llm_service_amd.llm.types import Message
+
+    async def main():
+        path = str(tmp_path / "t.db")
+        db = LocalDBClient(path)
+        await db.initialize()
+        await db.create_thread(thread_id="t1", system_message="sys")
+        assert [m.content for m in await db.get_thread_messages("t1")] == ["sys"]  # now cached
+        for i in range(20):
+            await db.add_messages("t1", [Message(role="user", content=f"u{i}")], wait=False)
+            await db.add_message("t1", Message(role="assistant", content=f"a{i}", token_ids=[i, i + 1]), wait=False)
+        got = await db.get_thread_messages("t1")
+        assert [m.content for m in got][:3] == ["sys", "u0", "a0"] and len(got) == 41
+        got[1].content = "edited by a caller"  # must not leak into the cache
+        assert (await db.get_thread_messages("t1"))[1].content == "u0"
+        await db.sync()
+        fresh = LocalDBClient(path)
+        await fresh.initialize()
+        back = await fresh.get_thread_messages("t1")
+        assert [m.content for m in back] == [m.content for m in await db.get_thread_messages("t1")]
+        assert back[2].token_ids == [0, 1]
+        assert await db.delete_thread_messages("t1") == 41 and await db.get_thread_messages("t1") == []
+        await db.close()
+        await fresh.close()
+
+    asyncio.run(main())
