@@ -95,13 +95,15 @@ def main():
     for S in (1, 2, 4):
         part = torch.empty(B, Hq, S, D, device=dev)
         lse = torch.empty(B, Hq, S, device=dev)
-        us = timeit(lambda: ops.attn_decode(q, k, v, bt, lens, ks, part, lse, S, 0, scale))
+        it = ops.uniform_decode_items(lens, ks, S, 0)  # built once: the engine plans items on the host
+        us = timeit(lambda: ops.attn_decode_items(q, k, v, bt, it, part, lse, scale))
         print(json.dumps({"case": "decode_suffix", "S": S, "us": round(us, 1),
                           "GB/s": round(B * Ls * kv_bytes_tok / us / 1e3, 1)}))
     for S in (4, 8, 16):
         part = torch.empty(B, Hq, S, D, device=dev)
         lse = torch.empty(B, Hq, S, device=dev)
-        us = timeit(lambda: ops.attn_decode(q, k, v, bt, lens, None, part, lse, S, 0, scale), iters=5)
+        it = ops.uniform_decode_items(lens, None, S, 0)
+        us = timeit(lambda: ops.attn_decode_items(q, k, v, bt, it, part, lse, scale), iters=5)
         print(json.dumps({"case": "decode_full", "S": S, "us": round(us, 1),
                           "GB/s_logical": round(B * (P + Ls) * kv_bytes_tok / us / 1e3, 1)}))
 
