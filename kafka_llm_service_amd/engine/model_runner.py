@@ -261,8 +261,8 @@ class ModelRunner:
         self.G = model.hq // model.hkv
         self.tile = ops.tile_rows(0) // self.G  # tokens per attention work item
         self.cascade_min_prefix = cascade_min_prefix
-        self.target_wgs = target_wgs
-        self.prefill_kv_chunk = prefill_kv_chunk
+        self.target_wgs = int(os.environ.get("KAFKA_CASCADE_WGS", target_wgs))
+        self.prefill_kv_chunk = int(os.environ.get("KAFKA_PREFILL_KV_CHUNK", prefill_kv_chunk))
         self.use_cascade = use_cascade
         self.vocab = model.cfg.vocab_size
         pin = self.device.type == "cuda"
