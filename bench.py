@@ -75,6 +75,8 @@ def parse(argv=None):
     ap.add_argument("--ttft-max-steps", type=int, default=4000)
     ap.add_argument("--no-cascade", action="store_true")
     ap.add_argument("--graphs", action="store_true")
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="paged KV cache precision (fp8 = e4m3 + per-token scales; an opt-in A/B, not the headline)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
@@ -188,7 +190,7 @@ def main(argv=None):
     from kafka_llm_service_amd.engine.sequence import SamplingParams
 
     cfg = EngineConfig(model=args.model, device=dev, seed=args.seed, max_num_seqs=max(256, 2 * args.threads),
-                       use_cascade=not args.no_cascade, use_graphs=args.graphs,
+                       use_cascade=not args.no_cascade, use_graphs=args.graphs, kv_dtype=args.kv_dtype,
                        max_model_len=131072 if args.prefix_tokens > 6000 else 8192, tp=tp, tp_rank=st.tp_rank)
     eng = LLMEngine(cfg)
     leaders = None
@@ -344,7 +346,7 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
                    "shared_prefix_tokens": args.prefix_tokens, "history_turns": args.history_turns,
                    "mixed_prefix": args.mixed_prefix, "max_out": [args.min_out, args.max_out],
                    "temperature": args.temperature, "cascade": not args.no_cascade, "graphs": args.graphs,
-                   "kv_dtype": "bf16"},
+                   "kv_dtype": args.kv_dtype},
         "ttft_p50_ms": round(p50, 2) if p50 else None, "ttft_p99_ms": round(p99, 2) if p99 else None,
         "ttft_samples": len(ttfts), "ttft_extra_steps": extra,
         "vs_baseline_basis": "derived 1-GPU bound 17k tok/s/GPU (BASELINE.md §3); reference publishes none",

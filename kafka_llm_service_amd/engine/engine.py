@@ -51,6 +51,9 @@ class EngineConfig:
     target_wgs: int = 256               # tile-kernel workgroups per pass (8-wave WGs, one per CU)
     prefill_kv_chunk: int = 1024        # key-range split for long-context prefill tiles
     use_graphs: bool = False
+    # paged KV cache: "bf16", or "fp8" = e4m3 with one power-of-two scale per (token, kv head) for K and for V
+    # (half the bytes per page: twice the pages, half the decode attention traffic; ops/csrc/rope_kv.hip)
+    kv_dtype: str = "bf16"
     # decode GEMMs: "stream" = weight-streaming MFMA kernel on wave-tiled weight copies (csrc/wstream_gemm.hip),
     # "blas" = hipBLASLt only; "auto" = stream on GPU (env KAFKA_DECODE_GEMM overrides)
     decode_gemm: str = "auto"           # auto | stream | stream_only (tiled weights only) | blas
@@ -130,7 +133,7 @@ class LLMEngine:
         self.load_s = time.perf_counter() - t0
         self.eos = set(cfg.eos_token_ids or mc.eos_token_ids)
         hkv, D, L = self.model.hkv, self.model.D, mc.num_layers
-        page_bytes = 2 * L * hkv * 16 * D * 2
+        page_bytes = L * ops.kv_page_bytes(hkv, D, cfg.kv_dtype)
         self.fi = faults.get()
         if self.fi.kv_blocks:
             nb = self.fi.kv_blocks
@@ -147,8 +150,9 @@ class LLMEngine:
         # zeroed once: attention tiles read whole 16-key pages and 32-key blocks, and a masked key still multiplies
         # its V row by p = 0 — finite leftovers of other sequences are harmless, NaN bit patterns in never-written
         # memory are not (0 * NaN = NaN; tests/test_engine_gpu.py poisons the allocator to keep this honest)
-        self.k_cache = torch.zeros(L, nb, hkv, 16, D, dtype=torch.bfloat16, device=self.device)
-        self.v_cache = torch.zeros(L, nb, hkv, D, 16, dtype=torch.bfloat16, device=self.device)
+        kshape, vshape, kv_dt = ops.kv_cache_shapes(nb, hkv, D, cfg.kv_dtype)
+        self.k_cache = torch.zeros(L, *kshape, dtype=kv_dt, device=self.device)
+        self.v_cache = torch.zeros(L, *vshape, dtype=kv_dt, device=self.device)
         self.kvm = KVManager(nb, 16, cfg.enable_prefix_cache)
         max_blocks = (cfg.max_model_len + 15) // 16
         self.sched = Scheduler(SchedulerConfig(max_num_seqs=cfg.max_num_seqs,
@@ -172,7 +176,7 @@ class LLMEngine:
         self._inflight: _InFlight | None = None  # the step on the GPU that has not been collected yet
         self._n_added = 0
         self.stop_checker_factory = None  # set by the frontend: (request params) -> incremental stop-string checker
-        log.info("engine ready: %s tp=%d kv pages=%d (%.1f GB) load %.1fs", mc.name, cfg.tp, nb,
+        log.info("engine ready: %s tp=%d kv pages=%d (%s, %.1f GB) load %.1fs", mc.name, cfg.tp, nb, cfg.kv_dtype,
                  nb * page_bytes / 1e9, self.load_s)
 
     # ------------------------------------------------------------------------------------------------------------

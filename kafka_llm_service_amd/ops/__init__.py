@@ -17,6 +17,9 @@ from . import reference as ref
 from ._ext import ext
 
 PAGE = ref.PAGE
+kv_cache_shapes = ref.kv_cache_shapes
+kv_page_bytes = ref.kv_page_bytes
+is_fp8_cache = ref.is_fp8_cache
 
 
 def _gpu(t: torch.Tensor) -> bool:

@@ -24,6 +24,15 @@
 //   attn_merge_kernel    log-sum-exp merge of S partials per (row, head) -> bf16.
 //   (attn_prefill_kernel variants: 0 = 8 waves / 256 rows per item, K/V staged once per workgroup in LDS;
 //    1 = 4 waves / 128 rows, LDS; 2 = 4 waves / 128 rows, per-wave register loads. ops.tile_rows(variant).)
+//
+// fp8 KV cache (FP8 template flag; page layout in rope_kv.hip): e4m3 pages with one power-of-two exponent per
+// (token, kv head) for K and for V. Register path (decode, variant 2): a lane's 16-B K load is the A-fragments of
+// two k-steps of ONE key, so the key's exponent is the scale operand of v_cvt_scalef32_pk_bf16_fp8 (dequant is one
+// VALU op per 2 elements); V^T fragments dequantize unscaled and the per-key V exponent goes into P instead
+// (v_ldexp on the 16 probabilities of the lane after the row sum — P . diag(2^e) . V). LDS path (tile kernel):
+// the staging threads dequantize K (scaled) and V (unscaled) into the same bf16 LDS tiles, and the two pages' V
+// exponents ride along in 32 B at the end of the stage. MFMA stays bf16: QK^T with an fp8 Q would add a second
+// quantization error for no gain in a kernel that is bound by bytes (decode) or by staging (tile).
 #include "common.h"
 
 #include <cstdlib>
@@ -55,6 +64,23 @@ __device__ __forceinline__ float xor32_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int KPAGE8 = PAGE * 128 + 32;  // fp8 K page bytes per (block, kv head): data + K/V exponents
+constexpr int VPAGE8 = PAGE * 128;
+constexpr int KEXP8 = PAGE * 128, VEXP8 = PAGE * 128 + 16;
+
+__device__ __forceinline__ float exp2i(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
+
+// 8 e4m3 bytes (two dwords) -> bf16x8 times `sc` (a power of two)
+__device__ __forceinline__ bf16x8 dq8(uint32_t lo, uint32_t hi, float sc) {
+  const bf16x2 a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, sc, false);
+  const bf16x2 b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, sc, true);
+  const bf16x2 c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, sc, false);
+  const bf16x2 d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, sc, true);
+  return bf16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
 template <int D>
 struct WaveAcc {
   f32x16 o[D / 32];
@@ -70,6 +96,37 @@ struct KVFrag {
   bf16x8 k[D / 16];
   bf16x8 v[2][D / 32];
 };
+
+// fp8: 16-B unit j of the lane's key = A-fragments of k-steps 2j, 2j + 1; V^T rows as 8-B loads; the lane's key
+// exponent (K) and its 8 keys' exponents per page (V)
+template <int D>
+struct KVFrag8 {
+  u32x4 k[D / 32];
+  u32x2 v[2][D / 32];
+  int kexp;
+  u32x2 vexp[2];
+};
+
+template <int D>
+__device__ __forceinline__ void load_kv8(KVFrag8<D>& f, const uint8_t* __restrict__ k_cache,
+                                         const uint8_t* __restrict__ v_cache, int Hkv, int kvh, int page0,
+                                         int page1, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  const int kp = (r >> 4) ? page1 : page0;
+  const uint8_t* kb = k_cache + ((int64_t)kp * Hkv + kvh) * KPAGE8;
+#pragma unroll
+  for (int j = 0; j < D / 32; ++j)
+    f.k[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(kb + ((2 * j + h) * PAGE + (r & 15)) * 16));
+  f.kexp = (int)*reinterpret_cast<const int8_t*>(kb + KEXP8 + (r & 15));
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int vp = s2 ? page1 : page0;
+    const uint8_t* vb = v_cache + ((int64_t)vp * Hkv + kvh) * VPAGE8 + r * PAGE + 8 * h;
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t) f.v[s2][t] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(vb + 32 * t * PAGE));
+    f.vexp[s2] = *reinterpret_cast<const u32x2*>(k_cache + ((int64_t)vp * Hkv + kvh) * KPAGE8 + VEXP8 + 8 * h);
+  }
+}
 
 template <int D>
 __device__ __forceinline__ void load_kv(KVFrag<D>& f, const bf16* __restrict__ k_cache,
@@ -102,10 +159,11 @@ __device__ __forceinline__ void block_pages(const int* __restrict__ bt, int key0
 //     blocks of a row it almost never fires;
 //   * the softmax scale is folded into one FMA in front of exp2.
 // acc.m is kept in the scaled log2 domain.
-template <int D>
+// VS (fp8 cache): P column scaled by the per-key V exponents vexp (lane half h: keys of page s2 in register order)
+template <int D, bool VS = false>
 __device__ __forceinline__ void softmax_pv(f32x16& s, bool masked, int key0, int lo, int hi, int limit,
                                            float scale_log2, const bf16x8 (&vf)[2][D / 32], WaveAcc<D>& acc,
-                                           int lane) {
+                                           int lane, u32x2 ve0 = {0u, 0u}, u32x2 ve1 = {0u, 0u}) {
   const int h = lane >> 5;
   if (masked) {
 #pragma unroll
@@ -136,6 +194,14 @@ __device__ __forceinline__ void softmax_pv(f32x16& s, bool masked, int key0, int
   }
   psum = xor32_sum(psum);
   acc.l += psum;
+  if constexpr (VS) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t w0 = j < 4 ? ve0[0] : ve0[1], w1 = j < 4 ? ve1[0] : ve1[1];
+      s[j] = ldexpf(s[j], __builtin_amdgcn_sbfe(w0, 8 * (j & 3), 8));
+      s[8 + j] = ldexpf(s[8 + j], __builtin_amdgcn_sbfe(w1, 8 * (j & 3), 8));
+    }
+  }
   bf16x8 pf[2];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -159,28 +225,58 @@ __device__ __forceinline__ void attn_compute(const KVFrag<D>& f, int key0, int l
   softmax_pv<D>(s, masked, key0, lo, hi, limit, scale_log2, f.v, acc, lane);
 }
 
+template <int D>
+__device__ __forceinline__ void attn_compute8(const KVFrag8<D>& f, int key0, int lo, int hi, int limit,
+                                              const bf16x8 (&qf)[D / 16], float scale_log2, WaveAcc<D>& acc,
+                                              int lane, bool masked) {
+  const float ks = exp2i(f.kexp);
+  f32x16 s = {};
+#pragma unroll
+  for (int j = 0; j < D / 32; ++j) {
+    s = mfma32(dq8(f.k[j][0], f.k[j][1], ks), qf[2 * j], s);
+    s = mfma32(dq8(f.k[j][2], f.k[j][3], ks), qf[2 * j + 1], s);
+  }
+  bf16x8 vf[2][D / 32];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t) vf[s2][t] = dq8(f.v[s2][t][0], f.v[s2][t][1], 1.f);
+  softmax_pv<D, true>(s, masked, key0, lo, hi, limit, scale_log2, vf, acc, lane, f.vexp[0], f.vexp[1]);
+}
+
 // Key blocks first, first+stride, ... < nblk (block b covers keys [base + 32 b, base + 32 b + 32)), software
 // pipelined one block deep. The prefetch of the block after the last one is clamped to the last block (pad, don't
 // branch: no divergent load, no extra waitcnt).
-template <int D>
-__device__ __forceinline__ void attn_blocks(const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+template <int D, bool FP8>
+__device__ __forceinline__ void attn_blocks(const void* __restrict__ k_cache, const void* __restrict__ v_cache,
                                             int Hkv, int kvh, const int* __restrict__ bt, int base, int first,
                                             int nblk, int stride, int end, int lo, int hi, int limit,
                                             const bf16x8 (&qf)[D / 16], float scale_log2, WaveAcc<D>& acc,
                                             int lane) {
   if (first >= nblk) return;
+  using Frag = std::conditional_t<FP8, KVFrag8<D>, KVFrag<D>>;
+  auto load = [&](Frag& f, int p0, int p1) {
+    if constexpr (FP8)
+      load_kv8<D>(f, static_cast<const uint8_t*>(k_cache), static_cast<const uint8_t*>(v_cache), Hkv, kvh, p0, p1,
+                  lane);
+    else
+      load_kv<D>(f, static_cast<const bf16*>(k_cache), static_cast<const bf16*>(v_cache), Hkv, kvh, p0, p1, lane);
+  };
   int p0, p1;
-  KVFrag<D> cur;
+  Frag cur;
   block_pages(bt, base + 32 * first, end, p0, p1);
-  load_kv<D>(cur, k_cache, v_cache, Hkv, kvh, p0, p1, lane);
+  load(cur, p0, p1);
   for (int b = first; b < nblk; b += stride) {
     const int nb = (b + stride < nblk) ? b + stride : b;
-    KVFrag<D> nxt;
+    Frag nxt;
     block_pages(bt, base + 32 * nb, end, p0, p1);
-    load_kv<D>(nxt, k_cache, v_cache, Hkv, kvh, p0, p1, lane);
+    load(nxt, p0, p1);
     const int key0 = base + 32 * b;
-    attn_compute<D>(cur, key0, lo, hi, limit, qf, scale_log2, acc, lane,
-                    (key0 < lo) | (key0 + 32 > hi) | (key0 + 31 > limit));
+    const bool masked = (key0 < lo) | (key0 + 32 > hi) | (key0 + 31 > limit);
+    if constexpr (FP8)
+      attn_compute8<D>(cur, key0, lo, hi, limit, qf, scale_log2, acc, lane, masked);
+    else
+      attn_compute<D>(cur, key0, lo, hi, limit, qf, scale_log2, acc, lane, masked);
     cur = nxt;
   }
 }
@@ -218,10 +314,10 @@ struct DecodeItem {
   int b, lo, hi, split, nsplit, npre, pad0, pad1;
 };
 
-template <int D, bool HEADS_FAST>
+template <int D, bool HEADS_FAST, bool FP8>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
-                                                           const bf16* __restrict__ k_cache,
-                                                           const bf16* __restrict__ v_cache, int Hkv, int G,
+                                                           const void* __restrict__ k_cache,
+                                                           const void* __restrict__ v_cache, int Hkv, int G,
                                                            const int* __restrict__ block_tables, int bt_stride,
                                                            const DecodeItem* __restrict__ items, int B,
                                                            float* __restrict__ out_part, float* __restrict__ lse_part,
@@ -252,8 +348,8 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
   if (w < nb) {
     bf16x8 qf[D / 16];
     load_q_frags<D>(qf, q + (int64_t)b * q_stride + (int64_t)(kvh * G + r) * D, r < G, h);
-    attn_blocks<D>(k_cache, v_cache, Hkv, kvh, bt, a0, w, nb, 4, hi, lo, hi, 0x7fffffff, qf, scale_log2, acc,
-                   lane);
+    attn_blocks<D, FP8>(k_cache, v_cache, Hkv, kvh, bt, a0, w, nb, 4, hi, lo, hi, 0x7fffffff, qf, scale_log2, acc,
+                        lane);
   }
   // cross-wave combine
   if (r < G) {
@@ -490,6 +586,64 @@ __device__ __forceinline__ void wait_vmcnt_dyn(int n) {
   wait_vmcnt<0>();
 }
 
+// fp8 staging: 512 16-B chunks per 32-key block — K units [0, 256) (page qd >> 7, unit qd & 127 = plane p, key o)
+// and V^T rows [256, 512) (page (qd - 256) >> 7, d = qd & 127) — plus one aux load each (the dword holding the K
+// unit's key exponent; the page's 16 V exponents), so every thread issues the same 2 * 512 / NT loads as bf16.
+template <int NT>
+struct StageRegs8 {
+  u32x4 c[512 / NT];
+  u32x4 aux[512 / NT];
+};
+
+__device__ __forceinline__ uint32_t asm_load4(const uint8_t* p) {
+  uint32_t r;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+
+template <int NT>
+__device__ __forceinline__ void stage_load8(StageRegs8<NT>& sr, const uint8_t* __restrict__ k_cache,
+                                            const uint8_t* __restrict__ v_cache, int Hkv, int kvh, int p0, int p1,
+                                            int tid) {
+#pragma unroll
+  for (int i = 0; i < 512 / NT; ++i) {
+    const int qd = tid + NT * i;
+    if (qd < 256) {  // wave-uniform (NT = 512: waves 0-3; NT = 256: i == 0)
+      const uint8_t* kb = k_cache + ((int64_t)((qd >> 7) ? p1 : p0) * Hkv + kvh) * KPAGE8;
+      sr.c[i] = __builtin_bit_cast(u32x4, asm_load16(reinterpret_cast<const bf16*>(kb + (qd & 127) * 16)));
+      sr.aux[i][0] = asm_load4(kb + KEXP8 + (qd & 12));
+    } else {
+      const int vq = qd - 256, page = (vq >> 7) ? p1 : p0;
+      sr.c[i] = __builtin_bit_cast(
+          u32x4, asm_load16(reinterpret_cast<const bf16*>(v_cache + ((int64_t)page * Hkv + kvh) * VPAGE8 + (vq & 127) * 16)));
+      sr.aux[i] = __builtin_bit_cast(
+          u32x4, asm_load16(reinterpret_cast<const bf16*>(k_cache + ((int64_t)page * Hkv + kvh) * KPAGE8 + VEXP8)));
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void stage_store8(const StageRegs8<NT>& sr, char* lds, int tid) {
+#pragma unroll
+  for (int i = 0; i < 512 / NT; ++i) {
+    const int qd = tid + NT * i;
+    const u32x4 w = sr.c[i];
+    if (qd < 256) {
+      const int pc = qd & 127, p = pc >> 4, o = pc & 15, key = ((qd >> 7) << 4) | o;
+      const float sc = exp2i(__builtin_amdgcn_sbfe(sr.aux[i][0], 8 * (o & 3), 8));
+      const int c1 = 4 * (p >> 1) + (p & 1);  // d chunk (8 elements) of the unit's first half; second = c1 + 2
+      *reinterpret_cast<bf16x8*>(lds + key * 256 + 16 * (c1 ^ (key & 15))) = dq8(w[0], w[1], sc);
+      *reinterpret_cast<bf16x8*>(lds + key * 256 + 16 * ((c1 + 2) ^ (key & 15))) = dq8(w[2], w[3], sc);
+    } else {
+      const int vq = qd - 256, pg = vq >> 7, d = vq & 127;
+      char* row = lds + KT_BYTES + pg * 4096 + d * 32;
+      *reinterpret_cast<bf16x8*>(row + 16 * (0 ^ ((d >> 3) & 1))) = dq8(w[0], w[1], 1.f);
+      *reinterpret_cast<bf16x8*>(row + 16 * (1 ^ ((d >> 3) & 1))) = dq8(w[2], w[3], 1.f);
+      if (d == 0) *reinterpret_cast<u32x4*>(lds + KT_BYTES + VT_BYTES + pg * 16) = sr.aux[i];
+    }
+  }
+}
+
 template <int NT>
 __device__ __forceinline__ void stage_store(const StageRegs<NT>& sr, char* lds, int tid) {
 #pragma unroll
@@ -506,7 +660,7 @@ __device__ __forceinline__ void stage_store(const StageRegs<NT>& sr, char* lds, 
 // One 32-key step reading K/V fragments from an LDS stage. All 8 K-fragment reads are issued before the first
 // QK^T MFMA and all 8 V-fragment reads right behind the QK^T MFMAs (sched_barrier pins the order; left alone hipcc
 // issues one ds_read at a time, each waited with lgkmcnt(0) before its MFMA).
-template <int D>
+template <int D, bool FP8>
 __device__ __forceinline__ void attn_compute_lds(const char* lds, int key0, int lo, int hi, int limit,
                                                  const bf16x8 (&qf)[D / 16], float scale_log2, WaveAcc<D>& acc,
                                                  int lane, bool masked) {
@@ -528,14 +682,20 @@ __device__ __forceinline__ void attn_compute_lds(const char* lds, int key0, int 
       vf[s2][t] = *reinterpret_cast<const bf16x8*>(lds + KT_BYTES + s2 * 4096 + d * 32 + 16 * (h ^ ((d >> 3) & 1)));
     }
   __builtin_amdgcn_sched_barrier(0);
-  softmax_pv<D>(s, masked, key0, lo, hi, limit, scale_log2, vf, acc, lane);
+  if constexpr (FP8) {
+    const char* ve = lds + KT_BYTES + VT_BYTES + 8 * h;
+    softmax_pv<D, true>(s, masked, key0, lo, hi, limit, scale_log2, vf, acc, lane,
+                        *reinterpret_cast<const u32x2*>(ve), *reinterpret_cast<const u32x2*>(ve + 16));
+  } else {
+    softmax_pv<D>(s, masked, key0, lo, hi, limit, scale_log2, vf, acc, lane);
+  }
 }
 
-template <int D, int NW, bool LDS>
+template <int D, int NW, bool LDS, bool FP8>
 __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkItem* __restrict__ items,
                                                             const bf16* __restrict__ q, int64_t q_stride,
-                                                            const bf16* __restrict__ k_cache,
-                                                            const bf16* __restrict__ v_cache, int Hkv, int G,
+                                                            const void* __restrict__ k_cache,
+                                                            const void* __restrict__ v_cache, int Hkv, int G,
                                                             const int* __restrict__ block_tables, int bt_stride,
                                                             const int* __restrict__ q_limit, bf16* __restrict__ out,
                                                             int64_t out_stride, float* __restrict__ out_part,
@@ -554,7 +714,8 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkIte
   const int* bt = block_tables + (int64_t)it.bt_row * bt_stride;
   // LDS variant: the Q fragments and the page ids of the item's key range are requested here, together with
   // q_limit, so the prologue pays one memory round trip for all three instead of one each
-  __shared__ __attribute__((aligned(16))) char lds[LDS ? 2 * STAGE_BYTES : 16];
+  constexpr int SB = FP8 ? STAGE_BYTES + 32 : STAGE_BYTES;  // fp8: + the two pages' V exponents
+  __shared__ __attribute__((aligned(16))) char lds[LDS ? 2 * SB : 16];
   __shared__ int s_hi[NW];
   __shared__ int s_pages[LDS ? MAX_STAGED_PAGES : 1];
   bf16x8 qf[D / 16];
@@ -582,8 +743,8 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkIte
     if (hi > lo) {
       load_q_frags<D>(qf, q + (int64_t)token * q_stride + (int64_t)(kvh * G + g) * D, valid, h);
       const int base = lo & ~31;
-      attn_blocks<D>(k_cache, v_cache, Hkv, kvh, bt, base, 0, (hi - base + 31) >> 5, 1, hi, lo, hi, limit, qf,
-                     scale_log2, acc, lane);
+      attn_blocks<D, FP8>(k_cache, v_cache, Hkv, kvh, bt, base, 0, (hi - base + 31) >> 5, 1, hi, lo, hi, limit,
+                          qf, scale_log2, acc, lane);
     }
   } else {
     if (lane == 0) s_hi[w] = hi;
@@ -615,17 +776,32 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkIte
       // computed, and written to LDS (double buffer) right before it is needed. (PF = 4 measured the same as 2 on
       // the cascade pass, profiles/README.md: the kernel is not waiting on HBM latency.)
       constexpr int PF = ATTN_PREFETCH;
-      StageRegs<NW * 64> rs[PF];
+      using Regs = std::conditional_t<FP8, StageRegs8<NW * 64>, StageRegs<NW * 64>>;
+      auto sload = [&](Regs& r2, int a, int b2) {
+        if constexpr (FP8)
+          stage_load8<NW * 64>(r2, static_cast<const uint8_t*>(k_cache), static_cast<const uint8_t*>(v_cache), Hkv,
+                               kvh, a, b2, tid);
+        else
+          stage_load<NW * 64>(r2, static_cast<const bf16*>(k_cache), static_cast<const bf16*>(v_cache), Hkv, kvh, a,
+                              b2, tid);
+      };
+      auto sstore = [&](const Regs& r2, char* dst) {
+        if constexpr (FP8)
+          stage_store8<NW * 64>(r2, dst, tid);
+        else
+          stage_store<NW * 64>(r2, dst, tid);
+      };
+      Regs rs[PF];
       int p0, p1;
       pages_of(base, p0, p1);
-      stage_load<NW * 64>(rs[0], k_cache, v_cache, Hkv, kvh, p0, p1, tid);
+      sload(rs[0], p0, p1);
       wait_vmcnt<0>();
-      stage_store<NW * 64>(rs[0], lds, tid);
+      sstore(rs[0], lds);
 #pragma unroll
       for (int j = 1; j <= PF; ++j) {
         if (j < nblk) {
           pages_of(base + 32 * j, p0, p1);
-          stage_load<NW * 64>(rs[j % PF], k_cache, v_cache, Hkv, kvh, p0, p1, tid);
+          sload(rs[j % PF], p0, p1);
         }
       }
       __syncthreads();
@@ -635,16 +811,16 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkIte
         const int key0 = base + 32 * b;
         if (key0 < hi) {  // wave-uniform: skip blocks past this wave's causal limit
           const bool masked = (key0 < lo) | (key0 + 32 > hi) | (key0 + 31 > wmin);
-          attn_compute_lds<D>(lds + (b & 1) * STAGE_BYTES, key0, lo, hi, limit, qf, scale_log2, acc, lane, masked);
+          attn_compute_lds<D, FP8>(lds + (b & 1) * SB, key0, lo, hi, limit, qf, scale_log2, acc, lane, masked);
         }
         if (b + 1 < nblk) {
           // stage (J+1) % PF holds block b+1; blocks b+2 .. min(b+PF, nblk-1) may still be in flight behind it
           const int younger = min(PF - 1, nblk - 2 - b);
           wait_vmcnt_dyn<LOADS, PF - 1>(younger);
-          stage_store<NW * 64>(rs[(J + 1) % PF], lds + ((b + 1) & 1) * STAGE_BYTES, tid);
+          sstore(rs[(J + 1) % PF], lds + ((b + 1) & 1) * SB);
           if (b + 1 + PF < nblk) {
             pages_of(key0 + 32 * (1 + PF), p0, p1);
-            stage_load<NW * 64>(rs[(J + 1) % PF], k_cache, v_cache, Hkv, kvh, p0, p1, tid);
+            sload(rs[(J + 1) % PF], p0, p1);
           }
         }
         __syncthreads();
@@ -740,10 +916,11 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(const float* __restrict
 // items: int32 [n_items, 8] DecodeItem records (host-checked: npre + nsplit <= S_total, and <= 64 with `out` — the
 // fused merge gives one wave lane per partial; items with nsplit > 1 merge through the ticket counters
 // ([B * Hkv] int32, zero, re-armed by the kernel)).
-extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const bf16* k_cache, const bf16* v_cache,
-                              int n_items, int B, int Hkv, int G, int D, const int* block_tables, int bt_stride,
-                              const int* items, float* out_part, float* lse_part, int S_total, float scale,
-                              bf16* out, int64_t out_stride, int* tickets, hipStream_t st) {
+extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const void* k_cache,
+                                              const void* v_cache, int fp8, int n_items, int B, int Hkv, int G, int D,
+                                              const int* block_tables, int bt_stride, const int* items,
+                                              float* out_part, float* lse_part, int S_total, float scale, bf16* out,
+                                              int64_t out_stride, int* tickets, hipStream_t st) {
   if (n_items == 0) return hipSuccess;
   if (D != 128 || G > 8 || G < 1) return hipErrorInvalidValue;
   if (out != nullptr && tickets == nullptr) return hipErrorInvalidValue;
@@ -753,37 +930,52 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
     return e == nullptr || e[0] != '0';
   }();
   const auto* di = reinterpret_cast<const DecodeItem*>(items);
-  if (heads_fast)
-    attn_decode_kernel<128, true><<<dim3(Hkv, n_items), 256, 0, st>>>(
-        q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, di, B, out_part, lse_part, S_total,
-        scale_log2, out, out_stride, tickets);
+  auto go = [&](auto kern, dim3 grid) {
+    kern<<<grid, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, di, B, out_part,
+                               lse_part, S_total, scale_log2, out, out_stride, tickets);
+  };
+  const dim3 hf(Hkv, n_items), sf(n_items, Hkv);
+  if (fp8)
+    heads_fast ? go(attn_decode_kernel<128, true, true>, hf) : go(attn_decode_kernel<128, false, true>, sf);
   else
-    attn_decode_kernel<128, false><<<dim3(n_items, Hkv), 256, 0, st>>>(
-        q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, di, B, out_part, lse_part, S_total,
-        scale_log2, out, out_stride, tickets);
+    heads_fast ? go(attn_decode_kernel<128, true, false>, hf) : go(attn_decode_kernel<128, false, false>, sf);
   return hipGetLastError();
 }
 
-extern "C" hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride, const bf16* k_cache,
-                               const bf16* v_cache, int Hkv, int G, int D, const int* block_tables, int bt_stride,
-                               const int* q_limit, bf16* out, int64_t out_stride, float* out_part, float* lse_part,
-                               int S_total, float scale, int variant, hipStream_t st) {
+template <bool FP8>
+static void launch_prefill(const AttnWorkItem* it, int n_items, const bf16* q, int64_t q_stride,
+                           const void* k_cache, const void* v_cache, int Hkv, int G, const int* block_tables,
+                           int bt_stride, const int* q_limit, bf16* out, int64_t out_stride, float* out_part,
+                           float* lse_part, int S_total, float scale_log2, int variant, hipStream_t st) {
+  if (variant == 0)  // 8 waves, 256 query rows per item, K/V staged in LDS
+    attn_prefill_kernel<128, 8, true, FP8><<<dim3(n_items, Hkv), 512, 0, st>>>(
+        it, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
+        lse_part, S_total, scale_log2);
+  else if (variant == 1)  // 4 waves, 128 rows, LDS
+    attn_prefill_kernel<128, 4, true, FP8><<<dim3(n_items, Hkv), 256, 0, st>>>(
+        it, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
+        lse_part, S_total, scale_log2);
+  else  // 4 waves, 128 rows, per-wave register loads
+    attn_prefill_kernel<128, 4, false, FP8><<<dim3(n_items, Hkv), 256, 0, st>>>(
+        it, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
+        lse_part, S_total, scale_log2);
+}
+
+extern "C" hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride,
+                                               const void* k_cache, const void* v_cache, int fp8, int Hkv, int G,
+                                               int D, const int* block_tables, int bt_stride, const int* q_limit,
+                                               bf16* out, int64_t out_stride, float* out_part, float* lse_part,
+                                               int S_total, float scale, int variant, hipStream_t st) {
   if (n_items == 0) return hipSuccess;
   if (D != 128 || G < 1 || G > 32 || (128 % G) != 0) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
   const auto* it = reinterpret_cast<const AttnWorkItem*>(items);
-  if (variant == 0)  // 8 waves, 256 query rows per item, K/V staged in LDS
-    attn_prefill_kernel<128, 8, true><<<dim3(n_items, Hkv), 512, 0, st>>>(
-        it, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
-        lse_part, S_total, scale_log2);
-  else if (variant == 1)  // 4 waves, 128 rows, LDS
-    attn_prefill_kernel<128, 4, true><<<dim3(n_items, Hkv), 256, 0, st>>>(
-        it, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
-        lse_part, S_total, scale_log2);
-  else  // 4 waves, 128 rows, per-wave register loads
-    attn_prefill_kernel<128, 4, false><<<dim3(n_items, Hkv), 256, 0, st>>>(
-        it, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
-        lse_part, S_total, scale_log2);
+  if (fp8)
+    launch_prefill<true>(it, n_items, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out,
+                         out_stride, out_part, lse_part, S_total, scale_log2, variant, st);
+  else
+    launch_prefill<false>(it, n_items, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out,
+                          out_stride, out_part, lse_part, S_total, scale_log2, variant, st);
   return hipGetLastError();
 }
 

@@ -20,14 +20,19 @@ hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int S, int64_t
                                 const int64_t* positions, const float* cos_sin, bf16* q_out, int64_t q_stride,
                                 bf16* k_cache, bf16* v_cache, const int64_t* slot_mapping, int T, int Hq, int Hkv,
                                 int D, int block_size, hipStream_t st);
-hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const bf16* k_cache, const bf16* v_cache,
-                              int n_items, int B, int Hkv, int G, int D, const int* block_tables, int bt_stride,
-                              const int* items, float* out_part, float* lse_part, int S_total, float scale,
-                              bf16* out, int64_t out_stride, int* tickets, hipStream_t st);
-hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride, const bf16* k_cache,
-                               const bf16* v_cache, int Hkv, int G, int D, const int* block_tables, int bt_stride,
-                               const int* q_limit, bf16* out, int64_t out_stride, float* out_part, float* lse_part,
-                               int S_total, float scale, int variant, hipStream_t st);
+hipError_t kafka_launch_rope_kv_fp8(const bf16* qkv, const float* qp, int S, int64_t ps, int64_t qkv_stride,
+                                    const int64_t* positions, const float* cos_sin, bf16* q_out, int64_t q_stride,
+                                    uint8_t* k_cache, uint8_t* v_cache, const int64_t* slot_mapping, int T, int Hq,
+                                    int Hkv, int D, hipStream_t st);
+hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const void* k_cache, const void* v_cache, int fp8,
+                                    int n_items, int B, int Hkv, int G, int D, const int* block_tables, int bt_stride,
+                                    const int* items, float* out_part, float* lse_part, int S_total, float scale,
+                                    bf16* out, int64_t out_stride, int* tickets, hipStream_t st);
+hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride,
+                                     const void* k_cache, const void* v_cache, int fp8, int Hkv, int G, int D,
+                                     const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
+                                     int64_t out_stride, float* out_part, float* lse_part, int S_total, float scale,
+                                     int variant, hipStream_t st);
 hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows, int Hq, int S, int D, bf16* out,
                              int64_t out_stride, float* lse_out, hipStream_t st);
 hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
@@ -132,6 +137,28 @@ static void silu_mul(at::Tensor out, at::Tensor x) {
     CHECK_HIP(kafka_launch_silu_mul(bptr(out), bptr(x), x.stride(0), T, F, cur_stream()));
 }
 
+// Paged KV caches: bf16 K[blocks, Hkv, 16, 128] / V[blocks, Hkv, 128, 16], or fp8 (e4m3 + per-token exponents,
+// rope_kv.hip) as uint8 K[blocks, Hkv, 16 * 128 + 32] / V[blocks, Hkv, 128 * 16].
+static bool is_fp8_cache(const at::Tensor& k) { return k.scalar_type() == at::kByte; }
+
+static void check_cache_pair(const at::Tensor& k_cache, const at::Tensor& v_cache) {
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous(), "caches must be contiguous");
+  TORCH_CHECK(k_cache.is_cuda() && v_cache.is_cuda(), "caches must be GPU tensors");
+  if (is_fp8_cache(k_cache)) {
+    CHECK_DT(v_cache, at::kByte);
+    TORCH_CHECK(k_cache.dim() == 3 && v_cache.dim() == 3 && k_cache.size(2) == 16 * 128 + 32 &&
+                    v_cache.size(2) == 128 * 16 && k_cache.size(0) == v_cache.size(0) &&
+                    k_cache.size(1) == v_cache.size(1),
+                "fp8 paged caches must be uint8 K[blocks,Hkv,2080] / V[blocks,Hkv,2048]");
+    return;
+  }
+  CHECK_DT(k_cache, at::kBFloat16); CHECK_DT(v_cache, at::kBFloat16);
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4 && k_cache.size(2) == 16 && k_cache.size(3) == 128 &&
+                  v_cache.size(2) == 128 && v_cache.size(3) == 16 && k_cache.size(0) == v_cache.size(0) &&
+                  k_cache.size(1) == v_cache.size(1),
+              "paged caches must be K[blocks,Hkv,16,128] / V[blocks,Hkv,128,16]");
+}
+
 static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin, at::Tensor q_out,
                           at::Tensor k_cache, at::Tensor v_cache, c10::optional<at::Tensor> slot_mapping, int64_t Hq,
                           int64_t Hkv) {
@@ -139,16 +166,24 @@ static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_s
   const bool slab = is_slab(qkv);
   if (slab) check_slab(qkv); else CHECK_DT(qkv, at::kBFloat16);
   CHECK_DT(positions, at::kLong); CHECK_DT(cos_sin, at::kFloat);
-  CHECK_DT(k_cache, at::kBFloat16); CHECK_DT(v_cache, at::kBFloat16);
   TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && cos_sin.is_contiguous() &&
                   positions.is_contiguous(), "rope_kv_write: caches/positions/cos_sin must be contiguous");
-  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4, "k/v cache must be [blocks, Hkv, ., .]");
-  const int D = k_cache.size(3);
-  const int bs = k_cache.size(2);
-  TORCH_CHECK(k_cache.size(1) == Hkv && v_cache.size(1) == Hkv && v_cache.size(2) == D && v_cache.size(3) == bs &&
-                  v_cache.size(0) == k_cache.size(0), "rope_kv_write: cache shape mismatch");
-  TORCH_CHECK(bs == 16, "page size must be 16");
-  TORCH_CHECK(D == 128 || D == 64, "head dim must be 64 or 128");
+  const bool fp8 = is_fp8_cache(k_cache);
+  int D, bs = 16;
+  if (fp8) {
+    check_cache_pair(k_cache, v_cache);
+    D = 128;
+    TORCH_CHECK(k_cache.size(1) == Hkv, "rope_kv_write: cache shape mismatch");
+  } else {
+    CHECK_DT(k_cache, at::kBFloat16); CHECK_DT(v_cache, at::kBFloat16);
+    TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4, "k/v cache must be [blocks, Hkv, ., .]");
+    D = k_cache.size(3);
+    bs = k_cache.size(2);
+    TORCH_CHECK(k_cache.size(1) == Hkv && v_cache.size(1) == Hkv && v_cache.size(2) == D && v_cache.size(3) == bs &&
+                    v_cache.size(0) == k_cache.size(0), "rope_kv_write: cache shape mismatch");
+    TORCH_CHECK(bs == 16, "page size must be 16");
+    TORCH_CHECK(D == 128 || D == 64, "head dim must be 64 or 128");
+  }
   const int T = qkv.size(slab ? 1 : 0);
   const int64_t W = (Hq + 2 * Hkv) * D;
   TORCH_CHECK(slab ? qkv.size(2) == W : (qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) == W), "qkv shape");
@@ -161,20 +196,18 @@ static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_s
     TORCH_CHECK(slot_mapping->numel() == T && slot_mapping->is_contiguous(), "slot_mapping shape");
     sm = slot_mapping->data_ptr<int64_t>();
   }
-  CHECK_HIP(kafka_launch_rope_kv(slab ? nullptr : bptr(qkv), slab ? qkv.data_ptr<float>() : nullptr,
-                                  slab ? qkv.size(0) : 0, slab ? (int64_t)T * W : 0, slab ? W : qkv.stride(0),
-                                  positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), bptr(q_out),
-                                  q_out.stride(0), bptr(k_cache), bptr(v_cache), sm, T, Hq, Hkv, D, bs,
-                                  cur_stream()));
-}
-
-static void check_cache_pair(const at::Tensor& k_cache, const at::Tensor& v_cache) {
-  CHECK_DT(k_cache, at::kBFloat16); CHECK_DT(v_cache, at::kBFloat16);
-  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous(), "caches must be contiguous");
-  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4 && k_cache.size(2) == 16 && k_cache.size(3) == 128 &&
-                  v_cache.size(2) == 128 && v_cache.size(3) == 16 && k_cache.size(0) == v_cache.size(0) &&
-                  k_cache.size(1) == v_cache.size(1),
-              "paged caches must be K[blocks,Hkv,16,128] / V[blocks,Hkv,128,16]");
+  if (fp8)
+    CHECK_HIP(kafka_launch_rope_kv_fp8(slab ? nullptr : bptr(qkv), slab ? qkv.data_ptr<float>() : nullptr,
+                                        slab ? qkv.size(0) : 0, slab ? (int64_t)T * W : 0, slab ? W : qkv.stride(0),
+                                        positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), bptr(q_out),
+                                        q_out.stride(0), k_cache.data_ptr<uint8_t>(), v_cache.data_ptr<uint8_t>(), sm,
+                                        T, Hq, Hkv, D, cur_stream()));
+  else
+    CHECK_HIP(kafka_launch_rope_kv(slab ? nullptr : bptr(qkv), slab ? qkv.data_ptr<float>() : nullptr,
+                                    slab ? qkv.size(0) : 0, slab ? (int64_t)T * W : 0, slab ? W : qkv.stride(0),
+                                    positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), bptr(q_out),
+                                    q_out.stride(0), bptr(k_cache), bptr(v_cache), sm, T, Hq, Hkv, D, bs,
+                                    cur_stream()));
 }
 
 // items: int32 [n, 8] decode work items (b, lo, hi, split, nsplit, npre, 0, 0) — see attention.hip DecodeItem.
@@ -210,7 +243,8 @@ static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at
                 "attn_decode: the fused merge needs an int32 ticket buffer of >= B * Hkv zeros");
     tp = tickets->data_ptr<int>();
   }
-  CHECK_HIP(kafka_launch_attn_decode(bptr(q), q.stride(0), bptr(k_cache), bptr(v_cache), items.size(0), B, Hkv,
+  CHECK_HIP(kafka_launch_attn_decode(bptr(q), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                      is_fp8_cache(k_cache) ? 1 : 0, items.size(0), B, Hkv,
                                       Hq / Hkv, 128, block_tables.data_ptr<int>(), block_tables.stride(0),
                                       items.data_ptr<int>(), out_part.data_ptr<float>(), lse_part.data_ptr<float>(),
                                       S_total, scale, op, ostride, tp, cur_stream()));
@@ -253,8 +287,8 @@ static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at:
     lp = lse_part->data_ptr<float>();
   }
   TORCH_CHECK(op != nullptr || pp != nullptr, "attn_prefill needs out or out_part");
-  CHECK_HIP(kafka_launch_attn_prefill(items.data_ptr<int>(), items.size(0), bptr(q), q.stride(0), bptr(k_cache),
-                                       bptr(v_cache), Hkv, G, 128, block_tables.data_ptr<int>(),
+  CHECK_HIP(kafka_launch_attn_prefill(items.data_ptr<int>(), items.size(0), bptr(q), q.stride(0), k_cache.data_ptr(),
+                                       v_cache.data_ptr(), is_fp8_cache(k_cache) ? 1 : 0, Hkv, G, 128, block_tables.data_ptr<int>(),
                                        block_tables.stride(0), q_limit.data_ptr<int>(), op, os, pp, lp, S_total,
                                        scale, (int)variant, cur_stream()));
 }

@@ -15,6 +15,16 @@
 // page position 8*h + j.
 // cos/sin come from a host-built table [max_pos, D] (cos in [0, D/2), sin in [D/2, D)) so the kernel does no
 // transcendental math (llama3 / linear / none scaling is folded into the table on the host).
+//
+// fp8 KV cache (kv_dtype="fp8", OCP e4m3, D = 128): rope_kv_fp8_kernel quantizes each (token, kv head) vector of K
+// and of V with its own power-of-two scale 2^e (e = exponent of amax / 448, so the largest element lands in
+// [224, 448]; a power of two loses no mantissa and dequantizes with an exponent add). Per (block, kv head):
+//   K page  KPAGE8 = 2080 B: 2048 B e4m3 data in 16-B units [8 planes p = 2j + h][16 keys o]; unit (p, o) holds
+//           d = 32j + 8h + {0..7} followed by d = 32j + 16 + 8h + {0..7} — the bf16 MFMA A-fragments of k-steps 2j
+//           and 2j + 1 of lane (key o, half h), i.e. ONE 16-B load per two k-steps; then int8 exponents: K of key
+//           o at byte 2048 + o, V of key o at byte 2064 + vt_pos(o) (the order in which the PV step's P registers
+//           hold the keys, so a lane's 8 V exponents of a page are one 8-B load).
+//   V page  2048 B: V^T [D][16] e4m3, key o at position vt_pos(o) (as the bf16 layout).
 #include "common.h"
 
 namespace kafka {
@@ -83,6 +93,143 @@ __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ 
       for (int j = 0; j < 8; ++j) dst[(int64_t)(c + j) * block_size] = (bf16)x[j];
     }
   }
+}
+
+constexpr int KPAGE8 = 16 * 128 + 32;
+constexpr int MAX_HKV8 = 64;
+
+// e such that amax * 2^-e <= 448 (frexp of amax / 448); 0 for an all-zero vector
+__device__ __forceinline__ int fp8_exponent(float amax) {
+  int e = 0;
+  frexpf(amax / 448.f, &e);
+  return amax > 0.f ? e : 0;
+}
+
+// 8 fp32 (already scaled) -> 8 e4m3 bytes, RNE, saturated to +-448
+__device__ __forceinline__ uint2 pack_fp8x8(const float (&x)[8]) {
+  int w[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    float c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = __builtin_amdgcn_fmed3f(x[4 * i + j], 448.f, -448.f);
+    int v = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+    w[i] = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], v, true);
+  }
+  return make_uint2((unsigned)w[0], (unsigned)w[1]);
+}
+
+// One workgroup per token, one pass (host-checked: every unit has its own thread). K/V amax per (token, head) is
+// reduced through LDS (atomicMax on the float bits: non-negative floats order like their bit patterns).
+__global__ __launch_bounds__(1024) void rope_kv_fp8_kernel(const bf16* __restrict__ qkv, const float* __restrict__ qp,
+                                                           int S, int64_t ps, int64_t qkv_stride,
+                                                           const int64_t* __restrict__ positions,
+                                                           const float* __restrict__ cos_sin,
+                                                           bf16* __restrict__ q_out, int64_t q_stride,
+                                                           uint8_t* __restrict__ k_cache, uint8_t* __restrict__ v_cache,
+                                                           const int64_t* __restrict__ slot_mapping, int Hq, int Hkv) {
+  constexpr int D = 128, HALF = 64, RU = HALF / 8, VU = D / 8;
+  __shared__ unsigned s_amax[2 * MAX_HKV8];
+  const int64_t t = blockIdx.x;
+  const int64_t pos = positions[t];
+  const int64_t slot = slot_mapping ? slot_mapping[t] : -1;
+  const int64_t row = t * qkv_stride;
+  const float* cs = cos_sin + pos * D;
+  const int n_rope = (Hq + Hkv) * RU;
+  const int n_total = n_rope + Hkv * VU;
+  const int64_t blk = slot >= 0 ? slot / 16 : 0;
+  const int off = slot >= 0 ? (int)(slot % 16) : 0;
+  const int u = threadIdx.x;
+  for (int i = u; i < 2 * Hkv; i += blockDim.x) s_amax[i] = 0u;
+  __syncthreads();
+  float y1[8], y2[8];
+  int kind = 0, head = 0, c = 0;  // kind 1: K unit (y1 = d c.., y2 = d 64 + c..), 2: V unit (y1 = d c..)
+  float amax = 0.f;
+  if (u < n_rope) {
+    head = u / RU;
+    c = (u % RU) * 8;
+    float x1[8], x2[8];
+    load_in8(x1, qkv, qp, S, ps, row + head * D + c);
+    load_in8(x2, qkv, qp, S, ps, row + head * D + HALF + c);
+    f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + c);
+    f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + c + 4);
+    f32x4 s0 = *reinterpret_cast<const f32x4*>(cs + HALF + c);
+    f32x4 s1 = *reinterpret_cast<const f32x4*>(cs + HALF + c + 4);
+    float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+    float sv[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = x1[j], b = x2[j];
+      y1[j] = a * cv[j] - b * sv[j];
+      y2[j] = b * cv[j] + a * sv[j];
+    }
+    if (head < Hq) {
+      bf16x8 o1, o2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o1[j] = (bf16)y1[j];
+        o2[j] = (bf16)y2[j];
+      }
+      bf16* dst = q_out + t * q_stride + head * D;
+      store_bf16x8(dst + c, o1);
+      store_bf16x8(dst + HALF + c, o2);
+    } else if (slot >= 0) {
+      kind = 1;
+      head -= Hq;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fmaxf(fabsf(y1[j]), fabsf(y2[j])));
+      atomicMax(&s_amax[head], __float_as_uint(amax));
+    }
+  } else if (u < n_total && slot >= 0) {
+    kind = 2;
+    const int v = u - n_rope;
+    head = v / VU;
+    c = (v % VU) * 8;
+    load_in8(y1, qkv, qp, S, ps, row + (Hq + Hkv + head) * D + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(y1[j]));
+    atomicMax(&s_amax[Hkv + head], __float_as_uint(amax));
+  }
+  __syncthreads();
+  if (kind == 0) return;
+  uint8_t* kpage = k_cache + (blk * Hkv + head) * (int64_t)KPAGE8;
+  const int e = fp8_exponent(__uint_as_float(s_amax[(kind == 2 ? Hkv : 0) + head]));
+  const float inv = ldexpf(1.f, -e);
+  if (kind == 1) {
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      float z[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = (part ? y2[j] : y1[j]) * inv;
+      const int q8 = ((part ? HALF : 0) + c) >> 3;  // 8-element chunk of d
+      const int p = 2 * (q8 >> 2) + (q8 & 1), second = (q8 >> 1) & 1;
+      *reinterpret_cast<uint2*>(kpage + (p * 16 + off) * 16 + 8 * second) = pack_fp8x8(z);
+    }
+    if (c == 0) kpage[2048 + off] = (uint8_t)(int8_t)e;
+  } else {
+    float z[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = y1[j] * inv;
+    const uint2 w = pack_fp8x8(z);
+    uint8_t* dst = v_cache + (blk * Hkv + head) * (int64_t)(D * 16) + vt_pos(off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[(c + j) * 16] = (uint8_t)(((j < 4 ? w.x : w.y) >> (8 * (j & 3))) & 0xff);
+    if (c == 0) kpage[2064 + vt_pos(off)] = (uint8_t)(int8_t)e;
+  }
+}
+
+extern "C" hipError_t kafka_launch_rope_kv_fp8(const bf16* qkv, const float* qp, int S, int64_t ps,
+                                              int64_t qkv_stride, const int64_t* positions, const float* cos_sin,
+                                              bf16* q_out, int64_t q_stride, uint8_t* k_cache, uint8_t* v_cache,
+                                              const int64_t* slot_mapping, int T, int Hq, int Hkv, int D,
+                                              hipStream_t st) {
+  if (T == 0) return hipSuccess;
+  const int units = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
+  if (D != 128 || Hkv > MAX_HKV8 || units > 1024) return hipErrorInvalidValue;
+  const int nt = ((units + 63) / 64) * 64;
+  rope_kv_fp8_kernel<<<T, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
+                                       v_cache, slot_mapping, Hq, Hkv);
+  return hipGetLastError();
 }
 
 // qp != nullptr: the input is S fp32 slabs [S][T][(Hq + 2 Hkv) D] (slab stride ps) instead of bf16 qkv

@@ -4,6 +4,10 @@ They define the numerics the CDNA4 kernels are tested against, and they are the 
 unit tests (no GPU in CI). They use exactly the same tensor layouts as the kernels, including the paged KV layout
   K page: [num_blocks, Hkv, 16, D] holding D/8 chunk planes [D/8][16 keys][8] (k_planes / k_natural below)
   V page: [num_blocks, Hkv, D, 16]  (V^T, key offset o at vt_pos(o)).
+or, for the fp8 cache (kv_dtype="fp8", ops/csrc/rope_kv.hip), uint8 pages
+  K page: [num_blocks, Hkv, 16 * D + 32]: e4m3 units [D/32 j][2 h][16 keys][2 s][8 e] holding d = 32j + 16s + 8h + e,
+          then int8 exponents: K of key o at 16D + o, V of key o at 16D + 16 + vt_pos(o) (value = e4m3 * 2^e)
+  V page: [num_blocks, Hkv, D * 16]: e4m3 V^T [D][16], key o at vt_pos(o).
 """
 from __future__ import annotations
 
@@ -23,6 +27,73 @@ def vt_pos(o: torch.Tensor | int):
 
 
 _VT_PERM = torch.tensor([vt_pos(o) for o in range(PAGE)], dtype=torch.long)
+
+
+FP8_MAX = 448.0
+FP8_EXP_MIN, FP8_EXP_MAX = -100, 100
+
+
+def is_fp8_cache(k_cache: torch.Tensor) -> bool:
+    return k_cache.dtype == torch.uint8
+
+
+def cache_head_dim(k_cache: torch.Tensor, v_cache: torch.Tensor) -> int:
+    return v_cache.shape[-1] // PAGE if is_fp8_cache(k_cache) else k_cache.shape[-1]
+
+
+def kv_cache_shapes(num_blocks: int, hkv: int, D: int, kv_dtype: str = "bf16"):
+    """(K shape, V shape, torch dtype) of one layer's paged cache."""
+    if kv_dtype == "fp8":
+        return (num_blocks, hkv, PAGE * D + 32), (num_blocks, hkv, D * PAGE), torch.uint8
+    if kv_dtype != "bf16":
+        raise ValueError(f"kv_dtype must be bf16 or fp8, not {kv_dtype!r}")
+    return (num_blocks, hkv, PAGE, D), (num_blocks, hkv, D, PAGE), torch.bfloat16
+
+
+def kv_page_bytes(hkv: int, D: int, kv_dtype: str = "bf16") -> int:
+    """Bytes of K + V for one 16-token page of one layer."""
+    return hkv * (2 * PAGE * D + 32) if kv_dtype == "fp8" else hkv * 2 * PAGE * D * 2
+
+
+def fp8_quant(x: torch.Tensor):
+    """Per-vector e4m3 quantization over the last dim: (bytes uint8 [..., D], exponent int [...]) with
+    x ~= e4m3(bytes) * 2^e and e = frexp exponent of amax / 448 (the kernel's rule, rope_kv.hip)."""
+    x = x.float()
+    amax = x.abs().amax(-1)
+    _, e = torch.frexp(amax / FP8_MAX)
+    e = torch.where(amax > 0, e, torch.zeros_like(e)).clamp(FP8_EXP_MIN, FP8_EXP_MAX)
+    y = torch.ldexp(x, -e[..., None].float()).clamp(-FP8_MAX, FP8_MAX)
+    return y.to(torch.float8_e4m3fn).view(torch.uint8), e
+
+
+def fp8_dequant_pages(k_pages: torch.Tensor, v_pages: torch.Tensor):
+    """fp8 pages (K [n, Hkv, 16D + 32], V [n, Hkv, 16D] uint8) -> fp32 K [n, Hkv, 16, D] and V [n, Hkv, D, 16]
+    (V in natural key order)."""
+    n, hkv = k_pages.shape[:2]
+    D = v_pages.shape[-1] // PAGE
+    data = k_pages[..., :PAGE * D].contiguous().view(torch.float8_e4m3fn).float()
+    k = data.view(n, hkv, D // 32, 2, PAGE, 2, 8).permute(0, 1, 4, 2, 5, 3, 6).reshape(n, hkv, PAGE, D)
+    ke = k_pages[..., PAGE * D:PAGE * D + PAGE].contiguous().view(torch.int8).float()
+    ve = k_pages[..., PAGE * D + PAGE:PAGE * D + 2 * PAGE].contiguous().view(torch.int8).float()
+    k = k * torch.exp2(ke)[..., None]
+    v = v_pages.contiguous().view(torch.float8_e4m3fn).float().view(n, hkv, D, PAGE) * torch.exp2(ve)[:, :, None, :]
+    return k, v[..., _VT_PERM.to(v.device)]
+
+
+def fp8_pack_pages(k: torch.Tensor, v: torch.Tensor):
+    """Natural-order K, V [n, Hkv, 16, D] -> fp8 pages (K [n, Hkv, 16D + 32], V [n, Hkv, 16D] uint8), every
+    (key, head) vector quantized on its own (the layout rope_kv_write produces)."""
+    n, hkv, _, D = k.shape
+    kq, ke = fp8_quant(k)
+    vq, ve = fp8_quant(v)
+    kp = torch.zeros(n, hkv, PAGE * D + 2 * PAGE, dtype=torch.uint8, device=k.device)
+    kp[..., :PAGE * D] = kq.view(n, hkv, PAGE, D // 32, 2, 2, 8).permute(0, 1, 3, 5, 2, 4, 6).reshape(n, hkv, -1)
+    kp[..., PAGE * D:PAGE * D + PAGE] = ke.to(torch.int8).view(torch.uint8)
+    perm = _VT_PERM.to(k.device)
+    kp[..., PAGE * D + PAGE + perm] = ve.to(torch.int8).view(torch.uint8)
+    vt = torch.zeros(n, hkv, D, PAGE, dtype=torch.uint8, device=k.device)
+    vt[..., perm] = vq.transpose(2, 3)
+    return kp, vt.reshape(n, hkv, D * PAGE)
 
 
 def k_planes(k_cache: torch.Tensor) -> torch.Tensor:
@@ -56,16 +127,31 @@ def silu_mul(x: torch.Tensor) -> torch.Tensor:
 
 def rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq: int, Hkv: int) -> None:
     T = qkv.shape[0]
-    D = k_cache.shape[-1]
+    D = cache_head_dim(k_cache, v_cache)
     half = D // 2
     x = qkv.float().view(T, Hq + 2 * Hkv, D)
     cs = cos_sin[positions.long()].float()  # [T, D]
     cos, sin = cs[:, None, :half], cs[:, None, half:]
     qk = x[:, : Hq + Hkv]
     x1, x2 = qk[..., :half], qk[..., half:]
-    rot = torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(qkv.dtype)
+    rot32 = torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1)
+    rot = rot32.to(qkv.dtype)
     q_out.copy_(rot[:, :Hq])
     if slot_mapping is None:
+        return
+    if is_fp8_cache(k_cache):
+        kq, ke = fp8_quant(rot32[:, Hq:])
+        vq, ve = fp8_quant(x[:, Hq + Hkv:])
+        kd = kq.view(T, Hkv, D // 32, 2, 2, 8).permute(0, 1, 2, 4, 3, 5)  # (j, s, h, e) -> (j, h, s, e)
+        for t in range(T):
+            s = int(slot_mapping[t])
+            if s < 0:
+                continue
+            blk, off = divmod(s, PAGE)
+            k_cache[blk, :, :PAGE * D].view(Hkv, D // 32, 2, PAGE, 2, 8)[:, :, :, off] = kd[t]
+            k_cache[blk, :, PAGE * D + off] = ke[t].to(torch.int8).view(torch.uint8)
+            k_cache[blk, :, PAGE * D + PAGE + vt_pos(off)] = ve[t].to(torch.int8).view(torch.uint8)
+            v_cache[blk].view(Hkv, D, PAGE)[:, :, vt_pos(off)] = vq[t]
         return
     k = rot[:, Hq:]
     v = x[:, Hq + Hkv:].to(qkv.dtype)
@@ -82,9 +168,12 @@ def gather_kv(k_cache, v_cache, block_table, length: int):
     """Materialise [length, Hkv, D] K and V for one sequence from the paged caches (fp32)."""
     nb = (length + PAGE - 1) // PAGE
     ids = block_table[:nb].long()
-    k = k_natural(k_cache[ids].float())  # [nb, Hkv, 16, D]
-    v = v_cache[ids].float()  # [nb, Hkv, D, 16]
-    v = v[..., _VT_PERM.to(v.device)]  # undo the page permutation -> [nb, Hkv, D, 16] natural key order
+    if is_fp8_cache(k_cache):
+        k, v = fp8_dequant_pages(k_cache[ids], v_cache[ids])
+    else:
+        k = k_natural(k_cache[ids].float())  # [nb, Hkv, 16, D]
+        v = v_cache[ids].float()  # [nb, Hkv, D, 16]
+        v = v[..., _VT_PERM.to(v.device)]  # undo the page permutation -> [nb, Hkv, D, 16] natural key order
     k = k.permute(0, 2, 1, 3).reshape(nb * PAGE, k.shape[1], k.shape[3])[:length]
     v = v.permute(0, 3, 1, 2).reshape(nb * PAGE, v.shape[1], v.shape[2])[:length]
     return k, v
