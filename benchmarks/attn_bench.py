@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--prefix", type=int, default=18000)
     ap.add_argument("--suffix", type=int, default=2000)
     ap.add_argument("--chunks", default="384,576,1024")
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     Hq, Hkv, D = 32, 8, 128
@@ -52,8 +53,13 @@ def main():
     n_pref = P // 16
     suf_pages = (Ls + 16) // 16 + 1
     nb = n_pref + B * suf_pages + 16
-    k = torch.randn(nb, Hkv, 16, D, device=dev, dtype=torch.bfloat16)
-    v = torch.randn(nb, Hkv, D, 16, device=dev, dtype=torch.bfloat16)
+    if args.kv_dtype == "fp8":  # same random values, packed as e4m3 pages with per-token scales
+        from kafka_llm_service_amd.ops import reference as ref
+
+        k, v = ref.fp8_pack_pages(torch.randn(nb, Hkv, 16, D, device=dev), torch.randn(nb, Hkv, 16, D, device=dev))
+    else:
+        k = torch.randn(nb, Hkv, 16, D, device=dev, dtype=torch.bfloat16)
+        v = torch.randn(nb, Hkv, D, 16, device=dev, dtype=torch.bfloat16)
     maxb = n_pref + suf_pages + 2
     bt = torch.zeros(B + 1, maxb, dtype=torch.int32)
     c = n_pref
@@ -67,7 +73,7 @@ def main():
     q_limit = (lens - 1).to(torch.int32)
     scale = D ** -0.5
     out = torch.empty(B, Hq, D, device=dev, dtype=torch.bfloat16)
-    kv_bytes_tok = Hkv * D * 2 * 2
+    kv_bytes_tok = Hkv * D * 2 * 2 if args.kv_dtype == "bf16" else Hkv * (2 * D + 2)
 
     # cascade prefix pass, several chunk sizes
     for chunk in [int(x) for x in args.chunks.split(",")]:
