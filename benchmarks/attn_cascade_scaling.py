@@ -14,7 +14,7 @@ from kafka_llm_service_amd import ops
 dev = torch.device("cuda:0")
 Hq, Hkv, D, B = 32, 8, 128, 64
 G = Hq // Hkv
-for P in (4608, 9216, 18432, 36864, 73728):
+for P in [int(x) for x in os.environ.get("PREFIXES", "4608,9216,18432,36864,73728").split(",")]:
     nc = 32
     chunk = P // nc
     n_pref = P // 16

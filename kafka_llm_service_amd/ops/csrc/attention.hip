@@ -839,8 +839,68 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkIte
       }
     }
   }
-  if (!valid) return;
   const int head = kvh * G + g;
+  if constexpr (LDS && D == 128) {
+    // Output through a per-wave LDS transpose. The accumulators hold one (token, head) row per lane pair, 16 B per
+    // lane per d-chunk, and consecutive rows lie a whole partial slab apart ((token * Hq + head) * S_total): stored
+    // straight from registers every instruction writes 32 B into 32 different lines (the cascade pass's 32 MB of
+    // partials then took ~10 us of its ~39). Through LDS each store instruction writes 8 whole 128-B row lines.
+    // Every wave has its own 4 KB slice of the (now idle) stage buffers; rows are 128 B with 16-B chunks XOR-swizzled
+    // by row. fp32 partials: 4 rounds of 32 d; bf16 output: 2 rounds of 64 d.
+    if (!__any(valid)) return;  // wave-uniform
+    const bool part = it.split >= 0;
+    const float inv = acc.l > 0.f ? 1.f / acc.l : 0.f;
+    if (part && valid && h == 0)
+      lse_part[((int64_t)token * Hq + head) * S_total + it.split] = acc.l > 0.f ? acc.m + log2f(acc.l) : -INFINITY;
+    char* slab = lds + w * 4096;
+    const int nvalid = it.q_count * G - w * 32;  // rows of this wave below it (uniform)
+    const int cc = lane & 7;
+    // read back 4 rows x 16 B per lane (8 lanes = one 128-B row line) and store them
+    auto flush = [&](int rd) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int row = (lane >> 3) + 8 * k;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(slab + row * 128 + 16 * (cc ^ (row & 7)));
+        if (row < nvalid) {
+          const int R2 = w * 32 + row, tok2 = it.q_start + R2 / G, head2 = kvh * G + R2 % G;
+          if (part)
+            *reinterpret_cast<f32x4*>(out_part + (((int64_t)tok2 * Hq + head2) * S_total + it.split) * D + 32 * rd +
+                                      4 * cc) = v;
+          else
+            *reinterpret_cast<f32x4*>(out + (int64_t)tok2 * out_stride + (int64_t)head2 * D + 64 * rd + 8 * cc) = v;
+        }
+      }
+    };
+    if (part) {
+#pragma unroll
+      for (int rd = 0; rd < 4; ++rd) {
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) {
+          const int c = 2 * i4 + h;
+          f32x4 v = {acc.o[rd][4 * i4] * inv, acc.o[rd][4 * i4 + 1] * inv, acc.o[rd][4 * i4 + 2] * inv,
+                     acc.o[rd][4 * i4 + 3] * inv};
+          *reinterpret_cast<f32x4*>(slab + r * 128 + 16 * (c ^ (r & 7))) = v;
+        }
+        flush(rd);
+      }
+    } else {
+#pragma unroll
+      for (int rd = 0; rd < 2; ++rd) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int i4 = 0; i4 < 4; ++i4) {
+            bf16x4 v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (bf16)(acc.o[2 * rd + tt][4 * i4 + j] * inv);
+            *reinterpret_cast<bf16x4*>(slab + r * 128 + 16 * ((4 * tt + i4) ^ (r & 7)) + 8 * h) = v;
+          }
+        flush(rd);
+      }
+    }
+    return;
+  }
+  if (!valid) return;
   if (it.split < 0) {
     const float inv = acc.l > 0.f ? 1.f / acc.l : 0.f;
     bf16* orow = out + (int64_t)token * out_stride + (int64_t)head * D;
