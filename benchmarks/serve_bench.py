@@ -104,11 +104,32 @@ def _system_message(chars: int) -> str | None:
     return " ".join(out)
 
 
+# The reference's 13 prompt sections (src/prompts/sections/*.md, 70,568 characters) encode to 36,364 tokens with the
+# engine's tokenizer (engine/tokenizer.py; measured once, the reference is not read at run time). Our own re-worded
+# sections are 47,002 characters / 19,571 tokens (PARITY.md #18). ``--system-tokens ref`` serves a shared prefix of
+# the reference prompt's size so the HTTP numbers compare like for like.
+REFERENCE_PROMPT_TOKENS = 36364
+
+
+@functools.lru_cache(maxsize=4)
+def _system_message_tokens(n: int) -> str:
+    """A synthetic system prompt of exactly ``n`` tokens under the engine's tokenizer."""
+    from kafka_llm_service_amd.engine.tokenizer import get_tokenizer
+
+    tok = get_tokenizer()
+    text = _system_message(8 * n)
+    ids = tok.encode(text)[:n]
+    return tok.decode(ids)
+
+
 async def _thread(client, url, k, args, res):
     if getattr(args, "stagger", 0) > 0 and k >= 0:
         # steady-state arrivals: thread k starts at a deterministic point in [0, stagger) instead of all at once
         await asyncio.sleep(args.stagger * ((k * 0.6180339887) % 1.0))
-    body = {"system_message": _system_message(args.system_chars)} if args.system_chars > 0 else {}
+    if args.system_tokens:
+        body = {"system_message": _system_message_tokens(args.system_tokens)}
+    else:
+        body = {"system_message": _system_message(args.system_chars)} if args.system_chars > 0 else {}
     r = await client.post(f"{url}/v1/threads", json=body)
     tid = r.json()["thread_id"]
     for i in range(args.turns):
@@ -180,6 +201,7 @@ def run(url, args):
         "metric": "serve: p50 TTFT + output tok/s, /v1/threads/{id}/chat/completions",
         "backend": args.backend, "model": args.model, "threads": args.threads, "turns": args.turns,
         "stream": not args.no_stream, "client_procs": P, "system_chars": args.system_chars,
+        "system_tokens": args.system_tokens,
         "stagger_s": args.stagger, "requests": res["requests"], "wall_s": round(wall, 3),
         "client_cpu_s": round(res["client_cpu"], 3),
         "ttft_p50_ms": ms(_pct(res["ttft"], 0.5)), "ttft_p99_ms": ms(_pct(res["ttft"], 0.99)),
@@ -210,8 +232,13 @@ def main():
     ap.add_argument("--system-chars", type=int, default=0,
                     help="create threads with a shared synthetic system message of this many characters "
                          "(70000 ~ the reference's rendered Kafka prompt) instead of the server's Kafka prompt")
+    ap.add_argument("--system-tokens", default=None,
+                    help="shared synthetic system message of exactly this many engine tokens; 'ref' = the size of "
+                         f"the reference's Kafka prompt ({REFERENCE_PROMPT_TOKENS} tokens)")
     ap.add_argument("--ignore-eos", action="store_true", default=True)
     args = ap.parse_args()
+    if args.system_tokens is not None:
+        args.system_tokens = REFERENCE_PROMPT_TOKENS if args.system_tokens == "ref" else int(args.system_tokens)
     proc = None
     url = args.url
     if url is None:
