@@ -49,7 +49,8 @@ class EngineConfig:
     use_cascade: bool = True
     cascade_min_prefix: int = 512
     target_wgs: int = 256               # tile-kernel workgroups per pass (8-wave WGs, one per CU)
-    prefill_kv_chunk: int = 1024        # key-range split for long-context prefill tiles
+    prefill_kv_chunk: int = 1024        # a new turn on > 2x this many cached keys splits its key range so all
+                                        # tiles make ~target_wgs workgroups (chunks >= min(256, this))
     use_graphs: bool = False
     # paged KV cache: "bf16", or "fp8" = e4m3 with one power-of-two scale per (token, kv head) for K and for V
     # (half the bytes per page: twice the pages, half the decode attention traffic; ops/csrc/rope_kv.hip)

@@ -390,7 +390,11 @@ class ModelRunner:
             max_kv = max(b for _, _, b in pre)
             few = len(items) * self.model.hkv < self.target_wgs // 2 and max_kv > 2 * self.prefill_kv_chunk
             if few or max_kv > MAX_ITEM_KEYS:
-                ck = self.prefill_kv_chunk if few else MAX_ITEM_KEYS
+                if few:  # key chunk sized so all tiles together make ~target_wgs workgroups (one round on the CUs)
+                    keys = sum(it[4] for it in items) * self.model.hkv
+                    ck = max(min(256, self.prefill_kv_chunk), -(-keys // (self.target_wgs * 32)) * 32)
+                else:
+                    ck = MAX_ITEM_KEYS
                 split_items = []
                 for (q0, cnt, btr, lo, hi, _, _, _) in items:
                     for c in range(math.ceil(hi / ck)):
