@@ -91,7 +91,7 @@ class MoEBlock:
         [T, d] the next layer expects. With tensor-parallel attention this moves more bytes than the default
         all-reduce combine (capacity padding + the all-gather), so it is not the default; it is the building block
         for data-parallel attention, where tokens are not replicated."""
-        import torch.distributed as dist
+        from kafka_llm_service_amd.parallel import comm
 
         T, d = x.shape
         ep, q, k, El = self.ep, self.r, self.k, self.e_local
@@ -115,8 +115,8 @@ class MoEBlock:
             meta[dest, pos] = (te - dest * El).to(torch.int32)
         recv = torch.empty_like(send)
         rmeta = torch.empty_like(meta)
-        dist.all_to_all_single(recv, send, group=grp)
-        dist.all_to_all_single(rmeta, meta, group=grp)
+        comm.all_to_all_single(recv, send, grp)
+        comm.all_to_all_single(rmeta, meta, grp)
         # local expert MLP over the received rows (k = 1 routing; empty slots carry expert -1 and are skipped)
         rows = recv.view(ep * C, d)
         re = rmeta.view(-1).long()
@@ -136,10 +136,10 @@ class MoEBlock:
         y = torch.zeros(ep * C, d, dtype=torch.float32, device=dev)
         ops.grouped_gemm(a, lw.w2, rr, gather=False, e_lo=0, combine_out=y)
         back = torch.empty_like(send)
-        dist.all_to_all_single(back, y.to(x.dtype).view(ep, C, d), group=grp)
+        comm.all_to_all_single(back, y.to(x.dtype).view(ep, C, d), grp)
         own = torch.zeros(Tl, d, dtype=torch.float32, device=dev)
         if n_own:
             own.index_add_(0, tok - lo, back[dest, pos].float() * tw[:, None])
         full = torch.empty(ep * Tl, d, dtype=x.dtype, device=dev)
-        dist.all_gather_into_tensor(full, own.to(x.dtype), group=grp)
+        comm.all_gather_into(full, own.to(x.dtype), ep, grp)
         return full[:T]

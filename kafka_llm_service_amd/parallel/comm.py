@@ -75,7 +75,24 @@ def all_gather_lastdim(x: torch.Tensor, world: int, group) -> torch.Tensor:
     return torch.cat(parts, dim=-1)
 
 
-def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, out_splits: list[int], in_splits: list[int],
-                      group) -> torch.Tensor:
+def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, group, out_splits: list[int] | None = None,
+                      in_splits: list[int] | None = None) -> torch.Tensor:
+    """dist.all_to_all_single; device tensors over a gloo group (several ranks on one GPU) go through host memory."""
+    if inp.is_cuda and _is_gloo(group):
+        h = torch.empty_like(out, device="cpu")
+        dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(h)
+        return out
     dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+    return out
+
+
+def all_gather_into(out: torch.Tensor, inp: torch.Tensor, world: int, group) -> torch.Tensor:
+    """out [world * n, ...] = concat over ranks of inp [n, ...] (host-staged over gloo)."""
+    if inp.is_cuda and _is_gloo(group):
+        parts = [torch.empty_like(inp, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, inp.contiguous().cpu(), group=group)
+        out.copy_(torch.cat(parts, 0))
+        return out
+    dist.all_gather_into_tensor(out, inp.contiguous(), group=group)
     return out

@@ -156,16 +156,19 @@ def _capture_logits(eng, prompts, sp):
     return outs, seen
 
 
-def _tp_main(rank, world, port, q, graphs):
+def _tp_main(rank, world, port, q, graphs, model):
     dev = rank % torch.cuda.device_count()
     _env(rank, world, port, dev)
     os.environ["KAFKA_TP_BACKEND"] = "gloo"
+    if model.endswith("+a2a"):  # experts dispatched / combined by all-to-all instead of the all-reduce combine
+        os.environ["KAFKA_MOE_A2A"] = "1"
     from kafka_llm_service_amd.engine import tp_worker
     from kafka_llm_service_amd.engine.sequence import SamplingParams
     from kafka_llm_service_amd.parallel import comm
     from kafka_llm_service_amd.parallel import state as pstate
 
-    eng, st = tp_worker.build_tp_engine(dict(CFG, device=f"cuda:{dev}", use_graphs=graphs), tp=world)
+    eng, st = tp_worker.build_tp_engine(dict(CFG, model=model.replace("+a2a", ""), device=f"cuda:{dev}",
+                                             use_graphs=graphs), tp=world)
     try:
         assert os.environ.get("KAFKA_CUSTOM_AR", "1") == "0" or comm.get_custom(st.tp_group) is not None, \
             "custom all-reduce not registered"
@@ -186,15 +189,19 @@ def _tp_main(rank, world, port, q, graphs):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("graphs", [False, True], ids=["eager", "graphs"])
-def test_tp2_engine_on_one_gpu_matches_tp1(cuda, graphs):
+@pytest.mark.parametrize("model,graphs", [("small-llama", False), ("small-llama", True), ("tiny-mixtral", False),
+                                          ("tiny-mixtral+a2a", False)],
+                         ids=["eager", "graphs", "mixtral-ep", "mixtral-ep-a2a"])
+def test_tp2_engine_on_one_gpu_matches_tp1(cuda, model, graphs):
+    """TP=2 (Mixtral: experts sharded over the 2 ranks, EP) on one GPU == the TP=1 model: same first-step logits up
+    to reduction order, every greedy token the dense oracle's argmax."""
     from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
     from kafka_llm_service_amd.engine.sequence import SamplingParams
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_tp_main, args=(r, 2, port, q, graphs)) for r in range(2)]
+    ps = [ctx.Process(target=_tp_main, args=(r, 2, port, q, graphs, model)) for r in range(2)]
     for p in ps:
         p.start()
     res = {}
@@ -208,7 +215,7 @@ def test_tp2_engine_on_one_gpu_matches_tp1(cuda, graphs):
     assert res["follower"][0] >= 6 and ahead > 0
     if graphs:
         assert gstats["replays"] >= 1
-    ref = LLMEngine(EngineConfig(**dict(CFG, device="cuda:0")))
+    ref = LLMEngine(EngineConfig(**dict(CFG, model=model.replace("+a2a", ""), device="cuda:0")))
     sp = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
     want_outs, want = _capture_logits(ref, _prompts(ref.model_cfg.vocab_size), sp)
     # first step (prefill of all prompts, identical batches): the TP=2 logits equal TP=1 up to bf16 reduction order
