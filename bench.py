@@ -171,6 +171,9 @@ def main(argv=None):
     args = parse(argv)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return spawn_ranks(args.gpus)
+    from kafka_llm_service_amd.utils.affinity import pin_local_process
+
+    pin_local_process(int(os.environ.get("LOCAL_RANK", "0")), int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

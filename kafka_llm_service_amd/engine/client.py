@@ -99,8 +99,11 @@ class InProcessClient:
 
 
 # ---------------------------------------------------------------------------------------------------------------
-def _worker_main(rank: int, cfg_dict: dict, conn) -> None:
+def _worker_main(rank: int, cfg_dict: dict, conn, n_local: int = 1) -> None:
     """One DP replica (tp = 1): owns one GPU, steps its engine, exchanges small pickled messages over a pipe."""
+    from kafka_llm_service_amd.utils.affinity import pin_local_process
+
+    pin_local_process(rank, n_local)
     import torch
 
     from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
@@ -215,7 +218,8 @@ class DPClient:
         ctx, cfg = self._ctx, self._cfg
         if self.tp == 1:
             parent, child = ctx.Pipe()
-            p = ctx.Process(target=_worker_main, args=(r, cfg, child), daemon=True, name=f"kafka-replica{r}")
+            p = ctx.Process(target=_worker_main, args=(r, cfg, child, self.n_replicas), daemon=True,
+                            name=f"kafka-replica{r}")
             p.start()
             self.procs[r], self._group_procs[r] = p, [p]
             return [parent]
