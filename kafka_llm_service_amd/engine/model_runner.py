@@ -42,6 +42,7 @@ class HostStep:
     cascade_prefix: int = 0  # longest cascade prefix of the step (tokens; 0 = no cascade)
     n_items: int = 0
     prefill_splits: int = 0
+    n_merge: int = 0        # prefill row ranges whose tiles were split: i32[-2 n_merge:] = (lo, hi) pairs
     i64: np.ndarray | None = None
     i32: np.ndarray | None = None
     # (row, seq, position): decode inputs whose token was still being sampled at planning time, filled at launch
@@ -67,7 +68,7 @@ class SampleParams:
 
 
 _PLAN_SCALARS = ("B", "T", "nbt", "bt_w", "n_rows", "s_total", "n_dec_items", "n_prefix_items", "cascade_prefix",
-                 "n_items", "prefill_splits", "n_late", "late_off")
+                 "n_items", "prefill_splits", "n_merge", "n_late", "late_off")
 PLAN_HDR = 32  # int64 header of a broadcast step plan
 
 
@@ -125,6 +126,45 @@ MIN_DECODE_KEYS = 256      # smallest key range of one decode work item
 DECODE_TARGET_ITEMS = int(os.environ.get("KAFKA_DECODE_TARGET", "768"))  # A/B: profiles/r02/decode_items_ab.jsonl
 MAX_PARTIALS = 64           # partial slots per row that the decode kernel's fused merge reads (one lane each)
 MAX_PREFIX_CHUNKS = 32
+
+
+def plan_prefill_items(tiles: list[tuple[int, int, int, int, int]], hkv: int, target_wgs: int, min_chunk: int,
+                       max_keys: int = MAX_ITEM_KEYS) -> tuple[list[tuple], int, list[tuple[int, int]]]:
+    """Work items of the prefill tile kernel from query tiles (q0, count, bt_row, extent, hi): ``extent`` = keys the
+    tile attends (its last token's position + 1), ``hi`` = key bound of the chunk.
+
+    The tile kernel's time per workgroup is ~a + b x (32-key blocks), so a launch is as long as its longest item. A
+    causal prompt's tiles grow linearly (a 2k prompt: 2 .. 64 blocks) and a new turn's few tiles each span a ~20k-token
+    context: when the launch is at most ~two rounds of workgroups, tiles longer than the balanced share
+    (sum of extents x Hkv / target_wgs, >= min_chunk) are split into equal key pieces whose (O, lse) partials are
+    merged afterwards; shorter tiles still write bf16 rows directly. Larger launches only get longest-first order
+    (the dispatcher then packs the tail). Returns (items, partial slots per row, merged row ranges)."""
+    if not tiles:
+        return [], 0, []
+    total = sum(t[3] for t in tiles) * hkv
+    longest = max(t[3] for t in tiles)
+    if len(tiles) * hkv >= 2 * target_wgs:
+        ck = max_keys  # many tiles: split only what exceeds the LDS page-staging bound
+    else:
+        ck = min(max(min_chunk, -(-total // (target_wgs * 32)) * 32), max_keys)
+        if longest < 3 * ck // 2 and longest <= max_keys:
+            ck = max_keys  # nothing long enough for a split to shorten the launch by much
+    items, splits, ranges = [], 0, []
+    for q0, cnt, btr, ext, hi in tiles:
+        if ext <= ck:
+            items.append((q0, cnt, btr, 0, hi, -1, 0, 0))
+            continue
+        nsp = -(-ext // ck)
+        ps = -(-ext // (nsp * 32)) * 32
+        nsp = -(-ext // ps)
+        items += [(q0, cnt, btr, c * ps, min(hi, (c + 1) * ps), c, 0, 0) for c in range(nsp)]
+        splits = max(splits, nsp)
+        if ranges and ranges[-1][1] == q0:
+            ranges[-1] = (ranges[-1][0], q0 + cnt)
+        else:
+            ranges.append((q0, q0 + cnt))
+    items.sort(key=lambda it: it[3] - it[4])  # longest key range first
+    return items, splits, ranges
 
 
 def prefix_groups(bt: np.ndarray, nfull: np.ndarray, min_blocks: int) -> tuple[list[int], list[tuple[int, int]]]:
@@ -330,7 +370,7 @@ class ModelRunner:
             self.kvm.fill_slots(s.seq_id, p, p + 1, slots, i)
             sample_seqs.append(s)
             logit_rows.append(i)
-        items = []
+        tiles = []
         r = B
         for j, (s, a, b) in enumerate(pre):
             n = b - a
@@ -340,7 +380,8 @@ class ModelRunner:
             self.kvm.fill_slots(s.seq_id, a, b, slots, r)
             bt_row = B + j
             for t0 in range(0, n, self.tile):
-                items.append((r + t0 - B, min(self.tile, n - t0), bt_row, 0, b, -1, 0, 0))
+                cnt = min(self.tile, n - t0)
+                tiles.append((r + t0 - B, cnt, bt_row, a + t0 + cnt, b))
             if b == s.total_len:
                 sample_seqs.append(s)
                 logit_rows.append(r + n - 1)
@@ -384,25 +425,16 @@ class ModelRunner:
             if pit:
                 h.n_prefix_items = len(pit)
                 i32_parts.append(np.asarray(pit, dtype=np.int32).reshape(-1))
-        if items:
-            # few query tiles against a long key range (a new turn of a thread with a ~20k-token cached context):
-            # split every tile's key range so the pass fills the GPU, merge the partials afterwards
-            max_kv = max(b for _, _, b in pre)
-            few = len(items) * self.model.hkv < self.target_wgs // 2 and max_kv > 2 * self.prefill_kv_chunk
-            if few or max_kv > MAX_ITEM_KEYS:
-                if few:  # key chunk sized so all tiles together make ~target_wgs workgroups (one round on the CUs)
-                    keys = sum(it[4] for it in items) * self.model.hkv
-                    ck = max(min(256, self.prefill_kv_chunk), -(-keys // (self.target_wgs * 32)) * 32)
-                else:
-                    ck = MAX_ITEM_KEYS
-                split_items = []
-                for (q0, cnt, btr, lo, hi, _, _, _) in items:
-                    for c in range(math.ceil(hi / ck)):
-                        split_items.append((q0, cnt, btr, c * ck, min(hi, (c + 1) * ck), c, 0, 0))
-                items = split_items
-                h.prefill_splits = math.ceil(max_kv / ck)
+        if tiles:
+            # long tiles (a new turn against a ~20k-token cached context, the late tiles of a causal prompt) are
+            # split along the key range so the launch is balanced; their partials are merged afterwards
+            items, h.prefill_splits, ranges = plan_prefill_items(tiles, self.model.hkv, self.target_wgs,
+                                                                 min(256, self.prefill_kv_chunk))
             h.n_items = len(items)
             i32_parts.append(np.asarray(items, dtype=np.int32).reshape(-1))
+            if ranges:
+                h.n_merge = len(ranges)
+                i32_parts.append(np.asarray(ranges, dtype=np.int32).reshape(-1))
         h.i64 = np.concatenate([tokens, positions, slots, np.asarray(logit_rows, dtype=np.int64)])
         h.i32 = np.concatenate(i32_parts)
         h.stats = {"B": B, "T": T, "cascade_prefix": h.cascade_prefix, "cascade_groups": len(groups),
@@ -444,6 +476,8 @@ class ModelRunner:
             if h.prefill_splits:
                 Tp = T - B
                 meta.prefill_splits = h.prefill_splits
+                mr = h.i32[h.i32.size - 2 * h.n_merge:].reshape(-1, 2)  # host copy of the plan (every TP rank)
+                meta.prefill_merge = [(int(lo), int(hi)) for lo, hi in mr]
                 meta.prefill_part = torch.empty(Tp, Hq, h.prefill_splits, D, dtype=torch.float32,
                                                 device=self.device)
                 meta.prefill_lse = torch.full((Tp, Hq, h.prefill_splits), float("-inf"), dtype=torch.float32,

@@ -39,11 +39,12 @@ class AttnMeta:
     # prefill
     prefill_items: torch.Tensor | None = None  # int32 [m, 8] (q_start relative to row B)
     q_limit: torch.Tensor | None = None        # int32 [T] absolute causal limit per query token
-    # long-context prefill with few query tiles: items are split along the key range (flash-decoding style) into
-    # partials [T - B, Hq, prefill_splits, D] merged by log-sum-exp
+    # long prefill tiles are split along the key range (flash-decoding style) into partials
+    # [T - B, Hq, prefill_splits, D] merged by log-sum-exp over ``prefill_merge``; the other tiles write rows directly
     prefill_splits: int = 0
     prefill_part: torch.Tensor | None = None
     prefill_lse: torch.Tensor | None = None
+    prefill_merge: list = field(default_factory=list)  # (lo, hi) prefill row ranges of split tiles
     scale: float = 1.0
     extra: dict = field(default_factory=dict)
 
@@ -63,8 +64,9 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     if meta.prefill_items is not None and meta.num_tokens > B:
         if meta.prefill_splits:
             ops.attn_prefill(meta.prefill_items, q[B:], k_cache, v_cache, meta.block_tables, meta.q_limit[B:],
-                             meta.scale, out_part=meta.prefill_part, lse_part=meta.prefill_lse)
-            ops.attn_merge(meta.prefill_part, meta.prefill_lse, out[B:])
+                             meta.scale, out=out[B:], out_part=meta.prefill_part, lse_part=meta.prefill_lse)
+            for lo, hi in meta.prefill_merge:
+                ops.attn_merge(meta.prefill_part[lo:hi], meta.prefill_lse[lo:hi], out[B + lo:B + hi])
         else:
             ops.attn_prefill(meta.prefill_items, q[B:], k_cache, v_cache, meta.block_tables, meta.q_limit[B:],
                              meta.scale, out=out[B:])

@@ -338,3 +338,32 @@ def test_tiled_only_mixtral_and_export(tmp_path):
     back = build_model(m.cfg, "cpu", weights=str(tmp_path))
     assert torch.equal(back.lm_head, ref_eng.model.lm_head)
     assert torch.equal(back.layers[1].qkv, ref_eng.model.layers[1].qkv)
+
+
+def test_plan_prefill_items_balances_causal_tiles():
+    """A causal 2k-token chunk (32 tiles of 64 tokens, extents 64..2048): tiles longer than the balanced share are
+    split into equal key pieces (contiguous merge ranges), short tiles stay whole, items come longest-first, and
+    every tile's keys [0, extent) are covered exactly once."""
+    from kafka_llm_service_amd.engine.model_runner import plan_prefill_items
+
+    tiles = [(64 * i, 64, 0, 64 * (i + 1), 2048) for i in range(32)]
+    items, splits, ranges = plan_prefill_items(tiles, hkv=8, target_wgs=256, min_chunk=256)
+    assert splits == 2 and len(ranges) == 1 and ranges[0][1] == 2048
+    assert all((it[4] - it[3]) >= (nx[4] - nx[3]) for it, nx in zip(items, items[1:]))
+    for q0, cnt, _, ext, _ in tiles:
+        mine = sorted((it[3], it[4]) for it in items if it[0] == q0)
+        whole = [it for it in items if it[0] == q0 and it[5] < 0]
+        if whole:
+            assert len(mine) == 1 and mine[0] == (0, 2048)  # kernel clamps to the causal limit itself
+            assert not any(lo <= q0 < hi for lo, hi in ranges)
+        else:
+            assert mine[0][0] == 0 and mine[-1][1] >= ext and all(a[1] == b[0] for a, b in zip(mine, mine[1:]))
+            assert any(lo <= q0 < hi for lo, hi in ranges)
+    # a short prompt is never split; a many-tile launch only splits past the LDS page bound
+    assert plan_prefill_items([(0, 64, 0, 64, 300), (64, 64, 0, 128, 300)], 8, 256, 256)[1] == 0
+    many = [(64 * i, 64, 0, 64 * (i + 1), 8192) for i in range(128)]
+    assert plan_prefill_items(many, 8, 256, 256)[1] == 0
+    # a new turn: 2 tiles against a 20k context -> ~target_wgs workgroups in total
+    turn = [(0, 64, 0, 20000, 20064), (64, 40, 0, 20104, 20104)]
+    items, splits, ranges = plan_prefill_items(turn, 8, 256, 256)
+    assert 200 <= len(items) * 8 <= 320 and ranges == [(0, 104)]

@@ -464,3 +464,34 @@ def test_slab_consumers(cuda, T):
     _close(q, q2, atol=0.05, rtol=0.01, msg="slab q")
     _close(k, k2, atol=0.05, rtol=0.01, msg="slab k")
     _close(v, v2, atol=0.02, rtol=0.01, msg="slab v")
+
+
+@pytest.mark.parametrize("ctx,qlen", [(0, 2048), (300, 1000)])
+def test_attn_prefill_balanced_split(cuda, ctx, qlen):
+    """Causal prefill planned by model_runner.plan_prefill_items: long tiles split into key pieces (partials merged
+    per row range), short tiles written directly, all in one launch == the fp32 reference."""
+    from kafka_llm_service_amd.engine.model_runner import plan_prefill_items
+
+    torch.manual_seed(12)
+    Hq, Hkv, D = 32, 8, 128
+    G = Hq // Hkv
+    L = ctx + qlen
+    k, v, bt = _random_paged(1, [L], Hkv, cuda, seed=13)
+    q = torch.randn(qlen, Hq, D, device=cuda, dtype=torch.bfloat16)
+    q_limit = torch.arange(ctx, L, dtype=torch.int32)
+    tile = ops.tile_rows(0) // G
+    tiles = [(t0, min(tile, qlen - t0), 0, ctx + t0 + min(tile, qlen - t0), L) for t0 in range(0, qlen, tile)]
+    items, splits, ranges = plan_prefill_items(tiles, Hkv, 256, 256)
+    assert splits >= 2 and ranges
+    it = torch.tensor(items, dtype=torch.int32, device=cuda)
+    out = torch.full((qlen, Hq, D), float("nan"), device=cuda, dtype=torch.bfloat16)
+    part = torch.empty(qlen, Hq, splits, D, device=cuda)
+    lse = torch.full((qlen, Hq, splits), float("-inf"), device=cuda)
+    scale = 1 / math.sqrt(D)
+    ops.attn_prefill(it, q, k, v, bt, q_limit.to(cuda), scale, out=out, out_part=part, lse_part=lse)
+    for lo, hi in ranges:
+        ops.attn_merge(part[lo:hi], lse[lo:hi], out[lo:hi])
+    whole = torch.tensor([[t0, cnt, 0, 0, L, -1, 0, 0] for t0, cnt, _, _, _ in tiles], dtype=torch.int32)
+    out_ref = torch.zeros(qlen, Hq, D, dtype=torch.bfloat16)
+    ref.attn_prefill_items(whole, q.cpu(), k.cpu(), v.cpu(), bt.cpu(), q_limit, scale, out=out_ref)
+    _close(out, out_ref, atol=0.02, msg="balanced split prefill")
