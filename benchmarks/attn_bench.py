@@ -153,6 +153,28 @@ def main():
         flops = 2 * T * T * Hq * D  # causal: half of 4*T*T*Hq*D
         print(json.dumps({"case": "prefill_causal_2k", "variant": var, "us": round(us, 1),
                           "TF/s": round(flops / us / 1e6, 1)}))
+    # the engine's plan (model_runner.plan_prefill_items): long tiles split into key pieces + per-range merges
+    from kafka_llm_service_amd.engine.model_runner import plan_prefill_items
+
+    for T in (2048, 4096, 8192):
+        qp = torch.randn(T, Hq, D, device=dev, dtype=torch.bfloat16)
+        ql = torch.arange(0, T, dtype=torch.int32, device=dev)
+        o = torch.empty(T, Hq, D, device=dev, dtype=torch.bfloat16)
+        tile = ops.tile_rows(0) // G
+        tiles = [(t0, min(tile, T - t0), 0, t0 + min(tile, T - t0), T) for t0 in range(0, T, tile)]
+        items, splits, ranges = plan_prefill_items(tiles, Hkv, 256, 256)
+        it = torch.tensor(items, dtype=torch.int32, device=dev)
+        part = torch.empty(T, Hq, max(splits, 1), D, device=dev)
+        lse = torch.full((T, Hq, max(splits, 1)), float("-inf"), device=dev)
+
+        def fp():
+            ops.attn_prefill(it, qp, k, v, bt, ql, scale, out=o, out_part=part, lse_part=lse)
+            for lo, hi in ranges:
+                ops.attn_merge(part[lo:hi], lse[lo:hi], o[lo:hi])
+        us = timeit(fp, iters=5)
+        flops = 2 * T * T * Hq * D
+        print(json.dumps({"case": "prefill_causal_planned", "T": T, "splits": splits, "items": len(items),
+                          "us": round(us, 1), "TF/s": round(flops / us / 1e6, 1)}))
 
 
 if __name__ == "__main__":

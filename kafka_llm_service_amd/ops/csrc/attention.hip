@@ -17,7 +17,7 @@
 //   attn_decode_kernel   grid (splits, Hkv, B): one query token per sequence, its G = Hq/Hkv heads packed in the
 //                        q columns, the sequence's keys split over `splits` workgroups and over the 4 waves of each
 //                        (flash-decoding); waves combine through LDS, splits through attn_merge_kernel.
-//   attn_prefill_kernel  grid (work items, Hkv): a tile of up to 128 (token, head) query rows against a paged key
+//   attn_prefill_kernel  grid (Hkv, work items): a tile of up to 128 (token, head) query rows against a paged key
 //                        range; per-row causal limit; writes bf16 output directly or an (O, lse) partial. Used for
 //                        chunked prefill and for the cascade pass where the rows are the decode sequences of a
 //                        batch and the keys are the shared system-prompt prefix (read once for all sequences).
@@ -524,7 +524,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
 }
 
 // ------------------------------------------------------------------------------------------------------------------
-// Prefill / cascade: grid (num_items, Hkv), 256 threads; wave w owns tile rows [32w, 32w+32), row R -> token R / G,
+// Prefill / cascade: grid (Hkv, num_items), 256 or 512 threads; wave w owns tile rows [32w, 32w+32), row R -> token R / G,
 // head kvh*G + R % G.
 // LDS staging for the tile kernel: every 32-key block is loaded ONCE per workgroup (256 threads x 4 x 16 B) and
 // read by all 4 waves from LDS, instead of once per wave from L2 (the 4 waves own different query rows but need the
@@ -705,8 +705,11 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkIte
                                                             int64_t out_stride, float* __restrict__ out_part,
                                                             float* __restrict__ lse_part, int S_total,
                                                             float scale_log2) {
-  const AttnWorkItem it = items[blockIdx.x];
-  const int kvh = blockIdx.y;
+  // grid (Hkv, items): the Hkv heads of an item are consecutive workgroups, so a launch longer than one round of the
+  // CUs starts the host's longest-first items on every head before any short one (and an item's heads read the same
+  // pages together)
+  const AttnWorkItem it = items[blockIdx.y];
+  const int kvh = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int Hq = Hkv * G;
@@ -1012,15 +1015,15 @@ static void launch_prefill(const AttnWorkItem* it, int n_items, const bf16* q, i
                            int bt_stride, const int* q_limit, bf16* out, int64_t out_stride, float* out_part,
                            float* lse_part, int S_total, float scale_log2, int variant, hipStream_t st) {
   if (variant == 0)  // 8 waves, 256 query rows per item, K/V staged in LDS
-    attn_prefill_kernel<128, 8, true, FP8><<<dim3(n_items, Hkv), 512, 0, st>>>(
+    attn_prefill_kernel<128, 8, true, FP8><<<dim3(Hkv, n_items), 512, 0, st>>>(
         it, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
         lse_part, S_total, scale_log2);
   else if (variant == 1)  // 4 waves, 128 rows, LDS
-    attn_prefill_kernel<128, 4, true, FP8><<<dim3(n_items, Hkv), 256, 0, st>>>(
+    attn_prefill_kernel<128, 4, true, FP8><<<dim3(Hkv, n_items), 256, 0, st>>>(
         it, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
         lse_part, S_total, scale_log2);
   else  // 4 waves, 128 rows, per-wave register loads
-    attn_prefill_kernel<128, 4, false, FP8><<<dim3(n_items, Hkv), 256, 0, st>>>(
+    attn_prefill_kernel<128, 4, false, FP8><<<dim3(Hkv, n_items), 256, 0, st>>>(
         it, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
         lse_part, S_total, scale_log2);
 }
@@ -1031,7 +1034,7 @@ extern "C" hipError_t kafka_launch_attn_prefill(const void* items, int n_items, 
                                                bf16* out, int64_t out_stride, float* out_part, float* lse_part,
                                                int S_total, float scale, int variant, hipStream_t st) {
   if (n_items == 0) return hipSuccess;
-  if (D != 128 || G < 1 || G > 32 || (128 % G) != 0) return hipErrorInvalidValue;
+  if (D != 128 || G < 1 || G > 32 || (128 % G) != 0 || n_items > 65535) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
   const auto* it = reinterpret_cast<const AttnWorkItem*>(items);
   if (fp8)
