@@ -11,7 +11,8 @@ import os
 FLAGS = {"backend": "KAFKA_LLM_BACKEND", "model": "KAFKA_MODEL", "weights": "KAFKA_WEIGHTS", "dp": "KAFKA_DP",
          "tp": "KAFKA_TP", "max_model_len": "KAFKA_MAX_MODEL_LEN", "db": "KAFKA_DB", "db_path": "LOCAL_DB_PATH",
          "sandbox": "KAFKA_SANDBOX", "sandbox_url": "LOCAL_SANDBOX_URL", "tool_choice": "KAFKA_TOOL_CHOICE",
-         "prompt_sections": "KAFKA_PROMPT_SECTIONS", "served_model_name": "DEFAULT_MODEL"}
+         "prompt_sections": "KAFKA_PROMPT_SECTIONS", "served_model_name": "DEFAULT_MODEL",
+         "kv_dtype": "KAFKA_KV_DTYPE"}
 
 
 def main() -> None:

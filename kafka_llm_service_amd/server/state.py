@@ -67,7 +67,21 @@ class ServerConfig:
                             ignore_eos=e.get("KAFKA_IGNORE_EOS", "0") == "1",
                             warm_prefix=e.get("KAFKA_WARM_PREFIX", "1") == "1",
                             engine_process=_engine_process(e.get("KAFKA_ENGINE_PROCESS", "auto")),
-                            prompt_sections=[x for x in e.get("KAFKA_PROMPT_SECTIONS", "").split(",") if x] or None)
+                            prompt_sections=[x for x in e.get("KAFKA_PROMPT_SECTIONS", "").split(",") if x] or None,
+                            engine_kwargs=_engine_kwargs(e))
+
+
+def _engine_kwargs(e) -> dict[str, Any]:
+    """Engine options from the environment: KAFKA_KV_DTYPE (bf16 | fp8 KV cache), KAFKA_GRAPHS=1 (hipGraph decode
+    steps), KAFKA_MAX_NUM_SEQS."""
+    kw: dict[str, Any] = {}
+    if e.get("KAFKA_KV_DTYPE"):
+        kw["kv_dtype"] = e["KAFKA_KV_DTYPE"]
+    if e.get("KAFKA_GRAPHS", "0") == "1":
+        kw["use_graphs"] = True
+    if e.get("KAFKA_MAX_NUM_SEQS"):
+        kw["max_num_seqs"] = int(e["KAFKA_MAX_NUM_SEQS"])
+    return kw
 
 
 def _engine_process(v: str) -> bool:
