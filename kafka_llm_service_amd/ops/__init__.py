@@ -169,12 +169,27 @@ def attn_merge(part, lse, out, lse_out=None) -> None:
         ref.attn_merge(part, lse, out, lse_out)
 
 
+_SAMPLE_WS: dict = {}
+
+
+def _sample_ws(dev: torch.device, n: int) -> torch.Tensor:
+    """Sampler workspace: 65536 zeroed per-row tickets (re-armed by the kernel) + split winners; allocated once per
+    device, large enough for graph capture never to allocate."""
+    t = _SAMPLE_WS.get(dev)
+    if t is None or t.numel() < n:
+        t = _SAMPLE_WS[dev] = torch.zeros(max(n, 65536 + 2 * 4096 * 8), dtype=torch.int32, device=dev)
+    return t
+
+
 def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, step=None, out=None) -> torch.Tensor:
     B = logits.shape[0]
     if out is None:
         out = torch.empty(B, dtype=torch.long, device=logits.device)
     if _gpu(logits):
-        ext().sample(logits, temperature, top_p, top_k, seeds, step, out)
+        V = logits.shape[1]
+        nsplit = 8 if V >= 16384 else 1  # a vocabulary row over 8 workgroups (greedy / plain temperature rows)
+        ws = _sample_ws(logits.device, 65536 + 2 * B * nsplit) if nsplit > 1 else None
+        ext().sample(logits, temperature, top_p, top_k, seeds, step, out, ws, nsplit)
     else:
         ref.sample(logits, temperature, top_p, top_k, seeds, step, out)
     return out

@@ -37,7 +37,7 @@ hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows
                              int64_t out_stride, float* lse_out, hipStream_t st);
 hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
                          const float* top_p, const int* top_k, const int64_t* seeds, const int64_t* step,
-                         int64_t* out_tokens, hipStream_t st);
+                         int64_t* out_tokens, int* ws, int nsplit, hipStream_t st);
 int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits);
 hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt, int kc,
                                      int splits, int nt, int kw, int glu, bf16* Y, int64_t ldy, float* P,
@@ -312,7 +312,7 @@ static void attn_merge(at::Tensor part, at::Tensor lse, at::Tensor out, c10::opt
 
 static void sample(at::Tensor logits, c10::optional<at::Tensor> temperature, c10::optional<at::Tensor> top_p,
                    c10::optional<at::Tensor> top_k, c10::optional<at::Tensor> seeds, c10::optional<at::Tensor> step,
-                   at::Tensor out) {
+                   at::Tensor out, c10::optional<at::Tensor> ws, int64_t nsplit) {
   CHECK_CUDA(logits); CHECK_DT(out, at::kLong);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [B, V]");
   const bool is_bf16 = logits.scalar_type() == at::kBFloat16;
@@ -330,10 +330,18 @@ static void sample(at::Tensor logits, c10::optional<at::Tensor> temperature, c10
     TORCH_CHECK(step->scalar_type() == at::kLong && step->numel() >= 1, "step must be int64[1]");
     st = step->data_ptr();
   }
+  int* wp = nullptr;
+  if (ws.has_value() && nsplit > 1) {  // split rows: tickets [65536] | partials [B][nsplit][2]
+    TORCH_CHECK(ws->is_cuda() && ws->scalar_type() == at::kInt && ws->is_contiguous() &&
+                    ws->numel() >= 65536 + 2 * (int64_t)B * nsplit && nsplit <= 64,
+                "sample: workspace must be int32 [>= 65536 + 2 * B * nsplit]");
+    wp = ws->data_ptr<int>();
+  }
   CHECK_HIP(kafka_launch_sample(logits.data_ptr(), is_bf16, logits.stride(0), B, V,
                                  (const float*)fp(temperature, at::kFloat), (const float*)fp(top_p, at::kFloat),
                                  (const int*)fp(top_k, at::kInt), (const int64_t*)fp(seeds, at::kLong),
-                                 (const int64_t*)st, out.data_ptr<int64_t>(), cur_stream()));
+                                 (const int64_t*)st, out.data_ptr<int64_t>(), wp, wp ? (int)nsplit : 1,
+                                 cur_stream()));
 }
 
 // (mt, kc, splits) of the weight-streaming decode GEMM for a shape, or (0, 0, 0) if unsupported
@@ -589,7 +597,8 @@ PYBIND11_MODULE(_kafka_ops, m) {
         py::arg("block_tables"), py::arg("q_limit"), py::arg("out"), py::arg("out_part"), py::arg("lse_part"),
         py::arg("scale"), py::arg("variant") = 0);
   m.def("attn_merge", &attn_merge);
-  m.def("sample", &sample);
+  m.def("sample", &sample, py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"),
+        py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none(), py::arg("nsplit") = 1);
   m.def("wstream_plan", &wstream_plan);
   m.def("wstream_gemm", &wstream_gemm);
   m.def("wstream_gemm_cfg", &wstream_gemm_cfg);

@@ -8,6 +8,10 @@
 //                             pivot to x_c and redraw. Accepted draws are exactly distributed as the renormalised
 //                             top-k/top-p distribution; rounds are bounded (fallback: argmax).
 // All reads are 16-byte vectors; every pass is one streaming read of the row (bf16 or fp32 logits).
+// Greedy and plain-temperature rows (no top-k / top-p) are split over `nsplit` workgroups (grid (B, nsplit)): each
+// takes a slice of the vocabulary, publishes its (value, index) winner, and the last of a row's workgroups to take
+// its ticket reduces them — the noise of index i is the same in every split, so the token is the one-workgroup
+// result. A 64-row decode batch then runs 512 workgroups instead of 64 (128k-entry rows: 62 -> ~10 us).
 #include "common.h"
 
 namespace kafka {
@@ -33,6 +37,7 @@ struct Vec8<float> {
 };
 
 constexpr int SNT = 1024;
+constexpr int SAMPLE_MAX_ROWS = 65536;  // ws: tickets [SAMPLE_MAX_ROWS] | partials [B][nsplit][2]
 
 struct ArgMax {
   float v;
@@ -72,35 +77,69 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
                                                       const float* __restrict__ temperature,
                                                       const float* __restrict__ top_p, const int* __restrict__ top_k,
                                                       const int64_t* __restrict__ seeds, const int64_t* __restrict__ step_ptr,
-                                                      int64_t* __restrict__ out_tokens, int max_rounds) {
+                                                      int64_t* __restrict__ out_tokens, int max_rounds,
+                                                      int* __restrict__ ws) {
   __shared__ float sv[SNT / 64];
   __shared__ int si[SNT / 64];
   __shared__ float red[SNT / 64];
-  const int row = blockIdx.x;
+  const int row = blockIdx.x, sp = blockIdx.y, nsplit = gridDim.y;
   const T* x = logits + (int64_t)row * stride;
   const float temp = temperature ? temperature[row] : 0.f;
   const int nvec = V >> 3;
   const int tail0 = nvec << 3;
+  const float tp = top_p ? top_p[row] : 1.f;
+  const int tk = top_k ? top_k[row] : 0;
+  const bool filtered = temp > 0.f && ((tp < 1.f) || (tk > 0 && tk < V));
 
-  if (!(temp > 0.f)) {
+  if (!filtered) {
+    // argmax of x (greedy) or of x / T + Gumbel noise over this workgroup's slice of the row
+    const bool greedy = !(temp > 0.f);
+    const float inv_t = greedy ? 1.f : 1.f / temp;
+    const uint64_t seed = seeds ? (uint64_t)seeds[row] : 0x1234ull;
+    const uint64_t stream = (uint64_t)(step_ptr ? step_ptr[0] : 0) << 8;  // round 0 of the filtered path
+    const int per = (nvec + nsplit - 1) / nsplit;
+    const int v0 = sp * per, v1 = min(nvec, v0 + per);
     ArgMax a{-INFINITY, 0x7fffffff};
-    for (int vi = threadIdx.x; vi < nvec; vi += SNT) {
+    for (int vi = v0 + threadIdx.x; vi < v1; vi += SNT) {
       float v[8];
       Vec8<T>::load(x + vi * 8, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) a = better(a, ArgMax{v[j], vi * 8 + j});
+      for (int j = 0; j < 8; ++j) {
+        const float xv = v[j] * inv_t;
+        a = better(a, ArgMax{greedy ? xv : xv + gumbel(seed, stream, vi * 8 + j), vi * 8 + j});
+      }
     }
-    for (int i = tail0 + threadIdx.x; i < V; i += SNT) a = better(a, ArgMax{(float)x[i], i});
+    if (sp == nsplit - 1)
+      for (int i = tail0 + threadIdx.x; i < V; i += SNT) {
+        const float xv = (float)x[i] * inv_t;
+        a = better(a, ArgMax{greedy ? xv : xv + gumbel(seed, stream, i), i});
+      }
     a = block_argmax(a, sv, si);
-    if (threadIdx.x == 0) out_tokens[row] = a.i;
+    if (threadIdx.x != 0) return;
+    if (nsplit == 1) {
+      out_tokens[row] = a.i;
+      return;
+    }
+    // ws: tickets (zero, re-armed here) | [B][nsplit][2] (value bits, index)
+    int* tk_row = ws + row;
+    int* part = ws + SAMPLE_MAX_ROWS + ((int64_t)row * nsplit + sp) * 2;
+    __hip_atomic_store(part, __float_as_int(a.v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part + 1, a.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int t = __hip_atomic_fetch_add(tk_row, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (t != nsplit - 1) return;
+    __hip_atomic_store(tk_row, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int* p0 = ws + SAMPLE_MAX_ROWS + (int64_t)row * nsplit * 2;
+    ArgMax r{-INFINITY, 0x7fffffff};
+    for (int k = 0; k < nsplit; ++k)
+      r = better(r, ArgMax{__int_as_float(__hip_atomic_load(p0 + 2 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                           __hip_atomic_load(p0 + 2 * k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)});
+    out_tokens[row] = r.i;
     return;
   }
+  if (sp != 0) return;  // top-k / top-p rows: one workgroup runs the whole-row rejection sampler
   const float inv_t = 1.f / temp;
   const int64_t step = step_ptr ? step_ptr[0] : 0;
-  const float tp = top_p ? top_p[row] : 1.f;
-  const int tk = top_k ? top_k[row] : 0;
   const uint64_t seed = seeds ? (uint64_t)seeds[row] : 0x1234ull;
-  const bool filtered = (tp < 1.f) || (tk > 0 && tk < V);
 
   // pass 1: max of x (needed for the mass test only)
   float mx = -INFINITY;
@@ -194,16 +233,21 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
   if (threadIdx.x == 0) out_tokens[row] = result;
 }
 
+// ws (optional): int32 workspace of >= SAMPLE_MAX_ROWS + 2 * B * nsplit entries whose first SAMPLE_MAX_ROWS are zero
+// (tickets, re-armed by the kernel); without it every row is one workgroup.
 extern "C" hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
                          const float* top_p, const int* top_k, const int64_t* seeds, const int64_t* step,
-                         int64_t* out_tokens, hipStream_t st) {
+                         int64_t* out_tokens, int* ws, int nsplit, hipStream_t st) {
   if (B == 0) return hipSuccess;
+  if (ws == nullptr || nsplit < 1) nsplit = 1;
+  if (B > SAMPLE_MAX_ROWS || nsplit > 64) return hipErrorInvalidValue;
+  const dim3 grid(B, nsplit);
   if (is_bf16)
-    sample_kernel<bf16><<<B, SNT, 0, st>>>(reinterpret_cast<const bf16*>(logits), stride, V, temperature, top_p,
-                                           top_k, seeds, step, out_tokens, 32);
+    sample_kernel<bf16><<<grid, SNT, 0, st>>>(reinterpret_cast<const bf16*>(logits), stride, V, temperature, top_p,
+                                              top_k, seeds, step, out_tokens, 32, ws);
   else
-    sample_kernel<float><<<B, SNT, 0, st>>>(reinterpret_cast<const float*>(logits), stride, V, temperature, top_p,
-                                            top_k, seeds, step, out_tokens, 32);
+    sample_kernel<float><<<grid, SNT, 0, st>>>(reinterpret_cast<const float*>(logits), stride, V, temperature, top_p,
+                                               top_k, seeds, step, out_tokens, 32, ws);
   return hipGetLastError();
 }
 

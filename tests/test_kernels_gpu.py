@@ -495,3 +495,25 @@ def test_attn_prefill_balanced_split(cuda, ctx, qlen):
     out_ref = torch.zeros(qlen, Hq, D, dtype=torch.bfloat16)
     ref.attn_prefill_items(whole, q.cpu(), k.cpu(), v.cpu(), bt.cpu(), q_limit, scale, out=out_ref)
     _close(out, out_ref, atol=0.02, msg="balanced split prefill")
+
+
+def test_sample_split_rows_equal_one_workgroup(cuda):
+    """Greedy and plain-temperature rows split over 8 workgroups (ticket reduce) pick exactly the token of the
+    one-workgroup kernel (same per-index noise); top-k / top-p rows keep the whole-row path. Three launches check
+    that the tickets re-arm."""
+    from kafka_llm_service_amd.ops._ext import ext
+
+    torch.manual_seed(14)
+    B, V = 64, 128256
+    logits = torch.randn(B, V, device=cuda).to(torch.bfloat16)
+    temp = torch.tensor([0.0, 0.7, 1.3, 0.7] * (B // 4), device=cuda)
+    topp = torch.tensor([1.0, 1.0, 1.0, 0.9] * (B // 4), device=cuda)
+    topk = torch.tensor([0, 0, 0, 50] * (B // 4), dtype=torch.int32, device=cuda)
+    seeds = torch.arange(B, dtype=torch.long, device=cuda) * 7 + 3
+    step = torch.tensor([5], dtype=torch.long, device=cuda)
+    one = torch.empty(B, dtype=torch.long, device=cuda)
+    ext().sample(logits, temp, topp, topk, seeds, step, one, None, 1)
+    for it in range(3):
+        split = ops.sample(logits, temp, topp, topk, seeds, step)
+        assert torch.equal(split.cpu(), one.cpu()), f"launch {it}"
+    assert torch.equal(one[0::4].cpu(), logits[0::4].float().argmax(-1).cpu())
