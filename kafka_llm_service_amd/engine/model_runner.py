@@ -299,7 +299,9 @@ class ModelRunner:
         self.max_num_seqs = max_num_seqs
         self.max_blocks = max_blocks_per_seq
         self.G = model.hq // model.hkv
-        self.tile = ops.tile_rows(0) // self.G  # tokens per attention work item
+        # tile-kernel variant (ops.tile_rows): 0 = 8 waves x 256 query rows per workgroup, 1 = 4 waves x 128 rows
+        self.variant = int(os.environ.get("KAFKA_TILE_VARIANT", "0"))
+        self.tile = ops.tile_rows(self.variant) // self.G  # tokens per attention work item
         self.cascade_min_prefix = cascade_min_prefix
         self.target_wgs = int(os.environ.get("KAFKA_CASCADE_WGS", target_wgs))
         self.prefill_kv_chunk = int(os.environ.get("KAFKA_PREFILL_KV_CHUNK", prefill_kv_chunk))
@@ -452,7 +454,7 @@ class ModelRunner:
         B, T, nbt = h.B, h.T, h.nbt
         t_tokens, t_pos, t_slots = d64[0:T], d64[T:2 * T], d64[2 * T:3 * T]
         t_rows = d64[3 * T:3 * T + h.n_rows]
-        meta = AttnMeta(num_decode=B, num_tokens=T, scale=self.model.scale)
+        meta = AttnMeta(num_decode=B, num_tokens=T, scale=self.model.scale, variant=self.variant)
         o = 0
         n_bt = nbt * h.bt_w
         meta.block_tables = d32[o:o + n_bt].view(nbt, h.bt_w)

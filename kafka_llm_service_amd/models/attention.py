@@ -46,6 +46,7 @@ class AttnMeta:
     prefill_lse: torch.Tensor | None = None
     prefill_merge: list = field(default_factory=list)  # (lo, hi) prefill row ranges of split tiles
     scale: float = 1.0
+    variant: int = 0                           # tile-kernel variant (ops.tile_rows): 0 = 8 waves / 256 rows
     extra: dict = field(default_factory=dict)
 
 
@@ -57,19 +58,20 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         qd = q[:B]
         if meta.prefix_items is not None:
             ops.attn_prefill(meta.prefix_items, qd, k_cache, v_cache, meta.block_tables, meta.q_limit,
-                             meta.scale, out_part=meta.part, lse_part=meta.lse)
+                             meta.scale, out_part=meta.part, lse_part=meta.lse, variant=meta.variant)
         # the decode kernel merges each row's prefix partials and its own pieces and writes the final rows
         ops.attn_decode_items(qd, k_cache, v_cache, meta.block_tables, meta.decode_items, meta.part, meta.lse,
                               meta.scale, out=out[:B])
     if meta.prefill_items is not None and meta.num_tokens > B:
         if meta.prefill_splits:
             ops.attn_prefill(meta.prefill_items, q[B:], k_cache, v_cache, meta.block_tables, meta.q_limit[B:],
-                             meta.scale, out=out[B:], out_part=meta.prefill_part, lse_part=meta.prefill_lse)
+                             meta.scale, out=out[B:], out_part=meta.prefill_part, lse_part=meta.prefill_lse,
+                             variant=meta.variant)
             for lo, hi in meta.prefill_merge:
                 ops.attn_merge(meta.prefill_part[lo:hi], meta.prefill_lse[lo:hi], out[B + lo:B + hi])
         else:
             ops.attn_prefill(meta.prefill_items, q[B:], k_cache, v_cache, meta.block_tables, meta.q_limit[B:],
-                             meta.scale, out=out[B:])
+                             meta.scale, out=out[B:], variant=meta.variant)
     return out
 
 

@@ -696,7 +696,7 @@ __device__ __forceinline__ void attn_compute_lds(const char* lds, int key0, int 
 }
 
 template <int D, int NW, bool LDS, bool FP8>
-__global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const AttnWorkItem* __restrict__ items,
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_prefill_kernel(const AttnWorkItem* __restrict__ items,
                                                             const bf16* __restrict__ q, int64_t q_stride,
                                                             const void* __restrict__ k_cache,
                                                             const void* __restrict__ v_cache, int Hkv, int G,
