@@ -128,6 +128,18 @@ MAX_PARTIALS = 64           # partial slots per row that the decode kernel's fus
 MAX_PREFIX_CHUNKS = 32
 
 
+def pad_step_rows(T: int) -> int:
+    """Token rows of a mixed step whose GEMMs go to hipBLASLt (129..256 rows): measured on MI355X (Llama-3-8B shapes,
+    ``benchmarks/gemm_bench.py``, profiles/r02/gemm_sweep_M129_320.log) the library picks slow kernels for 129..152
+    rows (QKV 40 vs 26 us) and at multiples of 32 (down-proj at 192 rows: 101 vs 60 us), so the step is padded with
+    inert rows (no KV slot, no attention item, no logits) to the next 16 k + 8 >= 168."""
+    if T <= 128 or T > 256:
+        return T
+    t = max(T, 168)
+    t += (8 - t % 16) % 16
+    return t if t <= 256 else T
+
+
 def plan_prefill_items(tiles: list[tuple[int, int, int, int, int]], hkv: int, target_wgs: int, min_chunk: int,
                        max_keys: int = MAX_ITEM_KEYS) -> tuple[list[tuple], int, list[tuple[int, int]]]:
     """Work items of the prefill tile kernel from query tiles (q0, count, bt_row, extent, hi): ``extent`` = keys the
@@ -301,6 +313,9 @@ class ModelRunner:
         self.G = model.hq // model.hkv
         # tile-kernel variant (ops.tile_rows): 0 = 8 waves x 256 query rows per workgroup, 1 = 4 waves x 128 rows
         self.variant = int(os.environ.get("KAFKA_TILE_VARIANT", "0"))
+        # mixed steps of 129..256 rows padded away from hipBLASLt's slow sizes (dense TP = 1 GPU models)
+        self.pad_rows = (self.device.type == "cuda" and model.tp == 1 and not getattr(model, "tiled_only", False)
+                         and os.environ.get("KAFKA_PAD_ROWS", "1") == "1")
         self.tile = ops.tile_rows(self.variant) // self.G  # tokens per attention work item
         self.cascade_min_prefix = cascade_min_prefix
         self.target_wgs = int(os.environ.get("KAFKA_CASCADE_WGS", target_wgs))
@@ -334,7 +349,8 @@ class ModelRunner:
         dec = list(batch.decode)
         B = len(dec)
         pre = batch.prefill
-        T = B + sum(e - s for _, s, e in pre)
+        T_real = B + sum(e - s for _, s, e in pre)
+        T = pad_step_rows(T_real) if self.pad_rows else T_real
         rows = B + len(pre)
         nbt = max(1, rows)
         need = max([-(-s.total_len // PAGE) for s in dec] + [-(-b // PAGE) for _, _, b in pre] + [1])
@@ -388,6 +404,11 @@ class ModelRunner:
                 sample_seqs.append(s)
                 logit_rows.append(r + n - 1)
             r += n
+        if T > T_real:  # inert padding rows: token 0 at position 0, no KV write, not attended, no logits
+            tokens[T_real:] = 0
+            positions[T_real:] = 0
+            slots[T_real:] = -1
+            q_limit[T_real:] = 0
         # ---- decode metadata (+ cascade over each group's shared prefix)
         h = HostStep(B=B, T=T, nbt=nbt, bt_w=bt_w, n_rows=len(logit_rows), patch=patch)
         i32_parts = [bt.reshape(-1), q_limit]

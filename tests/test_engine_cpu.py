@@ -367,3 +367,25 @@ def test_plan_prefill_items_balances_causal_tiles():
     turn = [(0, 64, 0, 20000, 20064), (64, 40, 0, 20104, 20104)]
     items, splits, ranges = plan_prefill_items(turn, 8, 256, 256)
     assert 200 <= len(items) * 8 <= 320 and ranges == [(0, 104)]
+
+
+def test_padded_mixed_steps_match_unpadded(base_engine):
+    """Steps of 129..256 token rows padded with inert rows (pad_step_rows) produce the same greedy tokens."""
+    from kafka_llm_service_amd.engine.model_runner import pad_step_rows
+
+    assert [pad_step_rows(t) for t in (64, 128, 129, 160, 168, 170, 185, 192, 250, 256, 300)] == \
+        [64, 128, 168, 168, 168, 184, 200, 200, 250, 256, 300]
+    prompts = _prompts(seed=21, shared=100, tails=(50,))  # first step: one 150-token prefill -> padded to 168 rows
+    ref = _engine(model=base_engine.model).generate(prompts, GREEDY)
+    e = _engine(model=base_engine.model)
+    e.runner.pad_rows = True
+    seen = []
+    orig = e.runner.build_host
+
+    def build_host(batch):
+        h, ss = orig(batch)
+        seen.append(h.T)
+        return h, ss
+    e.runner.build_host = build_host
+    assert e.generate(prompts, GREEDY) == ref
+    assert 168 in seen
