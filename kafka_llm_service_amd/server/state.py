@@ -73,7 +73,7 @@ class ServerConfig:
 
 def _engine_kwargs(e) -> dict[str, Any]:
     """Engine options from the environment: KAFKA_KV_DTYPE (bf16 | fp8 KV cache), KAFKA_GRAPHS=1 (hipGraph decode
-    steps), KAFKA_MAX_NUM_SEQS."""
+    steps), KAFKA_MAX_NUM_SEQS, KAFKA_MAX_BATCHED_TOKENS."""
     kw: dict[str, Any] = {}
     if e.get("KAFKA_KV_DTYPE"):
         kw["kv_dtype"] = e["KAFKA_KV_DTYPE"]
@@ -81,6 +81,8 @@ def _engine_kwargs(e) -> dict[str, Any]:
         kw["use_graphs"] = True
     if e.get("KAFKA_MAX_NUM_SEQS"):
         kw["max_num_seqs"] = int(e["KAFKA_MAX_NUM_SEQS"])
+    if e.get("KAFKA_MAX_BATCHED_TOKENS"):  # prefill tokens per step (smaller: earlier first tokens in a burst)
+        kw["max_num_batched_tokens"] = kw["max_prefill_chunk"] = int(e["KAFKA_MAX_BATCHED_TOKENS"])
     return kw
 
 
