@@ -170,6 +170,7 @@ def attn_merge(part, lse, out, lse_out=None) -> None:
 
 
 _SAMPLE_WS: dict = {}
+_SAMPLE_SPLIT = int(__import__("os").environ.get("KAFKA_SAMPLE_SPLIT", "8"))
 
 
 def _sample_ws(dev: torch.device, n: int) -> torch.Tensor:
@@ -187,7 +188,7 @@ def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, step=No
         out = torch.empty(B, dtype=torch.long, device=logits.device)
     if _gpu(logits):
         V = logits.shape[1]
-        nsplit = 8 if V >= 16384 else 1  # a vocabulary row over 8 workgroups (greedy / plain temperature rows)
+        nsplit = _SAMPLE_SPLIT if V >= 16384 else 1  # a row over 8 workgroups (greedy / plain temperature)
         ws = _sample_ws(logits.device, 65536 + 2 * B * nsplit) if nsplit > 1 else None
         ext().sample(logits, temperature, top_p, top_k, seeds, step, out, ws, nsplit)
     else:

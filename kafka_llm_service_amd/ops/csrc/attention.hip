@@ -955,19 +955,22 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(const float* __restrict
   if (M != -INFINITY) {
     const float* p = part + ((row * Hq + hh) * S) * D + c;
     int s = 0;
+    // a slot with lse = -inf (a row with fewer pieces than S) has weight 0 and was never written: select it away
+    // instead of multiplying (0 x a stale NaN is NaN)
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    auto part_at = [&](int s2, float w) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(p + s2 * D);
+      return w > 0.f ? a * w : z;
+    };
     for (; s + 4 <= S; s += 4) {
       const float w0 = exp2f(l[s] - M), w1 = exp2f(l[s + 1] - M), w2 = exp2f(l[s + 2] - M),
                   w3 = exp2f(l[s + 3] - M);
-      const f32x4 a = *reinterpret_cast<const f32x4*>(p + (s + 0) * D);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(p + (s + 1) * D);
-      const f32x4 cc = *reinterpret_cast<const f32x4*>(p + (s + 2) * D);
-      const f32x4 d = *reinterpret_cast<const f32x4*>(p + (s + 3) * D);
-      acc += a * w0 + b * w1 + cc * w2 + d * w3;
+      acc += part_at(s, w0) + part_at(s + 1, w1) + part_at(s + 2, w2) + part_at(s + 3, w3);
       L += (w0 + w1) + (w2 + w3);
     }
     for (; s < S; ++s) {
       const float w0 = exp2f(l[s] - M);
-      acc += *reinterpret_cast<const f32x4*>(p + s * D) * w0;
+      acc += part_at(s, w0);
       L += w0;
     }
   }

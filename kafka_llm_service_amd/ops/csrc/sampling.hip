@@ -117,7 +117,7 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
     a = block_argmax(a, sv, si);
     if (threadIdx.x != 0) return;
     if (nsplit == 1) {
-      out_tokens[row] = a.i;
+      out_tokens[row] = a.i < V ? a.i : 0;  // an all-NaN row (a broken upstream kernel) must not yield an id >= V
       return;
     }
     // ws: tickets (zero, re-armed here) | [B][nsplit][2] (value bits, index)
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
     for (int k = 0; k < nsplit; ++k)
       r = better(r, ArgMax{__int_as_float(__hip_atomic_load(p0 + 2 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
                            __hip_atomic_load(p0 + 2 * k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)});
-    out_tokens[row] = r.i;
+    out_tokens[row] = r.i < V ? r.i : 0;
     return;
   }
   if (sp != 0) return;  // top-k / top-p rows: one workgroup runs the whole-row rejection sampler
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
     a = block_argmax(a, sv, si);
     result = a.i;
   }
-  if (threadIdx.x == 0) out_tokens[row] = result;
+  if (threadIdx.x == 0) out_tokens[row] = result >= 0 && result < V ? result : 0;
 }
 
 // ws (optional): int32 workspace of >= SAMPLE_MAX_ROWS + 2 * B * nsplit entries whose first SAMPLE_MAX_ROWS are zero

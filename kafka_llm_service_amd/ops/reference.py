@@ -286,7 +286,8 @@ def attn_merge(part, lse, out, lse_out=None):
     Mu = torch.where(torch.isinf(M), torch.zeros_like(M), M)
     f = torch.exp2(l - Mu)
     L = f.sum(-1, keepdim=True)
-    o = (f[..., None] * p).sum(2) / torch.where(L > 0, L, torch.ones_like(L))
+    pz = torch.where(f[..., None] > 0, p, torch.zeros_like(p))  # unwritten slots (lse -inf) may hold anything
+    o = (f[..., None] * pz).sum(2) / torch.where(L > 0, L, torch.ones_like(L))
     out.copy_(o.to(out.dtype))
     if lse_out is not None:
         lse_out.view(rows, -1).copy_(torch.where(L[..., 0] > 0, Mu[..., 0] + torch.log2(L[..., 0]),

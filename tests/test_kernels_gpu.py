@@ -517,3 +517,20 @@ def test_sample_split_rows_equal_one_workgroup(cuda):
         split = ops.sample(logits, temp, topp, topk, seeds, step)
         assert torch.equal(split.cpu(), one.cpu()), f"launch {it}"
     assert torch.equal(one[0::4].cpu(), logits[0::4].float().argmax(-1).cpu())
+
+
+def test_attn_merge_ignores_unwritten_slots(cuda):
+    """Rows with fewer pieces than the partial buffer's S: their extra slots keep lse = -inf and whatever bytes the
+    allocator left there (NaN here) — the merge must not turn 0 x NaN into NaN."""
+    torch.manual_seed(15)
+    rows, Hq, S, D = 40, 32, 4, 128
+    part = torch.randn(rows, Hq, S, D, device=cuda)
+    lse = torch.randn(rows, Hq, S, device=cuda)
+    part[::2, :, 2:] = float("nan")
+    lse[::2, :, 2:] = float("-inf")
+    out = torch.empty(rows, Hq, D, device=cuda, dtype=torch.bfloat16)
+    ops.attn_merge(part, lse, out)
+    ref_out = torch.empty(rows, Hq, D, dtype=torch.bfloat16)
+    ref.attn_merge(part.cpu(), lse.cpu(), ref_out)
+    assert torch.isfinite(out.float()).all() and torch.isfinite(ref_out.float()).all()
+    _close(out, ref_out, atol=0.02, msg="merge with unwritten slots")
