@@ -44,6 +44,7 @@ class EngineConfig:
     max_num_batched_tokens: int = 8192
     max_prefill_chunk: int = 8192
     prefill_tokens_while_decoding: int = 512  # TPOT guard (engine/scheduler.py); 0 = off
+    step_rows_fit: int | None = None    # row fit (engine/scheduler.py); None = env KAFKA_STEP_ROWS_FIT, default 0
     max_model_len: int = 131072
     enable_prefix_cache: bool = True
     use_cascade: bool = True
@@ -160,6 +161,8 @@ class LLMEngine:
                                                max_num_batched_tokens=cfg.max_num_batched_tokens,
                                                max_prefill_chunk=cfg.max_prefill_chunk,
                                                prefill_tokens_while_decoding=cfg.prefill_tokens_while_decoding,
+                                               step_rows_fit=(cfg.step_rows_fit if cfg.step_rows_fit is not None
+                                                              else int(os.environ.get("KAFKA_STEP_ROWS_FIT", "0"))),
                                                max_model_len=cfg.max_model_len, max_blocks_per_seq=max_blocks),
                                self.kvm)
         kc = [self.k_cache[i] for i in range(L)]

@@ -33,6 +33,13 @@ class SchedulerConfig:
     # for one ~100 ms step; a new turn of a cached thread (tens of tokens) still fits in the next step
     prefill_tokens_while_decoding: int = 512
     tpot_guard_decodes: int = 16
+    # Row fit: while the guard holds, prefill is also capped so the whole step stays within `step_rows_fit` rows
+    # (0 = off) as long as that leaves at least `step_rows_fit_min` prefill tokens. Steps of <= 128 rows run the
+    # weight-streaming decode GEMM (ops.STREAM_MAX_M); a 64-stream step that admits 100 new-turn tokens would
+    # otherwise take hipBLASLt at M = 164 (~172 vs ~128 us of GEMM per Llama-3-8B layer, profiles/wstream_sweep_r01.log,
+    # profiles/r02/gemm_sweep_M129_320.log). A new turn longer than the room is chunked over two steps.
+    step_rows_fit: int = 0
+    step_rows_fit_min: int = 32
 
 
 @dataclass
@@ -133,6 +140,9 @@ class Scheduler:
             budget -= 1
         if cfg.prefill_tokens_while_decoding and len(batch.decode) >= cfg.tpot_guard_decodes:
             budget = min(budget, cfg.prefill_tokens_while_decoding)
+            room = cfg.step_rows_fit - len(batch.decode)
+            if cfg.step_rows_fit and room >= cfg.step_rows_fit_min:
+                budget = min(budget, room)
         # 2. running prefills
         for seq in list(self.running):
             if budget <= 0:

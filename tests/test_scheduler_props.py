@@ -110,3 +110,42 @@ def test_tpot_guard_caps_prefill_while_decoding():
     sch.add(big)
     b = sch.schedule()
     assert len(b.decode) == 4 and sum(e - s for _, s, e in b.prefill) == 512
+
+
+def test_step_rows_fit_keeps_mixed_steps_on_the_streaming_gemm():
+    """With the row fit on, a step with D decodes takes at most fit - D prefill tokens (while that is >= the fit
+    minimum), so the step stays on the weight-streaming GEMM; the rest of the turn follows in the next step. With
+    fewer rows of room than the minimum, only the TPOT guard applies."""
+    from kafka_llm_service_amd.engine.scheduler import Scheduler, SchedulerConfig
+    from kafka_llm_service_amd.engine.sequence import SamplingParams, Sequence
+    from kafka_llm_service_amd.runtime import KVManager
+
+    def setup(n_dec, fit):
+        kv = KVManager(8192, 16, True)
+        sch = Scheduler(SchedulerConfig(max_num_batched_tokens=8192, prefill_tokens_while_decoding=512,
+                                        tpot_guard_decodes=4, step_rows_fit=fit, step_rows_fit_min=32), kv)
+        sp = SamplingParams(max_tokens=8, ignore_eos=True)
+        decs = [Sequence(f"d{i}", list(range(100 * i + 1, 100 * i + 33)), sp) for i in range(n_dec)]
+        for d in decs:
+            sch.add(d)
+        sch.schedule()
+        for d in decs:
+            d.num_computed = d.total_len
+            d.output_ids.append(7)
+            kv.append_token(d.seq_id, 7)
+        return sch, sp
+
+    sch, sp = setup(64, 128)
+    turn = Sequence("turn", list(range(50000, 50000 + 90)), sp)
+    sch.add(turn)
+    b = sch.schedule()
+    assert len(b.decode) == 64 and b.num_tokens == 128 and b.prefill == [(turn, 0, 64)]
+    turn.num_computed = 64
+    b = sch.schedule()
+    assert b.prefill == [(turn, 64, 90)] and b.num_tokens == 64 + 26
+    sch, sp = setup(100, 128)  # 28 rows of room < 32: the guard's 512 applies
+    sch.add(Sequence("turn", list(range(50000, 50000 + 90)), sp))
+    assert sum(e - s for _, s, e in sch.schedule().prefill) == 90
+    sch, sp = setup(64, 0)  # off
+    sch.add(Sequence("turn", list(range(50000, 50000 + 90)), sp))
+    assert sum(e - s for _, s, e in sch.schedule().prefill) == 90
