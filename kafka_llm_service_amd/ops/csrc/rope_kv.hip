@@ -25,6 +25,8 @@
 //           o at byte 2048 + o, V of key o at byte 2064 + vt_pos(o) (the order in which the PV step's P registers
 //           hold the keys, so a lane's 8 V exponents of a page are one 8-B load).
 //   V page  2048 B: V^T [D][16] e4m3, key o at position vt_pos(o) (as the bf16 layout).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace kafka {
@@ -52,7 +54,7 @@ __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ 
   const int n_total = n_rope + Hkv * VU;
   const int64_t blk = slot >= 0 ? slot / block_size : 0;
   const int off = slot >= 0 ? (int)(slot % block_size) : 0;
-  for (int u = threadIdx.x; u < n_total; u += blockDim.x) {
+  for (int u = blockIdx.y * blockDim.x + threadIdx.x; u < n_total; u += gridDim.y * blockDim.x) {
     if (u < n_rope) {
       const int head = u / RU;
       const int c = (u % RU) * 8;
@@ -242,13 +244,27 @@ extern "C" hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int
   if (D != 128 && D != 64) return hipErrorInvalidValue;
   // one thread per work unit (8 rotation pairs of a Q/K head, or 8 V elements), so a token's whole row is one
   // round of loads instead of a strided loop paying the HBM latency twice (448 units for Llama-3-8B)
+  // A token's units are spread over gridDim.y workgroups of 64 threads (env KAFKA_ROPE_WG overrides; 0 = one
+  // workgroup per token): at decode T is the batch (64), and one workgroup per token leaves 3/4 of the CUs idle
+  // while each busy CU pulls the token's S slabs (~100 KB) through its own L2 port. Bench A/B
+  // (profiles/r02/rope_wg_ab.jsonl): 64 -> +0.5 % tok/s over one workgroup per token (128 / 256 in between).
+  static const int wg_env = [] {
+    const char* e = getenv("KAFKA_ROPE_WG");
+    return e ? atoi(e) : 64;
+  }();
   const int units = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
-  const int nt = units <= 256 ? 256 : (units <= 512 ? 512 : 1024);
+  int nt = units <= 256 ? 256 : (units <= 512 ? 512 : 1024);
+  int ny = 1;
+  if (wg_env >= 64 && wg_env <= 1024 && wg_env % 64 == 0 && wg_env < units) {
+    nt = wg_env;
+    ny = (units + nt - 1) / nt;
+  }
+  const dim3 grid(T, ny);
   if (D == 128)
-    rope_kv_kernel<128><<<T, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
+    rope_kv_kernel<128><<<grid, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
                                           v_cache, slot_mapping, Hq, Hkv, block_size);
   else
-    rope_kv_kernel<64><<<T, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
+    rope_kv_kernel<64><<<grid, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
                                          v_cache, slot_mapping, Hq, Hkv, block_size);
   return hipGetLastError();
 }
