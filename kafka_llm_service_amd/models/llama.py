@@ -15,6 +15,7 @@ synthetic benchmarks — no checkpoints are downloadable here) is the default.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -24,6 +25,13 @@ from kafka_llm_service_amd import ops
 from kafka_llm_service_amd.models.attention import AttnMeta, paged_attention
 from kafka_llm_service_amd.models.config import ModelConfig
 from kafka_llm_service_amd.parallel import state as pstate
+
+# env KAFKA_FUSE_QKV_ROPE=1: decode-sized steps run RoPE + the paged KV write in the streaming QKV GEMM's epilogue
+# (ops.linear_stream_rope) instead of the rope_kv kernel. Correct (tests/test_kernels_gpu.py::test_wstream_qkv_rope)
+# but measured 4 % SLOWER (7,160 vs 7,477 tok/s, profiles/r02/qkv_rope_fused_ab_rejected.jsonl): the split-K ticket
+# adds write-through partial stores, a device-scope atomic and uncached partial loads to the GEMM's tail — more
+# serialized round trips than the 5.7 us rope_kv launch it removes. Off by default.
+FUSE_QKV_ROPE = os.environ.get("KAFKA_FUSE_QKV_ROPE", "0") == "1"
 
 
 @dataclass
@@ -163,6 +171,8 @@ class TransformerLM:
         eps = cfg.rms_norm_eps
         tp = self.tp > 1
         delta, pending = None, False
+        fuse_rope = (self.stream and FUSE_QKV_ROPE and 0 < T <= ops.STREAM_MAX_M and self.layers[0].qkv_t is not None
+                     and ops.qkv_rope_fusable(k_caches[0], self.D))
         for i, lw in enumerate(self.layers):
             if delta is None:
                 ops.rmsnorm(h, lw.input_norm, eps, out=x)
@@ -171,9 +181,13 @@ class TransformerLM:
                 pstate.tp_all_reduce_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x)
             else:
                 ops.fused_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x)
-            qkv = self._linear(x, lw.qkv, lw.qkv_t)
-            ops.rope_kv_write(qkv, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i], inp.slot_mapping,
-                              self.hq, self.hkv)
+            if fuse_rope:  # RoPE + KV write in the streaming QKV GEMM's epilogue (no rope_kv launch)
+                ops.linear_stream_rope(x, lw.qkv_t, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i],
+                                       inp.slot_mapping, self.hq, self.hkv)
+            else:
+                qkv = self._linear(x, lw.qkv, lw.qkv_t)
+                ops.rope_kv_write(qkv, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i], inp.slot_mapping,
+                                  self.hq, self.hkv)
             paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out)
             o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t)
             if tp:

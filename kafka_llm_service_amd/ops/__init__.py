@@ -89,12 +89,13 @@ def rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping
 _TICKETS: dict = {}
 
 
-def _tickets(dev: torch.device, n: int) -> torch.Tensor:
-    """Zeroed int32 counters for the decode kernel's ticket merge (re-armed by the kernel itself, so one buffer per
-    device serves every layer and step; allocated once, large, so graph capture never allocates)."""
-    t = _TICKETS.get(dev)
+def _tickets(dev: torch.device, n: int, pool: str = "decode") -> torch.Tensor:
+    """Zeroed int32 counters for a kernel's ticket merge (re-armed by the kernel itself, so one buffer per device and
+    pool serves every layer and step; allocated once, large, so graph capture never allocates). Pools: "decode"
+    (decode attention, per row x kv head), "qkv_rope" (fused QKV epilogue, per head tile)."""
+    t = _TICKETS.get((dev, pool))
     if t is None or t.numel() < n:
-        t = _TICKETS[dev] = torch.zeros(max(n, 1 << 16), dtype=torch.int32, device=dev)
+        t = _TICKETS[(dev, pool)] = torch.zeros(max(n, 1 << 16), dtype=torch.int32, device=dev)
     return t
 
 
@@ -263,6 +264,31 @@ def linear_stream(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, nt: bo
         return y.to(x.dtype)
     ks = K // S
     return torch.stack([xf[:, s * ks:(s + 1) * ks] @ w[:, s * ks:(s + 1) * ks].t() for s in range(S)])
+
+
+def qkv_rope_fusable(k_cache: torch.Tensor, D: int) -> bool:
+    """Whether linear_stream_rope covers this cache (bf16 pages, head dim 128; fp8 keeps rope_kv_write)."""
+    return D == 128 and k_cache.dtype == torch.bfloat16
+
+
+def linear_stream_rope(x, wt, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq: int, Hkv: int,
+                       max_splits: int = 8) -> None:
+    """QKV projection of a decode-sized step (wave-tiled weight ``wt``, N = (Hq + 2 Hkv) * 128) with RoPE and the
+    paged KV write fused into the streaming GEMM's epilogue: the same results as ``linear_stream`` followed by
+    ``rope_kv_write``, without the rope_kv launch (the last split-K workgroup of each head tile finishes it)."""
+    M, K = x.shape
+    N = wt.shape[0] * 32
+    plan = stream_plan(M, N, K, max_splits)
+    if plan is None or N != (Hq + 2 * Hkv) * 128:
+        raise ValueError(f"linear_stream_rope: unsupported shape M={M} N={N} K={K}")
+    if _gpu(x):
+        S = plan[2]
+        p = torch.empty(S, M, N, dtype=torch.float32, device=x.device) if S > 1 else None
+        ext().wstream_qkv_rope(x, wt, p, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, int(Hq),
+                               int(Hkv), _tickets(x.device, N // 128, pool="qkv_rope"), int(max_splits))
+        return
+    rope_kv_write(linear_stream(x, wt, max_splits), positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq,
+                  Hkv)
 
 
 def linear_glu(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8) -> torch.Tensor:

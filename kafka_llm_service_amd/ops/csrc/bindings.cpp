@@ -43,6 +43,10 @@ hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt,
                                      int splits, int nt, int kw, int glu, bf16* Y, int64_t ldy, float* P,
                                      hipStream_t st);
 hipError_t kafka_launch_slab_reduce(const float* P, int S, int M, int N, bf16* Y, int64_t ldy, hipStream_t st);
+hipError_t kafka_launch_wstream_qkv_rope(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt,
+                                         int kc, int splits, float* P, const int64_t* positions, const float* cos_sin,
+                                         bf16* q_out, int64_t q_stride, bf16* k_cache, bf16* v_cache,
+                                         const int64_t* slots, int Hq, int Hkv, int* tickets, hipStream_t st);
 hipError_t kafka_launch_wstream_grouped(const bf16* X, int64_t ldx, const bf16* Wt, int e_local, int N, int K,
                                         const int* perm_tok, const float* perm_w, const int* expert_off, int e_lo,
                                         int max_rows, int gather, bf16* Y, int64_t ldy, float* out, int64_t ldo,
@@ -385,6 +389,49 @@ static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> 
                                       yp, ldy, pp, cur_stream()));
 }
 
+// QKV projection on the streaming kernel with RoPE + the paged KV write in its epilogue (bf16 cache, head dim 128):
+// replaces wstream_gemm + rope_kv_write on decode-sized steps. p: fp32 scratch [splits, M, N] when the plan splits K.
+static void wstream_qkv_rope(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> p, at::Tensor positions,
+                             at::Tensor cos_sin, at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache,
+                             c10::optional<at::Tensor> slot_mapping, int64_t Hq, int64_t Hkv, at::Tensor tickets,
+                             int64_t max_splits) {
+  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
+  CHECK_DT(positions, at::kLong); CHECK_DT(cos_sin, at::kFloat); CHECK_DT(q_out, at::kBFloat16);
+  CHECK_DT(k_cache, at::kBFloat16); CHECK_DT(v_cache, at::kBFloat16); CHECK_DT(tickets, at::kInt);
+  TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0, "wstream_qkv_rope: x must be [M, K] with 16-B rows");
+  TORCH_CHECK(wt.dim() == 4 && wt.is_contiguous() && wt.size(2) == 64 && wt.size(3) == 8, "wstream_qkv_rope: wt");
+  const int M = x.size(0), K = x.size(1), N = wt.size(0) * 32;
+  TORCH_CHECK(wt.size(1) * 16 == K && N == (Hq + 2 * Hkv) * 128, "wstream_qkv_rope: K / N mismatch");
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && k_cache.dim() == 4 && v_cache.dim() == 4 &&
+                  k_cache.size(1) == Hkv && k_cache.size(2) == 16 && k_cache.size(3) == 128 &&
+                  v_cache.size(1) == Hkv && v_cache.size(2) == 128 && v_cache.size(3) == 16 &&
+                  v_cache.size(0) == k_cache.size(0), "wstream_qkv_rope: cache shape");
+  TORCH_CHECK(positions.is_contiguous() && positions.numel() == M && cos_sin.is_contiguous() && cos_sin.dim() == 2 &&
+                  cos_sin.size(1) == 128, "wstream_qkv_rope: positions / cos_sin");
+  TORCH_CHECK(q_out.dim() == 3 && q_out.size(0) == M && q_out.size(1) == Hq && q_out.size(2) == 128 &&
+                  q_out.stride(2) == 1 && q_out.stride(1) == 128, "wstream_qkv_rope: q_out shape");
+  TORCH_CHECK(tickets.is_contiguous() && tickets.numel() >= N / 128, "wstream_qkv_rope: tickets");
+  const int64_t* sm = nullptr;
+  if (slot_mapping.has_value()) {
+    CHECK_DT(slot_mapping.value(), at::kLong);
+    TORCH_CHECK(slot_mapping->is_contiguous() && slot_mapping->numel() == M, "wstream_qkv_rope: slot_mapping");
+    sm = slot_mapping->data_ptr<int64_t>();
+  }
+  int mt = 0, kc = 0, s = 0;
+  TORCH_CHECK(kafka_wstream_plan(M, N, K, (int)max_splits, &mt, &kc, &s) == 0, "wstream_qkv_rope: unsupported shape");
+  float* pp = nullptr;
+  if (s > 1) {
+    TORCH_CHECK(p.has_value(), "wstream_qkv_rope: scratch required for a split plan");
+    CHECK_DT(p.value(), at::kFloat);
+    TORCH_CHECK(p->is_contiguous() && p->numel() >= (int64_t)s * M * N, "wstream_qkv_rope: scratch too small");
+    pp = p->data_ptr<float>();
+  }
+  CHECK_HIP(kafka_launch_wstream_qkv_rope(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, pp,
+                                          positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), bptr(q_out),
+                                          q_out.stride(0), bptr(k_cache), bptr(v_cache), sm, (int)Hq, (int)Hkv,
+                                          tickets.data_ptr<int>(), cur_stream()));
+}
+
 // explicit-configuration variant (microbenchmark sweeps): (mt, kc, splits) as given, no planning
 static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y, c10::optional<at::Tensor> p,
                              int64_t mt, int64_t kc, int64_t s, bool nt, int64_t kw) {
@@ -601,6 +648,7 @@ PYBIND11_MODULE(_kafka_ops, m) {
         py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none(), py::arg("nsplit") = 1);
   m.def("wstream_plan", &wstream_plan);
   m.def("wstream_gemm", &wstream_gemm);
+  m.def("wstream_qkv_rope", &wstream_qkv_rope);
   m.def("wstream_gemm_cfg", &wstream_gemm_cfg);
   m.def("slab_reduce", &slab_reduce);
   m.def("wstream_grouped", &wstream_grouped);

@@ -1,4 +1,6 @@
 // Rotary embedding on Q/K fused with the paged KV-cache write (gfx950).
+// (Decode-sized steps with a bf16 cache run the same math in the streaming QKV GEMM's epilogue instead —
+// wstream_gemm.hip, RopeKV; this kernel serves prefill, the fp8 cache and the hipBLASLt path.)
 //
 // Input is the fused QKV projection output [T, (Hq + 2*Hkv) * D] — bf16, or S fp32 split-K slabs of the decode
 // GEMM (wstream_gemm.hip) summed while loading. One workgroup per token, one thread per 8-element unit:

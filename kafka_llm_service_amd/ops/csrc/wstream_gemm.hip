@@ -25,11 +25,31 @@
 
 namespace kafka {
 
-template <int MT, int KC, bool NT, int KW>
+// QKV-projection epilogue (ROPE instantiations): rotate-half RoPE on the q / k heads, q to q_out, k / v straight
+// into their paged-cache layouts (bf16 cache, head dim 128, 16-token pages: the layouts of rope_kv.hip) — the
+// rope_kv kernel and its launch gap leave the decode step. A 128-column workgroup tile is exactly one head. With
+// split-K (S > 1) every split publishes its fp32 partial with agent-coherent write-through stores and takes a
+// ticket; the LAST split of a column tile sums the others (agent-coherent loads; no fence that would write back the
+// whole L2, see attention.hip's ticket merge), applies the epilogue and re-arms the counter.
+struct RopeKV {
+  const int64_t* positions;  // [M]
+  const float* cos_sin;      // [max_pos, 128]: cos in [0, 64), sin in [64, 128)
+  bf16* q_out;               // [M, Hq, 128] (row stride q_stride)
+  int64_t q_stride;
+  bf16* k_cache;             // [blocks, Hkv, 16, 128] as 16 chunk planes [16 keys][8]
+  bf16* v_cache;             // [blocks, Hkv, 128, 16] V^T, key o at rope_vt_pos(o)
+  const int64_t* slots;      // [M] cache slot per row (-1: no KV write), or nullptr
+  int Hq, Hkv;
+  int* tickets;              // [N / 128] zeroed once, re-armed by the last split
+};
+
+__device__ __forceinline__ int rope_vt_pos(int o) { return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1); }
+
+template <int MT, int KC, bool NT, int KW, bool ROPE = false>
 __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                                  const bf16x8* __restrict__ Wt, int M, int N, int K,
                                                                  int ks, bf16* __restrict__ Y, int64_t ldy,
-                                                                 float* __restrict__ P, int glu) {
+                                                                 float* __restrict__ P, int glu, RopeKV ra) {
   constexpr int NTH = 256 * KW;
   constexpr int ROWS = 32 * MT;
   constexpr int CPR = KC / 8;             // 16-B chunks per X row of one K chunk
@@ -145,6 +165,87 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
 #pragma unroll
           for (int i = 0; i < 16; ++i) acc[mt][i] += red[((((j - 1) * 4 + ct) * MT + mt) * 16 + i) * 64 + lane];
     }
+  }
+  if constexpr (ROPE) {
+    static_assert(KW == 1, "rope epilogue: one K part per chunk");
+    __shared__ int s_last;
+    const int S = gridDim.y;
+    const int n = nb * 32 + r;  // N % 128 == 0 (host-checked): every wave is active
+    if (S > 1) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (m < M)
+            __hip_atomic_store(P + ((int64_t)blockIdx.y * M + m) * N + n, acc[mt][i], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        int* tk = ra.tickets + blockIdx.x;
+        const int t = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = t == S - 1;
+        if (t == S - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (!s_last) return;
+      for (int s2 = 0; s2 < S; ++s2) {
+        if (s2 == (int)blockIdx.y) continue;
+        float v[MT][16];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int m = min(mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h, M - 1);
+            v[mt][i] = __hip_atomic_load(P + ((int64_t)s2 * M + m) * N + n, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+          }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[mt][i] += v[mt][i];
+      }
+    }
+    // rotate-half partner d +- 64 lives in wave ct ^ 2 (same lane): exchange through LDS (the X stage is dead)
+    float* red = reinterpret_cast<float*>(&xs[0][0]);
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[((ct * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
+    __syncthreads();
+    const int head = blockIdx.x, d = 32 * ct + r, j = d & 63;
+    const bool is_q = head < ra.Hq, is_k = !is_q && head < ra.Hq + ra.Hkv;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (m >= M) continue;
+        float y = acc[mt][i];
+        if (is_q || is_k) {
+          const float xp = red[(((ct ^ 2) * MT + mt) * 16 + i) * 64 + lane];
+          const float* cs = ra.cos_sin + ra.positions[m] * 128;
+          const float c = cs[j], sn = cs[64 + j];
+          y = ct < 2 ? y * c - xp * sn : y * c + xp * sn;
+        }
+        if (is_q) {
+          ra.q_out[(int64_t)m * ra.q_stride + head * 128 + d] = (bf16)y;
+        } else if (ra.slots != nullptr) {
+          const int64_t slot = ra.slots[m];
+          if (slot >= 0) {
+            const int64_t blk = slot >> 4;
+            const int off = (int)(slot & 15);
+            if (is_k)
+              ra.k_cache[(blk * ra.Hkv + (head - ra.Hq)) * 2048 + ((d >> 3) * 16 + off) * 8 + (d & 7)] = (bf16)y;
+            else
+              ra.v_cache[(blk * ra.Hkv + (head - ra.Hq - ra.Hkv)) * 2048 + d * 16 + rope_vt_pos(off)] = (bf16)y;
+          }
+        }
+      }
+    return;
   }
   if (glu && P == nullptr) {
     // fused SwiGLU epilogue (weight tiles GLU-interleaved: tile 2j = gate rows [32j, 32j+32), tile 2j+1 = the
@@ -389,9 +490,11 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
 #define KAFKA_WS(MT_, KC_, KW_)                                                                             \
   do {                                                                                                     \
     if (nt)                                                                                                \
-      wstream_gemm_kernel<MT_, KC_, true, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu); \
+      wstream_gemm_kernel<MT_, KC_, true, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, \
+                                                                           RopeKV{});                               \
     else                                                                                                   \
-      wstream_gemm_kernel<MT_, KC_, false, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu); \
+      wstream_gemm_kernel<MT_, KC_, false, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, \
+                                                                            RopeKV{});                              \
   } while (0)
   if (mt == 1 && kc == 256 && kw == 1) KAFKA_WS(1, 256, 1);
   else if (mt == 1 && kc == 256 && kw == 2) KAFKA_WS(1, 256, 2);
@@ -404,6 +507,31 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   else if (mt == 4 && kc == 128 && kw == 2) KAFKA_WS(4, 128, 2);
   else return hipErrorInvalidValue;
 #undef KAFKA_WS
+  return hipGetLastError();
+}
+
+// QKV projection + RoPE + paged KV write (see RopeKV): the plan's (mt, kc, splits); P = fp32 scratch
+// [splits, M, N] when splits > 1; N = (Hq + 2 Hkv) * 128.
+extern "C" hipError_t kafka_launch_wstream_qkv_rope(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K,
+                                                   int mt, int kc, int splits, float* P, const int64_t* positions,
+                                                   const float* cos_sin, bf16* q_out, int64_t q_stride,
+                                                   bf16* k_cache, bf16* v_cache, const int64_t* slots, int Hq,
+                                                   int Hkv, int* tickets, hipStream_t st) {
+  if (M < 1) return hipSuccess;
+  if (N != (Hq + 2 * Hkv) * 128 || K % (kc * splits) != 0 || (splits > 1 && (P == nullptr || tickets == nullptr)))
+    return hipErrorInvalidValue;
+  const dim3 grid(N / 128, splits);
+  const int ks = K / splits;
+  const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
+  const RopeKV ra{positions, cos_sin, q_out, q_stride, k_cache, v_cache, slots, Hq, Hkv, tickets};
+  if (mt == 1 && kc == 256)
+    wstream_gemm_kernel<1, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra);
+  else if (mt == 2 && kc == 256)
+    wstream_gemm_kernel<2, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra);
+  else if (mt == 4 && kc == 128)
+    wstream_gemm_kernel<4, 128, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
