@@ -18,6 +18,7 @@ the decode path is hipGraph-capturable (fixed shapes per batch bucket).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -50,10 +51,47 @@ class AttnMeta:
     extra: dict = field(default_factory=dict)
 
 
+# Mixed steps: the new-turn prefill tiles (MFMA/LDS-bound) are independent of the decode path (HBM-bound) inside a
+# layer — both read the post-RoPE q and write disjoint rows of out — so with KAFKA_PREFILL_STREAM=1 they run on a
+# side stream concurrently with the cascade + decode kernels (joined before the O projection).
+PREFILL_STREAM = os.environ.get("KAFKA_PREFILL_STREAM", "0") == "1"
+_SIDE: dict = {}
+
+
+def _side_stream(dev: torch.device):
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = (torch.cuda.Stream(device=dev), [torch.cuda.Event() for _ in range(2)])
+    return s
+
+
+def _prefill_part(q, k_cache, v_cache, meta: AttnMeta, out: torch.Tensor) -> None:
+    B = meta.num_decode
+    if meta.prefill_splits:
+        ops.attn_prefill(meta.prefill_items, q[B:], k_cache, v_cache, meta.block_tables, meta.q_limit[B:],
+                         meta.scale, out=out[B:], out_part=meta.prefill_part, lse_part=meta.prefill_lse,
+                         variant=meta.variant)
+        for lo, hi in meta.prefill_merge:
+            ops.attn_merge(meta.prefill_part[lo:hi], meta.prefill_lse[lo:hi], out[B + lo:B + hi])
+    else:
+        ops.attn_prefill(meta.prefill_items, q[B:], k_cache, v_cache, meta.block_tables, meta.q_limit[B:],
+                         meta.scale, out=out[B:], variant=meta.variant)
+
+
 def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, meta: AttnMeta,
                     out: torch.Tensor) -> torch.Tensor:
     """q [T, Hq, D] (post-RoPE) -> out [T, Hq, D] bf16."""
     B = meta.num_decode
+    has_prefill = meta.prefill_items is not None and meta.num_tokens > B
+    side = None
+    if has_prefill and B > 0 and PREFILL_STREAM and q.is_cuda and not torch.cuda.is_current_stream_capturing():
+        side, (ev_q, ev_done) = _side_stream(q.device)
+        main = torch.cuda.current_stream(q.device)
+        ev_q.record(main)
+        with torch.cuda.stream(side):
+            side.wait_event(ev_q)
+            _prefill_part(q, k_cache, v_cache, meta, out)
+            ev_done.record(side)
     if B > 0:
         qd = q[:B]
         if meta.prefix_items is not None:
@@ -62,16 +100,10 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         # the decode kernel merges each row's prefix partials and its own pieces and writes the final rows
         ops.attn_decode_items(qd, k_cache, v_cache, meta.block_tables, meta.decode_items, meta.part, meta.lse,
                               meta.scale, out=out[:B])
-    if meta.prefill_items is not None and meta.num_tokens > B:
-        if meta.prefill_splits:
-            ops.attn_prefill(meta.prefill_items, q[B:], k_cache, v_cache, meta.block_tables, meta.q_limit[B:],
-                             meta.scale, out=out[B:], out_part=meta.prefill_part, lse_part=meta.prefill_lse,
-                             variant=meta.variant)
-            for lo, hi in meta.prefill_merge:
-                ops.attn_merge(meta.prefill_part[lo:hi], meta.prefill_lse[lo:hi], out[B + lo:B + hi])
-        else:
-            ops.attn_prefill(meta.prefill_items, q[B:], k_cache, v_cache, meta.block_tables, meta.q_limit[B:],
-                             meta.scale, out=out[B:], variant=meta.variant)
+    if side is not None:
+        torch.cuda.current_stream(q.device).wait_event(ev_done)
+    elif has_prefill:
+        _prefill_part(q, k_cache, v_cache, meta, out)
     return out
 
 

@@ -318,7 +318,7 @@ struct DecodeItem {
   int b, lo, hi, split, nsplit, npre, pad0, pad1;
 };
 
-template <int D, bool HEADS_FAST, bool FP8>
+template <int D, bool HEADS_FAST, bool FP8, int MG = 16>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
                                                            const void* __restrict__ k_cache,
                                                            const void* __restrict__ v_cache, int Hkv, int G,
@@ -421,12 +421,13 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
       f32x4 acc4 = Ls > 0.f ? os * (sW[g][split_offset] / Ls) : f32x4{0.f, 0.f, 0.f, 0.f};
       const float* pp = out_part + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
       int s2 = 0;
-      for (; s2 + 8 <= split_offset; s2 += 8) {
-        f32x4 v[8];
+      // MG prefix partials per round trip (the cascade writes 32 per row: 2 round trips at MG = 16, 4 at 8)
+      for (; s2 + MG <= split_offset; s2 += MG) {
+        f32x4 v[MG];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const f32x4*>(pp + (s2 + j) * D);
+        for (int j = 0; j < MG; ++j) v[j] = *reinterpret_cast<const f32x4*>(pp + (s2 + j) * D);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc4 += v[j] * sW[g][s2 + j];
+        for (int j = 0; j < MG; ++j) acc4 += v[j] * sW[g][s2 + j];
       }
       for (; s2 < split_offset; ++s2) acc4 += *reinterpret_cast<const f32x4*>(pp + s2 * D) * sW[g][s2];
       const float inv = sWt[g] > 0.f ? 1.f / sWt[g] : 0.f;
@@ -1004,11 +1005,24 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
     kern<<<grid, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, di, B, out_part,
                                lse_part, S_total, scale_log2, out, out_stride, tickets);
   };
+  // prefix partials per load round trip in the fused merge (env KAFKA_DECODE_MERGE_GROUP = 8 / 16 / 32; bench A/B
+  // profiles/r02/decode_merge_group_ab.jsonl: 7,491 / 7,489 / 7,505 tok/s — the epilogue is not on the critical path)
+  static const int mg = [] {
+    const char* e = getenv("KAFKA_DECODE_MERGE_GROUP");
+    const int v = e ? atoi(e) : 32;
+    return v == 8 || v == 16 ? v : 32;
+  }();
   const dim3 hf(Hkv, n_items), sf(n_items, Hkv);
   if (fp8)
     heads_fast ? go(attn_decode_kernel<128, true, true>, hf) : go(attn_decode_kernel<128, false, true>, sf);
+  else if (!heads_fast)
+    go(attn_decode_kernel<128, false, false>, sf);
+  else if (mg == 8)
+    go(attn_decode_kernel<128, true, false, 8>, hf);
+  else if (mg == 32)
+    go(attn_decode_kernel<128, true, false, 32>, hf);
   else
-    heads_fast ? go(attn_decode_kernel<128, true, false>, hf) : go(attn_decode_kernel<128, false, false>, sf);
+    go(attn_decode_kernel<128, true, false, 16>, hf);
   return hipGetLastError();
 }
 
