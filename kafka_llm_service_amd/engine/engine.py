@@ -161,8 +161,7 @@ class LLMEngine:
                                                max_num_batched_tokens=cfg.max_num_batched_tokens,
                                                max_prefill_chunk=cfg.max_prefill_chunk,
                                                prefill_tokens_while_decoding=cfg.prefill_tokens_while_decoding,
-                                               step_rows_fit=(cfg.step_rows_fit if cfg.step_rows_fit is not None
-                                                              else int(os.environ.get("KAFKA_STEP_ROWS_FIT", "0"))),
+                                               step_rows_fit=self._step_rows_fit(),
                                                max_model_len=cfg.max_model_len, max_blocks_per_seq=max_blocks),
                                self.kvm)
         kc = [self.k_cache[i] for i in range(L)]
@@ -184,6 +183,20 @@ class LLMEngine:
                  nb * page_bytes / 1e9, self.load_s)
 
     # ------------------------------------------------------------------------------------------------------------
+
+    def _step_rows_fit(self) -> int:
+        """Row fit of the scheduler (engine/scheduler.py): explicit config, else env KAFKA_STEP_ROWS_FIT, else on
+        (ops.STREAM_MAX_M) only for tiled-only weights — there a step beyond the streaming kernel's rows untiles
+        every projection for hipBLASLt, which costs far more than splitting a new turn over two steps (Llama-3-70B
+        on one GPU: profiles/r02/bench_70b_tp1_*), while with both weight copies the fit measured slower
+        (profiles/r02/step_rows_fit_rejected.jsonl)."""
+        if self.cfg.step_rows_fit is not None:
+            return self.cfg.step_rows_fit
+        env = os.environ.get("KAFKA_STEP_ROWS_FIT")
+        if env is not None:
+            return int(env)
+        return ops.STREAM_MAX_M if self.model.tiled_only else 0
+
     def add_request(self, request_id: str, prompt_ids: list[int], params: SamplingParams | None = None,
                     meta: dict | None = None) -> Sequence:
         if request_id in self.requests:

@@ -4,6 +4,7 @@ the result (SURVEY.md §4.4 "Engine integration")."""
 import pytest
 import torch
 
+from kafka_llm_service_amd import ops
 from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
 from kafka_llm_service_amd.engine.sequence import SamplingParams
 from kafka_llm_service_amd.models.oracle import dense_logits
@@ -257,6 +258,8 @@ def test_tiled_only_weights_match_stream():
     eng = _engine(decode_gemm="stream_only")
     m = eng.model
     assert m.tiled_only and m.layers[0].qkv is None and m.layers[0].gate_up is None and m.layers[0].qkv_t is not None
+    # tiled-only steps keep to the streaming kernel's rows (scheduler row fit), the two-copy mode does not
+    assert eng.sched.cfg.step_rows_fit == ops.STREAM_MAX_M and ref_eng.sched.cfg.step_rows_fit == 0
     prompts = _prompts(seed=9)
     a = ref_eng.generate(prompts, GREEDY)
     b = eng.generate(prompts, GREEDY)
