@@ -60,7 +60,7 @@ def main():
             return out
 
         us = timeit(layer)
-        us_s = timeit(layer_stream) if T <= ops.STREAM_MAX_M else None
+        us_s = timeit(layer_stream) if T <= 512 else None
         r = ops.moe_route(torch.nn.functional.linear(x, router), K)
         used = int((r.expert_off[1:] - r.expert_off[:-1] > 0).sum().item())
         bytes_w = used * (2 * F * d + d * F) * 2

@@ -21,6 +21,14 @@ import torch.nn.functional as F
 from kafka_llm_service_amd import ops
 from kafka_llm_service_amd.parallel import state as pstate
 
+# Steps of up to this many tokens run the expert MLP on the grouped weight-streaming kernel. Unlike the dense
+# projections it is not limited to 128 rows: each expert's segment is cut into 64-row tiles, so an expert's weights
+# are streamed once per 64 of ITS rows (top-2 of 8 at T = 256 is ~64 rows per expert). Measured
+# (profiles/r02/moe_stream_max_t_ab.jsonl, moe_bench_stream512.log): T = 512 layer 1,252 vs 1,391 us on the LDS-tiled
+# grouped GEMM; Mixtral-8x7B 128-thread bench 4,783 (128) -> 4,958 tok/s (640 = 128 decodes + the TPOT guard's 512
+# prefill tokens), TTFT 62 -> 58 ms. Env KAFKA_MOE_STREAM_MAX_T overrides.
+MOE_STREAM_MAX_T = int(os.environ.get("KAFKA_MOE_STREAM_MAX_T", "640"))
+
 
 def route(logits: torch.Tensor, k: int):
     """softmax -> top-k -> renormalise (Mixtral). Returns (weights f32 [T,k], experts int64 [T,k])."""
@@ -50,7 +58,7 @@ class MoEBlock:
         r = ops.moe_route(logits, self.k)
         if self.ep > 1 and self.a2a:
             return self._a2a(x, lw, r)
-        if self.model.stream and lw.w13_t is not None and T <= ops.STREAM_MAX_M:
+        if self.model.stream and lw.w13_t is not None and T <= MOE_STREAM_MAX_T:
             # decode-sized steps: expert weights streamed from their wave-tiled copies, SwiGLU fused into the gate_up
             # epilogue, weighted combine fused into the down epilogue (csrc/wstream_gemm.hip, grouped variant)
             a = ops.grouped_stream_glu(x, lw.w13_t, r, e_lo=self.e0)
