@@ -40,8 +40,10 @@ def main():
             blas = timeit(lambda i: F.linear(x, ws[i % nrot]))
             two = timeit(lambda i: (ops.linear_stream(x[:h], wts[i % nrot]), ops.linear_stream(x[h:], wts[i % nrot])))
             one128 = timeit(lambda i: ops.linear_stream(x[:128], wts[i % nrot]))
+            tiled = timeit(lambda i: ops.linear_stream(x, wts[i % nrot]))  # one launch, 2 row tiles per slice
             print(json.dumps({"gemm": name, "M": M, "hipblaslt_us": round(blas, 1), "stream_two_halves_us": round(two, 1),
-                              "stream_128_rows_us": round(one128, 1)}), flush=True)
+                              "stream_128_rows_us": round(one128, 1), "stream_row_tiles_us": round(tiled, 1)}),
+                  flush=True)
         del ws, wts
         torch.cuda.empty_cache()
 

@@ -133,7 +133,7 @@ def pad_step_rows(T: int) -> int:
     ``benchmarks/gemm_bench.py``, profiles/r02/gemm_sweep_M129_320.log) the library picks slow kernels for 129..152
     rows (QKV 40 vs 26 us) and at multiples of 32 (down-proj at 192 rows: 101 vs 60 us), so the step is padded with
     inert rows (no KV slot, no attention item, no logits) to the next 16 k + 8 >= 168."""
-    if T <= 128 or T > 256:
+    if T <= ops.STREAM_MAX_M or T > 256:  # (steps the streaming GEMM takes need no padding)
         return T
     t = max(T, 168)
     t += (8 - t % 16) % 16

@@ -171,7 +171,7 @@ class TransformerLM:
         eps = cfg.rms_norm_eps
         tp = self.tp > 1
         delta, pending = None, False
-        fuse_rope = (self.stream and FUSE_QKV_ROPE and 0 < T <= ops.STREAM_MAX_M and self.layers[0].qkv_t is not None
+        fuse_rope = (self.stream and FUSE_QKV_ROPE and 0 < T <= min(128, ops.STREAM_MAX_M) and self.layers[0].qkv_t is not None
                      and ops.qkv_rope_fusable(k_caches[0], self.D))
         for i, lw in enumerate(self.layers):
             if delta is None:

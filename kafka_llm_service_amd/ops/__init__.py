@@ -11,6 +11,8 @@ Kernel inventory:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import reference as ref
@@ -216,19 +218,24 @@ def untile_weight(wt: torch.Tensor, glu: bool = False) -> torch.Tensor:
     return wt.reshape(nb, kb, 2, 32, 8).permute(0, 3, 1, 2, 4).reshape(nb * 32, kb * 16)
 
 
-STREAM_MAX_M = 128
+# Steps of up to this many rows run the dense projections on the weight-streaming kernel (csrc/wstream_gemm.hip).
+# The kernel takes up to 256 rows (beyond 128 as two row tiles whose workgroups share each weight slice through the
+# MALL) but there it loses to hipBLASLt (gate_up 101 vs 66 us at 168..248 rows; bench 7,359 vs 7,546 tok/s,
+# profiles/r02/stream_max_m_256_rejected.jsonl), so the default stays 128. Env KAFKA_STREAM_MAX_M (1..256).
+STREAM_MAX_M = max(1, min(256, int(os.environ.get("KAFKA_STREAM_MAX_M", "128"))))
+STREAM_KERNEL_MAX_M = 256
 
 
 def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, int] | None:
     """(row tiles, K chunk, splits) of the decode GEMM for a shape, None if unsupported (same rule as
     kafka_wstream_plan in csrc/wstream_gemm.hip, mirrored so CPU runs take the same split decisions)."""
-    if M < 1 or M > STREAM_MAX_M or N % 32 or N <= 0:
+    if M < 1 or M > STREAM_KERNEL_MAX_M or N % 32 or N <= 0:
         return None
     mt = 1 if M <= 32 else (2 if M <= 64 else 4)
     kc = 128 if mt == 4 else 256
     if K % kc or K <= 0:
         return None
-    nx, chunks, s = (N + 127) // 128, K // kc, 1
+    nx, chunks, s = (N + 127) // 128 * ((M + 127) // 128), K // kc, 1
     target = 256 if mt == 4 else 192
     while s * 2 <= max_splits and s * 2 <= 8 and chunks % (s * 2) == 0 and nx * s < target:
         s *= 2

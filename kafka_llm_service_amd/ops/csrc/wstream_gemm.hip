@@ -49,7 +49,8 @@ template <int MT, int KC, bool NT, int KW, bool ROPE = false>
 __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                                  const bf16x8* __restrict__ Wt, int M, int N, int K,
                                                                  int ks, bf16* __restrict__ Y, int64_t ldy,
-                                                                 float* __restrict__ P, int glu, RopeKV ra) {
+                                                                 float* __restrict__ P, int glu, RopeKV ra,
+                                                                 int row_tiles) {
   constexpr int NTH = 256 * KW;
   constexpr int ROWS = 32 * MT;
   constexpr int CPR = KC / 8;             // 16-B chunks per X row of one K chunk
@@ -62,7 +63,15 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ct = w & 3, kh = w >> 2;  // column tile of the workgroup, K part of the chunk
   const int r = lane & 31, h = lane >> 5;
-  const int nb = blockIdx.x * 4 + ct;
+  // row tiles (M > 32 MT): the row_tiles workgroups of one weight slice are consecutive in dispatch order, so the
+  // slice is fetched from HBM once and the other row tiles read it back from the MALL; P stays [S][M_total][N]
+  const int cb = blockIdx.x / row_tiles, row0 = (blockIdx.x % row_tiles) * ROWS;
+  const int Mtot = M;
+  M = min(ROWS, Mtot - row0);
+  X += (int64_t)row0 * ldx;
+  if (Y != nullptr) Y += (int64_t)row0 * ldy;
+  if (P != nullptr) P += (int64_t)row0 * N;
+  const int nb = cb * 4 + ct;
   // wave-uniform: a tail wave past the last column tile streams a valid tile and skips only its stores — every
   // load and MFMA stays unconditional, so hipcc's waitcnt pass sees straight-line code and keeps counted vmcnt
   // waits (a divergent `if` around the loads collapses them to vmcnt(0..1) at the join)
@@ -178,13 +187,13 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
         for (int i = 0; i < 16; ++i) {
           const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
           if (m < M)
-            __hip_atomic_store(P + ((int64_t)blockIdx.y * M + m) * N + n, acc[mt][i], __ATOMIC_RELAXED,
+            __hip_atomic_store(P + ((int64_t)blockIdx.y * Mtot + m) * N + n, acc[mt][i], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        int* tk = ra.tickets + blockIdx.x;
+        int* tk = ra.tickets + cb;
         const int t = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = t == S - 1;
         if (t == S - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -199,7 +208,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int m = min(mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h, M - 1);
-            v[mt][i] = __hip_atomic_load(P + ((int64_t)s2 * M + m) * N + n, __ATOMIC_RELAXED,
+            v[mt][i] = __hip_atomic_load(P + ((int64_t)s2 * Mtot + m) * N + n, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
           }
 #pragma unroll
@@ -216,7 +225,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
 #pragma unroll
       for (int i = 0; i < 16; ++i) red[((ct * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
     __syncthreads();
-    const int head = blockIdx.x, d = 32 * ct + r, j = d & 63;
+    const int head = cb, d = 32 * ct + r, j = d & 63;
     const bool is_q = head < ra.Hq, is_k = !is_q && head < ra.Hq + ra.Hkv;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -284,7 +293,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
       const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
       if (m < M) {
         if (P)
-          P[((int64_t)blockIdx.y * M + m) * N + n] = acc[mt][i];
+          P[((int64_t)blockIdx.y * Mtot + m) * N + n] = acc[mt][i];
         else
           Y[(int64_t)m * ldy + n] = (bf16)acc[mt][i];
       }
@@ -458,11 +467,11 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 // Host plan: row tiles MT, K chunk KC and split count S for a shape; returns 0 if supported.
 //   max_splits caps S (1 forces a direct bf16 output).
 extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits) {
-  if (M < 1 || M > 128 || N % 32 != 0 || N <= 0) return 1;
+  if (M < 1 || M > 256 || N % 32 != 0 || N <= 0) return 1;
   const int MT = M <= 32 ? 1 : (M <= 64 ? 2 : 4);
   const int KC = MT == 4 ? 128 : 256;
   if (K % KC != 0 || K <= 0) return 2;
-  const int nx = (N + 127) / 128;
+  const int nx = (N + 127) / 128 * ((M + 127) / 128);  // workgroups per split (row tiles beyond 128 rows)
   const int chunks = K / KC;
   // split until the grid reaches ~192 (MT <= 2) / 256 (MT = 4) workgroups: measured on MI355X
   // (benchmarks/wstream_sweep.py, profiles/wstream_sweep_r01.log) — every extra split adds 2 x M x N x 4 B of slab
@@ -483,7 +492,8 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   if (glu && (N % 64 != 0 || kw != 1)) return hipErrorInvalidValue;
   if (K % (kc * splits) != 0 || (splits > 1 && P == nullptr) || (splits == 1 && P == nullptr && Y == nullptr))
     return hipErrorInvalidValue;
-  const dim3 grid((N + 127) / 128, splits);
+  const int rt = (M + 32 * mt - 1) / (32 * mt);  // row tiles of 32 * mt rows (M > 128: 2 tiles of 128)
+  const dim3 grid((N + 127) / 128 * rt, splits);
   const int ks = K / splits;
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   float* p = splits > 1 ? P : nullptr;
@@ -491,10 +501,10 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   do {                                                                                                     \
     if (nt)                                                                                                \
       wstream_gemm_kernel<MT_, KC_, true, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, \
-                                                                           RopeKV{});                               \
+                                                                           RopeKV{}, rt);                           \
     else                                                                                                   \
       wstream_gemm_kernel<MT_, KC_, false, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, \
-                                                                            RopeKV{});                              \
+                                                                            RopeKV{}, rt);                          \
   } while (0)
   if (mt == 1 && kc == 256 && kw == 1) KAFKA_WS(1, 256, 1);
   else if (mt == 1 && kc == 256 && kw == 2) KAFKA_WS(1, 256, 2);
@@ -518,18 +528,19 @@ extern "C" hipError_t kafka_launch_wstream_qkv_rope(const bf16* X, int64_t ldx, 
                                                    bf16* k_cache, bf16* v_cache, const int64_t* slots, int Hq,
                                                    int Hkv, int* tickets, hipStream_t st) {
   if (M < 1) return hipSuccess;
-  if (N != (Hq + 2 * Hkv) * 128 || K % (kc * splits) != 0 || (splits > 1 && (P == nullptr || tickets == nullptr)))
+  if (M > 128 || N != (Hq + 2 * Hkv) * 128 || K % (kc * splits) != 0 ||
+      (splits > 1 && (P == nullptr || tickets == nullptr)))
     return hipErrorInvalidValue;
   const dim3 grid(N / 128, splits);
   const int ks = K / splits;
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   const RopeKV ra{positions, cos_sin, q_out, q_stride, k_cache, v_cache, slots, Hq, Hkv, tickets};
   if (mt == 1 && kc == 256)
-    wstream_gemm_kernel<1, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra);
+    wstream_gemm_kernel<1, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1);
   else if (mt == 2 && kc == 256)
-    wstream_gemm_kernel<2, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra);
+    wstream_gemm_kernel<2, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1);
   else if (mt == 4 && kc == 128)
-    wstream_gemm_kernel<4, 128, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra);
+    wstream_gemm_kernel<4, 128, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
