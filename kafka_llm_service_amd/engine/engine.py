@@ -128,10 +128,10 @@ class LLMEngine:
                 self.model.enable_stream_weights(tiled_only=True)
         elif mode == "stream_only" and not self.model.stream:
             self.model.enable_stream_weights(tiled_only=True)
-        if self.model.tiled_only and cfg.max_num_seqs > ops.STREAM_MAX_M:
+        if self.model.tiled_only and cfg.max_num_seqs > self.model.stream_max_m:
             # decode batches beyond the streaming kernel's rows would untile every projection every step
-            log.info("tiled-only weights: max_num_seqs %d -> %d", cfg.max_num_seqs, ops.STREAM_MAX_M)
-            cfg.max_num_seqs = ops.STREAM_MAX_M
+            log.info("tiled-only weights: max_num_seqs %d -> %d", cfg.max_num_seqs, self.model.stream_max_m)
+            cfg.max_num_seqs = self.model.stream_max_m
         self.load_s = time.perf_counter() - t0
         self.eos = set(cfg.eos_token_ids or mc.eos_token_ids)
         hkv, D, L = self.model.hkv, self.model.D, mc.num_layers
@@ -195,6 +195,9 @@ class LLMEngine:
         env = os.environ.get("KAFKA_STEP_ROWS_FIT")
         if env is not None:
             return int(env)
+        # 128 rather than the kernel's 256: with two row tiles the streaming GEMM is slower per row, and splitting a
+        # long new turn costs less (Llama-3-70B TP = 1: 1,516 vs 1,422 tok/s, TTFT 140 vs 119 ms,
+        # profiles/r02/bench_70b_tp1_rowfit256_ab.jsonl)
         return ops.STREAM_MAX_M if self.model.tiled_only else 0
 
     def add_request(self, request_id: str, prompt_ids: list[int], params: SamplingParams | None = None,

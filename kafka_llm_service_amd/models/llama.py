@@ -81,6 +81,7 @@ class TransformerLM:
         self.lm_head_t = None
         self.stream = False  # decode GEMMs on the weight-streaming kernel (enable_stream_weights)
         self.tiled_only = False  # row-major dense weights dropped (enable_stream_weights(tiled_only=True))
+        self.stream_max_m = ops.STREAM_MAX_M  # rows up to which a step's projections stream
 
     # ------------------------------------------------------------------------------------------------------------
     def stream_weight_bytes(self) -> int:
@@ -137,13 +138,17 @@ class TransformerLM:
                 added += self.lm_head_t.numel() * self.lm_head_t.element_size()
         self.stream = True
         self.tiled_only = tiled_only
+        # tiled-only: any larger step would untile every projection for hipBLASLt, so the streaming kernel takes
+        # steps up to its 256-row limit (two row tiles beyond 128) — slower than hipBLASLt there, far cheaper than
+        # untiling
+        self.stream_max_m = ops.STREAM_KERNEL_MAX_M if tiled_only else ops.STREAM_MAX_M
         if tiled_only and self.device.type == "cuda":
             torch.cuda.empty_cache()
         return added
 
     def _linear(self, x: torch.Tensor, w: torch.Tensor, wt: torch.Tensor | None, max_splits: int = 8):
         """x @ w^T: the weight-streaming kernel for decode-sized x (bf16 or a split-K slab out), else hipBLASLt."""
-        if self.stream and wt is not None and 0 < x.shape[0] <= ops.STREAM_MAX_M:
+        if self.stream and wt is not None and 0 < x.shape[0] <= self.stream_max_m:
             return ops.linear_stream(x, wt, max_splits)
         return F.linear(x, self._dense(w, wt))
 
@@ -171,7 +176,7 @@ class TransformerLM:
         eps = cfg.rms_norm_eps
         tp = self.tp > 1
         delta, pending = None, False
-        fuse_rope = (self.stream and FUSE_QKV_ROPE and 0 < T <= min(128, ops.STREAM_MAX_M) and self.layers[0].qkv_t is not None
+        fuse_rope = (self.stream and FUSE_QKV_ROPE and 0 < T <= min(128, self.stream_max_m) and self.layers[0].qkv_t is not None
                      and ops.qkv_rope_fusable(k_caches[0], self.D))
         for i, lw in enumerate(self.layers):
             if delta is None:
@@ -198,7 +203,7 @@ class TransformerLM:
                 delta = self.moe(x, lw)
                 pending = tp and not self.moe.reduced
             else:
-                if self.stream and lw.glu and 0 < T <= ops.STREAM_MAX_M:
+                if self.stream and lw.glu and 0 < T <= self.stream_max_m:
                     a = ops.linear_glu(x, lw.gate_up_t)  # SwiGLU in the GEMM epilogue (or on its slabs)
                 else:
                     a = ops.silu_mul(F.linear(x, self._dense(lw.gate_up, lw.gate_up_t, bool(lw.glu))))
