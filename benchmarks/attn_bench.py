@@ -80,7 +80,7 @@ def main():
       nc = math.ceil(P / chunk)
       part = torch.empty(B, Hq, nc + 2, D, device=dev)
       lse = torch.empty(B, Hq, nc + 2, device=dev)
-      for var in (0, 1, 2):
+      for var in (0, 3):
         tile = ops.tile_rows(var) // G
         items = [(g0, min(tile, B - g0), 0, ci * chunk, min(P, (ci + 1) * chunk), ci, 0, 0)
                  for g0 in range(0, B, tile) for ci in range(nc)]
@@ -145,7 +145,7 @@ def main():
     qp = torch.randn(T, Hq, D, device=dev, dtype=torch.bfloat16)
     ql = torch.arange(0, T, dtype=torch.int32, device=dev)
     o = torch.empty(T, Hq, D, device=dev, dtype=torch.bfloat16)
-    for var in (0, 1, 2):
+    for var in (0, 3):
         tile = ops.tile_rows(var) // G
         items = [(t0, min(tile, T - t0), 0, 0, t0 + tile, -1, 0, 0) for t0 in range(0, T, tile)]
         it = torch.tensor(items, dtype=torch.int32, device=dev)

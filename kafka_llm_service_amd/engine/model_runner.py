@@ -311,8 +311,12 @@ class ModelRunner:
         self.max_num_seqs = max_num_seqs
         self.max_blocks = max_blocks_per_seq
         self.G = model.hq // model.hkv
-        # tile-kernel variant (ops.tile_rows): 0 = 8 waves x 256 query rows per workgroup, 1 = 4 waves x 128 rows
-        self.variant = int(os.environ.get("KAFKA_TILE_VARIANT", "0"))
+        # tile-kernel variant (ops.tile_rows): 3 = LDS-DMA ring kernel (csrc/attn_tile.hip, 8 waves x 256 query rows,
+        # bf16 pages); 0 = register-staged 8 waves x 256 rows (fp8 pages); 1 = 4 waves x 128 rows
+        fp8 = bool(k_caches) and ops.is_fp8_cache(k_caches[0])
+        self.variant = int(os.environ.get("KAFKA_TILE_VARIANT", "0" if fp8 else "3"))
+        if fp8 and self.variant == 3:
+            raise ValueError("tile variant 3 reads bf16 KV pages only")
         # mixed steps of 129..256 rows padded away from hipBLASLt's slow sizes (dense TP = 1 GPU models)
         self.pad_rows = (self.device.type == "cuda" and model.tp == 1 and not getattr(model, "tiled_only", False)
                          and os.environ.get("KAFKA_PAD_ROWS", "1") == "1")

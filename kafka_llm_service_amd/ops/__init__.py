@@ -162,7 +162,7 @@ def attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, scale: float
 
 def tile_rows(variant: int = 0) -> int:
     """Query rows ((token, head) pairs of one KV head) per attn_prefill work item for a kernel variant."""
-    return 256 if variant == 0 else 128
+    return 256 if variant in (0, 3) else 128
 
 
 def attn_merge(part, lse, out, lse_out=None) -> None:

@@ -218,7 +218,7 @@ def test_attn_decode_multi_group_cascade(cuda):
         _close(out, o_ref, atol=0.02, msg=f"multi-group cascade launch {launch}")
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_attn_decode_kv_start_cascade(cuda, variant):
     """Cascade: prefix partial from attn_prefill (rows = decode seqs) + suffix partial from attn_decode == full."""
     torch.manual_seed(4)
@@ -259,7 +259,7 @@ def test_attn_decode_kv_start_cascade(cuda, variant):
     _close(out, o_ref, atol=0.02, msg="cascade")
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8)])
 def test_attn_prefill_causal(cuda, Hq, Hkv, variant):
     torch.manual_seed(6)
@@ -290,6 +290,37 @@ def test_attn_prefill_causal(cuda, Hq, Hkv, variant):
     out_ref = torch.zeros(T, Hq, D, dtype=torch.bfloat16)
     ref.attn_prefill_items(items.cpu(), q.cpu(), k.cpu(), v.cpu(), bt.cpu(), q_limit.cpu(), scale, out=out_ref)
     _close(out, out_ref, atol=0.02, msg="prefill")
+
+
+@pytest.mark.parametrize("variant", [0, 3])
+@pytest.mark.parametrize("spike_at", [5, 300, 1500])
+def test_attn_tile_rescale_spike(cuda, variant, spike_at):
+    """Forces the online-softmax rescale branch at a chosen key (cdna_hip_programming.md §5.4 rule 26): one key row
+    scaled x12 makes every query's running max jump there (variant 3 rescales only past 2^8 growth, so the jump must
+    be large and the O / l / pending-P scaling exact). Non-causal rows over a 2,000-key range (31 ring tiles: the
+    3-slot DMA ring wraps many times), split into two key chunks with partials, vs the fp32 reference."""
+    torch.manual_seed(11)
+    Hq, Hkv, D, B = 32, 8, 128, 64
+    L = 2000
+    k, v, bt = _random_paged(1, [L], Hkv, cuda, seed=12)
+    pg, off = bt[0, spike_at // 16].item(), spike_at % 16
+    ref.k_planes(k)[pg, :, :, off, :] *= 12  # the whole key row (pages are stored plane-major)
+    q = torch.randn(B, Hq, D, device=cuda, dtype=torch.bfloat16)
+    G = Hq // Hkv
+    tile = ops.tile_rows(variant) // G
+    items = [[t0, min(tile, B - t0), 0, c0, c1, c, 0, 0] for t0 in range(0, B, tile)
+             for c, (c0, c1) in enumerate([(0, 1024), (1024, L)])]
+    items = torch.tensor(items, dtype=torch.int32, device=cuda)
+    q_limit = torch.full((B,), L - 1, dtype=torch.int32, device=cuda)
+    bt_rows = bt[:1].expand(B, -1).contiguous()
+    part = torch.empty(B, Hq, 2, D, device=cuda)
+    lse = torch.empty(B, Hq, 2, device=cuda)
+    ops.attn_prefill(items, q, k, v, bt_rows, q_limit, 1 / math.sqrt(D), out_part=part, lse_part=lse,
+                     variant=variant)
+    out = torch.empty(B, Hq, D, device=cuda, dtype=torch.bfloat16)
+    ops.attn_merge(part, lse, out)
+    o_ref, _ = ref.attn_decode_full(q.cpu(), k.cpu(), v.cpu(), bt_rows.cpu(), torch.full((B,), L), 1 / math.sqrt(D))
+    _close(out, o_ref, atol=0.02, msg=f"spike at {spike_at}")
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
