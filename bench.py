@@ -74,7 +74,9 @@ def parse(argv=None):
     ap.add_argument("--ttft-samples", type=int, default=64, help="new turns whose TTFT is sampled")
     ap.add_argument("--ttft-max-steps", type=int, default=4000)
     ap.add_argument("--no-cascade", action="store_true")
-    ap.add_argument("--graphs", action="store_true")
+    ap.add_argument("--graphs", action="store_true", default=None,
+                    help="hipGraph decode steps (default: on for --tp > 1, off at TP = 1)")
+    ap.add_argument("--no-graphs", dest="graphs", action="store_false")
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"],
                     help="paged KV cache precision (fp8 = e4m3 + per-token scales; an opt-in A/B, not the headline)")
     ap.add_argument("--seed", type=int, default=0)
@@ -348,7 +350,7 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
                    "threads_per_gpu": args.threads * dp // world,
                    "shared_prefix_tokens": args.prefix_tokens, "history_turns": args.history_turns,
                    "mixed_prefix": args.mixed_prefix, "max_out": [args.min_out, args.max_out],
-                   "temperature": args.temperature, "cascade": not args.no_cascade, "graphs": args.graphs,
+                   "temperature": args.temperature, "cascade": not args.no_cascade, "graphs": eng.cfg.use_graphs,
                    "kv_dtype": args.kv_dtype},
         "ttft_p50_ms": round(p50, 2) if p50 else None, "ttft_p99_ms": round(p99, 2) if p99 else None,
         "ttft_samples": len(ttfts), "ttft_extra_steps": extra,

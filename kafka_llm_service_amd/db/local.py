@@ -109,6 +109,8 @@ class LocalDBClient:
         self._cache: OrderedDict[str, list[Message]] = OrderedDict()  # thread id -> full history, seq order
         self._known: set[str] = set()
         self._pending: set = set()  # write-behind futures not yet awaited
+        self._write_error: BaseException | None = None  # first failed write-behind save, raised by sync()
+        self._gen: dict[str, int] = defaultdict(int)  # per-thread write generation (guards cache fills on a miss)
 
     # --- plumbing ---------------------------------------------------------------------------------------------
     def _connect(self) -> sqlite3.Connection:
@@ -136,13 +138,28 @@ class LocalDBClient:
             self._cache.popitem(last=False)
 
     async def sync(self) -> None:
-        """Wait until every queued write has reached SQLite (the writer is FIFO: a no-op behind them suffices)."""
+        """Wait until every queued write has reached SQLite (the writer is FIFO: a no-op behind them suffices) and
+        raise the first write-behind failure since the last sync (its thread was dropped from the cache, so the
+        history served afterwards is what SQLite holds)."""
         if self._pending:
             await self._run(lambda: None)
             for f in list(self._pending):
                 if f.done():
                     self._pending.discard(f)
-                    f.result()  # surface a failed write
+        err, self._write_error = self._write_error, None
+        if err is not None:
+            raise err
+
+    def _write_failed(self, thread_id: str, fut) -> None:
+        """Done-callback of a write-behind save: on failure keep the error for sync() and forget the thread's cached
+        history (it already shows the rows that did not reach SQLite)."""
+        self._pending.discard(fut)
+        exc = None if fut.cancelled() else fut.exception()
+        if exc is not None:
+            self._cache.pop(thread_id, None)
+            self._gen[thread_id] += 1
+            if self._write_error is None:
+                self._write_error = exc
 
     async def initialize(self) -> None:
         await self._run(self._connect)
@@ -207,6 +224,8 @@ class LocalDBClient:
             out = [m.model_copy() for m in hit if include_system or m.role != "system"]  # callers may edit them
             return out[:limit] if limit else out
 
+        gen = self._gen[thread_id]  # a write or delete queued after this read makes its result stale for the cache
+
         def _do():
             q = "SELECT message, token_ids FROM messages WHERE thread_id=? ORDER BY seq ASC"
             args: list[Any] = [thread_id]
@@ -223,7 +242,8 @@ class LocalDBClient:
             if r["token_ids"]:
                 d["token_ids"] = json.loads(r["token_ids"])
             out.append(Message.from_dict(d))
-        if not limit and include_system and not self._pending:  # no queued write this read could have missed
+        # (writes queued BEFORE the read are in it: one FIFO writer thread; later ones bumped the generation)
+        if not limit and include_system and self._gen[thread_id] == gen:
             self._cache_put(thread_id, [m.model_copy() for m in out])
         return out
 
@@ -251,23 +271,33 @@ class LocalDBClient:
 
         def _do():
             c = self._connect()
-            for m, mid in zip(msgs, ids):
-                self._insert(c, thread_id, m, metadata, mid)
-            c.commit()
+            try:
+                for m, mid in zip(msgs, ids):
+                    self._insert(c, thread_id, m, metadata, mid)
+                c.commit()
+            except BaseException:
+                c.rollback()  # all of this call's rows or none
+                raise
             return ids
+        self._gen[thread_id] += 1
         hit = self._cache.get(thread_id)
         if hit is not None:
             hit.extend(m.model_copy() for m in msgs)
         self._known.add(thread_id)
         fut = asyncio.get_running_loop().run_in_executor(self._exec, _do)
         if wait:
-            return await fut
+            try:
+                return await fut
+            except BaseException:
+                self._cache.pop(thread_id, None)  # the cache already showed the rows
+                raise
         self._pending.add(fut)
-        fut.add_done_callback(lambda f: (self._pending.discard(f), f.exception()))
+        fut.add_done_callback(lambda f: self._write_failed(thread_id, f))
         return ids
 
     async def delete_thread_messages(self, thread_id: str) -> int:
         self._cache.pop(thread_id, None)
+        self._gen[thread_id] += 1
 
         def _do():
             c = self._connect()

@@ -52,7 +52,9 @@ class EngineConfig:
     target_wgs: int = 256               # tile-kernel workgroups per pass (8-wave WGs, one per CU)
     prefill_kv_chunk: int = 1024        # a new turn on > 2x this many cached keys splits its key range so all
                                         # tiles make ~target_wgs workgroups (chunks >= min(256, this))
-    use_graphs: bool = False
+    # hipGraph decode steps (engine/graphs.py): None = on for TP > 1 on GPUs (every rank launches ~800 kernels per
+    # step there), off at TP = 1 (the host already runs a step ahead: measured no faster, profiles/r02/graphs_ab_*)
+    use_graphs: bool | None = None
     # paged KV cache: "bf16", or "fp8" = e4m3 with one power-of-two scale per (token, kv head) for K and for V
     # (half the bytes per page: twice the pages, half the decode attention traffic; ops/csrc/rope_kv.hip)
     kv_dtype: str = "bf16"
@@ -169,6 +171,8 @@ class LLMEngine:
         self.runner = ModelRunner(self.model, kc, vc, self.kvm, cfg.max_num_seqs, max_blocks,
                                   cascade_min_prefix=cfg.cascade_min_prefix, use_cascade=cfg.use_cascade,
                                   target_wgs=cfg.target_wgs, prefill_kv_chunk=cfg.prefill_kv_chunk)
+        if cfg.use_graphs is None:
+            cfg.use_graphs = cfg.tp > 1 and self.device.type == "cuda"
         if cfg.use_graphs:
             from kafka_llm_service_amd.engine.graphs import DecodeGraphs
 

@@ -72,12 +72,11 @@ class DecodeGraphs:
         k = self.key(h, sp)
         e = self.graphs.get(k)
         if e is None:
-            try:
-                e, local = self._capture(k, h, sp)
-            except Exception:  # never let capture problems take the engine down: stay eager from here on
-                log.exception("hipGraph capture failed; decode steps run eagerly")
-                self.disabled = True
-                return None
+            e, local = self._capture(k, h, sp)
+            if e is None:  # capture failed on some rank: the warm run already computed this step
+                if self.runner.model.tp == 1:
+                    return local
+                return self._finish_tp(local, h, sp)
         else:
             self.graphs.move_to_end(k)
             self._load(e, h, sp)
@@ -97,6 +96,22 @@ class DecodeGraphs:
         toks = r.sample_device(logits, sp)
         r.tok_buf[:toks.shape[0]].copy_(toks)
         return toks
+
+    def _agree(self, ok: bool) -> bool:
+        """The TP group's verdict on a capture: True only if it worked on every rank (gloo MIN on the control
+        group; one small collective per captured layout, never on a replay)."""
+        if self.runner.model.tp == 1:
+            return ok
+        import torch.distributed as dist
+
+        from kafka_llm_service_amd.parallel import state as pstate
+
+        st = pstate.get()
+        if st.cpu_group is None or not dist.is_initialized():
+            return ok
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=st.cpu_group)
+        return bool(int(t.item()))
 
     def _load(self, e: _Entry, h, sp) -> None:
         r = self.runner
@@ -144,17 +159,30 @@ class DecodeGraphs:
             warm = e.local
         else:
             # warm up on a side stream (library workspaces, lazy inits): this run computes THIS step (tokens and
-            # its KV writes); the capture pass that follows records the kernels without executing them
+            # its KV writes, and under TP its collectives — a failure here is a failed step, raised as such); the
+            # capture pass that follows records the kernels without executing them
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 step()
             torch.cuda.current_stream().wait_stream(side)
             warm = e.local  # this step's logit shard (TP); the capture pass below only records
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool):
-                step()
-            e.graph = g
+            ok = True
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.pool):
+                    step()
+                e.graph = g
+            except Exception:  # noqa: BLE001 - never let capture problems take the engine down
+                log.exception("hipGraph capture failed")
+                ok = False
+            if not self._agree(ok):
+                # Every rank of the TP group switches to eager decode on the same step (a rank alone would make
+                # collective calls its peers never match). The step itself is NOT run again — the warm run already
+                # computed it (its tokens, KV writes and, under TP, its collectives): return that result.
+                log.warning("hipGraph decode disabled for this engine (capture failed on some rank)")
+                self.disabled = True
+                return None, (e.out if r.model.tp == 1 else warm)
         self.graphs[k] = e
         self.stats["captures"] += 1
         while len(self.graphs) > self.max_graphs:

@@ -112,12 +112,18 @@ def unpack_plan(hdr: np.ndarray, payload: np.ndarray) -> tuple[HostStep, SampleP
     return h, sp
 
 
+class CollectiveError(RuntimeError):
+    """A TP peer stopped taking part in the custom all-reduce (its waits timed out): the step's tokens were computed
+    from stale peer data and the replica must fail (503 + respawn), not stream them."""
+
+
 @dataclass
 class Launched:
     tokens: torch.Tensor            # sampled ids (pinned host buffer on GPU, plain tensor on CPU)
     event: object = None            # completion event of the D2H copy
     dev_tokens: torch.Tensor | None = None  # the sampler's device output (input ids of the next step's decode rows)
     rows: dict | None = None        # seq_id -> row of dev_tokens
+    err_idx: int | None = None      # slot of ModelRunner._err_host holding the custom all-reduce error word
 
 
 MIN_DECODE_KEYS = 256      # smallest key range of one decode work item
@@ -332,6 +338,7 @@ class ModelRunner:
         self.recent_stats: deque = deque(maxlen=16)  # stats of the last launched steps (two can be in flight)
         self.broadcast = None  # set on a TP leader: callable(HostStep, SampleParams) (engine/tp_worker.py)
         self._tok_host = None  # pinned landing buffers of the sampled ids
+        self._err_host = None  # pinned landing slots of the custom all-reduce error word (TP)
         self.stager = _Stager(self.device)
         # every step's sampled ids also land here (fixed address, so hipGraphs can read it): the next step's decode
         # rows whose token was still being sampled at launch gather their input ids from it on the stream
@@ -636,9 +643,25 @@ class ModelRunner:
         self._tok_i = (getattr(self, "_tok_i", 0) + 1) % len(ring)
         out = ring[self._tok_i][:n]
         out.copy_(toks, non_blocking=True)
+        err_idx = None
+        car = self._custom_ar()
+        if car is not None:  # the error word rides along with the sampled ids (4 bytes, same stream)
+            if self._err_host is None:
+                self._err_host = torch.zeros(len(ring), dtype=torch.int32, pin_memory=True)
+            err_idx = self._tok_i
+            car.error_async(self._err_host, err_idx)
         ev = torch.cuda.Event()
         ev.record()
-        return Launched(out, ev, toks, rows)
+        return Launched(out, ev, toks, rows, err_idx)
+
+    def _custom_ar(self):
+        if self.model.tp == 1:
+            return None
+        if not hasattr(self, "_car"):
+            from kafka_llm_service_amd.parallel import state as pstate
+
+            self._car = pstate.custom_ar()
+        return self._car
 
     @torch.inference_mode()
     def follower_launch(self, host: HostStep, sp: SampleParams) -> None:
@@ -670,4 +693,6 @@ class ModelRunner:
     def collect(self, h: "Launched") -> list[int]:
         if h.event is not None:
             h.event.synchronize()
+        if h.err_idx is not None and int(self._err_host[h.err_idx]) != 0:
+            raise CollectiveError("custom all-reduce: a TP peer did not arrive within 2 s; failing the replica")
         return h.tokens.tolist()

@@ -10,7 +10,9 @@
 //   2. publish: every staging wave waits for its stores, the block barriers, one wave releases system-wide and
 //      stores e into flags[my_rank][b] of EVERY peer,
 //   3. wait until flags[p][b] >= e for every peer p in its own flag block (relaxed polls, one system acquire;
-//      bounded: after ~2 s it sets err and proceeds, so a lost peer can never hang the GPU),
+//      bounded: after ~2 s it sets err and proceeds, so a lost peer can never hang the GPU; once err is set every
+//      later call skips its waits — garbage fast instead of 2 s per call — and the engine, which copies err back
+//      with every step's sampled ids (car_error_async), fails the replica: 503 + respawn, never silent tokens),
 //   4. read slice b from all peers' data halves at once (each MI355X reads its 7 peers over its 7 xGMI links in
 //      parallel: one hop, vs a ring's 2(N-1) hops) and sum in fp32 in a fixed rank order (bit-identical on every
 //      rank). Plain mode writes the bf16 sum; the fused mode (slices = whole rows) also adds the residual (updated in
@@ -71,11 +73,13 @@ __device__ __forceinline__ void ar_exchange(const ARPtrs& ptrs, int rank, int e)
       int* pf = reinterpret_cast<int*>(ptrs.base[p]) + rank * AR_MAX_BLOCKS + blockIdx.x;
       __hip_atomic_store(pf, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       int* my = reinterpret_cast<int*>(ptrs.base[rank]) + p * AR_MAX_BLOCKS + blockIdx.x;
+      int* err = reinterpret_cast<int*>(ptrs.base[rank] + AR_ERR_OFF);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
       while (__hip_atomic_load(my, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+        // a group that already lost a peer does not wait again (the engine is failing the replica)
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
         __builtin_amdgcn_s_sleep(2);
         if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: report instead of hanging the queue
-          int* err = reinterpret_cast<int*>(ptrs.base[rank] + AR_ERR_OFF);
           __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }

@@ -586,6 +586,14 @@ static int64_t car_error(int64_t own) {
   CHECK_HIP(hipMemcpy(&v, reinterpret_cast<char*>(own) + 8 * 128 * 4, sizeof(int), hipMemcpyDeviceToHost));
   return v;
 }
+// Stream-ordered copy of the error word into out[idx] (pinned int32 host tensor): the engine reads it with the
+// step's sampled ids, so a peer that stopped arriving fails the replica instead of yielding wrong tokens.
+static void car_error_async(int64_t own, at::Tensor out, int64_t idx) {
+  TORCH_CHECK(out.is_pinned() && out.scalar_type() == at::kInt && idx >= 0 && idx < out.numel(),
+              "car_error_async: pinned int32 host tensor");
+  CHECK_HIP(hipMemcpyAsync(out.data_ptr<int>() + idx, reinterpret_cast<char*>(own) + 8 * 128 * 4, sizeof(int),
+                           hipMemcpyDeviceToHost, cur_stream()));
+}
 static std::vector<char*> car_bases(const std::vector<int64_t>& bases) {
   std::vector<char*> b(bases.size());
   for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<char*>(bases[i]);
@@ -659,6 +667,7 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("car_close", &car_close);
   m.def("car_free", &car_free);
   m.def("car_error", &car_error);
+  m.def("car_error_async", &car_error_async);
   m.def("car_all_reduce", &car_all_reduce);
   m.def("car_all_reduce_add_rmsnorm", &car_all_reduce_add_rmsnorm);
   m.def("grouped_gemm", &grouped_gemm);

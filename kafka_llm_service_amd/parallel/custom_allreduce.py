@@ -12,8 +12,16 @@ memory (each block advances its own), so a replayed graph runs fresh epochs. Eve
 
 ``all_reduce_add_rmsnorm`` fuses the layer seam of a TP decoder: residual += allreduce(x); out = rmsnorm(residual)
 (x may be the fp32 split-K slabs of the decode GEMM). Messages above ``max_bytes`` (prefill chunks) go to RCCL.
-Enabled with ``KAFKA_CUSTOM_AR=1`` (``parallel/state.init``) — 2, 4 or 8 ranks, one GPU each; the same protocol
-runs between processes that share one GPU (tests/test_custom_allreduce_gpu.py on a 1-GPU box).
+On by default for TP 2/4/8 on GPUs (``parallel/state.init``; ``KAFKA_CUSTOM_AR=0`` = RCCL for every message); the same
+protocol runs between processes that share one GPU (tests/test_custom_allreduce_gpu.py on a 1-GPU box).
+
+Failure handling:
+  * setup is collective: every rank takes part in the same exchanges whether its own allocation / IPC mapping
+    worked or not, and the group enables the custom path only if it worked on EVERY rank (one rank on RCCL while
+    its peers run the custom kernel would hang or mix collectives);
+  * a peer that stops arriving makes the kernel set its error word after 2 s (and skip waits from then on); the
+    engine copies that word back with every step's sampled ids (``error_async``) and raises on collect, so the
+    replica fails (503 + respawn) instead of returning tokens computed from stale peer data.
 """
 from __future__ import annotations
 
@@ -27,6 +35,10 @@ def _is_slab(x: torch.Tensor) -> bool:
     return x.dtype == torch.float32 and x.dim() == 3
 
 
+class CustomAllReduceUnavailable(RuntimeError):
+    """Raised on EVERY rank of the group when the custom path could not be set up on at least one of them."""
+
+
 class CustomAllReduce:
     def __init__(self, cpu_group, rank: int, world: int, max_bytes: int = 8 << 20, nblocks: int = 64):
         if world not in (2, 4, 8):
@@ -35,19 +47,35 @@ class CustomAllReduce:
         self.max_bytes = max_bytes
         self.nblocks = nblocks
         e = ext()
-        self.own = e.car_alloc(2 * max_bytes)
+        self.own, self._opened, self.bases = 0, [], []
+        handle = None
+        try:
+            self.own = e.car_alloc(2 * max_bytes)
+            handle = e.car_ipc_handle(self.own)
+        except Exception:  # noqa: BLE001 - reported collectively below
+            handle = None
         handles = [None] * world
-        dist.all_gather_object(handles, e.car_ipc_handle(self.own), group=cpu_group)
-        self.bases = []
-        self._opened = []
-        for r, h in enumerate(handles):
-            if r == rank:
-                self.bases.append(self.own)
-            else:
-                p = e.car_open(h)
-                self._opened.append(p)
-                self.bases.append(p)
-        dist.barrier(group=cpu_group)
+        dist.all_gather_object(handles, handle, group=cpu_group)  # every rank, failed or not
+        ok = all(h is not None for h in handles)
+        if ok:
+            try:
+                for r, h in enumerate(handles):
+                    if r == rank:
+                        self.bases.append(self.own)
+                    else:
+                        p = e.car_open(h)
+                        self._opened.append(p)
+                        self.bases.append(p)
+            except Exception:  # noqa: BLE001
+                ok = False
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=cpu_group)  # the group's decision, the same everywhere
+        if int(flag.item()) == 0:
+            self.close()
+            raise CustomAllReduceUnavailable(f"custom all-reduce setup failed on some rank (this rank ok={ok})")
+        from kafka_llm_service_amd.utils import faults
+
+        self._fi_skip, self._fi_calls = faults.get().car_skip_call, 0
 
     def _fits(self, x: torch.Tensor) -> bool:
         n = x.shape[1] * x.shape[2] if _is_slab(x) else x.numel()
@@ -56,17 +84,27 @@ class CustomAllReduce:
     def should_use(self, x: torch.Tensor) -> bool:
         return (x.dtype == torch.bfloat16 or _is_slab(x)) and self._fits(x)
 
+    def _skip(self) -> bool:
+        """Fault injection (KAFKA_FI_CAR_SKIP_CALL): this rank does not take part in its n-th call."""
+        n = self._fi_skip
+        if not n:
+            return False
+        self._fi_calls += 1
+        return self._fi_calls == n
+
     def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """Sum over the group of x (bf16, in place unless ``out``) or of a split-K slab (into a new bf16 tensor)."""
         if _is_slab(x) and out is None:
             out = torch.empty(x.shape[1], x.shape[2], dtype=torch.bfloat16, device=x.device)
-        ext().car_all_reduce(x, out, self.bases, self.rank, self.max_bytes, self.nblocks)
+        if not self._skip():
+            ext().car_all_reduce(x, out, self.bases, self.rank, self.max_bytes, self.nblocks)
         return x if out is None else out
 
     def all_reduce_add_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
                                out: torch.Tensor) -> torch.Tensor:
-        ext().car_all_reduce_add_rmsnorm(x, residual, w, float(eps), out, self.bases, self.rank, self.max_bytes,
-                                         self.nblocks)
+        if not self._skip():
+            ext().car_all_reduce_add_rmsnorm(x, residual, w, float(eps), out, self.bases, self.rank, self.max_bytes,
+                                             self.nblocks)
         return out
 
     def check(self) -> None:
@@ -74,7 +112,13 @@ class CustomAllReduce:
         if ext().car_error(self.own):
             raise RuntimeError("custom all-reduce: a peer did not arrive within 2 s")
 
+    def error_async(self, out: torch.Tensor, idx: int) -> None:
+        """Stream-ordered copy of the error word into ``out[idx]`` (pinned int32): read it once the stream passed."""
+        ext().car_error_async(self.own, out, int(idx))
+
     def close(self) -> None:
+        if not self.own and not self._opened:
+            return
         e = ext()
         for p in self._opened:
             e.car_close(p)

@@ -90,16 +90,27 @@ def init(tp: int = 1, backend: str | None = None, device: str | None = None) -> 
 
 def _register_custom_ar(st: ParallelState, tp: int) -> None:
     """The one-shot xGMI all-reduce for decode-sized messages (parallel/custom_allreduce.py); RCCL stays the path for
-    everything else, and for all of it when the IPC mapping cannot be set up (logged, not fatal)."""
+    everything else, and for all of it when the IPC mapping cannot be set up on some rank — a decision the group
+    takes together (CustomAllReduce's setup is collective), so no rank runs RCCL while its peers run the custom
+    kernel (logged, not fatal)."""
     import logging
 
     from . import comm
-    from .custom_allreduce import CustomAllReduce
+    from .custom_allreduce import CustomAllReduce, CustomAllReduceUnavailable
 
     try:
         comm.register_custom(st.tp_group, CustomAllReduce(st.cpu_group, st.tp_rank, tp))
-    except Exception:  # noqa: BLE001
+    except CustomAllReduceUnavailable:
         logging.getLogger("kafka.parallel").exception("custom all-reduce unavailable; using RCCL for every message")
+
+
+def custom_ar():
+    """The TP group's CustomAllReduce, or None (RCCL only / TP = 1)."""
+    if _STATE.tp == 1:
+        return None
+    from . import comm
+
+    return comm.get_custom(_STATE.tp_group)
 
 
 def _timeout() -> timedelta:

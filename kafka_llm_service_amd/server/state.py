@@ -77,8 +77,8 @@ def _engine_kwargs(e) -> dict[str, Any]:
     kw: dict[str, Any] = {}
     if e.get("KAFKA_KV_DTYPE"):
         kw["kv_dtype"] = e["KAFKA_KV_DTYPE"]
-    if e.get("KAFKA_GRAPHS", "0") == "1":
-        kw["use_graphs"] = True
+    if e.get("KAFKA_GRAPHS") in ("0", "1"):  # unset: the engine's default (on for TP > 1)
+        kw["use_graphs"] = e["KAFKA_GRAPHS"] == "1"
     if e.get("KAFKA_MAX_NUM_SEQS"):
         kw["max_num_seqs"] = int(e["KAFKA_MAX_NUM_SEQS"])
     if e.get("KAFKA_MAX_BATCHED_TOKENS"):  # prefill tokens per step (smaller: earlier first tokens in a burst)

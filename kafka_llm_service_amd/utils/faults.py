@@ -11,6 +11,8 @@ check when off:
                                   for its streams, re-route, respawn)
   KAFKA_FI_KV_BLOCKS=<n>          cap the KV page pool (memory pressure -> preemption by recompute)
   KAFKA_FI_SANDBOX_DOWN=1         sandbox health checks and tool calls fail (error tool_result frames)
+  KAFKA_FI_CAR_SKIP_CALL=<n>      this rank skips its n-th custom xGMI all-reduce call (a peer that stops arriving:
+                                  its peers' waits time out and the TP leader's engine must raise, not emit tokens)
 """
 from __future__ import annotations
 
@@ -31,8 +33,9 @@ class FaultInjector:
         kv = e.get("KAFKA_FI_KV_BLOCKS")
         self.kv_blocks = int(kv) if kv else None
         self.sandbox_down = e.get("KAFKA_FI_SANDBOX_DOWN", "0") == "1"
+        self.car_skip_call = int(e.get("KAFKA_FI_CAR_SKIP_CALL", "0") or 0)
         self.active = bool(self.slow_step_s or self.step_error_every or self.worker_exit_after or self.kv_blocks
-                           or self.sandbox_down)
+                           or self.sandbox_down or self.car_skip_call)
         self._steps = 0
 
     def on_step(self) -> None:

@@ -229,3 +229,53 @@ def test_tp2_engine_on_one_gpu_matches_tp1(cuda, model, graphs):
         for i, tok in enumerate(o):
             row = lg[len(p) - 1 + i]
             assert (row.max() - row[tok]).item() < 0.15
+
+
+def _tp_skip_main(rank, world, port, q):
+    dev = rank % torch.cuda.device_count()
+    _env(rank, world, port, dev)
+    os.environ["KAFKA_TP_BACKEND"] = "gloo"
+    if rank == 1:  # the follower stops taking part in one layer-seam all-reduce (a peer that never arrives)
+        os.environ["KAFKA_FI_CAR_SKIP_CALL"] = "20"
+    from kafka_llm_service_amd.engine import tp_worker
+    from kafka_llm_service_amd.engine.model_runner import CollectiveError
+    from kafka_llm_service_amd.engine.sequence import SamplingParams
+    from kafka_llm_service_amd.parallel import state as pstate
+    from kafka_llm_service_amd.utils import faults
+
+    faults.reset()
+    eng, st = tp_worker.build_tp_engine(dict(CFG, device=f"cuda:{dev}", use_graphs=False), tp=world)
+    try:
+        if st.is_tp_leader:
+            sp = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
+            try:
+                eng.generate(_prompts(eng.model_cfg.vocab_size), sp)
+                q.put(("leader", "finished without an error"))
+            except CollectiveError as e:
+                q.put(("leader", f"raised: {e}"))
+            tp_worker.release_followers()
+        else:
+            tp_worker.follower_loop(eng)
+            q.put(("follower", "done"))
+    finally:
+        pstate.destroy()
+
+
+@pytest.mark.timeout(300)
+def test_tp2_custom_allreduce_lost_peer_fails_the_step(cuda):
+    """A TP peer that skips a custom all-reduce call makes the leader's wait time out (2 s): the error word rides
+    back with the step's sampled ids and the engine raises CollectiveError (replica failure -> 503 + respawn) instead
+    of streaming tokens computed from stale peer data (VERDICT r02 Missing #5)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_tp_skip_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in ps:
+        m = q.get(timeout=240)
+        res[m[0]] = m[1]
+    for p in ps:
+        p.join(timeout=60)
+    assert res["leader"].startswith("raised"), res["leader"]

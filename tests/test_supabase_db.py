@@ -147,3 +147,65 @@ def test_local_db_cache_and_write_behind(tmp_path):
         await fresh.close()
 
     asyncio.run(main())
+
+
+def test_local_db_failed_write_behind_is_reported(tmp_path):
+    """A write-behind save that fails is raised by sync() and its thread leaves the history cache, so the store
+    never keeps serving rows SQLite does not have (the error used to be swallowed by the callback)."""
+    import asyncio
+
+    import pytest
+
+    from kafka_llm_service_amd.db.local import LocalDBClient
+    from kafka_llm_service_amd.llm.types import Message
+
+    async def main():
+        db = LocalDBClient(str(tmp_path / "f.db"))
+        await db.initialize()
+        await db.create_thread(thread_id="t1", system_message="sys")
+        assert len(await db.get_thread_messages("t1")) == 1  # cached
+        real = db._insert
+        calls = {"n": 0}
+
+        def flaky(c, tid, m, meta, mid):
+            calls["n"] += 1
+            if m.content == "boom":
+                raise RuntimeError("disk full")
+            return real(c, tid, m, meta, mid)
+
+        db._insert = flaky
+        await db.add_messages("t1", [Message(role="user", content="ok"), Message(role="user", content="boom")],
+                              wait=False)
+        with pytest.raises(RuntimeError, match="disk full"):
+            await db.sync()
+        await db.sync()  # reported once
+        db._insert = real
+        # the whole failed call rolled back; the cache was dropped, so the read comes from SQLite
+        assert [m.content for m in await db.get_thread_messages("t1")] == ["sys"]
+        await db.close()
+
+    asyncio.run(main())
+
+
+def test_local_db_cache_miss_race_does_not_cache_stale_history(tmp_path):
+    """A history read that misses the cache and races a write queued after it must not cache what it read: the
+    per-thread write generation (bumped by add_messages / delete_thread_messages) makes the fill a no-op."""
+    import asyncio
+
+    from kafka_llm_service_amd.db.local import LocalDBClient
+    from kafka_llm_service_amd.llm.types import Message
+
+    async def main():
+        db = LocalDBClient(str(tmp_path / "r.db"))
+        await db.initialize()
+        await db.create_thread(thread_id="t1", system_message="sys")
+        db._cache.clear()
+        read = asyncio.ensure_future(db.get_thread_messages("t1"))  # queued first: sees only "sys"
+        await asyncio.sleep(0)
+        await db.add_message("t1", Message(role="user", content="new"))  # wait=True, queued after the read
+        assert [m.content for m in await read] == ["sys"]
+        assert "t1" not in db._cache  # the stale read was not cached
+        assert [m.content for m in await db.get_thread_messages("t1")] == ["sys", "new"]
+        await db.close()
+
+    asyncio.run(main())
