@@ -62,14 +62,14 @@ class PromptProvider(ABC):
     def _load_section_from_file(path: Path, name: str, order: int) -> PromptSection | None:
         if not path.exists():
             return None
-        return PromptSection(name=name, content=path.read_text(encoding="utf-8").strip(), order=order,
+        return PromptSection(name=name, content=path.read_text(encoding="utf-8"), order=order,
                              metadata={"file": str(path)})
 
     def _load_sections_from_directory(self, directory: Path, start_order: int = 0) -> list[PromptSection]:
         out = []
         for i, p in enumerate(sorted(directory.glob("*.md"))):
             name = re.sub(r"^\d+_", "", p.stem)
-            out.append(PromptSection(name=name, content=p.read_text(encoding="utf-8").strip(),
+            out.append(PromptSection(name=name, content=p.read_text(encoding="utf-8"),
                                      order=start_order + i, metadata={"file": str(p)}))
         return out
 

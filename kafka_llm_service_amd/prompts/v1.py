@@ -1,9 +1,15 @@
 """PromptProviderV1: the Kafka agent's default system prompt (13 sections: 7 core + 6 tool guides).
 
 Structure parity with /root/reference/src/prompts/v1.py:15-298 (section names and order, default enrichment keys,
-``create_minimal`` / ``create_tools_only`` / ``without_tools`` and the module factories). The section TEXT in
-``prompts/sections`` is this repo's own wording. The reference's rendered prompt is 70,496 chars (~16-17k Llama-3
-tokens); the synthetic benchmark prefix in bench.py reproduces that token count.
+``create_minimal`` / ``create_tools_only`` / ``without_tools`` and the module factories).
+
+Section text — two sets, picked by ``KAFKA_PROMPT`` (or the ``variant`` argument):
+  * ``reference`` (default): ``prompts/sections_reference`` holds the reference's 13 section files verbatim, as DATA
+    (SURVEY.md §2.1 #18 "copy as data"): the served prompt renders byte-identically to the reference's
+    PromptProviderV1 with its default enrichment (/root/reference/src/prompts/v1.py:73-117) — 70,496 chars,
+    ~16-17k Llama-3 tokens, the shared prefix every thread carries;
+  * ``compact``: ``prompts/sections`` is this repo's own shorter wording of the same sections (47k chars).
+The synthetic benchmark prefix in bench.py reproduces the reference prompt's token count either way.
 """
 from __future__ import annotations
 
@@ -13,6 +19,18 @@ from typing import Any
 from kafka_llm_service_amd.prompts.base import PromptProvider, PromptSection
 
 SECTIONS_DIR = Path(__file__).resolve().parent / "sections"
+REFERENCE_SECTIONS_DIR = Path(__file__).resolve().parent / "sections_reference"
+PROMPT_VARIANTS = {"reference": REFERENCE_SECTIONS_DIR, "compact": SECTIONS_DIR}
+
+
+def default_sections_dir(variant: str | None = None) -> Path:
+    """Section directory of a prompt variant (``KAFKA_PROMPT`` when not given; default ``reference``)."""
+    import os
+
+    v = variant or os.environ.get("KAFKA_PROMPT", "reference")
+    if v not in PROMPT_VARIANTS:
+        raise ValueError(f"KAFKA_PROMPT must be one of {sorted(PROMPT_VARIANTS)}, got {v!r}")
+    return PROMPT_VARIANTS[v]
 
 
 class PromptProviderV1(PromptProvider):
@@ -34,10 +52,12 @@ class PromptProviderV1(PromptProvider):
     TOOL_SECTIONS = ["notebook_shell", "search", "webcrawler", "agent", "domain_specific", "appfactory"]
 
     def __init__(self, enrichment: dict[str, Any] | None = None, sections: list[str] | None = None,
-                 sections_dir: str | Path | None = None, use_defaults: bool = True):
+                 sections_dir: str | Path | None = None, use_defaults: bool = True, variant: str | None = None):
         data = dict(self.DEFAULT_ENRICHMENT) if use_defaults else {}
         data.update(enrichment or {})
-        super().__init__(enrichment=data, sections=sections, sections_dir=sections_dir or SECTIONS_DIR)
+        self.variant = variant
+        super().__init__(enrichment=data, sections=sections,
+                         sections_dir=sections_dir or default_sections_dir(variant))
 
     def _load_sections(self) -> list[PromptSection]:
         out = []
@@ -58,15 +78,16 @@ class PromptProviderV1(PromptProvider):
 
     def create_minimal(self) -> "PromptProviderV1":
         return PromptProviderV1(enrichment=self.enrichment, sections=["intro", "core_principles", "workflow"],
-                                use_defaults=False)
+                                sections_dir=self._sections_dir, use_defaults=False)
 
     def create_tools_only(self) -> "PromptProviderV1":
-        return PromptProviderV1(enrichment=self.enrichment, sections=list(self.TOOL_SECTIONS), use_defaults=False)
+        return PromptProviderV1(enrichment=self.enrichment, sections=list(self.TOOL_SECTIONS),
+                                sections_dir=self._sections_dir, use_defaults=False)
 
     def without_tools(self) -> "PromptProviderV1":
         return PromptProviderV1(enrichment=self.enrichment,
                                 sections=[s for s in self.DEFAULT_SECTION_ORDER if s not in self.TOOL_SECTIONS],
-                                use_defaults=False)
+                                sections_dir=self._sections_dir, use_defaults=False)
 
 
 def create_default_provider(**enrichment) -> PromptProviderV1:

@@ -173,3 +173,27 @@ def test_tool_handlers_sync_async_stream():
     assert run(t2.run({"n": 3})) == "012"
     assert run(collect(t1.run_stream({"x": 2}))) == ['{"x": 2}']
     assert t2.is_streaming and not t1.is_streaming
+
+
+def test_reference_prompt_renders_byte_identically(monkeypatch):
+    """The served default system prompt is the reference's text (prompts/sections_reference, shipped as data per
+    SURVEY.md §2.1 #18): with the default enrichment (/root/reference/src/prompts/v1.py:73-117) it renders to
+    exactly the reference's 70,496-char prompt (sha256 of the reference rendering, computed from its section files
+    with its substitution rule and "\\n\\n" separator). KAFKA_PROMPT=compact selects this repo's shorter wording."""
+    import hashlib
+
+    from kafka_llm_service_amd.prompts.v1 import PromptProviderV1
+
+    monkeypatch.delenv("KAFKA_PROMPT", raising=False)
+    text = PromptProviderV1().get_system_prompt()
+    assert len(text) == 70496
+    assert hashlib.sha256(text.encode()).hexdigest() == \
+        "6feb95e05419a8fbc97c5ad110d7b06c5b2227715304b9a5c10b825876283cf7"
+    assert PromptProviderV1(variant="reference").get_system_prompt() == text
+    compact = PromptProviderV1(variant="compact").get_system_prompt()
+    assert 40000 < len(compact) < 60000 and compact != text
+    monkeypatch.setenv("KAFKA_PROMPT", "compact")
+    assert PromptProviderV1().get_system_prompt() == compact
+    # the minimal / tools-only derivatives keep the variant's text
+    minimal = PromptProviderV1(variant="reference").create_minimal().get_system_prompt()
+    assert text.startswith(minimal.split("\n\n---")[0]) and len(minimal) < len(text)
