@@ -34,7 +34,8 @@ class HostStep:
     B: int = 0
     T: int = 0
     nbt: int = 1
-    bt_w: int = 1           # block-table columns (pages of the longest row of the step)
+    bt_w: int = 1           # block-table columns (pages of the longest row of the step; a bucket under graphs)
+    bt_need: int = 0        # columns holding pages (<= bt_w): what a broadcast plan actually ships
     n_rows: int = 0
     s_total: int = 1        # partial slots per decode row (cascade prefix chunks + suffix pieces)
     n_dec_items: int = 0
@@ -68,7 +69,7 @@ class SampleParams:
 
 
 _PLAN_SCALARS = ("B", "T", "nbt", "bt_w", "n_rows", "s_total", "n_dec_items", "n_prefix_items", "cascade_prefix",
-                 "n_items", "prefill_splits", "n_merge", "n_late", "late_off")
+                 "n_items", "prefill_splits", "n_merge", "n_late", "late_off", "bt_need")
 PLAN_HDR = 32  # int64 header of a broadcast step plan
 
 
@@ -79,7 +80,12 @@ def pack_plan(h: HostStep, sp: SampleParams) -> tuple[np.ndarray, np.ndarray]:
     all-gathered logits itself, so its device copy of the sampled ids — the next step's late decode inputs — is
     identical to the leader's)."""
     n = sp.temp.shape[0]
-    parts = [h.i64.astype(np.int64, copy=False), h.i32.astype(np.int32, copy=False),
+    i32 = h.i32.astype(np.int32, copy=False)
+    nbt_w = h.nbt * h.bt_w
+    if 0 < h.bt_need < h.bt_w:  # ship only the block-table columns that hold pages (followers re-pad with zeros)
+        bt = i32[:nbt_w].reshape(h.nbt, h.bt_w)[:, :h.bt_need]
+        i32 = np.concatenate([bt.reshape(-1), i32[nbt_w:]])
+    parts = [h.i64.astype(np.int64, copy=False), i32,
              sp.temp.astype(np.float32, copy=False), sp.topp.astype(np.float32, copy=False),
              sp.topk.astype(np.int32, copy=False), sp.seeds.astype(np.int64, copy=False)]
     payload = np.concatenate([np.ascontiguousarray(a).reshape(-1).view(np.uint8) for a in parts])
@@ -87,7 +93,7 @@ def pack_plan(h: HostStep, sp: SampleParams) -> tuple[np.ndarray, np.ndarray]:
     hdr[0] = 1
     k = len(_PLAN_SCALARS)
     hdr[1:1 + k] = [getattr(h, f) for f in _PLAN_SCALARS]
-    hdr[1 + k:1 + k + 6] = [h.i64.size, h.i32.size, n, int(sp.greedy), int(bool(sp.procs) or sp.leader_tokens),
+    hdr[1 + k:1 + k + 6] = [h.i64.size, i32.size, n, int(sp.greedy), int(bool(sp.procs) or sp.leader_tokens),
                             payload.size]
     return hdr, payload
 
@@ -107,6 +113,11 @@ def unpack_plan(hdr: np.ndarray, payload: np.ndarray) -> tuple[HostStep, SampleP
 
     h.i64 = take(np.int64, n64)
     h.i32 = take(np.int32, n32)
+    if 0 < h.bt_need < h.bt_w:  # re-pad the shipped block-table columns to the step's layout width
+        nb = h.nbt * h.bt_need
+        bt = np.zeros((h.nbt, h.bt_w), dtype=np.int32)
+        bt[:, :h.bt_need] = h.i32[:nb].reshape(h.nbt, h.bt_need)
+        h.i32 = np.concatenate([bt.reshape(-1), h.i32[nb:]])
     sp = SampleParams(take(np.float32, n), take(np.float32, n), take(np.int32, n), take(np.int64, n), [],
                       bool(greedy), bool(lead))
     return h, sp
@@ -365,7 +376,10 @@ class ModelRunner:
         rows = B + len(pre)
         nbt = max(1, rows)
         need = max([-(-s.total_len // PAGE) for s in dec] + [-(-b // PAGE) for _, _, b in pre] + [1])
-        bt_w = self.max_blocks if self.graphs is not None else min(self.max_blocks, -(-need // 16) * 16)
+        # under graphs the width is a power-of-two bucket (>= 64 pages): the layout (and so the captured graph)
+        # changes only when the longest row crosses a bucket, and the per-step upload / TP broadcast stays small
+        bt_w = (min(self.max_blocks, max(64, 1 << (need - 1).bit_length())) if self.graphs is not None
+                else min(self.max_blocks, -(-need // 16) * 16))
         bt = np.zeros((nbt, bt_w), dtype=np.int32)
         groups: list[tuple[int, int]] = []
         seq_lens = np.fromiter((s.total_len for s in dec), dtype=np.int64, count=B)
@@ -421,7 +435,7 @@ class ModelRunner:
             slots[T_real:] = -1
             q_limit[T_real:] = 0
         # ---- decode metadata (+ cascade over each group's shared prefix)
-        h = HostStep(B=B, T=T, nbt=nbt, bt_w=bt_w, n_rows=len(logit_rows), patch=patch)
+        h = HostStep(B=B, T=T, nbt=nbt, bt_w=bt_w, bt_need=min(need, bt_w), n_rows=len(logit_rows), patch=patch)
         i32_parts = [bt.reshape(-1), q_limit]
         if B:
             kv_start = np.zeros(B, dtype=np.int64)

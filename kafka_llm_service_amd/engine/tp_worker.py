@@ -12,6 +12,12 @@ Design (SURVEY.md §2.4 "TP", §2.7 "broadcast scheduler decisions rank0 -> TP r
 The host broadcast is the ONLY control traffic, so followers can never disagree with the leader about batch
 composition, page ids or work items — correct by construction, and the data-plane collectives stay on the GPU.
 
+Plan transport (``KAFKA_PLAN_CHANNEL``): ``shm`` (default) is the native shared-memory ring of
+``runtime/csrc/plan_channel.cpp`` — the leader memcpys each plan into a slot and bumps a sequence word, followers
+spin/yield on it and read the slot in place (zero copy), acking once the plan is uploaded; ``gloo`` is two tensor
+broadcasts over the TCP control group. A plan larger than a slot is announced through the ring and sent over gloo.
+``benchmarks/plan_bcast_bench.py`` measures both at 2..8 ranks (profiles/r03/plan_bcast_*).
+
 ``DPClient(engine_cfg, n_replicas, tp=k)`` (engine/client.py) spawns ``n_replicas`` such groups (dp x tp processes,
 GPU ``dp_idx * tp + tp_rank``); each group gets its own rendezvous port, so replicas stay independent.
 """
@@ -20,6 +26,7 @@ from __future__ import annotations
 import logging
 import os
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -35,18 +42,143 @@ def leader_src() -> int:
     return st.rank - st.tp_rank
 
 
+_HDR_BYTES = 1 + len(_PLAN_SCALARS) + 5  # header slot holding the payload size
+_GLOO_MARK = 2                           # hdr[0]: the payload of this plan follows over gloo (larger than a slot)
+
+
+class PlanTransport:
+    """Leader -> followers plan transport of one TP group (see the module docstring). ``send`` on the leader,
+    ``recv`` + ``done`` on followers; ``close`` on both."""
+
+    def __init__(self, kind: str | None = None, slot_bytes: int | None = None, nslots: int = 3):
+        st = pstate.get()
+        self.src, self.grp, self.leader = leader_src(), st.cpu_group, st.is_tp_leader
+        self.timeout = float(os.environ.get("KAFKA_COLLECTIVE_TIMEOUT_S", "300"))
+        kind = kind or os.environ.get("KAFKA_PLAN_CHANNEL", "shm")
+        slot_bytes = slot_bytes or int(os.environ.get("KAFKA_PLAN_SLOT_BYTES", str(4 << 20)))
+        self.ch = None
+        if kind == "shm":
+            self.ch = self._open_shm(st, slot_bytes, nslots)
+        self.kind = "shm" if self.ch is not None else "gloo"
+
+    def _open_shm(self, st, slot_bytes: int, nslots: int):
+        """Collective: the leader creates the segment (if /dev/shm has room), every rank learns the name and
+        attaches; any failure anywhere -> the whole group uses gloo."""
+        import uuid
+
+        from kafka_llm_service_amd.runtime import native
+
+        name, ch = None, None
+        if self.leader:
+            try:
+                free = os.statvfs("/dev/shm").f_bavail * os.statvfs("/dev/shm").f_frsize
+                if free > 4 * nslots * slot_bytes:
+                    name = f"/kafka_plan_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+                    ch = native().PlanChannel(name, nslots, slot_bytes, st.tp - 1)
+            except Exception:  # noqa: BLE001 - fall back to gloo
+                log.exception("shared-memory plan channel unavailable")
+                name, ch = None, None
+        box = [name]
+        dist.broadcast_object_list(box, src=self.src, group=self.grp)
+        name = box[0]
+        ok = name is not None
+        if ok and not self.leader:
+            try:
+                ch = native().PlanChannel(name, st.tp_rank - 1)
+            except Exception:  # noqa: BLE001
+                log.exception("could not attach the plan channel %s", name)
+                ok, ch = False, None
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.grp)
+        if int(flag.item()) == 0:
+            if ch is not None:
+                ch.close()
+            return None
+        return ch
+
+    # --- leader ---------------------------------------------------------------------------------------------------
+    def send(self, hdr: np.ndarray, payload: np.ndarray) -> None:
+        if self.ch is not None:
+            if 16 + hdr.nbytes + payload.nbytes <= self.ch.slot_bytes:
+                self.ch.publish(hdr, payload, self.timeout)
+                return
+            mark = hdr.copy()
+            mark[0] = _GLOO_MARK
+            self.ch.publish(mark, np.zeros(0, dtype=np.uint8), self.timeout)
+        else:
+            dist.broadcast(torch.from_numpy(hdr), src=self.src, group=self.grp)
+            if int(hdr[0]) == 0:  # exit: no payload
+                return
+        dist.broadcast(torch.from_numpy(payload), src=self.src, group=self.grp)
+
+    def release(self) -> None:
+        self.send(np.zeros(PLAN_HDR, dtype=np.int64), np.zeros(0, dtype=np.uint8))
+
+    # --- followers ------------------------------------------------------------------------------------------------
+    def recv(self) -> tuple[np.ndarray, np.ndarray] | None:
+        """The next plan (header, payload), or None at exit. Views into the ring stay valid until ``done()``."""
+        if self.ch is not None:
+            hdr, payload = self.ch.recv(self.timeout)
+            if int(hdr[0]) == 0:
+                self.ch.ack()
+                return None
+            if int(hdr[0]) != _GLOO_MARK:
+                return hdr, payload
+            hdr = hdr.copy()
+            self.ch.ack()
+        else:
+            t = torch.zeros(PLAN_HDR, dtype=torch.int64)
+            dist.broadcast(t, src=self.src, group=self.grp)
+            hdr = t.numpy()
+            if int(hdr[0]) == 0:
+                return None
+        p = torch.empty(int(hdr[_HDR_BYTES]), dtype=torch.uint8)
+        dist.broadcast(p, src=self.src, group=self.grp)
+        hdr = hdr.copy()
+        hdr[0] = 1
+        self._gloo_plan = True
+        return hdr, p.numpy()
+
+    def done(self) -> None:
+        """The plan from the last ``recv`` has been consumed (uploaded): release its ring slot."""
+        if getattr(self, "_gloo_plan", False):
+            self._gloo_plan = False
+            return
+        if self.ch is not None:
+            self.ch.ack()
+
+    def close(self) -> None:
+        if self.ch is not None:
+            self.ch.close()
+            self.ch = None
+
+
+_TRANSPORT: PlanTransport | None = None
+
+
+def transport() -> PlanTransport:
+    """The process's plan transport (created collectively on first use; closed at exit so the leader's
+    shared-memory segment never outlives the group)."""
+    global _TRANSPORT
+    if _TRANSPORT is None:
+        import atexit
+
+        _TRANSPORT = PlanTransport()
+        atexit.register(close_transport)
+    return _TRANSPORT
+
+
 def attach_leader(engine) -> None:
     """Make ``engine`` (tp_rank 0) broadcast every launched step to its followers: a fixed int64 header and one
-    uint8 payload (model_runner.pack_plan), two gloo tensor broadcasts — no pickling on the step path."""
+    uint8 payload (model_runner.pack_plan) through the group's PlanTransport — no pickling on the step path."""
     st = pstate.get()
     if st.tp == 1:
         return
-    src, grp = leader_src(), st.cpu_group
+    tr = transport()
 
     def bcast(host, sp):
         hdr, payload = pack_plan(host, sp)
-        dist.broadcast(torch.from_numpy(hdr), src=src, group=grp)
-        dist.broadcast(torch.from_numpy(payload), src=src, group=grp)
+        tr.send(hdr, payload)
 
     engine.runner.broadcast = bcast
 
@@ -54,7 +186,7 @@ def attach_leader(engine) -> None:
 def release_followers() -> None:
     st = pstate.get()
     if st.tp > 1 and st.is_tp_leader:
-        dist.broadcast(torch.zeros(PLAN_HDR, dtype=torch.int64), src=leader_src(), group=st.cpu_group)
+        transport().release()
 
 
 @torch.inference_mode()
@@ -62,19 +194,16 @@ def follower_loop(engine) -> int:
     """Mirror the leader's steps until it sends the exit header. Returns the number of steps run. The follower only
     enqueues: its GPU runs each step when the collectives of that step meet the leader's (two steps can be in
     flight, as on the leader)."""
-    st = pstate.get()
-    src, grp = leader_src(), st.cpu_group
     runner = engine.runner
+    tr = transport()
     n = 0
-    hdr = torch.zeros(PLAN_HDR, dtype=torch.int64)
     while True:
-        dist.broadcast(hdr, src=src, group=grp)
-        if int(hdr[0]) == 0:
+        msg = tr.recv()
+        if msg is None:
             return n
-        payload = torch.empty(int(hdr[1 + len(_PLAN_SCALARS) + 5]), dtype=torch.uint8)
-        dist.broadcast(payload, src=src, group=grp)
-        host, sp = unpack_plan(hdr.numpy(), payload.numpy())
+        host, sp = unpack_plan(*msg)
         runner.follower_launch(host, sp)
+        tr.done()
         n += 1
 
 
@@ -91,6 +220,8 @@ def build_tp_engine(cfg_dict: dict, tp: int):
     cfg.device = dev or "cpu"
     cfg.tp, cfg.tp_rank = tp, st.tp_rank
     eng = LLMEngine(cfg)
+    if tp > 1:
+        transport()  # collective: every rank of the group sets up the plan transport together
     if st.is_tp_leader:
         attach_leader(eng)
     return eng, st
@@ -116,4 +247,12 @@ def tp_worker_main(dp_idx: int, tp_rank: int, tp: int, port: int, cfg_dict: dict
         else:
             follower_loop(eng)
     finally:
+        close_transport()
         pstate.destroy()
+
+
+def close_transport() -> None:
+    global _TRANSPORT
+    if _TRANSPORT is not None:
+        _TRANSPORT.close()
+        _TRANSPORT = None

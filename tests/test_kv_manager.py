@@ -118,3 +118,58 @@ def test_random_ops_keep_invariants(ops, prefix_cache):
         kv.free_sequence(s)
     assert kv.check_invariants()
     assert kv.available() == 24
+
+
+def test_plan_channel_ring_order_backpressure_and_timeout():
+    """Native shared-memory plan ring (runtime/csrc/plan_channel.cpp): followers see every plan in order (zero-copy
+    views), the leader blocks (bounded) when a follower falls nslots - 1 plans behind, and a dead peer is a
+    RuntimeError after the timeout instead of a hang."""
+    import os
+    import threading
+
+    import numpy as np
+    import pytest
+
+    from kafka_llm_service_amd.runtime import native
+
+    rt = native()
+    name = f"/kafka_plan_test_{os.getpid()}"
+    lead = rt.PlanChannel(name, 3, 4096, 2)
+    fol = [rt.PlanChannel(name, i) for i in range(2)]
+    got = {0: [], 1: []}
+
+    def follower(i):
+        for _ in range(10):
+            h, p = fol[i].recv(10.0)
+            got[i].append((int(h[1]), bytes(p[:4]), p.size))
+            fol[i].ack()
+
+    ts = [threading.Thread(target=follower, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for k in range(10):
+        hdr = np.zeros(32, dtype=np.int64)
+        hdr[1] = k
+        lead.publish(hdr, np.full(100 + k, k, dtype=np.uint8), 10.0)
+    for t in ts:
+        t.join(10)
+    for i in range(2):
+        assert got[i] == [(k, bytes([k] * 4), 100 + k) for k in range(10)]
+    # back-pressure: with no consumer the leader can run nslots ahead, then times out
+    for _ in range(3):
+        lead.publish(np.zeros(32, dtype=np.int64), np.zeros(8, dtype=np.uint8), 1.0)
+    with pytest.raises(RuntimeError, match="timeout"):
+        lead.publish(np.zeros(32, dtype=np.int64), np.zeros(8, dtype=np.uint8), 0.05)
+    with pytest.raises(Exception):
+        lead.publish(np.zeros(32, dtype=np.int64), np.zeros(8192, dtype=np.uint8), 1.0)  # larger than a slot
+    # a follower whose leader stopped publishing times out
+    for f in fol:
+        for _ in range(3):
+            f.recv(1.0)
+            f.ack()
+    with pytest.raises(RuntimeError, match="timeout"):
+        fol[0].recv(0.05)
+    for f in fol:
+        f.close()
+    lead.close()
+    assert not os.path.exists(f"/dev/shm{name}")
