@@ -41,8 +41,10 @@ class ServerConfig:
     # default tool_choice of engine-backed generations ("auto" | "required" | "none" | a JSON function object);
     # "required" makes random-init models drive the agent/tool loop with well-formed calls (BASELINE config 4)
     tool_choice: Any = "auto"
-    # subset of the Kafka v1 prompt sections (None = all 13, ~47k characters); small engines / CPU tests use a few
+    # subset of the Kafka v1 prompt sections (None = all 13: the reference's 70,496-character prompt, or ~47k with
+    # KAFKA_PROMPT=compact); small engines / CPU tests use a few
     prompt_sections: list[str] | None = None
+    agent_max_iterations: int = 50  # LLM <-> tool rounds per agent run (the reference's Agent default, base.py:78)
     warm_prefix: bool = True  # prefill + pin the shared system prefix on every replica before serving
     ignore_eos: bool = False  # benchmarks: generate exactly max_tokens (random-init weights emit EOS at random)
     # run a single engine in its own worker process (like a DP replica) instead of a thread of the API process: the
@@ -68,6 +70,7 @@ class ServerConfig:
                             warm_prefix=e.get("KAFKA_WARM_PREFIX", "1") == "1",
                             engine_process=_engine_process(e.get("KAFKA_ENGINE_PROCESS", "auto")),
                             prompt_sections=[x for x in e.get("KAFKA_PROMPT_SECTIONS", "").split(",") if x] or None,
+                            agent_max_iterations=int(e.get("KAFKA_AGENT_MAX_ITERATIONS", "50")),
                             engine_kwargs=_engine_kwargs(e))
 
 
@@ -146,7 +149,7 @@ class ServerState:
         tools = [get_weather_tool, count_tool] + PlannerTools(None).tools
         self.kafka = KafkaV1Provider(self.llm, tools=tools, sandbox_tools=sandbox_tools,
                                      mcp_servers=DEFAULT_MCP_SERVERS if cfg.mcp else [],
-                                     prompt_sections=cfg.prompt_sections)
+                                     prompt_sections=cfg.prompt_sections, max_iterations=cfg.agent_max_iterations)
         await self.kafka.initialize()
         if cfg.backend == "engine" and cfg.warm_prefix and hasattr(self.llm, "warm") and self.kafka.system_prompt:
             n = await self.llm.warm(self.kafka.system_prompt, await self.kafka.get_tools())
@@ -230,7 +233,8 @@ class ServerState:
             sandbox_tools = ShellTools(sb).tools + NotebookTools(sb).tools
         agent = KafkaV1Provider(self.llm, thread_id=thread_id, db_client=self.db,
                                 tools=[get_weather_tool, count_tool] + PlannerTools(thread_id).tools,
-                                sandbox_tools=sandbox_tools, prompt_sections=self.config.prompt_sections)
+                                sandbox_tools=sandbox_tools, prompt_sections=self.config.prompt_sections,
+                                max_iterations=self.config.agent_max_iterations)
         await agent.initialize()
         try:
             async for ev in agent.run_with_thread(messages, model=model, temperature=temperature,
