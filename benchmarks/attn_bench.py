@@ -114,31 +114,32 @@ def main():
                           "GB/s_logical": round(B * (P + Ls) * kv_bytes_tok / us / 1e3, 1)}))
 
     # new-turn prefill: 64 tokens against the full context of sequence 0
-    tile = ops.tile_rows(0) // G
     T = 64
     qp = torch.randn(T, Hq, D, device=dev, dtype=torch.bfloat16)
     ctx = P + Ls - T
     ql = torch.arange(ctx, ctx + T, dtype=torch.int32, device=dev)
-    for ck in (1024, 2048, 4096, 0):
-        if ck == 0:
-            items = [(t0, min(tile, T - t0), 0, 0, ctx + T, -1, 0, 0) for t0 in range(0, T, tile)]
-            it = torch.tensor(items, dtype=torch.int32, device=dev)
-            o = torch.empty(T, Hq, D, device=dev, dtype=torch.bfloat16)
-            us = timeit(lambda: ops.attn_prefill(it, qp, k, v, bt, ql, scale, out=o), iters=5)
-        else:
-            ns = math.ceil((ctx + T) / ck)
-            items = [(t0, min(tile, T - t0), 0, c0 * ck, min(ctx + T, (c0 + 1) * ck), c0, 0, 0)
-                     for t0 in range(0, T, tile) for c0 in range(ns)]
-            it = torch.tensor(items, dtype=torch.int32, device=dev)
-            part = torch.empty(T, Hq, ns, D, device=dev)
-            lse = torch.full((T, Hq, ns), float("-inf"), device=dev)
-            o = torch.empty(T, Hq, D, device=dev, dtype=torch.bfloat16)
+    for var in (0, 3):
+        tile = ops.tile_rows(var) // G
+        for ck in (1024, 2048, 4096, 0):
+            if ck == 0:
+                items = [(t0, min(tile, T - t0), 0, 0, ctx + T, -1, 0, 0) for t0 in range(0, T, tile)]
+                it = torch.tensor(items, dtype=torch.int32, device=dev)
+                o = torch.empty(T, Hq, D, device=dev, dtype=torch.bfloat16)
+                us = timeit(lambda: ops.attn_prefill(it, qp, k, v, bt, ql, scale, out=o, variant=var), iters=5)
+            else:
+                ns = math.ceil((ctx + T) / ck)
+                items = [(t0, min(tile, T - t0), 0, c0 * ck, min(ctx + T, (c0 + 1) * ck), c0, 0, 0)
+                         for t0 in range(0, T, tile) for c0 in range(ns)]
+                it = torch.tensor(items, dtype=torch.int32, device=dev)
+                part = torch.empty(T, Hq, ns, D, device=dev)
+                lse = torch.full((T, Hq, ns), float("-inf"), device=dev)
+                o = torch.empty(T, Hq, D, device=dev, dtype=torch.bfloat16)
 
-            def f():
-                ops.attn_prefill(it, qp, k, v, bt, ql, scale, out_part=part, lse_part=lse)
-                ops.attn_merge(part, lse, o)
-            us = timeit(f, iters=5)
-        print(json.dumps({"case": "prefill_newturn", "kv_chunk": ck, "us": round(us, 1)}))
+                def f():
+                    ops.attn_prefill(it, qp, k, v, bt, ql, scale, out_part=part, lse_part=lse, variant=var)
+                    ops.attn_merge(part, lse, o)
+                us = timeit(f, iters=5)
+            print(json.dumps({"case": "prefill_newturn", "variant": var, "kv_chunk": ck, "us": round(us, 1)}))
 
     # cold prefill throughput: 2048-token chunk at the start of a sequence (causal)
     T = 2048
@@ -156,11 +157,11 @@ def main():
     # the engine's plan (model_runner.plan_prefill_items): long tiles split into key pieces + per-range merges
     from kafka_llm_service_amd.engine.model_runner import plan_prefill_items
 
-    for T in (2048, 4096, 8192):
+    for var, T in [(v_, t_) for v_ in (0, 3) for t_ in (2048, 4096, 8192)]:
         qp = torch.randn(T, Hq, D, device=dev, dtype=torch.bfloat16)
         ql = torch.arange(0, T, dtype=torch.int32, device=dev)
         o = torch.empty(T, Hq, D, device=dev, dtype=torch.bfloat16)
-        tile = ops.tile_rows(0) // G
+        tile = ops.tile_rows(var) // G
         tiles = [(t0, min(tile, T - t0), 0, t0 + min(tile, T - t0), T) for t0 in range(0, T, tile)]
         items, splits, ranges = plan_prefill_items(tiles, Hkv, 256, 256)
         it = torch.tensor(items, dtype=torch.int32, device=dev)
@@ -168,12 +169,12 @@ def main():
         lse = torch.full((T, Hq, max(splits, 1)), float("-inf"), device=dev)
 
         def fp():
-            ops.attn_prefill(it, qp, k, v, bt, ql, scale, out=o, out_part=part, lse_part=lse)
+            ops.attn_prefill(it, qp, k, v, bt, ql, scale, out=o, out_part=part, lse_part=lse, variant=var)
             for lo, hi in ranges:
                 ops.attn_merge(part[lo:hi], lse[lo:hi], o[lo:hi])
         us = timeit(fp, iters=5)
         flops = 2 * T * T * Hq * D
-        print(json.dumps({"case": "prefill_causal_planned", "T": T, "splits": splits, "items": len(items),
+        print(json.dumps({"case": "prefill_causal_planned", "variant": var, "T": T, "splits": splits, "items": len(items),
                           "us": round(us, 1), "TF/s": round(flops / us / 1e6, 1)}))
 
 

@@ -3,8 +3,8 @@
 Layout of a node of ``world`` ranks:
   * ``tp`` consecutive ranks form one tensor-parallel group (Megatron column/row split, 2 all-reduces per layer),
   * the remaining factor ``dp = world // tp`` are independent engine replicas (DP) — each replica owns its own KV
-    cache and its own threads (thread-affinity routing, ``engine/dp_router.py``); replicas never communicate on the
-    hot path.
+    cache and its own threads (thread-affinity routing: ``route`` / ``DPClient`` in ``engine/client.py``);
+    replicas never communicate on the hot path.
   * ``ep`` (Mixtral) re-uses the TP group: experts are partitioned over its ranks; activations are already
     replicated after the attention all-reduce, so each rank gathers its experts' tokens locally and one all-reduce
     combines the partial outputs (``models/moe.py``; README "Expert parallelism").
