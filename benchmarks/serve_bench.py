@@ -79,6 +79,7 @@ async def _turn(client, url, tid, i, args, res):
     res.setdefault("by_turn", {}).setdefault(i, []).append(e2e)
     if ttft is not None:
         res["ttft"].append(ttft)
+        res.setdefault("ttft_by_turn", {}).setdefault(i, []).append(ttft)
         if out_tok > 1:
             res["tpot"].append((e2e - ttft) / (out_tok - 1))
     res["tokens"] += out_tok
@@ -196,6 +197,8 @@ def run(url, args):
         res["client_cpu"] += r["client_cpu"]
         for t, v in r.get("by_turn", {}).items():
             res["by_turn"].setdefault(t, []).extend(v)
+        for t, v in r.get("ttft_by_turn", {}).items():
+            res.setdefault("ttft_by_turn", {}).setdefault(t, []).extend(v)
     ms = lambda v: None if v is None else round(v * 1e3, 2)  # noqa: E731
     return {
         "metric": "serve: p50 TTFT + output tok/s, /v1/threads/{id}/chat/completions",
@@ -209,6 +212,8 @@ def run(url, args):
         "tpot_p50_ms": ms(statistics.median(res["tpot"])) if res["tpot"] else None,
         "output_tok_s": round(res["tokens"] / wall, 1), "requests_s": round(res["requests"] / wall, 1),
         "e2e_p50_ms_by_turn": {k: ms(_pct(v, 0.5)) for k, v in sorted(res["by_turn"].items())},
+        "ttft_p50_p99_ms_by_turn": {k: [ms(_pct(v, 0.5)), ms(_pct(v, 0.99))]
+                                    for k, v in sorted(res.get("ttft_by_turn", {}).items())},
     }
 
 

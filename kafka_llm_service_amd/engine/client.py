@@ -104,6 +104,13 @@ def _worker_main(rank: int, cfg_dict: dict, conn, n_local: int = 1) -> None:
     from kafka_llm_service_amd.utils.affinity import pin_local_process
 
     pin_local_process(rank, n_local)
+    from kafka_llm_service_amd.engine import fake
+
+    fe = fake.from_env()  # KAFKA_FAKE_ENGINE_STEP_MS: timing-only engine (API-path load tests on the CPU)
+    if fe is not None:
+        conn.send(("ready", {"device": "fake", "kv_pages": 0}))
+        serve_pipe(fe, conn)
+        return
     import torch
 
     from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
@@ -122,10 +129,32 @@ def _worker_main(rank: int, cfg_dict: dict, conn, n_local: int = 1) -> None:
 
 def serve_pipe(eng, conn) -> None:
     """Request loop of a replica (or TP-group leader): drain control messages, step while there is work, send a
-    heartbeat at least every HEARTBEAT_S (the parent's stall detector, ``DPClient._monitor``)."""
+    heartbeat at least every HEARTBEAT_S (the parent's stall detector, ``DPClient._monitor``).
+    ``KAFKA_ENGINE_PROFILE=<path>``: host-side cProfile of the loop, written when the replica is stopped."""
+    path = os.environ.get("KAFKA_ENGINE_PROFILE")
+    if not path:
+        return _serve_pipe(eng, conn)
+    import cProfile
+    import pstats
+
+    prof = cProfile.Profile()
+    try:
+        prof.runcall(_serve_pipe, eng, conn)
+    finally:
+        with open(f"{path}.{os.getpid()}", "w") as f:
+            st = pstats.Stats(prof, stream=f)
+            st.sort_stats("tottime").print_stats(50)
+            st.sort_stats("cumtime").print_stats(70)
+
+
+def _serve_pipe(eng, conn) -> None:
     from kafka_llm_service_amd.utils import faults
 
+    from kafka_llm_service_amd.obs import trace
+
     fi = faults.get()
+    tr = trace.tracer()
+    pinned: list[int] | None = None  # the shared prefix; "add" messages may reference it instead of carrying it
     last_hb = 0.0
     while True:
         now = time.monotonic()
@@ -139,15 +168,22 @@ def serve_pipe(eng, conn) -> None:
             msg = conn.recv()
             kind = msg[0]
             if kind == "add":
-                _, rid, prompt, pdict = msg
+                _, rid, prompt, pdict, *sent = msg
                 try:
+                    if isinstance(prompt, tuple):  # ("ref", n, suffix): the first n ids are the pinned prefix
+                        if pinned is None or len(pinned) < prompt[1]:
+                            raise ValueError("prompt references a shared prefix this replica was not sent")
+                        prompt = pinned[:prompt[1]] + prompt[2]
                     eng.add_request(rid, prompt, SamplingParams(**pdict))
                 except Exception as e:
                     conn.send(("error", rid, str(e)))
+                if sent and tr is not None:  # API submit -> engine admission (perf_counter is system-wide)
+                    tr.complete("pipe_in", "engine", sent[0], time.perf_counter(), f"req:{rid}")
             elif kind == "abort":
                 eng.abort(msg[1])
             elif kind == "pin":
-                eng.pin_prefix(msg[1])
+                pinned = list(msg[1])
+                eng.pin_prefix(pinned)
             elif kind == "health":
                 kv = eng.kv_stats()
                 conn.send(("health", {"running": eng.num_running, "waiting": eng.num_waiting,
@@ -162,7 +198,7 @@ def serve_pipe(eng, conn) -> None:
             outs = eng.step()
             if outs:
                 conn.send(("out", [(o.request_id, o.new_token_ids, o.finished, o.finish_reason, o.num_prompt_tokens,
-                                    o.num_output_tokens, o.num_cached_tokens) for o in outs]))
+                                    o.num_output_tokens, o.num_cached_tokens) for o in outs], time.perf_counter()))
 
 
 class DPClient:
@@ -205,6 +241,11 @@ class DPClient:
         self.restarts = [0] * n_replicas
         self._closing = False
         self._ids = itertools.count()
+        # the pinned shared prefix (~37k ids for the reference prompt): requests that start with it send only their
+        # suffix over the pipe (pickling the full id list cost ~0.8 ms of API-loop time per request, serialized over
+        # a burst of new turns) once the replica has been sent the prefix itself
+        self._pin: list[int] | None = None
+        self._pin_sent = [False] * n_replicas
         ports = base_port if base_port is not None else _free_port_base(n_replicas)
         pending = [self._spawn(r, ports + r) for r in range(n_replicas)]
         for r, conns in enumerate(pending):
@@ -249,6 +290,10 @@ class DPClient:
             self._gen[r] += 1
             self._alive[r] = True
             self._last_hb[r] = time.monotonic()
+            self._pin_sent[r] = False
+        if self._pin is not None:  # a respawned replica learns the shared prefix again before any request
+            self._send_quiet(r, ("pin", self._pin))
+            self._pin_sent[r] = True
         threading.Thread(target=self._reader, args=(r, conns[0], self._gen[r]), daemon=True,
                          name=f"kafka-dp-reader{r}").start()
 
@@ -290,6 +335,9 @@ class DPClient:
             pass
 
     def _reader(self, r: int, conn, gen: int) -> None:
+        from kafka_llm_service_amd.obs import trace
+
+        tr = trace.tracer()
         while True:
             try:
                 msg = conn.recv()
@@ -302,6 +350,9 @@ class DPClient:
             if kind == "hb":
                 self._last_hb[r] = time.monotonic()
             elif kind == "out":
+                if tr is not None and len(msg) > 2 and any(o[5] == 1 for o in msg[1]):  # engine send -> reader
+                    tr.complete("pipe_out", "api", msg[2], time.perf_counter(), f"replica{r}",
+                                {"outs": len(msg[1])})
                 batches: dict = {}
                 with self._lock:
                     for rid, toks, fin, reason, npt, nout, ncached in msg[1]:
@@ -348,8 +399,14 @@ class DPClient:
             self._streams[request_id] = (loop, q, r)
             self._loads[r] += 1
         pd = {k: v for k, v in params.__dict__.items() if k != "allowed_tokens_fn"}
+        pin = self._pin
+        n = len(pin) if pin is not None and self._pin_sent[r] else 0
+        if n and len(prompt_ids) > n and prompt_ids[n - 1] == pin[n - 1] and prompt_ids[:n] == pin:
+            payload = ("ref", n, list(prompt_ids[n:]))
+        else:
+            payload = list(prompt_ids)
         try:
-            self._send(r, ("add", request_id, list(prompt_ids), pd))
+            self._send(r, ("add", request_id, payload, pd, time.perf_counter()))
         except (OSError, BrokenPipeError):
             with self._lock:
                 self._streams.pop(request_id, None)
@@ -404,9 +461,11 @@ class DPClient:
 
     def pin_prefix(self, token_ids: list[int]) -> None:
         """Every replica holds (and pins) its own copy of the shared system prefix."""
+        self._pin = list(token_ids)
         for r in range(self.n_replicas):
             if self._alive[r]:
-                self._send_quiet(r, ("pin", list(token_ids)))
+                self._send_quiet(r, ("pin", self._pin))
+                self._pin_sent[r] = True
 
     def health(self) -> dict:
         for r in range(self.n_replicas):

@@ -164,6 +164,9 @@ class LLMEngine:
                                                max_prefill_chunk=cfg.max_prefill_chunk,
                                                prefill_tokens_while_decoding=cfg.prefill_tokens_while_decoding,
                                                step_rows_fit=self._step_rows_fit(),
+                                               prefill_cost_budget=int(os.environ.get("KAFKA_PREFILL_COST_BUDGET",
+                                                                                      "512")),
+                                               burst_sqrt_k=float(os.environ.get("KAFKA_BURST_SQRT_K", "2")),
                                                max_model_len=cfg.max_model_len, max_blocks_per_seq=max_blocks),
                                self.kvm)
         kc = [self.k_cache[i] for i in range(L)]

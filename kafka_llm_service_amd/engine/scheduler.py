@@ -15,6 +15,7 @@ The reference service has no scheduler — concurrency is one asyncio loop forwa
 """
 from __future__ import annotations
 
+import math
 from collections import deque
 from dataclasses import dataclass, field
 
@@ -40,6 +41,19 @@ class SchedulerConfig:
     # profiles/r02/gemm_sweep_M129_320.log). A new turn longer than the room is chunked over two steps.
     step_rows_fit: int = 0
     step_rows_fit_min: int = 32
+    # Burst splitting: new prefills admitted into one step may cost at most this many token-equivalents, a token at
+    # context position c counting 1 + c / attn_equiv_keys (its GEMM work plus its attention over c keys: at
+    # Llama-3-8B shapes ~30k keys of attention cost as much as the token's projections). The first admission of a
+    # step is never held back (a single cold prefill keeps its full chunk), so this only splits a BURST of new
+    # turns — e.g. 64 threads x 40 new tokens against a 37k-token shared prefix, ~5.6k token-equivalents — over
+    # a few steps, first arrivals first, instead of one ~100 ms step that every one of them waits for (0 = off).
+    # With a deep queue the per-step floor (weights streamed once per step, ~8 ms at Llama-3-8B) matters: at least
+    # ceil(sqrt(burst_sqrt_k x waiting)) admissions go into a step regardless of the cost budget — the group size
+    # that minimizes the mean completion time of n equal jobs over steps of (floor + group x job) when the floor is
+    # about burst_sqrt_k / 2 jobs (0 = off)
+    prefill_cost_budget: int = 512
+    attn_equiv_keys: int = 30000
+    burst_sqrt_k: float = 2.0
 
 
 @dataclass
@@ -113,6 +127,11 @@ class Scheduler:
         if self.kv.has_seq(seq.seq_id):
             self.kv.free_sequence(seq.seq_id)
 
+    def _cost(self, start: int, end: int) -> float:
+        """Token-equivalents of prefilling positions [start, end) (SchedulerConfig.prefill_cost_budget)."""
+        n = end - start
+        return n * (1.0 + (start + end) * 0.5 / max(1, self.cfg.attn_equiv_keys))
+
     def schedule(self, speculative: bool = False) -> ScheduledBatch:
         """Build the next batch. ``speculative``: planned while the previous step is still on the GPU (its sampled
         tokens are PENDING placeholders): sequences whose pending token is their last by length are left out, and a
@@ -157,15 +176,24 @@ class Scheduler:
             batch.prefill.append((seq, seq.num_computed, end))
             budget -= n
         # 3. admissions
+        cost = sum(self._cost(a, b) for _, a, b in batch.prefill)
+        admitted = 0
+        group = math.ceil(math.sqrt(cfg.burst_sqrt_k * len(self.waiting))) if cfg.burst_sqrt_k else 1
         while self.waiting and budget > 0 and len(self.running) < cfg.max_num_seqs:
             seq = self.waiting[0]
             toks = seq.all_ids()
             cached = self.kv.add_sequence(seq.seq_id, toks)
             n = min(seq.total_len - cached, budget, cfg.max_prefill_chunk)
             end = cached + n
+            c = self._cost(cached, end)
+            if cfg.prefill_cost_budget and admitted >= group and cost + c > cfg.prefill_cost_budget:
+                self.kv.free_sequence(seq.seq_id)  # next step (its prefix match is redone then)
+                break
             if not self.kv.ensure_capacity(seq.seq_id, end):
                 self.kv.free_sequence(seq.seq_id)
                 break
+            cost += c
+            admitted += 1
             self.waiting.popleft()
             seq.num_cached = cached if seq.preemptions == 0 else seq.num_cached
             seq.num_computed = cached

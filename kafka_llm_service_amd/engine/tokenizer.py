@@ -147,9 +147,22 @@ class IncrementalDetokenizer:
         self.prefix_offset = 0
         self.read_offset = 0
         self.text = ""
+        # the shipped byte-level BPE decodes a concatenation to the concatenation of the pieces' decodes whenever
+        # no UTF-8 sequence is split, so a token following fully emitted text is decoded ALONE (one decode per
+        # streamed token instead of two windows); an external tokenizer.json (e.g. SentencePiece spacing) keeps the
+        # window diff
+        self.byte_level = not getattr(tok, "external", True)
 
     def add(self, new_ids: list[int]) -> str:
-        self.ids.extend(new_ids)
+        if self.byte_level and self.read_offset == len(self.ids):
+            self.ids.extend(new_ids)
+            piece = self.tok.decode(new_ids, self.skip)
+            if not piece.endswith("\ufffd"):
+                self.prefix_offset = self.read_offset = len(self.ids)
+                self.text += piece
+                return piece
+        else:
+            self.ids.extend(new_ids)
         prefix = self.tok.decode(self.ids[self.prefix_offset:self.read_offset], self.skip)
         full = self.tok.decode(self.ids[self.prefix_offset:], self.skip)
         if len(full) <= len(prefix) or full.endswith("\ufffd"):

@@ -42,7 +42,26 @@ def main() -> None:
     from kafka_llm_service_amd.server.app import create_app
 
     setup_logging()
-    uvicorn.run(create_app(), host=a.host, port=a.port, log_level=a.log_level, workers=1)
+    prof_path = os.environ.get("KAFKA_API_PROFILE")  # event-loop (main thread) profile, written at shutdown
+    if not prof_path:
+        uvicorn.run(create_app(), host=a.host, port=a.port, log_level=a.log_level, workers=1)
+        return
+    import cProfile
+    import pstats
+
+    import signal
+    import sys
+
+    # uvicorn re-raises the captured SIGTERM after its graceful shutdown: make that an exit that runs `finally`
+    signal.signal(signal.SIGTERM, lambda *_: sys.exit(0))
+    prof = cProfile.Profile()
+    try:
+        prof.runcall(uvicorn.run, create_app(), host=a.host, port=a.port, log_level=a.log_level, workers=1)
+    finally:
+        with open(prof_path, "w") as f:
+            st = pstats.Stats(prof, stream=f)
+            st.sort_stats("tottime").print_stats(45)
+            st.sort_stats("cumtime").print_stats(60)
 
 
 if __name__ == "__main__":

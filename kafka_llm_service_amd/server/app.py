@@ -154,6 +154,12 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
         t_first = None
         finish = "stop"
         usage = None
+        # content frames are the per-token hot path of the API loop (64 streams x ~110 tokens/s each): the constant
+        # part of the frame is formatted once per request and only the text is JSON-encoded per token (the same
+        # bytes as _chunk(..., {"content": text}, None))
+        head = ('data: {"id":%s,"object":"chat.completion.chunk","created":%d,"model":%s,"choices":[{"index":0,'
+                '"delta":{"role":null,"content":' % (json.dumps(cid), created, json.dumps(model)))
+        tail = ',"tool_calls":null},"finish_reason":null}]}\n\n'
         try:
             yield _chunk(cid, created, model, {"role": "assistant"}, None)
             async for ev in st.run_agent(messages, req.model, req.temperature, req.max_tokens, thread_id,
@@ -182,18 +188,19 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
                         if tr is not None:  # request in -> first content frame handed to the response
                             tr.complete("api_http_ttft", "api", t0, t_first, f"thr:{thread_id}")
                         first = False
-                    yield _chunk(cid, created, model, {"content": text}, None)
+                    yield head + json.dumps(text) + tail
                 if ch[0].get("finish_reason") == "length":
                     finish = "length"
-            yield _chunk(cid, created, model, {}, finish)
+            end = _chunk(cid, created, model, {}, finish)
             if req.stream_options and req.stream_options.include_usage:
                 u = usage or {}
-                yield _sse({"id": cid, "object": "chat.completion.chunk", "created": created, "model": model,
-                            "choices": [], "usage": {k: u.get(k, 0) for k in ("prompt_tokens", "completion_tokens",
-                                                                             "total_tokens")}})
+                end += _sse({"id": cid, "object": "chat.completion.chunk", "created": created, "model": model,
+                             "choices": [], "usage": {k: u.get(k, 0) for k in ("prompt_tokens", "completion_tokens",
+                                                                              "total_tokens")}})
+            tail_frames = end  # finish + usage + [DONE] leave in one send
         except Exception as e:  # the reference's error frame (server.py:375-377)
             log.exception("completion stream failed")
-            yield _sse({"error": {"message": str(e), "type": "server_error"}})
+            tail_frames = _sse({"error": {"message": str(e), "type": "server_error"}})
         t_end = time.perf_counter()
         M.E2E.observe(t_end - t0)
         n_out = (usage or {}).get("completion_tokens", 0)
@@ -201,7 +208,7 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
             M.OUTPUT_TOKENS.inc(n_out)
             if n_out > 1 and t_first is not None:
                 M.TPOT.observe((t_end - t_first) / (n_out - 1))
-        yield "data: [DONE]\n\n"
+        yield tail_frames + "data: [DONE]\n\n"
 
     async def completion_json(messages, req: ChatCompletionRequest, thread_id: str | None) -> ChatCompletionResponse:
         content, usage, finish = "", {}, "stop"
@@ -237,8 +244,7 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
         tool_events = request.headers.get("x-kafka-tool-events") == "1"
         if req.stream:
             return StreamingResponse(_coalesce(completion_events(msgs, req, None, tool_events)),
-                                     media_type="text/event-stream",
-                                     headers=SSE_HEADERS)
+                                     media_type="text/event-stream", headers=SSE_HEADERS)
         return await completion_json(msgs, req, None)
 
     async def agent_events(gen) -> AsyncGenerator[str, None]:

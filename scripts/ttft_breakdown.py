@@ -29,7 +29,8 @@ def load(paths):
 def main():
     paths = [q for a in sys.argv[1:] for q in glob.glob(a)]
     evs = load(paths)
-    names = ["api_http_ttft", "api_db_load", "api_db_save", "api_render", "api_engine_first", "first_token"]
+    names = ["api_http_ttft", "api_db_load", "api_db_save", "api_render", "api_engine_first", "pipe_in", "first_token",
+             "pipe_out"]
     print(f"{'span':20s} {'n':>6s} {'p50 ms':>9s} {'p99 ms':>9s} {'mean ms':>9s}")
     for n in names:
         d = sorted(e["dur"] / 1e3 for e in evs if e["name"] == n)

@@ -123,7 +123,8 @@ def test_step_rows_fit_keeps_mixed_steps_on_the_streaming_gemm():
     def setup(n_dec, fit):
         kv = KVManager(8192, 16, True)
         sch = Scheduler(SchedulerConfig(max_num_batched_tokens=8192, prefill_tokens_while_decoding=512,
-                                        tpot_guard_decodes=4, step_rows_fit=fit, step_rows_fit_min=32), kv)
+                                        tpot_guard_decodes=4, step_rows_fit=fit, step_rows_fit_min=32,
+                                        prefill_cost_budget=0), kv)
         sp = SamplingParams(max_tokens=8, ignore_eos=True)
         decs = [Sequence(f"d{i}", list(range(100 * i + 1, 100 * i + 33)), sp) for i in range(n_dec)]
         for d in decs:
@@ -149,3 +150,37 @@ def test_step_rows_fit_keeps_mixed_steps_on_the_streaming_gemm():
     sch, sp = setup(64, 0)  # off
     sch.add(Sequence("turn", list(range(50000, 50000 + 90)), sp))
     assert sum(e - s for _, s, e in sch.schedule().prefill) == 90
+
+
+def test_burst_of_new_turns_is_split_by_attention_cost():
+    """64 new turns arriving together against a long cached context are admitted over several steps (first come,
+    first served) by the token-equivalent cost budget; a single cold prefill is never held back by it."""
+    from kafka_llm_service_amd.engine.scheduler import Scheduler, SchedulerConfig
+    from kafka_llm_service_amd.engine.sequence import SamplingParams, Sequence
+    from kafka_llm_service_amd.runtime import KVManager
+
+    kv = KVManager(16384, 16, True)
+    sch = Scheduler(SchedulerConfig(prefill_cost_budget=2048, attn_equiv_keys=30000, burst_sqrt_k=0), kv)
+    sp = SamplingParams(max_tokens=4, ignore_eos=True)
+    prefix = list(range(1, 36001))
+    warm = Sequence("warm", prefix + [7], sp)
+    sch.add(warm)
+    b = sch.schedule()  # one cold prefill: the budget does not chunk it further than the usual chunk limit
+    assert b.prefill == [(warm, 0, 8192)]
+    while warm.num_computed < warm.total_len - 1:
+        warm.num_computed = b.prefill[0][2]
+        kv.commit(warm.seq_id, warm.num_computed)
+        b = sch.schedule()
+    sch.finish(warm, "length")
+    turns = [Sequence(f"t{i}", prefix + list(range(90000 + 50 * i, 90000 + 50 * i + 40)), sp) for i in range(64)]
+    for t in turns:
+        sch.add(t)
+    seen = []
+    while sch.waiting:
+        b = sch.schedule()
+        seen.append([s.request_id for s, _, _ in b.prefill])
+        for s, a, e in b.prefill:
+            s.num_computed = e
+    # ~40 new tokens at ~36k context cost ~88 token-equivalents each: ~23 per step, admitted in arrival order
+    assert 3 <= len(seen) <= 4 and all(seen)
+    assert [r for step in seen for r in step] == [t.request_id for t in turns]

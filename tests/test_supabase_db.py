@@ -209,3 +209,33 @@ def test_local_db_cache_miss_race_does_not_cache_stale_history(tmp_path):
         await db.close()
 
     asyncio.run(main())
+
+
+def test_local_db_new_thread_history_is_cached_at_creation(tmp_path):
+    """A thread created by this client starts with its (empty) history cached, so the first turn's history load
+    never queues behind other threads' SQLite I/O (HTTP burst TTFT); re-creating an EXISTING thread (INSERT OR
+    IGNORE) must not cache an empty history over its stored rows."""
+    import asyncio
+
+    from kafka_llm_service_amd.db.local import LocalDBClient
+    from kafka_llm_service_amd.llm.types import Message
+
+    async def main():
+        path = str(tmp_path / "c.db")
+        db = LocalDBClient(path)
+        await db.initialize()
+        await db.create_thread(thread_id="t1")
+        await db.add_message("t1", Message(role="user", content="hi"))
+        real = db._connect
+        db._connect = lambda: (_ for _ in ()).throw(AssertionError("history read went to SQLite"))
+        assert [m.content for m in await db.get_thread_messages("t1")] == ["hi"]
+        db._connect = real
+        await db.close()
+        other = LocalDBClient(path)
+        await other.initialize()
+        await other.create_thread(thread_id="t1")  # already exists: nothing cached
+        assert "t1" not in other._cache
+        assert [m.content for m in await other.get_thread_messages("t1")] == ["hi"]
+        await other.close()
+
+    asyncio.run(main())
