@@ -166,7 +166,7 @@ class LLMEngine:
                                                step_rows_fit=self._step_rows_fit(),
                                                prefill_cost_budget=int(os.environ.get("KAFKA_PREFILL_COST_BUDGET",
                                                                                       "512")),
-                                               burst_sqrt_k=float(os.environ.get("KAFKA_BURST_SQRT_K", "2")),
+                                               burst_sqrt_k=float(os.environ.get("KAFKA_BURST_SQRT_K", "0")),
                                                max_model_len=cfg.max_model_len, max_blocks_per_seq=max_blocks),
                                self.kvm)
         kc = [self.k_cache[i] for i in range(L)]

@@ -47,13 +47,13 @@ class SchedulerConfig:
     # step is never held back (a single cold prefill keeps its full chunk), so this only splits a BURST of new
     # turns — e.g. 64 threads x 40 new tokens against a 37k-token shared prefix, ~5.6k token-equivalents — over
     # a few steps, first arrivals first, instead of one ~100 ms step that every one of them waits for (0 = off).
-    # With a deep queue the per-step floor (weights streamed once per step, ~8 ms at Llama-3-8B) matters: at least
-    # ceil(sqrt(burst_sqrt_k x waiting)) admissions go into a step regardless of the cost budget — the group size
-    # that minimizes the mean completion time of n equal jobs over steps of (floor + group x job) when the floor is
-    # about burst_sqrt_k / 2 jobs (0 = off)
+    # Optional: with a deep queue at least ceil(sqrt(burst_sqrt_k x waiting)) admissions go into a step regardless
+    # of the budget (the group size minimizing the mean completion of n equal jobs over steps of floor + group x
+    # job). Measured on MI355X it only trades later turns for the synchronized first one (profiles/r03/
+    # serve_burst_ab.jsonl: turn-0 p50 ~240 vs ~255 ms, turns 1-3 ~100-180 vs ~50-70 ms), so it is off (0).
     prefill_cost_budget: int = 512
     attn_equiv_keys: int = 30000
-    burst_sqrt_k: float = 2.0
+    burst_sqrt_k: float = 0.0
 
 
 @dataclass

@@ -88,66 +88,58 @@ class MoEBlock:
     # ------------------------------------------------------------------------------------------------------------
     def _a2a(self, x: torch.Tensor, lw, r) -> torch.Tensor:
         """Expert parallelism with an all-to-all dispatch and combine (``KAFKA_MOE_A2A=1``; BASELINE config 5's
-        "expert all-to-all").
+        "expert all-to-all"), device-side end to end: no host synchronisation, capturable into a hipGraph.
 
         Every rank holds all T tokens (replicated after the attention all-reduce) and computes the same routing.
-        Rank q OWNS tokens [q Tl, (q+1) Tl): it packs each owned (token, expert) pair into the bucket of the rank
-        that holds the expert (``all_to_all_single`` with equal splits: a capacity of Tl*k rows per destination, so
-        no host round trip for split sizes), the expert ranks run their local experts on what they received (the
-        same grouped-GEMM kernels over a k=1 routing of the received rows), the outputs travel back with a second
-        all-to-all, the owner applies the routing weights and the owners' rows are all-gathered into the replicated
-        [T, d] the next layer expects. With tensor-parallel attention this moves more bytes than the default
-        all-reduce combine (capacity padding + the all-gather), so it is not the default; it is the building block
-        for data-parallel attention, where tokens are not replicated."""
+        Rank q OWNS tokens [q Tl, (q+1) Tl). ``ops.ep_dispatch`` (csrc/moe.hip) packs each owned (token, expert)
+        pair into the block of the rank that holds the expert — fixed capacity C = Tl min(k, El) slots per
+        destination plus metadata rows carrying the count and each slot's local expert — so the transport needs no
+        split sizes from the host. Transport: the custom IPC all-to-all (parallel/custom_allreduce.py, the same
+        buffers and epochs as the decode all-reduce) when the image fits its buffer, else ``all_to_all_single``
+        (RCCL; gloo when the ranks share one GPU). The expert ranks route the received slots on the device
+        (``ops.ep_recv_route``), run their local experts with the same grouped kernels as the all-reduce path
+        (weights 1), send the rows back, the owners apply the routing weights (``ops.ep_combine``) and the owned
+        rows are all-gathered into the replicated [T, d] the next layer expects. With tensor-parallel attention
+        this moves more bytes than the default all-reduce combine (capacity padding + the all-gather), so it is
+        opt-in; it is the dispatch/combine a data-parallel attention layout needs, where tokens are not
+        replicated."""
         from kafka_llm_service_amd.parallel import comm
 
         T, d = x.shape
         ep, q, k, El = self.ep, self.r, self.k, self.e_local
         grp = pstate.get().tp_group
-        dev = x.device
-        Tl = (T + ep - 1) // ep
+        Tl, C, MR = ops.ep_layout(T, ep, k, El, d)
         lo, hi = min(T, q * Tl), min(T, (q + 1) * Tl)
         n_own = hi - lo
-        C = Tl * k  # rows per destination bucket (worst case: every owned pair goes to one rank)
-        te = r.topk_e[lo:hi].long().reshape(-1)                  # [n_own*k] global expert ids
-        tw = r.topk_w[lo:hi].float().reshape(-1)
-        tok = torch.arange(lo, hi, device=dev).repeat_interleave(k)
-        dest = te // El
-        # stable position of each pair inside its destination bucket
-        onehot = F.one_hot(dest, ep).to(torch.int32)
-        pos = ((torch.cumsum(onehot, 0) - 1) * onehot).sum(1)
-        send = torch.zeros(ep, C, d, dtype=x.dtype, device=dev)
-        meta = torch.full((ep, C), -1, dtype=torch.int32, device=dev)
-        if n_own:
-            send[dest, pos] = x[tok]
-            meta[dest, pos] = (te - dest * El).to(torch.int32)
-        recv = torch.empty_like(send)
-        rmeta = torch.empty_like(meta)
-        comm.all_to_all_single(recv, send, grp)
-        comm.all_to_all_single(rmeta, meta, grp)
-        # local expert MLP over the received rows (k = 1 routing; empty slots carry expert -1 and are skipped)
-        rows = recv.view(ep * C, d)
-        re = rmeta.view(-1).long()
-        valid = re >= 0
-        key = torch.where(valid, re, torch.full_like(re, El))     # empty slots sort past the last expert
-        perm = torch.argsort(key, stable=True)
-        counts = torch.bincount(key, minlength=El + 1)[:El]
-        eo = torch.zeros(El + 1, dtype=torch.int32, device=dev)
-        eo[1:] = torch.cumsum(counts, 0)
-        to = torch.zeros(El + 1, dtype=torch.int32, device=dev)
-        to[1:] = torch.cumsum((counts + ops.GG_BM - 1) // ops.GG_BM, 0)
-        n_valid = int(ep * C)  # perm covers every slot; segments stop at eo[El]
-        rr = ops.MoERouting(torch.ones(ep * C, 1, device=dev), re.to(torch.int32).view(-1, 1),
-                            perm.to(torch.int32), torch.ones(n_valid, device=dev), eo, to, El)
-        h = ops.grouped_gemm(rows, lw.w13, rr, gather=True, e_lo=0)
-        a = ops.silu_mul(h)
-        y = torch.zeros(ep * C, d, dtype=torch.float32, device=dev)
-        ops.grouped_gemm(a, lw.w2, rr, gather=False, e_lo=0, combine_out=y)
-        back = torch.empty_like(send)
-        comm.all_to_all_single(back, y.to(x.dtype).view(ep, C, d), grp)
-        own = torch.zeros(Tl, d, dtype=torch.float32, device=dev)
-        if n_own:
-            own.index_add_(0, tok - lo, back[dest, pos].float() * tw[:, None])
-        full = torch.empty(ep * Tl, d, dtype=x.dtype, device=dev)
-        comm.all_gather_into(full, own.to(x.dtype), ep, grp)
+        img, slot = ops.ep_dispatch(x, r.topk_e, lo, n_own, El, ep, C, MR)
+        car = comm.get_custom(grp)
+        if car is not None and not car.fits_bytes(img.numel() * img.element_size()):
+            car = None
+
+        def exchange(send: torch.Tensor) -> torch.Tensor:
+            recv = torch.empty_like(send)
+            if car is not None:
+                return car.all_to_all(send, recv)
+            return comm.all_to_all_single(recv, send, grp)
+
+        recv = exchange(img)
+        rr = ops.ep_recv_route(recv, C, El)
+        rows = recv.view(-1, d)
+        y = torch.zeros(rows.shape[0], d, dtype=torch.float32, device=x.device)
+        if self.model.stream and lw.w13_t is not None and rows.shape[0] <= MOE_STREAM_MAX_T:
+            a = ops.grouped_stream_glu(rows, lw.w13_t, rr, e_lo=0)
+            ops.grouped_stream_combine(a, lw.w2_t, rr, rows.shape[0], y, e_lo=0)
+        else:
+            h = ops.grouped_gemm(rows, lw.w13, rr, gather=True, e_lo=0)
+            ops.grouped_gemm(ops.silu_mul(h), lw.w2, rr, gather=False, e_lo=0, combine_out=y)
+        back = exchange(y.to(x.dtype).view(ep, C + MR, d))
+        own = torch.empty(Tl, d, dtype=x.dtype, device=x.device)
+        if n_own < Tl:
+            own[n_own:].zero_()  # past the last token (sliced off below; kept finite)
+        ops.ep_combine(back, slot, r.topk_w, lo, n_own, own)
+        full = torch.empty(ep * Tl, d, dtype=x.dtype, device=x.device)
+        if car is not None and car.fits_bytes(own.numel() * own.element_size()):
+            car.all_gather(own, full)
+        else:
+            comm.all_gather_into(full, own, ep, grp)
         return full[:T]

@@ -420,3 +420,60 @@ def grouped_gemm(x: torch.Tensor, w: torch.Tensor, r: MoERouting, gather: bool, 
     else:
         ref.grouped_gemm(x, w, r.perm_tok, r.perm_w, r.expert_off, e_lo, gather, y, combine_out)
     return combine_out if combine_out is not None else y
+
+
+# ---- expert-parallel all-to-all (csrc/moe.hip ep_*, models/moe.py MoEBlock._a2a) --------------------------------
+def ep_layout(T: int, ep: int, k: int, El: int, d: int) -> tuple[int, int, int]:
+    """(owned tokens per rank Tl, slot capacity C per destination, metadata rows MR) of the EP send image
+    [ep, C + MR, d]: a token's k experts are distinct, so at most min(k, El) of its pairs go to one rank."""
+    Tl = max(1, -(-T // ep))
+    C = Tl * min(k, El)
+    MR = -(-(16 + 4 * C) // (2 * d))
+    return Tl, C, MR
+
+
+def ep_dispatch(x: torch.Tensor, topk_e: torch.Tensor, lo: int, n_own: int, El: int, ep: int, C: int,
+                MR: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """Send image [ep, C + MR, d] bf16 of the owned (token, expert) pairs + their slot map (int32 [n_own * k]:
+    destination block row of each pair), computed on the device."""
+    d = x.shape[1]
+    k = topk_e.shape[1]
+    img = torch.empty(ep, C + MR, d, dtype=x.dtype, device=x.device)
+    slot = torch.empty(max(1, n_own * k), dtype=torch.int32, device=x.device)
+    te = topk_e if topk_e.dtype == torch.int32 else topk_e.to(torch.int32)
+    if _gpu(x):
+        ext().ep_dispatch(x, te.contiguous(), int(lo), int(n_own), int(El), int(C), img, slot)
+    else:
+        img.zero_()
+        ref.ep_dispatch(x, te, lo, n_own, El, C, img, slot)
+    return img, slot
+
+
+def ep_recv_route(img: torch.Tensor, C: int, El: int) -> "MoERouting":
+    """MoERouting over the rows of a received EP image: valid slots sorted stably by local expert."""
+    ep = img.shape[0]
+    dev = img.device
+    if _gpu(img):
+        pt = torch.empty(ep * C, dtype=torch.int32, device=dev)
+        pw = torch.empty(ep * C, dtype=torch.float32, device=dev)
+        eo = torch.empty(El + 1, dtype=torch.int32, device=dev)
+        to = torch.empty(El + 1, dtype=torch.int32, device=dev)
+        ext().ep_recv_route(img, int(C), int(El), GG_BM, pt, pw, eo, to)
+    else:
+        pt, pw, eo, to = ref.ep_recv_route(img, C, El, GG_BM)
+    rows = img.shape[0] * img.shape[1]  # combine outputs are indexed by image row (topk_* are not read)
+    tw = torch.zeros(rows, 1, dtype=torch.float32, device=dev)
+    return MoERouting(tw, tw.to(torch.int32), pt, pw, eo, to, El)
+
+
+def ep_combine(back: torch.Tensor, slot_map: torch.Tensor, topk_w: torch.Tensor, lo: int, n_own: int,
+               out: torch.Tensor) -> torch.Tensor:
+    """out[i] = sum_j topk_w[lo + i, j] * back_rows[slot_map[i k + j]] for the owned tokens (bf16)."""
+    rows = back.reshape(-1, back.shape[-1])
+    if n_own <= 0:
+        return out
+    if _gpu(back):
+        ext().ep_combine(rows, slot_map, topk_w.float().contiguous(), int(lo), int(n_own), out)
+    else:
+        ref.ep_combine(rows, slot_map, topk_w, lo, n_own, out)
+    return out

@@ -23,6 +23,12 @@
 // i.e. after every peer's launch of call e-2 had completed (stream order). Epochs advance together on all blocks
 // (every block takes part in every call, with or without rows), so e is the same for the whole call.
 // Loads of peer data use sc0 sc1 (system-coherent) so no stale line of an older call is returned.
+//
+// The same buffers, epochs and exchange carry the expert-parallel all-to-all and all-gather of the MoE layers
+// (a2a_pull_kernel): every rank stages its whole send image (per-destination parts of `bpd` bytes, or ONE part for
+// every destination in all-gather mode) into its data half, publishes, and then pulls from each peer the part
+// addressed to it. Block b stages image chunks [c0, c1) and pulls only chunks of that same range from the peers —
+// exactly what the peers' block b staged before releasing flag (p, b) — so the per-block flags order every read.
 #include "common.h"
 
 namespace kafka {
@@ -259,6 +265,66 @@ extern "C" hipError_t kafka_launch_car_allreduce_add_rmsnorm(char* const* bases,
   else return hipErrorInvalidValue;
 #undef KAFKA_CARN_R
 #undef KAFKA_CARN
+  return hipGetLastError();
+}
+
+
+// Pull-mode all-to-all (bcast = 0: part q of the image, at q * bpd, goes to rank q; recv part p = peer p's part for
+// this rank) or all-gather (bcast = 1: the image is one part of bpd bytes; recv part p = peer p's image).
+// nbytes = image bytes (ep * bpd, or bpd); bpd % 16 == 0.
+template <int NR>
+__global__ __launch_bounds__(256) void a2a_pull_kernel(ARPtrs ptrs, int rank, const ar_i32x4* __restrict__ send,
+                                                       int64_t n16, ar_i32x4* __restrict__ recv, int64_t bpd16,
+                                                       int bcast, int64_t max_bytes) {
+  __shared__ int s_e;
+  const int e = ar_epoch(ptrs, rank, &s_e);
+  const int b = blockIdx.x, nb = gridDim.x;
+  const int64_t per = (n16 + nb - 1) / nb;
+  const int64_t c0 = min(n16, (int64_t)b * per), c1 = min(n16, c0 + per);
+  const int64_t half = (int64_t)(e & 1) * max_bytes;
+  ar_i32x4* mine = reinterpret_cast<ar_i32x4*>(ptrs.base[rank] + AR_HEADER + half);
+  for (int64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) mine[c] = send[c];
+  ar_exchange<NR>(ptrs, rank, e);
+  // the part addressed to this rank, clipped to this block's staged range
+  const int64_t lo = bcast ? 0 : rank * bpd16, hi = lo + bpd16;
+  const int64_t a = max(lo, c0), z = min(hi, c1);
+  constexpr int U = 4;  // loads in flight per thread and peer
+  for (int64_t c = a + threadIdx.x; c < z; c += (int64_t)blockDim.x * U) {
+    ar_i32x4 v[NR][U];
+#pragma unroll
+    for (int p = 0; p < NR; ++p)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t cc = min(c + (int64_t)u * blockDim.x, z - 1);  // clamp, don't branch (stores are guarded)
+        v[p][u] = load_sys16_nowait(reinterpret_cast<const bf16*>(ptrs.base[p] + AR_HEADER + half) + cc * 8);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < NR; ++p)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t cc = c + (int64_t)u * blockDim.x;
+        if (cc < z) recv[p * bpd16 + (cc - lo)] = v[p][u];
+      }
+  }
+}
+
+extern "C" hipError_t kafka_launch_car_a2a(char* const* bases, int nranks, int rank, const void* send, int64_t nbytes,
+                                          void* recv, int64_t bpd, int bcast, int64_t max_bytes, int nblocks,
+                                          hipStream_t st) {
+  if (nranks < 2 || nranks > AR_MAX_RANKS || nblocks < 1 || nblocks > AR_MAX_BLOCKS || nbytes > max_bytes ||
+      nbytes % 16 != 0 || bpd % 16 != 0 || (bcast ? nbytes != bpd : nbytes != bpd * nranks))
+    return hipErrorInvalidValue;
+  ARPtrs p{};
+  for (int i = 0; i < nranks; ++i) p.base[i] = bases[i];
+  const auto* s = reinterpret_cast<const ar_i32x4*>(send);
+  auto* r = reinterpret_cast<ar_i32x4*>(recv);
+  switch (nranks) {
+    case 2: a2a_pull_kernel<2><<<nblocks, 256, 0, st>>>(p, rank, s, nbytes / 16, r, bpd / 16, bcast, max_bytes); break;
+    case 4: a2a_pull_kernel<4><<<nblocks, 256, 0, st>>>(p, rank, s, nbytes / 16, r, bpd / 16, bcast, max_bytes); break;
+    case 8: a2a_pull_kernel<8><<<nblocks, 256, 0, st>>>(p, rank, s, nbytes / 16, r, bpd / 16, bcast, max_bytes); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -67,6 +67,14 @@ hipError_t kafka_car_free(void* p);
 hipError_t kafka_launch_car_allreduce(char* const* bases, int nranks, int rank, const bf16* x, const float* xp, int S,
                                       int64_t ps, bf16* y, int64_t n8, int64_t max_bytes, int nblocks,
                                       hipStream_t st);
+hipError_t kafka_launch_car_a2a(char* const* bases, int nranks, int rank, const void* send, int64_t nbytes, void* recv,
+                                int64_t bpd, int bcast, int64_t max_bytes, int nblocks, hipStream_t st);
+hipError_t kafka_launch_ep_dispatch(const bf16* x, int64_t ldx, const int* topk_e, int lo, int n_pairs, int k, int El,
+                                    int ep, int C, int MR, int d, bf16* img, int* slot_map, hipStream_t st);
+hipError_t kafka_launch_ep_recv_route(const bf16* img, int ep, int C, int MR, int d, int El, int BM, int* perm_tok,
+                                      float* perm_w, int* expert_off, int* tile_off, hipStream_t st);
+hipError_t kafka_launch_ep_combine(const bf16* back, const int* slot_map, const float* topk_w, int lo, int n_own,
+                                   int k, int d, bf16* out, int64_t ldo, hipStream_t st);
 hipError_t kafka_launch_car_allreduce_add_rmsnorm(char* const* bases, int nranks, int rank, const bf16* x,
                                                   const float* xp, int S, int64_t ps, int T, int d, bf16* resid,
                                                   int64_t rs, const bf16* w, float eps, bf16* out, int64_t os,
@@ -641,6 +649,68 @@ static void car_all_reduce_add_rmsnorm(at::Tensor x, at::Tensor residual, at::Te
       bptr(out), out.stride(0), max_bytes, (int)nblocks, cur_stream()));
 }
 
+// Expert-parallel all-to-all (bcast = false: part q of `send` [nranks * bpd bytes] goes to rank q) or all-gather
+// (bcast = true: `send` is one part) over the IPC-mapped buffers; recv = nranks parts of bpd bytes.
+static void car_a2a(at::Tensor send, at::Tensor recv, int64_t bpd, bool bcast, std::vector<int64_t> bases,
+                    int64_t rank, int64_t max_bytes, int64_t nblocks) {
+  CHECK_CUDA(send); CHECK_CUDA(recv);
+  TORCH_CHECK(send.is_contiguous() && recv.is_contiguous(), "car_a2a: contiguous buffers");
+  const int64_t nbytes = send.numel() * send.element_size();
+  const int64_t nr = (int64_t)bases.size();
+  TORCH_CHECK(recv.numel() * recv.element_size() == nr * bpd, "car_a2a: recv must hold nranks parts");
+  TORCH_CHECK(nbytes == (bcast ? bpd : nr * bpd) && bpd % 16 == 0 && nbytes <= max_bytes,
+              "car_a2a: image size / part size / buffer capacity");
+  auto b = car_bases(bases);
+  CHECK_HIP(kafka_launch_car_a2a(b.data(), (int)nr, (int)rank, send.data_ptr(), nbytes, recv.data_ptr(), bpd,
+                                 bcast ? 1 : 0, max_bytes, (int)nblocks, cur_stream()));
+}
+
+// EP send image [ep, C + MR, d] bf16 of the owned (token, expert) pairs [lo * k, (lo + n_own) * k) + slot map
+static void ep_dispatch(at::Tensor x, at::Tensor topk_e, int64_t lo, int64_t n_own, int64_t El, int64_t C,
+                        at::Tensor img, at::Tensor slot_map) {
+  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_LASTDIM(x); CHECK_DT(topk_e, at::kInt); CHECK_DT(img, at::kBFloat16);
+  CHECK_DT(slot_map, at::kInt);
+  TORCH_CHECK(topk_e.dim() == 2 && topk_e.is_contiguous() && img.dim() == 3 && img.is_contiguous(),
+              "ep_dispatch: topk_e [T, k], img [ep, C + MR, d]");
+  const int k = topk_e.size(1), ep = img.size(0), d = img.size(2);
+  TORCH_CHECK(x.size(1) == d && x.stride(0) % 8 == 0 && lo >= 0 && lo + n_own <= topk_e.size(0) &&
+                  lo + n_own <= x.size(0) && slot_map.numel() >= n_own * k,
+              "ep_dispatch: shapes");
+  const int MR = img.size(1) - (int)C;  // metadata rows after the C row slots of each destination block
+  TORCH_CHECK(C >= 1 && MR >= 1 && 16 + 4 * C <= (int64_t)MR * d * 2 && El >= 1 && (int64_t)ep * El >= 1,
+              "ep_dispatch: metadata rows");
+  CHECK_HIP(kafka_launch_ep_dispatch(bptr(x), x.stride(0), topk_e.data_ptr<int>(), (int)lo, (int)(n_own * k), k,
+                                     (int)El, ep, (int)C, MR, d, bptr(img), slot_map.data_ptr<int>(), cur_stream()));
+}
+
+static void ep_recv_route(at::Tensor img, int64_t C, int64_t El, int64_t bm, at::Tensor perm_tok, at::Tensor perm_w,
+                          at::Tensor expert_off, at::Tensor tile_off) {
+  CHECK_CUDA(img); CHECK_DT(img, at::kBFloat16); CHECK_DT(perm_tok, at::kInt); CHECK_DT(perm_w, at::kFloat);
+  CHECK_DT(expert_off, at::kInt); CHECK_DT(tile_off, at::kInt);
+  TORCH_CHECK(img.dim() == 3 && img.is_contiguous(), "ep_recv_route: img [ep, C + MR, d]");
+  const int ep = img.size(0), d = img.size(2), MR = img.size(1) - (int)C;
+  TORCH_CHECK(MR >= 1 && perm_tok.numel() == ep * C && perm_w.numel() == ep * C && expert_off.numel() == El + 1 &&
+                  tile_off.numel() == El + 1 && El <= 16,
+              "ep_recv_route: sizes");
+  CHECK_HIP(kafka_launch_ep_recv_route(bptr(img), ep, (int)C, MR, d, (int)El, (int)bm, perm_tok.data_ptr<int>(),
+                                       perm_w.data_ptr<float>(), expert_off.data_ptr<int>(), tile_off.data_ptr<int>(),
+                                       cur_stream()));
+}
+
+// out[i] = sum_j topk_w[lo + i, j] * back[slot_map[i k + j]]   (back: [rows, d] bf16)
+static void ep_combine(at::Tensor back, at::Tensor slot_map, at::Tensor topk_w, int64_t lo, int64_t n_own,
+                       at::Tensor out) {
+  CHECK_CUDA(back); CHECK_DT(back, at::kBFloat16); CHECK_DT(slot_map, at::kInt); CHECK_DT(topk_w, at::kFloat);
+  CHECK_DT(out, at::kBFloat16); CHECK_LASTDIM(out);
+  TORCH_CHECK(back.is_contiguous() && topk_w.dim() == 2 && topk_w.is_contiguous(), "ep_combine: layouts");
+  const int k = topk_w.size(1), d = back.size(-1);
+  TORCH_CHECK(out.size(1) == d && out.size(0) >= n_own && out.stride(0) % 8 == 0 && slot_map.numel() >= n_own * k &&
+                  lo + n_own <= topk_w.size(0),
+              "ep_combine: shapes");
+  CHECK_HIP(kafka_launch_ep_combine(bptr(back), slot_map.data_ptr<int>(), topk_w.data_ptr<float>(), (int)lo,
+                                    (int)n_own, k, d, bptr(out), out.stride(0), cur_stream()));
+}
+
 PYBIND11_MODULE(_kafka_ops, m) {
   m.doc() = "kafka_llm_service_amd CDNA4 (gfx950) HIP kernels";
   m.def("rmsnorm", &rmsnorm);
@@ -670,5 +740,9 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("car_error_async", &car_error_async);
   m.def("car_all_reduce", &car_all_reduce);
   m.def("car_all_reduce_add_rmsnorm", &car_all_reduce_add_rmsnorm);
+  m.def("car_a2a", &car_a2a);
+  m.def("ep_dispatch", &ep_dispatch);
+  m.def("ep_recv_route", &ep_recv_route);
+  m.def("ep_combine", &ep_combine);
   m.def("grouped_gemm", &grouped_gemm);
 }

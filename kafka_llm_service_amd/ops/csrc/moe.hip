@@ -20,6 +20,21 @@
 //     * output:  bf16 Y[r, :] through an LDS transpose (16-B coalesced row stores), or
 //     * combine: out_f32[perm_tok[r], :] += perm_w[r] * Y[r, :] with float atomics — a token receives exactly k
 //                contributions onto a zeroed buffer, and for k = 2 IEEE addition makes the order irrelevant.
+//
+// Expert-parallel all-to-all (models/moe.py MoEBlock._a2a; transport: parallel/custom_allreduce.py all_to_all over
+// the IPC-mapped buffers, or all_to_all_single): everything that used to be bincount / one_hot / argsort / index_add
+// on the host-visible path is a kernel here, so a dispatch + combine never synchronises with the host and captures
+// into a hipGraph. The send image of a rank is [ep][C + MR][d] bf16: block q holds, for destination rank q, C row
+// slots (the activations of the owned (token, expert) pairs routed to q's experts, packed in pair order) and MR
+// metadata rows, read as int32: [count, 0, 0, 0, local expert of slot 0, ..., of slot C-1] (C = capacity).
+//   ep_dispatch_kernel   grid (pairs + ep): block i < pairs places pair i (its slot = the number of earlier pairs
+//                        with the same destination, a block-wide count — pairs <= a few thousand), copies the row
+//                        and records slot_map[i] = q (C + MR) + slot; block pairs + q writes q's count and marks its
+//                        unused slots -1.
+//   ep_recv_route_kernel one workgroup: the received image's valid slots sorted stably by local expert -> the
+//                        MoERouting arrays of the grouped GEMMs (perm_tok = slot row, perm_w = 1; invalid slots past
+//                        expert_off[El]).
+//   ep_combine_kernel    grid (owned tokens): out[t] = sum_j w[t, j] * back[slot_map[t k + j]] (fp32, bf16 store).
 #include "common.h"
 
 namespace kafka {
@@ -269,6 +284,157 @@ extern "C" hipError_t kafka_launch_grouped_gemm(const bf16* X, int64_t ldx, cons
       grouped_gemm_kernel<false, false><<<grid, 256, 0, st>>>(X, ldx, W, N, Kd, perm_tok, perm_w, expert_off,
                                                               tile_off, e_lo, e_n, Y, ldy, out, ldo);
   }
+  return hipGetLastError();
+}
+
+
+// ------------------------------------------------------------------------------------------------------------------
+// Expert-parallel dispatch / receive routing / combine (see the header).
+__device__ __forceinline__ int block_sum_i(int v, int* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  int t = 0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+  return t;
+}
+
+__global__ __launch_bounds__(256) void ep_dispatch_kernel(const bf16* __restrict__ x, int64_t ldx,
+                                                          const int* __restrict__ topk_e, int lo, int n_pairs, int k,
+                                                          int El, int ep, int C, int MR, int d,
+                                                          bf16* __restrict__ img, int* __restrict__ slot_map) {
+  __shared__ int red[4];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int64_t blk = (int64_t)(C + MR) * d;  // elements per destination block
+  const int* te = topk_e + (int64_t)lo * k;
+  if (b < n_pairs) {
+    const int e = te[b], q = e / El;
+    int c = 0;
+    for (int i = tid; i < b; i += 256) c += te[i] / El == q;
+    const int pos = block_sum_i(c, red);  // block-uniform
+    if (pos >= C) return;                   // cannot happen for C = Tl * min(k, El) (host-checked); never overflow
+    int* meta = reinterpret_cast<int*>(img + q * blk + (int64_t)C * d);
+    if (tid == 0) {
+      slot_map[b] = q * (C + MR) + pos;
+      meta[4 + pos] = e - q * El;
+    }
+    const bf16* src = x + (int64_t)(lo + b / k) * ldx;
+    bf16* dst = img + q * blk + (int64_t)pos * d;
+    for (int c8 = tid; c8 < (d >> 3); c8 += 256) store_bf16x8(dst + c8 * 8, load_bf16x8(src + c8 * 8));
+  } else {
+    const int q = b - n_pairs;
+    int c = 0;
+    for (int i = tid; i < n_pairs; i += 256) c += te[i] / El == q;
+    const int n = block_sum_i(c, red);
+    int* meta = reinterpret_cast<int*>(img + q * blk + (int64_t)C * d);
+    if (tid < 4) meta[tid] = tid == 0 ? n : 0;
+    for (int s = n + tid; s < C; s += 256) meta[4 + s] = -1;
+  }
+}
+
+__global__ __launch_bounds__(256) void ep_recv_route_kernel(const bf16* __restrict__ img, int ep, int C, int MR,
+                                                            int d, int El, int BM, int* __restrict__ perm_tok,
+                                                            float* __restrict__ perm_w, int* __restrict__ expert_off,
+                                                            int* __restrict__ tile_off) {
+  __shared__ int wsum[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int S = ep * C;                       // candidate slots, flattened (source p, slot s) -> p * C + s
+  const int per = (S + 255) / 256;
+  const int s0 = min(S, tid * per), s1 = min(S, s0 + per);
+  const int64_t blk = (int64_t)(C + MR) * d;
+  auto expert_of = [&](int f) {               // local expert of flattened slot f, -1 if unused
+    const int p = f / C, s = f % C;
+    const int* meta = reinterpret_cast<const int*>(img + p * blk + (int64_t)C * d);
+    return s < meta[0] ? meta[4 + s] : -1;
+  };
+  int base = 0, tbase = 0;
+  for (int e = 0; e < El; ++e) {
+    int c = 0;
+    for (int f = s0; f < s1; ++f) c += expert_of(f) == e;
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    __syncthreads();
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int wpre = 0, total = 0;
+    for (int i = 0; i < 4; ++i) {
+      wpre += i < w ? wsum[i] : 0;
+      total += wsum[i];
+    }
+    int pos = base + wpre + incl - c;
+    for (int f = s0; f < s1; ++f)
+      if (expert_of(f) == e) {
+        perm_tok[pos] = (f / C) * (C + MR) + f % C;  // row of the slot in the received image
+        perm_w[pos] = 1.f;
+        ++pos;
+      }
+    base += total;
+    tbase += (total + BM - 1) / BM;
+    if (tid == 0) {
+      expert_off[e + 1] = base;
+      tile_off[e + 1] = tbase;
+    }
+  }
+  if (tid == 0) {
+    expert_off[0] = 0;
+    tile_off[0] = 0;
+  }
+  // entries past the last segment: a valid row, weight 0 (no kernel reads them; keeps every index in range)
+  for (int i = base + tid; i < S; i += 256) {
+    perm_tok[i] = 0;
+    perm_w[i] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void ep_combine_kernel(const bf16* __restrict__ back, const int* __restrict__ slot_map,
+                                                         const float* __restrict__ topk_w, int lo, int k, int d,
+                                                         bf16* __restrict__ out, int64_t ldo) {
+  const int i = blockIdx.x;
+  const float* w = topk_w + (int64_t)(lo + i) * k;
+  const int* sm = slot_map + (int64_t)i * k;
+  for (int c8 = threadIdx.x; c8 < (d >> 3); c8 += 256) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < k; ++j) {  // the token's k expert outputs, in routing order (deterministic)
+      const bf16x8 v = load_bf16x8(back + (int64_t)sm[j] * d + c8 * 8);
+      const float wj = w[j];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] += wj * (float)v[t];
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) o[t] = (bf16)acc[t];
+    store_bf16x8(out + (int64_t)i * ldo + c8 * 8, o);
+  }
+}
+
+extern "C" hipError_t kafka_launch_ep_dispatch(const bf16* x, int64_t ldx, const int* topk_e, int lo, int n_pairs,
+                                              int k, int El, int ep, int C, int MR, int d, bf16* img, int* slot_map,
+                                              hipStream_t st) {
+  if (ep < 1 || El < 1 || d % 8 != 0 || (int64_t)(16 + 4 * (int64_t)C) > (int64_t)MR * d * 2) return hipErrorInvalidValue;
+  ep_dispatch_kernel<<<n_pairs + ep, 256, 0, st>>>(x, ldx, topk_e, lo, n_pairs, k, El, ep, C, MR, d, img, slot_map);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t kafka_launch_ep_recv_route(const bf16* img, int ep, int C, int MR, int d, int El, int BM,
+                                                int* perm_tok, float* perm_w, int* expert_off, int* tile_off,
+                                                hipStream_t st) {
+  if (ep < 1 || El < 1 || El > MOE_MAXE) return hipErrorInvalidValue;
+  ep_recv_route_kernel<<<1, 256, 0, st>>>(img, ep, C, MR, d, El, BM, perm_tok, perm_w, expert_off, tile_off);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t kafka_launch_ep_combine(const bf16* back, const int* slot_map, const float* topk_w, int lo,
+                                             int n_own, int k, int d, bf16* out, int64_t ldo, hipStream_t st) {
+  if (n_own < 1) return hipSuccess;
+  if (d % 8 != 0) return hipErrorInvalidValue;
+  ep_combine_kernel<<<n_own, 256, 0, st>>>(back, slot_map, topk_w, lo, k, d, out, ldo);
   return hipGetLastError();
 }
 

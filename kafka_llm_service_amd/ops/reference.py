@@ -388,3 +388,60 @@ def grouped_gemm(x, w, perm_tok, perm_w, expert_off, e_lo, gather, y, out):
             out.index_add_(0, perm_tok[a:b].long(), yy * perm_w[a:b, None])
         else:
             y[a:b] = yy.to(y.dtype)
+
+
+# ---- expert-parallel all-to-all (csrc/moe.hip ep_*): CPU references of the same image layout -------------------
+def _ep_meta(img: torch.Tensor, q: int, C: int) -> torch.Tensor:
+    """int32 view of destination block q's metadata rows: [count, 0, 0, 0, expert of slot 0 .. C-1, ...]."""
+    return img[q, C:].reshape(-1).view(torch.int32)
+
+
+def ep_dispatch(x, topk_e, lo, n_own, El, C, img, slot_map):
+    ep = img.shape[0]
+    k = topk_e.shape[1]
+    te = topk_e[lo:lo + n_own].reshape(-1).long()
+    counts = [0] * ep
+    for i, e in enumerate(te.tolist()):
+        q = e // El
+        pos = counts[q]
+        counts[q] += 1
+        slot_map[i] = q * img.shape[1] + pos
+        _ep_meta(img, q, C)[4 + pos] = e - q * El
+        img[q, pos] = x[lo + i // k]
+    for q in range(ep):
+        m = _ep_meta(img, q, C)
+        m[0:4] = torch.tensor([counts[q], 0, 0, 0], dtype=torch.int32)
+        m[4 + counts[q]:4 + C] = -1
+
+
+def ep_recv_route(img, C, El, bm):
+    ep, rows = img.shape[0], img.shape[1]
+    ents = []  # (expert, row) of every valid slot, in (source, slot) order
+    for p in range(ep):
+        m = _ep_meta(img, p, C)
+        n = int(m[0])
+        for s in range(n):
+            ents.append((int(m[4 + s]), p * rows + s))
+    S = ep * C
+    perm_tok = torch.zeros(S, dtype=torch.int32)
+    perm_w = torch.zeros(S, dtype=torch.float32)
+    eo = torch.zeros(El + 1, dtype=torch.int32)
+    to = torch.zeros(El + 1, dtype=torch.int32)
+    pos = 0
+    for e in range(El):
+        seg = [r for ex, r in ents if ex == e]
+        perm_tok[pos:pos + len(seg)] = torch.tensor(seg, dtype=torch.int32)
+        perm_w[pos:pos + len(seg)] = 1.0
+        pos += len(seg)
+        eo[e + 1] = pos
+        to[e + 1] = to[e] + (len(seg) + bm - 1) // bm
+    return perm_tok, perm_w, eo, to
+
+
+def ep_combine(back, slot_map, topk_w, lo, n_own, out):
+    k = topk_w.shape[1]
+    for i in range(n_own):
+        acc = torch.zeros(back.shape[-1], dtype=torch.float32)
+        for j in range(k):
+            acc += float(topk_w[lo + i, j]) * back[int(slot_map[i * k + j])].float()
+        out[i] = acc.to(out.dtype)

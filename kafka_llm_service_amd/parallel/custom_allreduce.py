@@ -107,6 +107,25 @@ class CustomAllReduce:
                                              self.nblocks)
         return out
 
+    def fits_bytes(self, nbytes: int) -> bool:
+        return nbytes % 16 == 0 and nbytes <= self.max_bytes
+
+    def all_to_all(self, send: torch.Tensor, recv: torch.Tensor) -> torch.Tensor:
+        """recv[p] = peer p's send[self.rank] for send/recv [world, ...] (contiguous, equal parts): the expert
+        dispatch / return of the MoE layers over the same IPC buffers and epochs (csrc/allreduce.hip a2a_pull_kernel;
+        no host sync, graph-capturable)."""
+        bpd = send.numel() * send.element_size() // self.world
+        if not self._skip():
+            ext().car_a2a(send, recv, int(bpd), False, self.bases, self.rank, self.max_bytes, self.nblocks)
+        return recv
+
+    def all_gather(self, send: torch.Tensor, recv: torch.Tensor) -> torch.Tensor:
+        """recv[p] = peer p's send (recv = world parts of send's size)."""
+        if not self._skip():
+            ext().car_a2a(send, recv, int(send.numel() * send.element_size()), True, self.bases, self.rank,
+                          self.max_bytes, self.nblocks)
+        return recv
+
     def check(self) -> None:
         """Raise if any wait timed out (a peer never arrived). Synchronises; for tests and health checks."""
         if ext().car_error(self.own):

@@ -169,6 +169,24 @@ def _tp_main(rank, world, port, q, graphs, model):
 
     eng, st = tp_worker.build_tp_engine(dict(CFG, model=model.replace("+a2a", ""), device=f"cuda:{dev}",
                                              use_graphs=graphs), tp=world)
+    a2a_calls = [0]
+    if model.endswith("+a2a"):
+        # the whole MoE block — router, device routing, EP dispatch, IPC all-to-all, expert GEMMs, return, combine,
+        # all-gather — must never synchronise with the host: torch raises on any sync
+        from kafka_llm_service_amd.models.moe import MoEBlock
+
+        orig_call = MoEBlock.__call__
+
+        def checked(self, x, lw):
+            if torch.cuda.is_current_stream_capturing():
+                return orig_call(self, x, lw)
+            torch.cuda.set_sync_debug_mode("error")
+            try:
+                return orig_call(self, x, lw)
+            finally:
+                torch.cuda.set_sync_debug_mode("default")
+                a2a_calls[0] += 1
+        MoEBlock.__call__ = checked
     try:
         assert os.environ.get("KAFKA_CUSTOM_AR", "1") == "0" or comm.get_custom(st.tp_group) is not None, \
             "custom all-reduce not registered"
@@ -178,10 +196,10 @@ def _tp_main(rank, world, port, q, graphs, model):
             tp_worker.release_followers()
             g = eng.runner.graphs
             q.put(("leader", outs, [s.numpy() for s in seen], g.stats if g is not None else None,
-                   eng.stats["planned_ahead"]))
+                   eng.stats["planned_ahead"], a2a_calls[0]))
         else:
             n = tp_worker.follower_loop(eng)
-            q.put(("follower", n))
+            q.put(("follower", n, a2a_calls[0]))
         if comm.get_custom(st.tp_group) is not None:
             comm.get_custom(st.tp_group).check()
     finally:
@@ -190,8 +208,8 @@ def _tp_main(rank, world, port, q, graphs, model):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("model,graphs", [("small-llama", False), ("small-llama", True), ("tiny-mixtral", False),
-                                          ("tiny-mixtral+a2a", False)],
-                         ids=["eager", "graphs", "mixtral-ep", "mixtral-ep-a2a"])
+                                          ("tiny-mixtral+a2a", False), ("tiny-mixtral+a2a", True)],
+                         ids=["eager", "graphs", "mixtral-ep", "mixtral-ep-a2a", "mixtral-ep-a2a-graphs"])
 def test_tp2_engine_on_one_gpu_matches_tp1(cuda, model, graphs):
     """TP=2 (Mixtral: experts sharded over the 2 ranks, EP) on one GPU == the TP=1 model: same first-step logits up
     to reduction order, every greedy token the dense oracle's argmax."""
@@ -211,10 +229,12 @@ def test_tp2_engine_on_one_gpu_matches_tp1(cuda, model, graphs):
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    outs, seen, gstats, ahead = res["leader"]
+    outs, seen, gstats, ahead, a2a_lead = res["leader"]
     assert res["follower"][0] >= 6 and ahead > 0
     if graphs:
         assert gstats["replays"] >= 1
+    if model.endswith("+a2a"):  # eager MoE calls ran under set_sync_debug_mode("error") on both ranks
+        assert a2a_lead > 0 and res["follower"][1] > 0
     ref = LLMEngine(EngineConfig(**dict(CFG, model=model.replace("+a2a", ""), device="cuda:0")))
     sp = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
     want_outs, want = _capture_logits(ref, _prompts(ref.model_cfg.vocab_size), sp)

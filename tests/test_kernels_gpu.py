@@ -600,3 +600,47 @@ def test_wstream_qkv_rope(cuda, M, Hq, Hkv, K):
         _close(q, q3, atol=0.016, rtol=0.008, msg="q vs unfused")
         _close(k, k3, atol=0.016, rtol=0.008, msg="k vs unfused")
         _close(v, v3, atol=0.016, rtol=0.008, msg="v vs unfused")
+
+
+@pytest.mark.parametrize("T,ep,E,k", [(37, 2, 8, 2), (64, 4, 8, 2), (5, 8, 8, 2)])
+def test_ep_dispatch_route_combine_match_reference(cuda, T, ep, E, k):
+    """csrc/moe.hip ep_dispatch / ep_recv_route / ep_combine == the fp32/host references of the same image layout
+    (rows, metadata, slot maps, expert-sorted routing bit-exact; combine to bf16 rounding), with the all-to-all
+    simulated by re-stacking the ranks' images."""
+    from kafka_llm_service_amd import ops
+
+    torch.manual_seed(T + ep)
+    d = 256
+    El = E // ep
+    x = torch.randn(T, d, device="cuda", dtype=torch.bfloat16)
+    r = ops.moe_route(torch.randn(T, E, device="cuda", dtype=torch.bfloat16), k)
+    Tl, C, MR = ops.ep_layout(T, ep, k, El, d)
+    imgs, slots = [], []
+    for q in range(ep):
+        lo, hi = min(T, q * Tl), min(T, (q + 1) * Tl)
+        img, slot = ops.ep_dispatch(x, r.topk_e, lo, hi - lo, El, ep, C, MR)
+        rimg, rslot = ops.ep_dispatch(x.cpu(), r.topk_e.cpu(), lo, hi - lo, El, ep, C, MR)
+        for p in range(ep):
+            meta, rmeta = img[p, C:].reshape(-1).view(torch.int32).cpu(), rimg[p, C:].reshape(-1).view(torch.int32)
+            n = int(rmeta[0])
+            assert int(meta[0]) == n and torch.equal(meta[4:4 + C], rmeta[4:4 + C])
+            assert torch.equal(img[p, :n].cpu(), rimg[p, :n])
+        assert torch.equal(slot[:(hi - lo) * k].cpu(), rslot[:(hi - lo) * k])
+        imgs.append(img)
+        slots.append(slot)
+    for p in range(ep):  # rank p's received image: block s = rank s's part for p
+        recv = torch.stack([imgs[s][p] for s in range(ep)])
+        rr = ops.ep_recv_route(recv, C, El)
+        ref = ops.ep_recv_route(recv.cpu(), C, El)
+        n = int(ref.expert_off[-1])
+        assert torch.equal(rr.expert_off.cpu(), ref.expert_off) and torch.equal(rr.tile_off.cpu(), ref.tile_off)
+        assert torch.equal(rr.perm_tok[:n].cpu(), ref.perm_tok[:n])
+        assert torch.all(rr.perm_w[:n].cpu() == 1) and torch.all(rr.perm_tok[n:].cpu() == 0)
+    for q in range(ep):  # combine over a synthetic returned image
+        lo, hi = min(T, q * Tl), min(T, (q + 1) * Tl)
+        back = torch.randn(ep, C + MR, d, device="cuda", dtype=torch.bfloat16)
+        out = torch.zeros(Tl, d, device="cuda", dtype=torch.bfloat16)
+        ops.ep_combine(back, slots[q], r.topk_w, lo, hi - lo, out)
+        ref_out = torch.zeros(Tl, d, dtype=torch.bfloat16)
+        ops.ep_combine(back.cpu(), slots[q].cpu(), r.topk_w.cpu(), lo, hi - lo, ref_out)
+        torch.testing.assert_close(out.cpu().float(), ref_out.float(), atol=2e-2, rtol=2e-2)

@@ -179,3 +179,44 @@ def test_plan_wire_format_roundtrip():
     for f in ("temp", "topp", "topk", "seeds"):
         assert (getattr(sp2, f) == getattr(sp, f)).all()
     assert sp2.greedy is False and sp2.leader_tokens is False
+
+
+def test_ep_ops_roundtrip_equals_direct_moe_on_cpu():
+    """dispatch -> (simulated) all-to-all -> device routing -> per-expert function -> return -> weighted combine
+    == sum_j w_j f_{e_j}(x) computed directly, for every rank's owned tokens (CPU references of csrc/moe.hip ep_*)."""
+    import torch
+
+    from kafka_llm_service_amd import ops
+
+    torch.manual_seed(0)
+    T, d, E, k, ep = 23, 64, 8, 2, 4
+    El = E // ep
+    x = torch.randn(T, d).to(torch.bfloat16)
+    r = ops.moe_route(torch.randn(T, E).to(torch.bfloat16), k)
+    Tl, C, MR = ops.ep_layout(T, ep, k, El, d)
+    scale = torch.arange(1, E + 1, dtype=torch.float32)  # expert e multiplies its row by e + 1
+    imgs, slots = [], []
+    for q in range(ep):
+        lo, hi = min(T, q * Tl), min(T, (q + 1) * Tl)
+        img, slot = ops.ep_dispatch(x, r.topk_e, lo, hi - lo, El, ep, C, MR)
+        imgs.append(img)
+        slots.append(slot)
+    backs = []
+    for p in range(ep):
+        recv = torch.stack([imgs[s][p] for s in range(ep)])
+        rr = ops.ep_recv_route(recv, C, El)
+        y = torch.zeros(ep * (C + MR), d)
+        rows = recv.view(-1, d)
+        for e in range(El):
+            a, b = int(rr.expert_off[e]), int(rr.expert_off[e + 1])
+            idx = rr.perm_tok[a:b].long()
+            y[idx] = rows[idx].float() * scale[p * El + e]
+        backs.append(y.to(torch.bfloat16).view(ep, C + MR, d))
+    for q in range(ep):
+        lo, hi = min(T, q * Tl), min(T, (q + 1) * Tl)
+        back = torch.stack([backs[p][q] for p in range(ep)])  # the return all-to-all
+        out = torch.zeros(Tl, d, dtype=torch.bfloat16)
+        ops.ep_combine(back, slots[q], r.topk_w, lo, hi - lo, out)
+        want = sum(r.topk_w[lo:hi, j:j + 1] * x[lo:hi].float() * scale[r.topk_e[lo:hi, j].long()][:, None]
+                   for j in range(k))
+        torch.testing.assert_close(out[:hi - lo].float(), want, atol=0.1, rtol=2e-2)
