@@ -338,6 +338,9 @@ class ModelRunner:
         self.pad_rows = (self.device.type == "cuda" and model.tp == 1 and not getattr(model, "tiled_only", False)
                          and os.environ.get("KAFKA_PAD_ROWS", "1") == "1")
         self.tile = ops.tile_rows(self.variant) // self.G  # tokens per attention work item
+        # the v3 cascade hands its prefix partials to the decode kernel as bf16 (normalised O, fp32 lse): ~33 MB
+        # less HBM traffic per Llama-3-8B layer at 64 threads on an 18k prefix (KAFKA_CASCADE_BF16=0: fp32)
+        self.cascade_bf16 = self.variant == 3 and os.environ.get("KAFKA_CASCADE_BF16", "1") != "0"
         self.cascade_min_prefix = cascade_min_prefix
         self.target_wgs = int(os.environ.get("KAFKA_CASCADE_WGS", target_wgs))
         self.prefill_kv_chunk = int(os.environ.get("KAFKA_PREFILL_KV_CHUNK", prefill_kv_chunk))
@@ -517,6 +520,8 @@ class ModelRunner:
             meta.s_total = h.s_total
             meta.part = torch.empty(B, Hq, h.s_total, D, dtype=torch.float32, device=self.device)
             meta.lse = torch.empty(B, Hq, h.s_total, dtype=torch.float32, device=self.device)
+            if h.n_prefix_items and self.cascade_bf16:
+                meta.pre_part = torch.empty(B, Hq, h.s_total, D, dtype=torch.bfloat16, device=self.device)
             meta.extra["cascade_prefix"] = h.cascade_prefix
         if h.n_items:
             meta.prefill_items = d32[o:o + h.n_items * 8].view(-1, 8)

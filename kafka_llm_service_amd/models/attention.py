@@ -36,6 +36,7 @@ class AttnMeta:
     prefix_items: torch.Tensor | None = None   # int32 [m, 8] cascade prefix work items (rows = decode tokens)
     s_total: int = 1                           # partial slots per decode row
     part: torch.Tensor | None = None           # f32 [B, Hq, s_total, D]
+    pre_part: torch.Tensor | None = None       # bf16, part's shape: the tile-v3 cascade's prefix partials
     lse: torch.Tensor | None = None            # f32 [B, Hq, s_total]
     # prefill
     prefill_items: torch.Tensor | None = None  # int32 [m, 8] (q_start relative to row B)
@@ -96,10 +97,11 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         qd = q[:B]
         if meta.prefix_items is not None:
             ops.attn_prefill(meta.prefix_items, qd, k_cache, v_cache, meta.block_tables, meta.q_limit,
-                             meta.scale, out_part=meta.part, lse_part=meta.lse, variant=meta.variant)
+                             meta.scale, out_part=meta.pre_part if meta.pre_part is not None else meta.part,
+                             lse_part=meta.lse, variant=meta.variant)
         # the decode kernel merges each row's prefix partials and its own pieces and writes the final rows
         ops.attn_decode_items(qd, k_cache, v_cache, meta.block_tables, meta.decode_items, meta.part, meta.lse,
-                              meta.scale, out=out[:B])
+                              meta.scale, out=out[:B], pre_part=meta.pre_part)
     if side is not None:
         torch.cuda.current_stream(q.device).wait_event(ev_done)
     elif has_prefill:

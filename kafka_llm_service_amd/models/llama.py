@@ -63,6 +63,11 @@ class TransformerLM:
         self.device = torch.device(device)
         self.dtype = dtype
         self.tp, self.tp_rank = tp, tp_rank
+        # expert parallelism: over the TP group by default; DP attention (enable_dp_attention) keeps attention
+        # unsharded (tp = 1, every rank its own sequences) and shards the experts over a separate group
+        self.ep, self.ep_rank = tp, tp_rank
+        self.dp_attention = False
+        self.ep_t_cap = 0  # DP attention: max tokens of this step over the group (the all-to-all capacity)
         if cfg.num_heads % tp or cfg.num_kv_heads % tp:
             raise ValueError(f"heads ({cfg.num_heads}/{cfg.num_kv_heads}) not divisible by tp={tp}")
         self.hq = cfg.num_heads // tp
@@ -82,6 +87,16 @@ class TransformerLM:
         self.stream = False  # decode GEMMs on the weight-streaming kernel (enable_stream_weights)
         self.tiled_only = False  # row-major dense weights dropped (enable_stream_weights(tiled_only=True))
         self.stream_max_m = ops.STREAM_MAX_M  # rows up to which a step's projections stream
+
+    def enable_dp_attention(self, ep: int, ep_rank: int) -> None:
+        """Data-parallel attention for a MoE model (call before the weights are created): attention, norms and the
+        vocabulary stay whole on every rank (tp must be 1), each rank runs its own sequences, and the experts are
+        sharded over the ``ep`` ranks of ``parallel.state``'s EP group with the device-side all-to-all dispatch and
+        combine (models/moe.py) — the layout where expert all-to-all beats an all-reduce combine: every rank sends
+        only its own tokens' rows, and attention/KV are split instead of replicated."""
+        if self.tp != 1 or not self.cfg.num_experts or self.cfg.num_experts % ep:
+            raise ValueError("DP attention needs tp = 1 and experts divisible by the EP size")
+        self.ep, self.ep_rank, self.dp_attention = ep, ep_rank, True
 
     # ------------------------------------------------------------------------------------------------------------
     def stream_weight_bytes(self) -> int:

@@ -42,13 +42,14 @@ class MoEBlock:
     def __init__(self, model):
         self.model = model
         # expert all-to-all dispatch/combine instead of the all-reduce combine (opt-in, see _a2a)
-        self.a2a = os.environ.get("KAFKA_MOE_A2A", "0") == "1"
+        self.dp = model.dp_attention  # tokens are this rank's own (not replicated): dispatch all, no all-gather
+        self.a2a = self.dp or os.environ.get("KAFKA_MOE_A2A", "0") == "1"
         cfg = model.cfg
         self.E = cfg.num_experts
         self.k = cfg.num_experts_per_tok
         self.F = cfg.intermediate_size
-        self.ep = model.tp
-        self.r = model.tp_rank
+        self.ep = model.ep
+        self.r = model.ep_rank
         self.e_local = self.E // self.ep
         self.e0 = self.r * self.e_local
 
@@ -107,10 +108,15 @@ class MoEBlock:
 
         T, d = x.shape
         ep, q, k, El = self.ep, self.r, self.k, self.e_local
-        grp = pstate.get().tp_group
-        Tl, C, MR = ops.ep_layout(T, ep, k, El, d)
-        lo, hi = min(T, q * Tl), min(T, (q + 1) * Tl)
-        n_own = hi - lo
+        st = pstate.get()
+        grp = st.ep_group if self.dp else st.tp_group
+        if self.dp:  # DP attention: all T tokens are this rank's; capacity from the group's largest step
+            Tl, C, MR = ops.ep_layout(max(T, self.model.ep_t_cap) * ep, ep, k, El, d)
+            lo, n_own = 0, T
+        else:
+            Tl, C, MR = ops.ep_layout(T, ep, k, El, d)
+            lo, hi = min(T, q * Tl), min(T, (q + 1) * Tl)
+            n_own = hi - lo
         img, slot = ops.ep_dispatch(x, r.topk_e, lo, n_own, El, ep, C, MR)
         car = comm.get_custom(grp)
         if car is not None and not car.fits_bytes(img.numel() * img.element_size()):
@@ -133,6 +139,9 @@ class MoEBlock:
             h = ops.grouped_gemm(rows, lw.w13, rr, gather=True, e_lo=0)
             ops.grouped_gemm(ops.silu_mul(h), lw.w2, rr, gather=False, e_lo=0, combine_out=y)
         back = exchange(y.to(x.dtype).view(ep, C + MR, d))
+        if self.dp:
+            out = torch.empty(T, d, dtype=x.dtype, device=x.device)
+            return ops.ep_combine(back, slot, r.topk_w, 0, T, out)
         own = torch.empty(Tl, d, dtype=x.dtype, device=x.device)
         if n_own < Tl:
             own[n_own:].zero_()  # past the last token (sliced off below; kept finite)
@@ -143,3 +152,34 @@ class MoEBlock:
         else:
             comm.all_gather_into(full, own, ep, grp)
         return full[:T]
+
+    def serve_idle(self, lw, d: int, dtype, device) -> None:
+        """DP attention, a rank with no tokens this step: its experts still serve the other ranks' tokens — the
+        same collectives as _a2a with an empty dispatch (every destination block has count 0)."""
+        from kafka_llm_service_amd.parallel import comm
+
+        ep, k, El = self.ep, self.k, self.e_local
+        grp = pstate.get().ep_group
+        Tl, C, MR = ops.ep_layout(self.model.ep_t_cap * ep, ep, k, El, d)
+        x = torch.zeros(1, d, dtype=dtype, device=device)
+        te = torch.zeros(1, k, dtype=torch.int32, device=device)
+        img, _ = ops.ep_dispatch(x, te, 0, 0, El, ep, C, MR)
+        car = comm.get_custom(grp)
+        if car is not None and not car.fits_bytes(img.numel() * img.element_size()):
+            car = None
+
+        def exchange(send):
+            recv = torch.empty_like(send)
+            return car.all_to_all(send, recv) if car is not None else comm.all_to_all_single(recv, send, grp)
+
+        recv = exchange(img)
+        rr = ops.ep_recv_route(recv, C, El)
+        rows = recv.view(-1, d)
+        y = torch.zeros(rows.shape[0], d, dtype=torch.float32, device=device)
+        if self.model.stream and lw.w13_t is not None and rows.shape[0] <= MOE_STREAM_MAX_T:
+            a = ops.grouped_stream_glu(rows, lw.w13_t, rr, e_lo=0)
+            ops.grouped_stream_combine(a, lw.w2_t, rr, rows.shape[0], y, e_lo=0)
+        else:
+            h = ops.grouped_gemm(rows, lw.w13, rr, gather=True, e_lo=0)
+            ops.grouped_gemm(ops.silu_mul(h), lw.w2, rr, gather=False, e_lo=0, combine_out=y)
+        exchange(y.to(dtype).view(ep, C + MR, d))

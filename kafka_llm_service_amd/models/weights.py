@@ -135,7 +135,8 @@ def random_init(model: TransformerLM, seed: int = 0, exact_tp: bool | None = Non
     if exact_tp is None:
         exact_tp = cfg.num_params() < 2e9 or tp == 1
     sh = _Shard(cfg, tp, r)
-    eps = ep_slice(cfg, tp, r)
+    eps = ep_slice(cfg, model.ep, model.ep_rank)
+    er = model.ep_rank if model.dp_attention else r  # the rank whose shard a per-rank seed draws
     for key, shape in full_shapes(cfg).items():
         kind = key.split(".")[-1]
         if kind in ("input_norm", "post_norm", "final_norm"):
@@ -149,7 +150,7 @@ def random_init(model: TransformerLM, seed: int = 0, exact_tp: bool | None = Non
             # same shapes as the shard, drawn directly on the device
             probe = torch.empty(shape, device="meta")
             lshape = _shard_tensor(sh, key, probe, eps).shape
-            t = _randn(lshape, _seed(f"{key}@{r}", seed), dev, dt)
+            t = _randn(lshape, _seed(f"{key}@{er}" if key.endswith(("w13", "w2")) else f"{key}@{r}", seed), dev, dt)
         _assign(model, key, t)
     _finish(model)
     return model
@@ -191,7 +192,7 @@ def load_safetensors(model: TransformerLM, path: str | Path) -> TransformerLM:
 
     cfg, tp, r = model.cfg, model.tp, model.tp_rank
     sh = _Shard(cfg, tp, r)
-    eps = ep_slice(cfg, tp, r)
+    eps = ep_slice(cfg, model.ep, model.ep_rank)
     dev, dt = model.device, model.dtype
 
     def put(key, t):

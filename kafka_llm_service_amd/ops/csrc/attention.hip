@@ -327,7 +327,8 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
                                                            float* __restrict__ out_part, float* __restrict__ lse_part,
                                                            int S_total, float scale_log2,
                                                            bf16* __restrict__ out, int64_t out_stride,
-                                                           int* __restrict__ tickets) {
+                                                           int* __restrict__ tickets,
+                                                           const bf16* __restrict__ pre_bf16) {
   __shared__ float sO[4][8][D];
   __shared__ float sM[4][8];
   __shared__ float sL[4][8];
@@ -419,17 +420,36 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
         }
       }
       f32x4 acc4 = Ls > 0.f ? os * (sW[g][split_offset] / Ls) : f32x4{0.f, 0.f, 0.f, 0.f};
-      const float* pp = out_part + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
+      const int64_t pbase = ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
       int s2 = 0;
       // MG prefix partials per round trip (the cascade writes 32 per row: 2 round trips at MG = 16, 4 at 8)
-      for (; s2 + MG <= split_offset; s2 += MG) {
-        f32x4 v[MG];
+      if (pre_bf16 != nullptr) {  // bf16 cascade partials (tile v3): half the bytes of the fp32 round trip
+        const bf16* pb = pre_bf16 + pbase;
+        for (; s2 + MG <= split_offset; s2 += MG) {
+          bf16x4 v[MG];
 #pragma unroll
-        for (int j = 0; j < MG; ++j) v[j] = *reinterpret_cast<const f32x4*>(pp + (s2 + j) * D);
+          for (int j = 0; j < MG; ++j) v[j] = *reinterpret_cast<const bf16x4*>(pb + (s2 + j) * D);
 #pragma unroll
-        for (int j = 0; j < MG; ++j) acc4 += v[j] * sW[g][s2 + j];
+          for (int j = 0; j < MG; ++j) {
+            const float wj = sW[g][s2 + j];
+            acc4 += f32x4{(float)v[j][0], (float)v[j][1], (float)v[j][2], (float)v[j][3]} * wj;
+          }
+        }
+        for (; s2 < split_offset; ++s2) {
+          const bf16x4 v = *reinterpret_cast<const bf16x4*>(pb + s2 * D);
+          acc4 += f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]} * sW[g][s2];
+        }
+      } else {
+        const float* pp = out_part + pbase;
+        for (; s2 + MG <= split_offset; s2 += MG) {
+          f32x4 v[MG];
+#pragma unroll
+          for (int j = 0; j < MG; ++j) v[j] = *reinterpret_cast<const f32x4*>(pp + (s2 + j) * D);
+#pragma unroll
+          for (int j = 0; j < MG; ++j) acc4 += v[j] * sW[g][s2 + j];
+        }
+        for (; s2 < split_offset; ++s2) acc4 += *reinterpret_cast<const f32x4*>(pp + s2 * D) * sW[g][s2];
       }
-      for (; s2 < split_offset; ++s2) acc4 += *reinterpret_cast<const f32x4*>(pp + s2 * D) * sW[g][s2];
       const float inv = sWt[g] > 0.f ? 1.f / sWt[g] : 0.f;
       bf16x4 o4;
 #pragma unroll
@@ -506,8 +526,16 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
   if (g < G) {
     f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
     const float* pp = out_part + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
+    int s0 = 0;
+    if (pre_bf16 != nullptr) {  // the cascade's bf16 prefix partials (written by an earlier kernel: plain loads)
+      const bf16* pb = pre_bf16 + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
+      for (; s0 < split_offset; ++s0) {
+        const bf16x4 v = *reinterpret_cast<const bf16x4*>(pb + s0 * D);
+        acc4 += f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]} * sW[g][s0];
+      }
+    }
     // groups of 16 partials with all loads in flight (the tail of the kernel: latency, not bandwidth)
-    for (int s2 = 0; s2 < n; s2 += 16) {
+    for (int s2 = s0; s2 < n; s2 += 16) {
       f32x4 v[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) v[j] = ld4(pp + min(s2 + j, n - 1) * D);
@@ -991,7 +1019,8 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
                                               const void* v_cache, int fp8, int n_items, int B, int Hkv, int G, int D,
                                               const int* block_tables, int bt_stride, const int* items,
                                               float* out_part, float* lse_part, int S_total, float scale, bf16* out,
-                                              int64_t out_stride, int* tickets, hipStream_t st) {
+                                              int64_t out_stride, int* tickets, const bf16* pre_bf16,
+                                              hipStream_t st) {
   if (n_items == 0) return hipSuccess;
   if (D != 128 || G > 8 || G < 1) return hipErrorInvalidValue;
   if (out != nullptr && tickets == nullptr) return hipErrorInvalidValue;
@@ -1003,7 +1032,7 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
   const auto* di = reinterpret_cast<const DecodeItem*>(items);
   auto go = [&](auto kern, dim3 grid) {
     kern<<<grid, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, di, B, out_part,
-                               lse_part, S_total, scale_log2, out, out_stride, tickets);
+                               lse_part, S_total, scale_log2, out, out_stride, tickets, pre_bf16);
   };
   // prefix partials per load round trip in the fused merge (env KAFKA_DECODE_MERGE_GROUP = 8 / 16 / 32; bench A/B
   // profiles/r02/decode_merge_group_ab.jsonl: 7,491 / 7,489 / 7,505 tok/s — the epilogue is not on the critical path)
@@ -1049,19 +1078,21 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
                                             const void* k_cache, const void* v_cache, int Hkv, int G, int D,
                                             const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
                                             int64_t out_stride, float* out_part, float* lse_part, int S_total,
-                                            float scale, hipStream_t st);
+                                            float scale, int part_bf16, hipStream_t st);
 
 extern "C" hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride,
                                                const void* k_cache, const void* v_cache, int fp8, int Hkv, int G,
                                                int D, const int* block_tables, int bt_stride, const int* q_limit,
                                                bf16* out, int64_t out_stride, float* out_part, float* lse_part,
-                                               int S_total, float scale, int variant, hipStream_t st) {
+                                               int S_total, float scale, int variant, int part_bf16,
+                                               hipStream_t st) {
   if (n_items == 0) return hipSuccess;
   if (variant == 3) {  // LDS-DMA ring, one wave per SIMD, 256 rows (attn_tile.hip); bf16 pages only
     if (fp8) return hipErrorInvalidValue;
     return kafka_launch_attn_tile(items, n_items, q, q_stride, k_cache, v_cache, Hkv, G, D, block_tables, bt_stride,
-                                  q_limit, out, out_stride, out_part, lse_part, S_total, scale, st);
+                                  q_limit, out, out_stride, out_part, lse_part, S_total, scale, part_bf16, st);
   }
+  if (part_bf16) return hipErrorInvalidValue;  // bf16 partials: tile v3 only
   if (D != 128 || G < 1 || G > 32 || (128 % G) != 0 || n_items > 65535) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
   const auto* it = reinterpret_cast<const AttnWorkItem*>(items);

@@ -102,7 +102,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
                                                            const int* __restrict__ q_limit, bf16* __restrict__ out,
                                                            int64_t out_stride, float* __restrict__ out_part,
                                                            float* __restrict__ lse_part, int S_total,
-                                                           float scale_log2) {
+                                                           float scale_log2, int part_bf16) {
   using namespace tile3;
   static_assert(NSLOT == 3 || NSLOT == 4, "ring depth");
   static_assert(RB == 1 || RB == 2, "row blocks per wave");
@@ -405,15 +405,18 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
         const f32x4 v = *reinterpret_cast<const f32x4*>(sl + row * 128 + 16 * (cc ^ (row & 7)));
         if (row < nvalid) {
           const int R2 = R0 + row, tok2 = it.q_start + R2 / G, head2 = kvh * G + R2 % G;
-          if (part)
+          if (part && !part_bf16)
             *reinterpret_cast<f32x4*>(out_part + (((int64_t)tok2 * Hq + head2) * S_total + it.split) * D + 32 * rd +
                                       4 * cc) = v;
+          else if (part)  // bf16 partial (O / l in [-max|v|, max|v|]: half the bytes of the cascade round trip)
+            *reinterpret_cast<f32x4*>(reinterpret_cast<bf16*>(out_part) +
+                                      (((int64_t)tok2 * Hq + head2) * S_total + it.split) * D + 64 * rd + 8 * cc) = v;
           else
             *reinterpret_cast<f32x4*>(out + (int64_t)tok2 * out_stride + (int64_t)head2 * D + 64 * rd + 8 * cc) = v;
         }
       }
     };
-    if (part) {
+    if (part && !part_bf16) {
 #pragma unroll
       for (int rd = 0; rd < 4; ++rd) {
 #pragma unroll
@@ -448,7 +451,7 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
                                             const void* k_cache, const void* v_cache, int Hkv, int G, int D,
                                             const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
                                             int64_t out_stride, float* out_part, float* lse_part, int S_total,
-                                            float scale, hipStream_t st) {
+                                            float scale, int part_bf16, hipStream_t st) {
   if (n_items == 0) return hipSuccess;
   if (D != 128 || G < 1 || G > 32 || (256 % G) != 0 || n_items > 65535) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
@@ -472,7 +475,7 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
   kern<<<dim3(Hkv, n_items), 512 / rb, 0, st>>>(
       reinterpret_cast<const TileItem*>(items), q, q_stride, static_cast<const bf16*>(k_cache),
       static_cast<const bf16*>(v_cache), Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
-      lse_part, S_total, scale_log2);
+      lse_part, S_total, scale_log2, part_bf16);
   return hipGetLastError();
 }
 

@@ -27,12 +27,13 @@ hipError_t kafka_launch_rope_kv_fp8(const bf16* qkv, const float* qp, int S, int
 hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const void* k_cache, const void* v_cache, int fp8,
                                     int n_items, int B, int Hkv, int G, int D, const int* block_tables, int bt_stride,
                                     const int* items, float* out_part, float* lse_part, int S_total, float scale,
-                                    bf16* out, int64_t out_stride, int* tickets, hipStream_t st);
+                                    bf16* out, int64_t out_stride, int* tickets, const bf16* pre_bf16,
+                                    hipStream_t st);
 hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride,
                                      const void* k_cache, const void* v_cache, int fp8, int Hkv, int G, int D,
                                      const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
                                      int64_t out_stride, float* out_part, float* lse_part, int S_total, float scale,
-                                     int variant, hipStream_t st);
+                                     int variant, int part_bf16, hipStream_t st);
 hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows, int Hq, int S, int D, bf16* out,
                              int64_t out_stride, float* lse_out, hipStream_t st);
 hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
@@ -226,7 +227,8 @@ static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_s
 // Their values are device data; the kernel drops an item whose b / slots fall outside the checked buffer shapes.
 static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
                         at::Tensor items, at::Tensor out_part, at::Tensor lse_part, double scale,
-                        c10::optional<at::Tensor> out, c10::optional<at::Tensor> tickets) {
+                        c10::optional<at::Tensor> out, c10::optional<at::Tensor> tickets,
+                        c10::optional<at::Tensor> pre_part) {
   CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
   CHECK_DT(block_tables, at::kInt); CHECK_DT(items, at::kInt); CHECK_DT(out_part, at::kFloat);
   CHECK_DT(lse_part, at::kFloat);
@@ -255,11 +257,18 @@ static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at
                 "attn_decode: the fused merge needs an int32 ticket buffer of >= B * Hkv zeros");
     tp = tickets->data_ptr<int>();
   }
+  const bf16* pre = nullptr;  // bf16 cascade prefix partials (slots < npre), same [B, Hq, S_total, 128] indexing
+  if (pre_part.has_value()) {
+    CHECK_DT(pre_part.value(), at::kBFloat16);
+    TORCH_CHECK(pre_part->is_contiguous() && pre_part->sizes() == out_part.sizes(),
+                "attn_decode: pre_part must match out_part's shape");
+    pre = bptr(pre_part.value());
+  }
   CHECK_HIP(kafka_launch_attn_decode(bptr(q), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                       is_fp8_cache(k_cache) ? 1 : 0, items.size(0), B, Hkv,
                                       Hq / Hkv, 128, block_tables.data_ptr<int>(), block_tables.stride(0),
                                       items.data_ptr<int>(), out_part.data_ptr<float>(), lse_part.data_ptr<float>(),
-                                      S_total, scale, op, ostride, tp, cur_stream()));
+                                      S_total, scale, op, ostride, tp, pre, cur_stream()));
 }
 
 static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
@@ -288,21 +297,25 @@ static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at:
   float* pp = nullptr;
   float* lp = nullptr;
   int S_total = 0;
+  int part_bf16 = 0;
   if (out_part.has_value()) {
     TORCH_CHECK(lse_part.has_value(), "lse_part required with out_part");
-    CHECK_DT(out_part.value(), at::kFloat); CHECK_DT(lse_part.value(), at::kFloat);
+    part_bf16 = out_part->scalar_type() == at::kBFloat16 ? 1 : 0;  // bf16 partials: tile variant 3 only
+    TORCH_CHECK(!part_bf16 || variant == 3, "attn_prefill: bf16 out_part needs tile variant 3");
+    if (!part_bf16) CHECK_DT(out_part.value(), at::kFloat);
+    CHECK_DT(lse_part.value(), at::kFloat);
     TORCH_CHECK(out_part->is_contiguous() && out_part->dim() == 4 && out_part->size(0) >= T &&
                     out_part->size(1) == Hq && out_part->size(3) == 128, "out_part must be [T, Hq, S, 128]");
     S_total = out_part->size(2);
     TORCH_CHECK(lse_part->is_contiguous() && lse_part->numel() >= (int64_t)T * Hq * S_total, "lse_part");
-    pp = out_part->data_ptr<float>();
+    pp = reinterpret_cast<float*>(out_part->data_ptr());
     lp = lse_part->data_ptr<float>();
   }
   TORCH_CHECK(op != nullptr || pp != nullptr, "attn_prefill needs out or out_part");
   CHECK_HIP(kafka_launch_attn_prefill(items.data_ptr<int>(), items.size(0), bptr(q), q.stride(0), k_cache.data_ptr(),
                                        v_cache.data_ptr(), is_fp8_cache(k_cache) ? 1 : 0, Hkv, G, 128, block_tables.data_ptr<int>(),
                                        block_tables.stride(0), q_limit.data_ptr<int>(), op, os, pp, lp, S_total,
-                                       scale, (int)variant, cur_stream()));
+                                       scale, (int)variant, part_bf16, cur_stream()));
 }
 
 static void attn_merge(at::Tensor part, at::Tensor lse, at::Tensor out, c10::optional<at::Tensor> lse_out) {
@@ -717,7 +730,9 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
   m.def("silu_mul", &silu_mul);
   m.def("rope_kv_write", &rope_kv_write);
-  m.def("attn_decode", &attn_decode);
+  m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
+        py::arg("items"), py::arg("out_part"), py::arg("lse_part"), py::arg("scale"), py::arg("out"),
+        py::arg("tickets"), py::arg("pre_part") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("items"), py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("block_tables"), py::arg("q_limit"), py::arg("out"), py::arg("out_part"), py::arg("lse_part"),
         py::arg("scale"), py::arg("variant") = 0);

@@ -216,8 +216,10 @@ def attn_decode_full(q, k_cache, v_cache, block_tables, seq_lens, scale, kv_star
     return out, lse
 
 
-def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale, out=None):
-    """Reference for the work-item decode kernel (ops/csrc/attention.hip attn_decode_kernel)."""
+def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale, out=None,
+                      pre_part=None):
+    """Reference for the work-item decode kernel (ops/csrc/attention.hip attn_decode_kernel). ``pre_part`` (bf16,
+    out_part's shape): the cascade's prefix partials (slots < npre) are read from it instead of out_part."""
     B, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     G = Hq // Hkv
@@ -241,8 +243,12 @@ def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_pa
         out_part[b, :, npre + split] = o
         lp[b, :, npre + split] = l2
     if out is not None:
+        npre = {int(it[0]): int(it[5]) for it in items.tolist()}
         for b, n in nparts.items():
-            attn_merge(out_part[b:b + 1, :, :n].contiguous(), lp[b:b + 1, :, :n].contiguous(), out[b:b + 1])
+            parts = out_part[b:b + 1, :, :n].clone()
+            if pre_part is not None:
+                parts[:, :, :npre[b]] = pre_part[b:b + 1, :, :npre[b]].float()
+            attn_merge(parts.contiguous(), lp[b:b + 1, :, :n].contiguous(), out[b:b + 1])
 
 
 def attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale, out=None, out_part=None,
@@ -274,7 +280,7 @@ def attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale,
         if split < 0:
             out[toks] = o.to(out.dtype)
         else:
-            out_part[toks, :, split] = o
+            out_part[toks, :, split] = o.to(out_part.dtype)
             lse_part.view(out_part.shape[0], Hq, out_part.shape[2])[toks, :, split] = l2
 
 

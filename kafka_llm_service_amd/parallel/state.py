@@ -35,6 +35,11 @@ class ParallelState:
     tp_group: object = None  # torch ProcessGroup over the tp ranks (None when tp == 1)
     cpu_group: object = None  # gloo group over the tp ranks for host-side broadcasts (scheduler decisions)
     backend: str = "none"
+    # DP attention (init_dp_attention): ranks of one EP group run their own sequences, experts sharded over them
+    ep: int = 1
+    ep_rank: int = 0
+    ep_group: object = None
+    ep_cpu_group: object = None  # gloo: the per-step agreement on the all-to-all capacity
 
     @property
     def is_tp_leader(self) -> bool:
@@ -84,6 +89,40 @@ def init(tp: int = 1, backend: str | None = None, device: str | None = None) -> 
             on_gpu = (device or "").startswith("cuda") or (device is None and torch.cuda.is_available())
             if on_gpu and tp in (2, 4, 8) and os.environ.get("KAFKA_CUSTOM_AR", "1") == "1":
                 _register_custom_ar(st, tp)
+    _STATE = st
+    return st
+
+
+def init_dp_attention(ep: int, backend: str | None = None, device: str | None = None) -> ParallelState:
+    """Data-parallel attention + expert parallelism (Mixtral): tp = 1, every ``ep`` consecutive ranks form an EP
+    group — each runs its own sequences with whole attention weights and its own KV cache, and the group shares the
+    experts through the device-side all-to-all of models/moe.py (the custom IPC transport registered on the group
+    when it can be set up, RCCL / gloo otherwise)."""
+    global _STATE
+    st = init(tp=1, backend=backend, device=device)
+    if ep <= 1:
+        return st
+    if st.world % ep:
+        raise ValueError(f"world size {st.world} not divisible by ep={ep}")
+    backend = st.backend
+    st.ep, st.ep_rank = ep, st.rank % ep
+    for g in range(st.world // ep):
+        ranks = list(range(g * ep, (g + 1) * ep))
+        pg = dist.new_group(ranks, backend=backend, timeout=_timeout())
+        cpg = dist.new_group(ranks, backend="gloo", timeout=_timeout()) if backend != "gloo" else pg
+        if st.rank in ranks:
+            st.ep_group, st.ep_cpu_group = pg, cpg
+    on_gpu = (device or "").startswith("cuda") or (device is None and torch.cuda.is_available())
+    if on_gpu and ep in (2, 4, 8) and os.environ.get("KAFKA_CUSTOM_AR", "1") == "1":
+        import logging
+
+        from . import comm
+        from .custom_allreduce import CustomAllReduce, CustomAllReduceUnavailable
+
+        try:
+            comm.register_custom(st.ep_group, CustomAllReduce(st.ep_cpu_group, st.ep_rank, ep))
+        except CustomAllReduceUnavailable:
+            logging.getLogger("kafka.parallel").exception("IPC all-to-all unavailable; using the library collective")
     _STATE = st
     return st
 

@@ -276,10 +276,12 @@ def test_out_of_vocab_prompt_rejected(base_engine):
     assert "oov" not in base_engine.requests
 
 
-def test_multi_group_cascade_equals_plain(base_engine):
+def test_multi_group_cascade_equals_plain(base_engine, monkeypatch):
     """Three system prompts (Kafka prompt, a thread created with its own system message — quirk Q4 — and a second
     custom prompt) plus a stateless row with no shared prefix: every group gets its own cascade pass and the
-    result equals plain per-row attention."""
+    result equals plain per-row attention (fp32 prefix partials: token-exact; the bf16 default is checked to
+    logit tolerance by test_bf16_cascade_partials_close_to_fp32)."""
+    monkeypatch.setenv("KAFKA_CASCADE_BF16", "0")
     groups = [_prompts(seed=10 + i, shared=96, tails=(3, 9, 30)) for i in range(3)]
     loner = _prompts(seed=20, shared=0, tails=(50,))
     prompts = [p for g in groups for p in g] + loner
@@ -392,3 +394,27 @@ def test_padded_mixed_steps_match_unpadded(base_engine):
     e.runner.build_host = build_host
     assert e.generate(prompts, GREEDY) == ref
     assert 168 in seen
+
+
+def test_bf16_cascade_partials_close_to_fp32(base_engine, monkeypatch):
+    """The tile-v3 cascade hands its prefix partials to the decode kernel as bf16 by default (half the bytes):
+    decode-step logits stay within bf16 rounding of the fp32-partial path."""
+    prompts = _prompts(seed=31, shared=96, tails=(3, 9, 30))
+    logits = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("KAFKA_CASCADE_BF16", mode)
+        e = _engine(model=base_engine.model, use_cascade=True, cascade_min_prefix=16)
+        e.generate([prompts[0][:96] + [7]], GREEDY)
+        seen = []
+        orig = e.runner.sample_device
+
+        def spy(lg, sp, seen=seen, orig=orig):
+            seen.append(lg.float().clone())
+            return orig(lg, sp)
+        e.runner.sample_device = spy
+        e.generate(prompts, GREEDY)
+        logits[mode] = seen
+        assert e.runner.cascade_bf16 == (mode == "1")
+    a, b = logits["0"][1], logits["1"][1]  # first decode step (the cascade pass ran)
+    assert a.shape == b.shape
+    assert (a - b).abs().max().item() < 0.05 * a.abs().max().item() + 0.05
