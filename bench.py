@@ -59,6 +59,8 @@ def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1, help="number of ranks (one per GPU)")
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel size per replica (e.g. 8 for llama3-70b)")
+    ap.add_argument("--dp-attention", action="store_true",
+                    help="MoE models: all ranks form one data-parallel-attention EP group (engine/dp_attention.py)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="llama3-8b")
@@ -217,14 +219,20 @@ def main(argv=None):
 
     dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
     tp = args.tp
-    st = pstate.init(tp=tp, device=dev) if world > 1 else pstate.get()
+    dpa = args.dp_attention and world > 1
+    if dpa:
+        if tp != 1:
+            raise SystemExit("bench.py: --dp-attention runs with --tp 1 (attention is data-parallel)")
+        st = pstate.init_dp_attention(world, device=dev)
+    else:
+        st = pstate.init(tp=tp, device=dev) if world > 1 else pstate.get()
     from kafka_llm_service_amd.engine import tp_worker
     from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
     from kafka_llm_service_amd.engine.sequence import SamplingParams
 
     cfg = EngineConfig(model=args.model, device=dev, seed=args.seed, max_num_seqs=max(256, 2 * args.threads),
                        use_cascade=not args.no_cascade, use_graphs=args.graphs, kv_dtype=args.kv_dtype,
-                       max_model_len=131072 if args.prefix_tokens > 6000 else 8192, tp=tp, tp_rank=st.tp_rank)
+                       max_model_len=131072 if args.prefix_tokens > 6000 else 8192, tp=tp, tp_rank=st.tp_rank, dp_attention=dpa)
     eng = LLMEngine(cfg)
     leaders = None
     if tp > 1:
@@ -236,6 +244,18 @@ def main(argv=None):
             tp_worker.follower_loop(eng)
             return _report(args, world, rank, dev, eng, {"out_tokens": 0, "ttft": [], "extra": 0}, 0.0, 0.0)
         tp_worker.attach_leader(eng)
+    if dpa:  # every rank steps in lockstep with its EP group (one forward per step on every rank)
+        from kafka_llm_service_amd.engine import dp_attention
+
+        agree = dp_attention.make_agree(st)
+
+        def gen(ps, sp):
+            return dp_attention.generate_lockstep(eng, st, ps, sp)
+
+        def step():
+            return eng.step_lockstep(agree)[0]
+    else:
+        gen, step = eng.generate, eng.step
     V = eng.model_cfg.vocab_size
     rng = random.Random(args.seed * 7919 + rank)
     prefix = [rng.randrange(1000, min(V, 120000)) for _ in range(args.prefix_tokens)]
@@ -252,8 +272,8 @@ def main(argv=None):
     prompts = [th.next_prompt(done) for th, (_, done) in zip(threads, budgets)]
     warm = SamplingParams(temperature=0, max_tokens=1, ignore_eos=True)
     for p in {tuple(t.prefix) for t in threads if t.prefix}:
-        eng.generate([list(p) + [5]], warm)
-    eng.generate(prompts, warm)
+        gen([list(p) + [5]], warm)
+    gen(prompts, warm)
     if dev.startswith("cuda"):
         torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
@@ -280,7 +300,7 @@ def main(argv=None):
 
     def run_step(record: bool):
         ts = time.perf_counter()
-        outs = eng.step()
+        outs = step()
         if steplog is not None:
             steplog.append((ts, len(outs), sum(1 for o in outs if o.num_output_tokens == 1)))
         for o in outs:
@@ -322,7 +342,12 @@ def main(argv=None):
             ps.sort_stats("cumtime").print_stats(60)
     _barrier(leaders)
     # ---- TTFT: keep the same load running (untimed) until enough new turns have produced their first token
-    while len(timing["ttft"]) < args.ttft_samples and timing["extra"] < args.ttft_max_steps:
+    def want_more() -> bool:
+        more = len(timing["ttft"]) < args.ttft_samples and timing["extra"] < args.ttft_max_steps
+        if dpa:  # the group keeps stepping while any rank still needs samples
+            more = bool(agree((int(more),))[0])
+        return more
+    while want_more():
         run_step(False)
         timing["extra"] += 1
     _barrier(leaders)
@@ -385,7 +410,8 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
                    "seq_len": args.prefix_tokens + args.history_turns * (args.user_tokens + (args.min_out +
                                                                                          args.max_out) // 2)
                    + args.user_tokens,
-                   "parallelism": f"dp{dp}" + (f"-tp{args.tp}" if args.tp > 1 else ""),
+                   "parallelism": (f"dpattn{world}-ep{world}" if args.dp_attention and world > 1 else
+                                   f"dp{dp}" + (f"-tp{args.tp}" if args.tp > 1 else "")),
                    "threads_per_gpu": args.threads * dp // world,
                    "shared_prefix_tokens": args.prefix_tokens, "history_turns": args.history_turns,
                    "mixed_prefix": args.mixed_prefix, "max_out": [args.min_out, args.max_out],

@@ -212,11 +212,19 @@ class DPClient:
     """
 
     def __init__(self, engine_cfg, n_replicas: int, start_timeout: float = 900.0, tp: int = 1,
-                 base_port: int | None = None, respawn: bool = True, stall_timeout: float | None = None):
+                 base_port: int | None = None, respawn: bool = True, stall_timeout: float | None = None,
+                 dp_attention: bool = False):
         self._ctx = mp.get_context("spawn")
         self.engine_cfg = engine_cfg
         self.n_replicas = n_replicas
         self.tp = tp
+        # Mixtral DP attention (engine/dp_attention.py): the replicas are the ranks of ONE EP group — each serves
+        # its own threads (same thread-affinity routing), all of them step in lockstep and share the experts; the
+        # group is spawned, and respawned, as a whole
+        self.dpa = dp_attention
+        if dp_attention and (tp != 1 or n_replicas < 2):
+            raise ValueError("DP attention needs tp = 1 and at least 2 replicas")
+        self._dpa_lock = threading.Lock()
         self.max_model_len = engine_cfg.max_model_len
         from kafka_llm_service_amd.models.config import get_config
 
@@ -247,6 +255,7 @@ class DPClient:
         self._pin: list[int] | None = None
         self._pin_sent = [False] * n_replicas
         ports = base_port if base_port is not None else _free_port_base(n_replicas)
+        self._dpa_port = ports  # DP attention: one rendezvous for the whole group
         pending = [self._spawn(r, ports + r) for r in range(n_replicas)]
         for r, conns in enumerate(pending):
             self._await_ready(r, conns)
@@ -257,6 +266,15 @@ class DPClient:
     def _spawn(self, r: int, port: int) -> list:
         """Start replica r's processes; returns [leader_conn, follower_conns...] (not yet ready)."""
         ctx, cfg = self._ctx, self._cfg
+        if self.dpa:
+            from kafka_llm_service_amd.engine.dp_attention import dpa_worker_main
+
+            parent, child = ctx.Pipe()
+            p = ctx.Process(target=dpa_worker_main, args=(r, self.n_replicas, self._dpa_port, cfg, child),
+                            daemon=True, name=f"kafka-dpa{r}")
+            p.start()
+            self.procs[r], self._group_procs[r] = p, [p]
+            return [parent]
         if self.tp == 1:
             parent, child = ctx.Pipe()
             p = ctx.Process(target=_worker_main, args=(r, cfg, child, self.n_replicas), daemon=True,
@@ -298,6 +316,8 @@ class DPClient:
                          name=f"kafka-dp-reader{r}").start()
 
     def _respawn(self, r: int) -> None:
+        if self.dpa:
+            return self._respawn_dpa_group()
         for p in self._group_procs[r]:
             if p.is_alive():
                 p.terminate()
@@ -310,6 +330,32 @@ class DPClient:
             log.warning("engine replica %d restarted", r)
         except Exception:
             log.exception("engine replica %d failed to restart", r)
+
+    def _respawn_dpa_group(self) -> None:
+        """A DP-attention rank died: its peers cannot step without it, so the whole group is stopped, its streams
+        failed (503 / error frames) and the group restarted on a fresh rendezvous (one thread does it; the other
+        ranks' readers, which see their pipes close meanwhile, leave it to that one)."""
+        if not self._dpa_lock.acquire(blocking=False):
+            return
+        try:
+            for q in range(self.n_replicas):
+                self._fail_replica(q)
+                for p in self._group_procs[q]:
+                    if p.is_alive():
+                        p.kill()
+                    p.join(timeout=30)
+            if self._closing or not self.respawn:
+                return
+            self._dpa_port = _free_port_base(1)
+            pending = [self._spawn(q, self._dpa_port) for q in range(self.n_replicas)]
+            for q, conns in enumerate(pending):
+                self._await_ready(q, conns)
+                self.restarts[q] += 1
+            log.warning("DP-attention group restarted")
+        except Exception:
+            log.exception("DP-attention group failed to restart")
+        finally:
+            self._dpa_lock.release()
 
     def _monitor(self) -> None:
         while not self._closing:
@@ -530,4 +576,5 @@ async def make_engine_client(server_cfg):
     n = max(1, server_cfg.dp)
     if n == 1 and server_cfg.tp == 1 and not getattr(server_cfg, "engine_process", False):
         return await asyncio.to_thread(InProcessClient, ecfg)
-    return await asyncio.to_thread(DPClient, ecfg, n, 900.0, max(1, server_cfg.tp))
+    dpa = bool(getattr(server_cfg, "dp_attention", False))
+    return await asyncio.to_thread(DPClient, ecfg, n, 900.0, max(1, server_cfg.tp), None, True, None, dpa)

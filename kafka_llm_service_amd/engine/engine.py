@@ -62,6 +62,10 @@ class EngineConfig:
     # "blas" = hipBLASLt only; "auto" = stream on GPU (env KAFKA_DECODE_GEMM overrides)
     decode_gemm: str = "auto"           # auto | stream | stream_only (tiled weights only) | blas
     async_scheduling: bool = True       # plan step n+1 on the host while step n runs on the GPU
+    # Mixtral data-parallel attention (engine/dp_attention.py): this rank serves its own sequences with whole
+    # attention weights; experts are sharded over parallel.state's EP group and every step runs in lockstep with
+    # the group (step_lockstep; synchronous scheduling)
+    dp_attention: bool = False
     eos_token_ids: list[int] = field(default_factory=list)
 
     def resolve_device(self) -> torch.device:
@@ -113,9 +117,18 @@ class LLMEngine:
             torch.cuda.set_device(self.device)
         mc = self.model_cfg
         t0 = time.perf_counter()
+        dpa = None
+        if cfg.dp_attention:
+            from kafka_llm_service_amd.parallel import state as pstate
+
+            st = pstate.get()
+            dpa = (st.ep, st.ep_rank)
+            cfg.async_scheduling = False  # one forward per step() call: the group's collectives line up
+            cfg.use_graphs = False
         self.model = model or build_model(mc, self.device, tp=cfg.tp, tp_rank=cfg.tp_rank, seed=cfg.seed,
                                           weights=cfg.weights, max_positions=min(cfg.max_model_len,
-                                                                                 mc.max_position_embeddings))
+                                                                                 mc.max_position_embeddings),
+                                          dp_attention=dpa)
         mode = os.environ.get("KAFKA_DECODE_GEMM", cfg.decode_gemm)
         if mode == "auto":
             mode = "stream" if self.device.type == "cuda" else "blas"
@@ -299,6 +312,30 @@ class LLMEngine:
                 self.stats["planned_ahead"] += 1
                 self._inflight = self._launch(plan.batch, plan.host, plan.sampled, None)
         return outs
+
+    def step_lockstep(self, agree, flag: int = 0) -> tuple[list[StepOutput], int, int]:
+        """One DP-attention group step: EXACTLY one forward on every rank of the group (an expert-only idle step on
+        a rank without tokens), so the per-layer all-to-alls line up. ``agree((tokens, unfinished, flag))``
+        returns the group maxima; the largest step sets the all-to-all capacity. Returns (outputs, group max
+        unfinished — 0: every rank is idle, group max flag — e.g. a stop request seen by any rank)."""
+        batch = self.sched.schedule()
+        cut = self._cut_outputs(batch)
+        host = sampled = None
+        T = 0
+        if not batch.empty:
+            host, sampled = self.runner.build_host(batch)
+            T = host.T
+        t_max, busy, fl = agree((T, int(self.has_unfinished()), int(flag)))
+        if t_max == 0:
+            return cut, busy, fl
+        self.model.ep_t_cap = t_max
+        self.stats["group_steps"] = self.stats.get("group_steps", 0) + 1
+        if host is None:
+            with trace.span("dp_idle_step"):
+                self.model.dp_idle_step()
+            return cut, busy, fl
+        cur = self._launch(batch, host, sampled, None)
+        return cut + self._finish_step(cur), busy, fl
 
     @staticmethod
     def _needs_landed(sampled: list[Sequence]) -> bool:

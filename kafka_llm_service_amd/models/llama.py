@@ -98,6 +98,12 @@ class TransformerLM:
             raise ValueError("DP attention needs tp = 1 and experts divisible by the EP size")
         self.ep, self.ep_rank, self.dp_attention = ep, ep_rank, True
 
+    def dp_idle_step(self) -> None:
+        """DP attention: a group step in which this rank has no tokens — only its experts' share of every MoE
+        layer's all-to-all runs (the other ranks' tokens routed here), in layer order like a real forward."""
+        for lw in self.layers:
+            self.moe.serve_idle(lw, self.cfg.hidden_size, self.dtype, self.device)
+
     # ------------------------------------------------------------------------------------------------------------
     def stream_weight_bytes(self) -> int:
         """Bytes enable_stream_weights would add (the wave-tiled copies; 0 in tiled-only mode)."""

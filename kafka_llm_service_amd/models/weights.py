@@ -270,8 +270,11 @@ def save_safetensors(model: TransformerLM, path: str | Path) -> None:
 
 
 def build_model(cfg: ModelConfig, device, tp: int = 1, tp_rank: int = 0, seed: int = 0, weights: str | None = None,
-                max_positions: int | None = None) -> TransformerLM:
+                max_positions: int | None = None, dp_attention: tuple[int, int] | None = None) -> TransformerLM:
+    """``dp_attention = (ep, ep_rank)``: whole attention on this rank, experts sharded over the EP group."""
     model = TransformerLM(cfg, device, tp=tp, tp_rank=tp_rank, max_positions=max_positions)
+    if dp_attention is not None:
+        model.enable_dp_attention(*dp_attention)
     if weights:
         return load_safetensors(model, weights)
     return random_init(model, seed)

@@ -50,6 +50,8 @@ class ServerConfig:
     # run a single engine in its own worker process (like a DP replica) instead of a thread of the API process: the
     # step loop's kernel launches then never compete with the HTTP/SSE event loop for the GIL
     engine_process: bool = False
+    # Mixtral: the ``dp`` replicas form one data-parallel-attention EP group (engine/dp_attention.py)
+    dp_attention: bool = False
     engine_kwargs: dict[str, Any] = field(default_factory=dict)
 
     @staticmethod
@@ -69,6 +71,7 @@ class ServerConfig:
                             ignore_eos=e.get("KAFKA_IGNORE_EOS", "0") == "1",
                             warm_prefix=e.get("KAFKA_WARM_PREFIX", "1") == "1",
                             engine_process=_engine_process(e.get("KAFKA_ENGINE_PROCESS", "auto")),
+                            dp_attention=e.get("KAFKA_DP_ATTENTION", "0") == "1",
                             prompt_sections=[x for x in e.get("KAFKA_PROMPT_SECTIONS", "").split(",") if x] or None,
                             agent_max_iterations=int(e.get("KAFKA_AGENT_MAX_ITERATIONS", "50")),
                             engine_kwargs=_engine_kwargs(e))

@@ -299,3 +299,70 @@ def test_tp2_custom_allreduce_lost_peer_fails_the_step(cuda):
     for p in ps:
         p.join(timeout=60)
     assert res["leader"].startswith("raised"), res["leader"]
+
+
+def _dpa_gpu_main(rank, world, port, q, layout):
+    dev = rank % torch.cuda.device_count()
+    _env(rank, world, port, dev)
+    os.environ["KAFKA_TP_BACKEND"] = "gloo"
+    from kafka_llm_service_amd.engine import dp_attention
+    from kafka_llm_service_amd.engine.sequence import SamplingParams
+    from kafka_llm_service_amd.models.moe import MoEBlock
+    from kafka_llm_service_amd.parallel import comm
+    from kafka_llm_service_amd.parallel import state as pstate
+
+    calls = [0]
+    for name in ("__call__", "serve_idle"):  # no host sync anywhere in a MoE layer, busy or idle
+        orig = getattr(MoEBlock, name)
+
+        def checked(self, *a, _orig=orig, **kw):
+            torch.cuda.set_sync_debug_mode("error")
+            try:
+                return _orig(self, *a, **kw)
+            finally:
+                torch.cuda.set_sync_debug_mode("default")
+                calls[0] += 1
+        setattr(MoEBlock, name, checked)
+    eng, st = dp_attention.build_dpa_engine(dict(CFG, model="tiny-mixtral", device=f"cuda:{dev}"), ep=world)
+    try:
+        assert comm.get_custom(st.ep_group) is not None, "IPC all-to-all not registered on the EP group"
+        mine = [p for i, p in enumerate(_prompts(eng.model_cfg.vocab_size))
+                if (i % world if layout == "spread" else 0) == rank]
+        sp = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
+        outs = dp_attention.generate_lockstep(eng, st, mine, sp)
+        comm.get_custom(st.ep_group).check()
+        q.put((rank, outs, eng.stats["group_steps"], calls[0]))
+    finally:
+        pstate.destroy()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("layout", ["spread", "one_idle"])
+def test_dp_attention_mixtral_on_one_gpu(cuda, layout):
+    """Mixtral with data-parallel attention, EP = 2 over two processes on one GPU: each rank decodes its own
+    sequences (or none), every MoE layer exchanges rows through the device-side dispatch + IPC all-to-all without
+    a host sync, and every greedy token is the EP = 1 model's argmax up to bf16 rounding."""
+    from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
+    from kafka_llm_service_amd.models.oracle import dense_logits
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_dpa_gpu_main, args=(r, 2, port, q, layout)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {m[0]: m[1:] for m in (q.get(timeout=240) for _ in range(2))}
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] == res[1][1] and res[0][2] > 0 and res[1][2] > 0
+    ref = LLMEngine(EngineConfig(**dict(CFG, model="tiny-mixtral", device="cuda:0")))
+    prompts = _prompts(ref.model_cfg.vocab_size)
+    for r in (0, 1):
+        mine = [p for i, p in enumerate(prompts) if (i % 2 if layout == "spread" else 0) == r]
+        assert len(res[r][0]) == len(mine)
+        for p, o in zip(mine, res[r][0]):
+            lg = dense_logits(ref.model, p + o)
+            for i, tok in enumerate(o):
+                row = lg[len(p) - 1 + i]
+                assert (row.max() - row[tok]).item() < 0.15

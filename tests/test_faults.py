@@ -196,3 +196,27 @@ def test_dp_warm_prefix_reaches_every_replica():
         asyncio.run(run())
     finally:
         asyncio.run(cli.close())
+
+
+@pytest.mark.timeout(300)
+def test_dp_attention_group_serves_threads_over_http():
+    """KAFKA_DP_ATTENTION: the two engine replicas of the API server are one DP-attention EP group (tiny Mixtral,
+    CPU, gloo): threads routed to either rank stream their replies while both ranks step in lockstep."""
+    from fastapi.testclient import TestClient
+
+    from kafka_llm_service_amd.db.local import MemoryDBClient
+    from kafka_llm_service_amd.server.app import create_app
+    from kafka_llm_service_amd.server.state import ServerConfig, ServerState
+
+    cfg = ServerConfig(backend="engine", model="tiny-mixtral", sandbox="none", dp=2, dp_attention=True,
+                       max_model_len=4096, default_max_tokens=6, prompt_sections=["intro"], warm_prefix=False,
+                       ignore_eos=True, engine_kwargs={"device": "cpu", "num_kv_blocks": 512})
+    st = ServerState(cfg, db=MemoryDBClient())
+    with TestClient(create_app(state=st)) as c:
+        assert st.engine_client.dpa and st.engine_client.n_replicas == 2
+        for i in range(4):
+            tid = c.post("/v1/threads").json()["thread_id"]
+            r = c.post(f"/v1/threads/{tid}/chat/completions",
+                       json={"model": "m", "messages": [{"role": "user", "content": f"hi {i}"}], "stream": False,
+                             "max_tokens": 6})
+            assert r.status_code == 200 and r.json()["usage"]["completion_tokens"] == 6

@@ -220,3 +220,57 @@ def test_ep_ops_roundtrip_equals_direct_moe_on_cpu():
         want = sum(r.topk_w[lo:hi, j:j + 1] * x[lo:hi].float() * scale[r.topk_e[lo:hi, j].long()][:, None]
                    for j in range(k))
         torch.testing.assert_close(out[:hi - lo].float(), want, atol=0.1, rtol=2e-2)
+
+
+def _dpa_owner(layout: str, i: int) -> int:
+    return i % 2 if layout == "spread" else 0
+
+
+def _dpa_main(rank: int, world: int, port: int, q, layout) -> None:
+    """One rank of a DP-attention group: its own prompts (possibly none), experts sharded over the group."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(world),
+                       "RANK": str(rank), "LOCAL_RANK": str(rank)})
+    from kafka_llm_service_amd.engine import dp_attention
+    from kafka_llm_service_amd.parallel import state as pstate
+
+    eng, st = dp_attention.build_dpa_engine(dict(CFG, model="tiny-mixtral"), ep=world)
+    try:
+        assert eng.model.dp_attention and eng.model.ep == world and eng.model.tp == 1
+        assert eng.model.layers[0].w13.shape[0] == eng.model_cfg.num_experts // world
+        mine = [p for i, p in enumerate(_prompts()) if _dpa_owner(layout, i) == rank]
+        outs = dp_attention.generate_lockstep(eng, st, mine, GREEDY)
+        q.put((rank, outs, eng.stats["group_steps"]))
+    finally:
+        pstate.destroy()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("layout", ["spread", "one_idle"])
+def test_dp_attention_mixtral_matches_single_rank(layout):
+    """Mixtral with data-parallel attention over 2 ranks (each rank its own sequences, whole attention weights,
+    half the experts, device-side all-to-all dispatch/combine in lockstep): every greedy token is the EP=1 model's
+    argmax up to a small logit margin — also when one rank has no sequences at all and only serves its experts."""
+    from kafka_llm_service_amd.models.oracle import dense_logits
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_dpa_main, args=(r, 2, port, q, layout)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {m[0]: m[1:] for m in (q.get(timeout=240) for _ in range(2))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] == res[1][1]  # lockstep: the same number of group steps on both ranks
+    ref = LLMEngine(EngineConfig(**dict(CFG, model="tiny-mixtral")))
+    prompts = _prompts()
+    for r in (0, 1):
+        mine = [p for i, p in enumerate(prompts) if _dpa_owner(layout, i) == r]
+        assert len(res[r][0]) == len(mine)
+        for p, o in zip(mine, res[r][0]):
+            assert len(o) == GREEDY.max_tokens
+            lg = dense_logits(ref.model, p + o)
+            for i, tok in enumerate(o):
+                row = lg[len(p) - 1 + i]
+                assert (row.max() - row[tok]).item() < 0.05
