@@ -33,6 +33,23 @@ from kafka_llm_service_amd.parallel import state as pstate
 # serialized round trips than the 5.7 us rope_kv launch it removes. Off by default.
 FUSE_QKV_ROPE = os.environ.get("KAFKA_FUSE_QKV_ROPE", "0") == "1"
 
+# TP decode seam overlap (KAFKA_TP_OVERLAP=1): the row-parallel O / down projection of a decode-sized step is
+# computed in two column halves; half 0's all-reduce runs on a second HIP stream while half 1's GEMM streams its
+# weights on the main one, then half 1's all-reduce, the join and the residual add + RMSNorm. Unlike a split of the
+# batch into two micro-batches it reads every weight once (decode GEMMs are weight-bound), and the per-element sums
+# are those of the one-shot all-reduce. Captured hipGraphs record the fork/join. Off by default: the gain needs
+# TP over xGMI to measure (ranks sharing one GPU overlap nothing), and the seam loses its fused AR + RMSNorm launch.
+TP_OVERLAP = os.environ.get("KAFKA_TP_OVERLAP", "0") == "1"
+_OVL: dict = {}
+_SEAM_DONE = object()  # forward(): the previous layer's overlapped seam already produced this layer's input
+
+
+def _overlap_stream(dev: torch.device):
+    s = _OVL.get(dev)
+    if s is None:
+        s = _OVL[dev] = (torch.cuda.Stream(device=dev), [torch.cuda.Event() for _ in range(3)])
+    return s
+
 
 @dataclass
 class StepInput:
@@ -200,7 +217,9 @@ class TransformerLM:
         fuse_rope = (self.stream and FUSE_QKV_ROPE and 0 < T <= min(128, self.stream_max_m) and self.layers[0].qkv_t is not None
                      and ops.qkv_rope_fusable(k_caches[0], self.D))
         for i, lw in enumerate(self.layers):
-            if delta is None:
+            if delta is _SEAM_DONE:
+                pass  # the previous layer's overlapped down seam already wrote residual and x
+            elif delta is None:
                 ops.rmsnorm(h, lw.input_norm, eps, out=x)
                 residual = h.clone()
             elif pending:
@@ -215,11 +234,14 @@ class TransformerLM:
                 ops.rope_kv_write(qkv, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i], inp.slot_mapping,
                                   self.hq, self.hkv)
             paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out)
-            o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t)
-            if tp:
-                pstate.tp_all_reduce_add_rmsnorm(o, residual, lw.post_norm, eps, out=x)
+            if tp and self._can_overlap(T, lw.o_t):
+                self._overlapped_seam(attn_out.view(T, -1), lw.o_t, residual, lw.post_norm, eps, x)
             else:
-                ops.fused_add_rmsnorm(o, residual, lw.post_norm, eps, out=x)
+                o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t)
+                if tp:
+                    pstate.tp_all_reduce_add_rmsnorm(o, residual, lw.post_norm, eps, out=x)
+                else:
+                    ops.fused_add_rmsnorm(o, residual, lw.post_norm, eps, out=x)
             if lw.router is not None:
                 delta = self.moe(x, lw)
                 pending = tp and not self.moe.reduced
@@ -228,8 +250,13 @@ class TransformerLM:
                     a = ops.linear_glu(x, lw.gate_up_t)  # SwiGLU in the GEMM epilogue (or on its slabs)
                 else:
                     a = ops.silu_mul(F.linear(x, self._dense(lw.gate_up, lw.gate_up_t, bool(lw.glu))))
-                delta = self._linear(a, lw.down, lw.down_t)
-                pending = tp
+                if tp and self._can_overlap(T, lw.down_t) and i + 1 < len(self.layers):
+                    # the next layer's input RMSNorm is the seam's normalisation: delta is consumed here
+                    self._overlapped_seam(a, lw.down_t, residual, self.layers[i + 1].input_norm, eps, x)
+                    delta, pending = _SEAM_DONE, False
+                else:
+                    delta = self._linear(a, lw.down, lw.down_t)
+                    pending = tp
         if pending:
             delta = pstate.tp_all_reduce(delta)
         rows = inp.logit_rows
@@ -242,6 +269,36 @@ class TransformerLM:
         if tp:
             logits = pstate.tp_all_gather_lastdim(logits)
         return logits[:, :cfg.vocab_size]
+
+    def _can_overlap(self, T: int, wt: torch.Tensor | None) -> bool:
+        if not (TP_OVERLAP and self.stream and wt is not None and 0 < T <= self.stream_max_m and self.device.type == "cuda"):
+            return False
+        car = pstate.custom_ar()
+        return car is not None and wt.shape[0] % 2 == 0 and T * wt.shape[0] * 32 * 2 <= car.max_bytes
+
+    def _overlapped_seam(self, a: torch.Tensor, wt: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor,
+                         eps: float, out: torch.Tensor) -> None:
+        """residual += allreduce(a @ W^T); out = rmsnorm(residual) * norm_w, with W's two column halves pipelined
+        against their all-reduces (TP_OVERLAP above)."""
+        car = pstate.custom_ar()
+        side, (ev_in, ev1, ev_done) = _overlap_stream(a.device)
+        main = torch.cuda.current_stream(a.device)
+        nb = wt.shape[0] // 2
+        T = a.shape[0]
+        halves = [torch.empty(T, nb * 32, dtype=self.dtype, device=a.device) for _ in range(2)]
+        y0 = ops.linear_stream(a, wt[:nb])
+        ev_in.record(main)
+        with torch.cuda.stream(side):
+            side.wait_event(ev_in)
+            car.all_reduce(y0, out=halves[0])  # overlaps the second half's GEMM below
+        y1 = ops.linear_stream(a, wt[nb:])
+        ev1.record(main)
+        with torch.cuda.stream(side):
+            side.wait_event(ev1)
+            car.all_reduce(y1, out=halves[1])
+            ev_done.record(side)
+        main.wait_event(ev_done)  # joined: every buffer the side stream read is released after it on main
+        ops.fused_add_rmsnorm(torch.cat(halves, 1), residual, norm_w, eps, out=out)
 
     def _embed(self, tokens: torch.Tensor) -> torch.Tensor:
         if self.tp == 1:

@@ -162,6 +162,9 @@ def _tp_main(rank, world, port, q, graphs, model):
     os.environ["KAFKA_TP_BACKEND"] = "gloo"
     if model.endswith("+a2a"):  # experts dispatched / combined by all-to-all instead of the all-reduce combine
         os.environ["KAFKA_MOE_A2A"] = "1"
+    if model.endswith("+overlap"):  # O / down projections in column halves pipelined against their all-reduces
+        os.environ["KAFKA_TP_OVERLAP"] = "1"
+        model = model.replace("+overlap", "")
     from kafka_llm_service_amd.engine import tp_worker
     from kafka_llm_service_amd.engine.sequence import SamplingParams
     from kafka_llm_service_amd.parallel import comm
@@ -187,6 +190,15 @@ def _tp_main(rank, world, port, q, graphs, model):
                 torch.cuda.set_sync_debug_mode("default")
                 a2a_calls[0] += 1
         MoEBlock.__call__ = checked
+    if os.environ.get("KAFKA_TP_OVERLAP") == "1":
+        from kafka_llm_service_amd.models.llama import TransformerLM
+
+        orig_seam = TransformerLM._overlapped_seam
+
+        def counted(self, *a, **kw):
+            a2a_calls[0] += 1  # the overlapped seam ran (eager, or recorded into a graph)
+            return orig_seam(self, *a, **kw)
+        TransformerLM._overlapped_seam = counted
     try:
         assert os.environ.get("KAFKA_CUSTOM_AR", "1") == "0" or comm.get_custom(st.tp_group) is not None, \
             "custom all-reduce not registered"
@@ -208,8 +220,10 @@ def _tp_main(rank, world, port, q, graphs, model):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("model,graphs", [("small-llama", False), ("small-llama", True), ("tiny-mixtral", False),
-                                          ("tiny-mixtral+a2a", False), ("tiny-mixtral+a2a", True)],
-                         ids=["eager", "graphs", "mixtral-ep", "mixtral-ep-a2a", "mixtral-ep-a2a-graphs"])
+                                          ("tiny-mixtral+a2a", False), ("tiny-mixtral+a2a", True),
+                                          ("small-llama+overlap", False), ("small-llama+overlap", True)],
+                         ids=["eager", "graphs", "mixtral-ep", "mixtral-ep-a2a", "mixtral-ep-a2a-graphs",
+                              "overlap", "overlap-graphs"])
 def test_tp2_engine_on_one_gpu_matches_tp1(cuda, model, graphs):
     """TP=2 (Mixtral: experts sharded over the 2 ranks, EP) on one GPU == the TP=1 model: same first-step logits up
     to reduction order, every greedy token the dense oracle's argmax."""
@@ -233,9 +247,10 @@ def test_tp2_engine_on_one_gpu_matches_tp1(cuda, model, graphs):
     assert res["follower"][0] >= 6 and ahead > 0
     if graphs:
         assert gstats["replays"] >= 1
-    if model.endswith("+a2a"):  # eager MoE calls ran under set_sync_debug_mode("error") on both ranks
+    if model.endswith(("+a2a", "+overlap")):  # eager MoE calls under sync-debug "error" / overlapped seams ran
         assert a2a_lead > 0 and res["follower"][1] > 0
-    ref = LLMEngine(EngineConfig(**dict(CFG, model=model.replace("+a2a", ""), device="cuda:0")))
+    ref = LLMEngine(EngineConfig(**dict(CFG, model=model.replace("+a2a", "").replace("+overlap", ""),
+                                        device="cuda:0")))
     sp = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
     want_outs, want = _capture_logits(ref, _prompts(ref.model_cfg.vocab_size), sp)
     # first step (prefill of all prompts, identical batches): the TP=2 logits equal TP=1 up to bf16 reduction order
