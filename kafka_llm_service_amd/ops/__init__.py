@@ -245,6 +245,44 @@ def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, 
     return mt, kc, s
 
 
+SKINNY_MIN_M, SKINNY_MAX_M = 129, 256
+
+
+def skinny_plan(M: int, N: int, K: int, max_splits: int = 8) -> int:
+    """Splits of the skinny GEMM (csrc/skinny_gemm.hip kafka_skinny_plan, mirrored for CPU runs); 0 = unsupported."""
+    if M < SKINNY_MIN_M or M > SKINNY_MAX_M or N % 128 or K % 64:
+        return 0
+    nx, s = N // 128, 1
+    while s * 2 <= max_splits and nx * s < 192 and K % (64 * s * 2) == 0 and K // (s * 2) >= 256:
+        s *= 2
+    return s
+
+
+def linear_skinny(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, glu: bool = False) -> torch.Tensor:
+    """y = x @ W^T for 129..256 rows from the wave-tiled weight (mixed decode + prefill steps): bf16 [M, N] (or the
+    activated [M, N/2] with ``glu``) for one split, else fp32 split-K slabs [S, M, N] in gate | up order for glu."""
+    M, K = x.shape
+    N = wt.shape[0] * 32
+    S = skinny_plan(M, N, K, max_splits)
+    if S == 0:
+        raise ValueError(f"linear_skinny: unsupported shape M={M} N={N} K={K}")
+    if _gpu(x):
+        if S == 1:
+            y = torch.empty(M, N // 2 if glu else N, dtype=x.dtype, device=x.device)
+            ext().skinny_gemm(x, wt, y, None, 1, bool(glu))
+            return y
+        p = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+        ext().skinny_gemm(x, wt, None, p, int(S), bool(glu))
+        return p
+    w = untile_weight(wt, glu).float()
+    y = x.float() @ w.t()
+    if S == 1:
+        return (ref.silu_mul(y) if glu else y).to(x.dtype)
+    p = torch.zeros(S, M, N, dtype=torch.float32)
+    p[0] = y
+    return p
+
+
 def linear_stream(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, nt: bool = True,
                   glu: bool = False) -> torch.Tensor:
     """y = x @ W^T for decode-sized M (<= 128) from the wave-tiled weight ``wt``: the weight-streaming MFMA kernel.

@@ -76,6 +76,9 @@ hipError_t kafka_launch_ep_recv_route(const bf16* img, int ep, int C, int MR, in
                                       float* perm_w, int* expert_off, int* tile_off, hipStream_t st);
 hipError_t kafka_launch_ep_combine(const bf16* back, const int* slot_map, const float* topk_w, int lo, int n_own,
                                    int k, int d, bf16* out, int64_t ldo, hipStream_t st);
+int kafka_skinny_plan(int M, int N, int K, int max_splits, int* splits);
+hipError_t kafka_launch_skinny_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int splits,
+                                    int glu, bf16* Y, int64_t ldy, float* P, hipStream_t st);
 hipError_t kafka_launch_car_allreduce_add_rmsnorm(char* const* bases, int nranks, int rank, const bf16* x,
                                                   const float* xp, int S, int64_t ps, int T, int d, bf16* resid,
                                                   int64_t rs, const bf16* w, float eps, bf16* out, int64_t os,
@@ -410,6 +413,42 @@ static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> 
                                       yp, ldy, pp, cur_stream()));
 }
 
+// Skinny MFMA GEMM (csrc/skinny_gemm.hip) for 129..256 rows on the wave-tiled weights: y bf16 for one split
+// ([M, N/2] activated with glu), else fp32 slabs p [splits, M, N]
+static int64_t skinny_plan(int64_t M, int64_t N, int64_t K, int64_t max_splits) {
+  int s = 0;
+  return kafka_skinny_plan((int)M, (int)N, (int)K, (int)max_splits, &s) == 0 ? s : 0;
+}
+
+static void skinny_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y, c10::optional<at::Tensor> p,
+                        int64_t splits, bool glu) {
+  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
+  TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0, "skinny_gemm: x must be [M, K] with 16-B rows");
+  TORCH_CHECK(wt.dim() == 4 && wt.is_contiguous() && wt.size(2) == 64 && wt.size(3) == 8,
+              "skinny_gemm: wt must be contiguous [N/32, K/16, 64, 8]");
+  const int M = x.size(0), K = x.size(1), N = wt.size(0) * 32;
+  TORCH_CHECK(wt.size(1) * 16 == K && M > 0 && M <= 256 && N % 128 == 0 && K % (64 * splits) == 0,
+              "skinny_gemm: shape");
+  bf16* yp = nullptr;
+  int64_t ldy = 0;
+  float* pp = nullptr;
+  if (splits == 1) {
+    TORCH_CHECK(y.has_value(), "skinny_gemm: y required for one split");
+    CHECK_DT(y.value(), at::kBFloat16); CHECK_LASTDIM(y.value());
+    TORCH_CHECK(y->dim() == 2 && y->size(0) == M && y->size(1) == (glu ? N / 2 : N), "skinny_gemm: y shape");
+    yp = bptr(y.value());
+    ldy = y->stride(0);
+  } else {
+    TORCH_CHECK(p.has_value(), "skinny_gemm: slab output required");
+    CHECK_DT(p.value(), at::kFloat);
+    TORCH_CHECK(p->is_contiguous() && p->dim() == 3 && p->size(0) == splits && p->size(1) == M && p->size(2) == N,
+                "skinny_gemm: slab shape must be [splits, M, N]");
+    pp = p->data_ptr<float>();
+  }
+  CHECK_HIP(kafka_launch_skinny_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, (int)splits, glu ? 1 : 0, yp, ldy, pp,
+                                     cur_stream()));
+}
+
 // QKV projection on the streaming kernel with RoPE + the paged KV write in its epilogue (bf16 cache, head dim 128):
 // replaces wstream_gemm + rope_kv_write on decode-sized steps. p: fp32 scratch [splits, M, N] when the plan splits K.
 static void wstream_qkv_rope(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> p, at::Tensor positions,
@@ -741,6 +780,8 @@ PYBIND11_MODULE(_kafka_ops, m) {
         py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none(), py::arg("nsplit") = 1);
   m.def("wstream_plan", &wstream_plan);
   m.def("wstream_gemm", &wstream_gemm);
+  m.def("skinny_plan", &skinny_plan);
+  m.def("skinny_gemm", &skinny_gemm);
   m.def("wstream_qkv_rope", &wstream_qkv_rope);
   m.def("wstream_gemm_cfg", &wstream_gemm_cfg);
   m.def("slab_reduce", &slab_reduce);

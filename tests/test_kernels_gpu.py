@@ -644,3 +644,29 @@ def test_ep_dispatch_route_combine_match_reference(cuda, T, ep, E, k):
         ref_out = torch.zeros(Tl, d, dtype=torch.bfloat16)
         ops.ep_combine(back.cpu(), slots[q].cpu(), r.topk_w.cpu(), lo, hi - lo, ref_out)
         torch.testing.assert_close(out.cpu().float(), ref_out.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [130, 168, 200, 256])
+@pytest.mark.parametrize("shape", [("qkv", 6144, 4096, False), ("o", 4096, 4096, False),
+                                   ("gate_up", 2 * 14336, 4096, True), ("down", 4096, 14336, False)],
+                         ids=lambda s: s[0] if isinstance(s, tuple) else str(s))
+def test_skinny_gemm_matches_fp32(cuda, M, shape):
+    """csrc/skinny_gemm.hip (129..256 rows, LDS-DMA ring, 2x2 MFMA tiles per wave) == fp32 X . W^T on the
+    Llama-3-8B projection shapes, split-K slabs summed; gate_up with the fused SwiGLU epilogue."""
+    from kafka_llm_service_amd import ops
+    from kafka_llm_service_amd.ops import reference as ref
+
+    _, N, K, glu = shape
+    torch.manual_seed(M + N)
+    x = (torch.randn(M, K, device="cuda") * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
+    wt = ops.tile_weight(w, glu=glu)
+    y = ops.linear_skinny(x, wt, glu=glu)
+    want = x.float() @ w.float().t()
+    if glu:
+        want = ref.silu_mul(want)
+        if ops.is_slab(y):
+            y = ref.silu_mul(y.sum(0))
+    elif ops.is_slab(y):
+        y = y.sum(0)
+    torch.testing.assert_close(y.float(), want, atol=2e-2, rtol=2e-2)
