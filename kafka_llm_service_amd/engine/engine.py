@@ -187,8 +187,10 @@ class LLMEngine:
         self.runner = ModelRunner(self.model, kc, vc, self.kvm, cfg.max_num_seqs, max_blocks,
                                   cascade_min_prefix=cfg.cascade_min_prefix, use_cascade=cfg.use_cascade,
                                   target_wgs=cfg.target_wgs, prefill_kv_chunk=cfg.prefill_kv_chunk)
-        if cfg.use_graphs is None:
-            cfg.use_graphs = cfg.tp > 1 and self.device.type == "cuda"
+        if cfg.use_graphs is None:  # env KAFKA_GRAPHS=0/1 overrides the default (on for TP > 1 on GPUs)
+            env = os.environ.get("KAFKA_GRAPHS")
+            cfg.use_graphs = (env == "1") if env in ("0", "1") else (cfg.tp > 1 and self.device.type == "cuda")
+            cfg.use_graphs = cfg.use_graphs and self.device.type == "cuda"
         if cfg.use_graphs:
             from kafka_llm_service_amd.engine.graphs import DecodeGraphs
 

@@ -6,8 +6,9 @@ Per layer (SURVEY.md §3.2 "Target equivalent"):
     -> fused_add_rmsnorm -> gate_up GEMM (column-parallel) -> silu_mul (HIP) -> down GEMM (row-parallel)
     -> [TP all-reduce]                                     (Mixtral: router -> expert MLPs, models/moe.py)
 Decode-sized steps (T <= 128) run every projection on the weight-streaming MFMA kernel (``ops/csrc/wstream_gemm.hip``,
-wave-tiled weight copies, SwiGLU fused into gate_up; the grouped variant for Mixtral's experts); prefill-sized steps
-use hipBLASLt through ``torch.nn.functional.linear`` (bf16, fp32 accumulate). Norm / RoPE / attention / sampling run
+wave-tiled weight copies, SwiGLU fused into gate_up; the grouped variant for Mixtral's experts); 129..256-row mixed
+steps run qkv / o / down on the skinny MFMA GEMM (``ops/csrc/skinny_gemm.hip``, SKINNY below); other prefill-sized
+steps use hipBLASLt through ``torch.nn.functional.linear`` (bf16, fp32 accumulate). Norm / RoPE / attention / sampling run
 in the hand-written kernels of ``ops/csrc``.
 
 Weights are stored HF-style ``[out, in]`` so safetensors checkpoints load without transposes; random init (seeded,
@@ -40,6 +41,13 @@ FUSE_QKV_ROPE = os.environ.get("KAFKA_FUSE_QKV_ROPE", "0") == "1"
 # are those of the one-shot all-reduce. Captured hipGraphs record the fork/join. Off by default: the gain needs
 # TP over xGMI to measure (ranks sharing one GPU overlap nothing), and the seam loses its fused AR + RMSNorm launch.
 TP_OVERLAP = os.environ.get("KAFKA_TP_OVERLAP", "0") == "1"
+
+# Projections of 129..256-row steps (decode + a new turn's prefill) that run on the skinny MFMA GEMM
+# (ops.linear_skinny, csrc/skinny_gemm.hip) instead of hipBLASLt: env KAFKA_SKINNY, a comma list of qkv / o / down
+# ("" = none; "+" also separates). gate_up stays on hipBLASLt (faster there). Same-box A/B, 2 interleaved rounds:
+# 7,857 (none) -> 7,924 tok/s (o+down or all three), profiles/r03/skinny_gemm/bench_ab_wired.jsonl.
+SKINNY = frozenset(p for p in os.environ.get("KAFKA_SKINNY", "qkv,o,down").replace("+", ",").split(",")
+                   if p in ("qkv", "o", "down"))
 _OVL: dict = {}
 _SEAM_DONE = object()  # forward(): the previous layer's overlapped seam already produced this layer's input
 
@@ -184,10 +192,16 @@ class TransformerLM:
             torch.cuda.empty_cache()
         return added
 
-    def _linear(self, x: torch.Tensor, w: torch.Tensor, wt: torch.Tensor | None, max_splits: int = 8):
-        """x @ w^T: the weight-streaming kernel for decode-sized x (bf16 or a split-K slab out), else hipBLASLt."""
-        if self.stream and wt is not None and 0 < x.shape[0] <= self.stream_max_m:
-            return ops.linear_stream(x, wt, max_splits)
+    def _linear(self, x: torch.Tensor, w: torch.Tensor, wt: torch.Tensor | None, max_splits: int = 8,
+                kind: str = ""):
+        """x @ w^T: the weight-streaming kernel for decode-sized x (bf16 or a split-K slab out), the skinny MFMA GEMM
+        for 129..256 rows of the projections in SKINNY, else hipBLASLt."""
+        M = x.shape[0]
+        if self.stream and wt is not None:
+            if 0 < M <= self.stream_max_m:
+                return ops.linear_stream(x, wt, max_splits)
+            if kind in SKINNY and ops.skinny_plan(M, wt.shape[0] * 32, x.shape[1], max_splits):
+                return ops.linear_skinny(x, wt, max_splits)
         return F.linear(x, self._dense(w, wt))
 
     @staticmethod
@@ -230,14 +244,14 @@ class TransformerLM:
                 ops.linear_stream_rope(x, lw.qkv_t, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i],
                                        inp.slot_mapping, self.hq, self.hkv)
             else:
-                qkv = self._linear(x, lw.qkv, lw.qkv_t)
+                qkv = self._linear(x, lw.qkv, lw.qkv_t, kind="qkv")
                 ops.rope_kv_write(qkv, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i], inp.slot_mapping,
                                   self.hq, self.hkv)
             paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out)
             if tp and self._can_overlap(T, lw.o_t):
                 self._overlapped_seam(attn_out.view(T, -1), lw.o_t, residual, lw.post_norm, eps, x)
             else:
-                o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t)
+                o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t, kind="o")
                 if tp:
                     pstate.tp_all_reduce_add_rmsnorm(o, residual, lw.post_norm, eps, out=x)
                 else:
@@ -255,7 +269,7 @@ class TransformerLM:
                     self._overlapped_seam(a, lw.down_t, residual, self.layers[i + 1].input_norm, eps, x)
                     delta, pending = _SEAM_DONE, False
                 else:
-                    delta = self._linear(a, lw.down, lw.down_t)
+                    delta = self._linear(a, lw.down, lw.down_t, kind="down")
                     pending = tp
         if pending:
             delta = pstate.tp_all_reduce(delta)

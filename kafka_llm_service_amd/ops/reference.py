@@ -225,11 +225,12 @@ def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_pa
     G = Hq // Hkv
     S_total = out_part.shape[2]
     lp = lse_part.view(out_part.shape[0], Hq, S_total)
-    nparts = {}
+    nparts, npres = {}, {}
     for b, lo, hi, split, nsplit, npre in (it[:6] for it in items.tolist()):
         if not (0 <= b < B and 0 <= split < nsplit and npre >= 0 and npre + nsplit <= S_total):
             continue  # padding / malformed item: dropped, as by the kernel
         nparts[b] = npre + nsplit
+        npres[b] = npre
         o = torch.zeros(Hq, D, dtype=torch.float32, device=q.device)
         l2 = torch.full((Hq,), float("-inf"), dtype=torch.float32, device=q.device)
         if hi > lo:
@@ -243,11 +244,10 @@ def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_pa
         out_part[b, :, npre + split] = o
         lp[b, :, npre + split] = l2
     if out is not None:
-        npre = {int(it[0]): int(it[5]) for it in items.tolist()}
         for b, n in nparts.items():
             parts = out_part[b:b + 1, :, :n].clone()
             if pre_part is not None:
-                parts[:, :, :npre[b]] = pre_part[b:b + 1, :, :npre[b]].float()
+                parts[:, :, :npres[b]] = pre_part[b:b + 1, :, :npres[b]].float()
             attn_merge(parts.contiguous(), lp[b:b + 1, :, :n].contiguous(), out[b:b + 1])
 
 

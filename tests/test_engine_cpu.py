@@ -396,6 +396,28 @@ def test_padded_mixed_steps_match_unpadded(base_engine):
     assert 168 in seen
 
 
+def test_skinny_projections_match_blas(monkeypatch):
+    """KAFKA_SKINNY: the qkv / o / down projections of 129..256-row steps on the skinny GEMM path (its split-K slabs
+    consumed by rope / add+RMSNorm like the decode GEMM's) give the same greedy tokens as the dense path."""
+    from kafka_llm_service_amd.models import llama
+
+    prompts = _prompts(seed=23, shared=100, tails=(50,))  # first step: one 150-row prefill
+    e0 = _engine(decode_gemm="stream")
+    monkeypatch.setattr(llama, "SKINNY", frozenset())
+    ref = e0.generate(prompts, GREEDY)
+    monkeypatch.setattr(llama, "SKINNY", frozenset({"qkv", "o", "down"}))
+    calls = []
+    orig = ops.linear_skinny
+
+    def spy(x, wt, *a, **k):
+        calls.append(x.shape[0])
+        return orig(x, wt, *a, **k)
+    monkeypatch.setattr(ops, "linear_skinny", spy)
+    e1 = _engine(decode_gemm="stream", model=e0.model)
+    assert e1.generate(prompts, GREEDY) == ref
+    assert calls and all(129 <= m <= 256 for m in calls) and len(calls) % 3 == 0
+
+
 def test_bf16_cascade_partials_close_to_fp32(base_engine, monkeypatch):
     """The tile-v3 cascade hands its prefix partials to the decode kernel as bf16 by default (half the bytes):
     decode-step logits stay within bf16 rounding of the fp32-partial path."""
