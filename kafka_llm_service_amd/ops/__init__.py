@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
 import torch
 
 from . import reference as ref
@@ -118,6 +119,90 @@ def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_pa
                           pre_part)
         return
     ref.attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale, out, pre_part)
+
+
+DECODE_SK_WGS = 512      # stream-K decode grid: two 4-wave workgroups per CU (the kernel's occupancy)
+DECODE_SK_F = int(os.environ.get("KAFKA_DECODE_SK_F", "4"))  # fixed cost of a piece, in 32-key blocks
+DECODE_SK_MAX_PARTIALS = 64
+
+
+def decode_sk_plan(seq_lens: np.ndarray, kv_start: np.ndarray, npre: np.ndarray, hkv: int,
+                   nwg: int = DECODE_SK_WGS, F: int = DECODE_SK_F) -> tuple[np.ndarray, np.ndarray, int]:
+    """Host plan of the stream-K decode kernel (csrc/attention.hip attn_decode_sk_kernel). Units (row b, kv head)
+    lie end to end on one cost line, unit (b, h) = F overhead blocks + nb_b 32-key blocks; workgroup w takes the
+    slice [w T, (w + 1) T). Returns (rows int32 [B + 1, 4] = (kv_lo, kv_hi, npre, C_b) + plan row (T, F, total, 0),
+    start int32 [nwg, 2] = first (row, kv head) per slice (row B: empty slice), partial slots per row)."""
+    lens = np.asarray(seq_lens, dtype=np.int64)
+    lo = np.asarray(kv_start, dtype=np.int64)
+    npre = np.asarray(npre, dtype=np.int64)
+    B = lens.shape[0]
+    a0 = lo - lo % 32
+    nb = np.where(lens > lo, (lens - a0 + 31) // 32, 0)
+    ucost = F + nb
+    rcost = hkv * ucost
+    C = np.zeros(B, dtype=np.int64)
+    if B > 1:
+        C[1:] = np.cumsum(rcost)[:-1]
+    total = int(rcost.sum())
+    # fewest blocks per slice that keep every unit within the fused merge's partial slots
+    room = max(1, DECODE_SK_MAX_PARTIALS - int(npre.max(initial=0)) - 1)
+    T = max(1, -(-total // nwg), -(-int(nb.max(initial=0)) // room))
+    s = np.arange(nwg, dtype=np.int64) * T
+    b = np.clip(np.searchsorted(C, s, side="right") - 1, 0, max(B - 1, 0))
+    kvh = np.minimum((s - C[b]) // np.maximum(ucost[b], 1), hkv - 1)
+    empty = s >= total
+    start = np.stack([np.where(empty, B, b), np.where(empty, 0, kvh)], 1).astype(np.int32)
+    rows = np.zeros((B + 1, 4), dtype=np.int32)
+    rows[:B, 0], rows[:B, 1], rows[:B, 2], rows[:B, 3] = lo, lens, npre, C
+    rows[B] = (T, F, total, 0)
+    # pieces per unit: slices its block range [C_u + F, C_u + F + nb) touches (same for every head of a row up to
+    # the offset; take the max over heads)
+    h = np.arange(hkv, dtype=np.int64)
+    bs = C[:, None] + h[None, :] * ucost[:, None] + F
+    pieces = np.where(nb[:, None] > 0, (bs + nb[:, None] - 1) // T - bs // T + 1, 1).max(1) if B else np.zeros(0)
+    s_total = int((npre + pieces).max(initial=1))
+    return rows, start, s_total
+
+
+def decode_sk_items(rows: np.ndarray, start: np.ndarray, hkv: int) -> list[tuple[int, int, int, int, int, int, int]]:
+    """The pieces a stream-K launch runs, as (b, kvh, lo, hi, split, nsplit, npre) — the kernel's walk mirrored on
+    the host (CPU reference path and tests)."""
+    B = rows.shape[0] - 1
+    T, F, total = int(rows[B, 0]), int(rows[B, 1]), int(rows[B, 2])
+    out = []
+    for w in range(start.shape[0]):
+        s0, e0 = w * T, min(w * T + T, total)
+        b, kvh = int(start[w, 0]), int(start[w, 1])
+        while b < B:
+            lo_b, hi_b, npre, c_b = (int(x) for x in rows[b])
+            a0 = lo_b & ~31
+            nb = (hi_b - a0 + 31) >> 5 if hi_b > lo_b else 0
+            cu = c_b + kvh * (F + nb)
+            if cu >= e0:
+                break
+            bs = cu + F
+            j0, j1 = max(s0, bs) - bs, min(e0, bs + nb) - bs
+            if j1 > j0 and nb > 0:
+                first, last = bs // T, (bs + nb - 1) // T
+                lo, hi = max(lo_b, a0 + 32 * j0), min(hi_b, a0 + 32 * j1)
+                out.append((b, kvh, lo, hi, w - first, last - first + 1, npre))
+            kvh += 1
+            if kvh == hkv:
+                kvh, b = 0, b + 1
+    return out
+
+
+def attn_decode_sk(q, k_cache, v_cache, block_tables, rows, start, out_part, lse_part, scale: float, out=None,
+                   pre_part=None) -> None:
+    """Stream-K paged decode (``decode_sk_plan``): every workgroup streams the same number of KV blocks; pieces write
+    partials at slot npre + split, whole units (or the last piece of a split one, by ticket) merge with the prefix
+    partials into ``out`` (see ``attn_decode_items`` for ``out`` / ``pre_part``)."""
+    if _gpu(q):
+        tk = _tickets(q.device, q.shape[0] * k_cache.shape[1]) if out is not None else None
+        ext().attn_decode_sk(q, k_cache, v_cache, block_tables, rows, start, out_part, lse_part, float(scale), out,
+                             tk, pre_part)
+        return
+    ref.attn_decode_sk(q, k_cache, v_cache, block_tables, rows, start, out_part, lse_part, scale, out, pre_part)
 
 
 def uniform_decode_items(seq_lens: torch.Tensor, kv_start: torch.Tensor | None, num_splits: int,

@@ -318,32 +318,36 @@ struct DecodeItem {
   int b, lo, hi, split, nsplit, npre, pad0, pad1;
 };
 
-template <int D, bool HEADS_FAST, bool FP8, int MG = 16>
-__global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
-                                                           const void* __restrict__ k_cache,
-                                                           const void* __restrict__ v_cache, int Hkv, int G,
-                                                           const int* __restrict__ block_tables, int bt_stride,
-                                                           const DecodeItem* __restrict__ items, int B,
-                                                           float* __restrict__ out_part, float* __restrict__ lse_part,
-                                                           int S_total, float scale_log2,
-                                                           bf16* __restrict__ out, int64_t out_stride,
-                                                           int* __restrict__ tickets,
-                                                           const bf16* __restrict__ pre_bf16) {
-  __shared__ float sO[4][8][D];
-  __shared__ float sM[4][8];
-  __shared__ float sL[4][8];
-  // HEADS_FAST: consecutive workgroups are the Hkv heads of one item (grid (Hkv, items)), else the items of one
-  // head (grid (items, Hkv)) — a placement choice only (which XCD's L2 sees which pages)
-  const DecodeItem it = items[HEADS_FAST ? blockIdx.y : blockIdx.x];
-  const int b = it.b, kvh = HEADS_FAST ? blockIdx.x : blockIdx.y, split = it.split, S = it.nsplit, split_offset = it.npre;
-  // a malformed item (host bug) is dropped instead of indexing out of bounds (workgroup-uniform)
-  if (b < 0 || b >= B || split < 0 || split >= S || split_offset < 0 || split_offset + S > S_total ||
-      (out != nullptr && split_offset + S > 64))
-    return;
+// LDS of one decode piece (4 waves' partial results + the fused merge's per-split weights)
+template <int D>
+struct DecodeSmem {
+  float sO[4][8][D];
+  float sM[4][8];
+  float sL[4][8];
+  float sW[8][65];
+  float sWt[8];
+  int s_last;
+};
+
+// One decode piece: keys [lo, hi) of row b, kv head kvh, piece `split` of S, partial slots from split_offset. Every
+// thread of the workgroup calls it with the same arguments (it synchronises the workgroup); returns when the
+// piece's partial or final rows are written.
+template <int D, bool FP8, int MG>
+__device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __restrict__ q, int64_t q_stride,
+                                             const void* __restrict__ k_cache, const void* __restrict__ v_cache,
+                                             int Hkv, int G, const int* __restrict__ block_tables, int bt_stride,
+                                             int b, int kvh, int lo, int hi, int split, int S, int split_offset,
+                                             float* __restrict__ out_part, float* __restrict__ lse_part, int S_total,
+                                             float scale_log2, bf16* __restrict__ out, int64_t out_stride,
+                                             int* __restrict__ tickets, const bf16* __restrict__ pre_bf16) {
+  auto& sO = sm.sO;
+  auto& sM = sm.sM;
+  auto& sL = sm.sL;
+  auto& sW = sm.sW;
+  auto& sWt = sm.sWt;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int Hq = Hkv * G;
-  const int lo = it.lo, hi = it.hi;
   const int a0 = lo & ~31;
   const int nb = hi > lo ? (hi - a0 + 31) >> 5 : 0;
   const int* bt = block_tables + (int64_t)b * bt_stride;
@@ -372,8 +376,6 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
     }
   }
   __syncthreads();
-  __shared__ float sW[8][65];
-  __shared__ float sWt[8];
   if (out != nullptr && S == 1) {
     // Fused merge (one split per sequence): fold in the cascade-prefix partials [0, split_offset) written earlier
     // on the stream and write the final bf16 rows — no merge kernel, no partial round trip of this split.
@@ -488,17 +490,16 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
   // would write back the whole L2 from every workgroup), waits for them, takes a ticket, and the LAST of the S
   // workgroups of (b, kvh) merges all split_offset + S partials (agent-coherent loads) and writes the bf16 rows —
   // no merge kernel launch. The last one also re-arms the counter for the next launch.
-  __shared__ int s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     int* tk = tickets + b * Hkv + kvh;
     const int t = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = t == S - 1;
+    sm.s_last = t == S - 1;
     if (t == S - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  if (!s_last) return;
+  if (!sm.s_last) return;
   auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   // 16-B agent-coherent loads (sc1: not served from this XCD's possibly stale L2); inline asm, so the group below
   // waits for them itself
@@ -549,6 +550,93 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
 #pragma unroll
     for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc4[j] * inv);
     *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
+  }
+}
+
+template <int D, bool HEADS_FAST, bool FP8, int MG = 16>
+__global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
+                                                           const void* __restrict__ k_cache,
+                                                           const void* __restrict__ v_cache, int Hkv, int G,
+                                                           const int* __restrict__ block_tables, int bt_stride,
+                                                           const DecodeItem* __restrict__ items, int B,
+                                                           float* __restrict__ out_part, float* __restrict__ lse_part,
+                                                           int S_total, float scale_log2,
+                                                           bf16* __restrict__ out, int64_t out_stride,
+                                                           int* __restrict__ tickets,
+                                                           const bf16* __restrict__ pre_bf16) {
+  __shared__ DecodeSmem<D> sm;
+  // HEADS_FAST: consecutive workgroups are the Hkv heads of one item (grid (Hkv, items)), else the items of one
+  // head (grid (items, Hkv)) — a placement choice only (which XCD's L2 sees which pages)
+  const DecodeItem it = items[HEADS_FAST ? blockIdx.y : blockIdx.x];
+  const int b = it.b, kvh = HEADS_FAST ? blockIdx.x : blockIdx.y, split = it.split, S = it.nsplit, split_offset = it.npre;
+  // a malformed item (host bug) is dropped instead of indexing out of bounds (workgroup-uniform)
+  if (b < 0 || b >= B || split < 0 || split >= S || split_offset < 0 || split_offset + S > S_total ||
+      (out != nullptr && split_offset + S > 64))
+    return;
+  decode_piece<D, FP8, MG>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, it.lo, it.hi,
+                           split, S, split_offset, out_part, lse_part, S_total, scale_log2, out, out_stride, tickets,
+                           pre_bf16);
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// Stream-K decode: the (row, kv head) units of a step laid end to end in one cost line — unit (b, kvh) occupies
+// [C_b + kvh (F + nb_b), + F + nb_b): F overhead blocks (its fixed cost: item / page-table / first-block latency,
+// combine, merge) then nb_b 32-key blocks — and workgroup w takes the equal slice [w T, (w + 1) T) of it. A unit
+// whose blocks cross slice boundaries is split into pieces (partials + ticket merge, as a split item); a unit inside
+// one slice merges directly. Every workgroup does the same cost: no second round of long pieces after the first
+// (the item plan's 2-round tail), and short histories are packed several to a workgroup.
+//   rows:  int32 [B + 1, 4]  (kv_lo, kv_hi, npre, C_b) per row, then the plan (T, F, total, 0) — device data, so a
+//          captured graph replays any step of the same batch size
+//   start: int32 [nwg, 2] (first row b, first kv head) of each slice (host: searchsorted over C_b; b = B: empty)
+
+template <int D, bool FP8, int MG = 32>
+__global__ __launch_bounds__(256, 2) void attn_decode_sk_kernel(const bf16* __restrict__ q, int64_t q_stride,
+                                                              const void* __restrict__ k_cache,
+                                                              const void* __restrict__ v_cache, int Hkv, int G,
+                                                              const int* __restrict__ block_tables, int bt_stride,
+                                                              const int4* __restrict__ rows,
+                                                              const int2* __restrict__ start, int B,
+                                                              float* __restrict__ out_part,
+                                                              float* __restrict__ lse_part, int S_total,
+                                                              float scale_log2, bf16* __restrict__ out,
+                                                              int64_t out_stride, int* __restrict__ tickets,
+                                                              const bf16* __restrict__ pre_bf16) {
+  __shared__ DecodeSmem<D> sm;
+  const int w = blockIdx.x;
+  const int4 pl = rows[B];
+  const int T = __builtin_amdgcn_readfirstlane(pl.x), F = __builtin_amdgcn_readfirstlane(pl.y);
+  const int total = __builtin_amdgcn_readfirstlane(pl.z);
+  if (T < 1 || F < 0) return;
+  const int s0 = w * T, e0 = min(s0 + T, total);
+  const int2 st = start[w];
+  int b = __builtin_amdgcn_readfirstlane(st.x), kvh = __builtin_amdgcn_readfirstlane(st.y);
+  if (b < 0 || b >= B || kvh < 0 || kvh >= Hkv) return;
+  // pieces of this slice (all values workgroup-uniform; every thread walks the same units)
+  for (int guard = 0; guard < 4096 && b < B; ++guard) {
+    const int4 rw = rows[b];
+    const int lo_b = __builtin_amdgcn_readfirstlane(rw.x), hi_b = __builtin_amdgcn_readfirstlane(rw.y);
+    const int npre = __builtin_amdgcn_readfirstlane(rw.z), c_b = __builtin_amdgcn_readfirstlane(rw.w);
+    const int a0 = lo_b & ~31;
+    const int nb = hi_b > lo_b ? (hi_b - a0 + 31) >> 5 : 0;
+    const int cu = c_b + kvh * (F + nb);  // cost start of unit (b, kvh)
+    if (cu >= e0) break;
+    const int bs = cu + F;  // first block's cost coordinate
+    const int j0 = max(s0, bs) - bs, j1 = min(e0, bs + nb) - bs;
+    if (j1 > j0 && nb > 0) {
+      const int first = bs / T, last = (bs + nb - 1) / T;
+      const int split = w - first, S = last - first + 1;
+      if (split >= 0 && split < S && npre >= 0 && npre + S <= S_total && !(out != nullptr && npre + S > 64)) {
+        const int lo = max(lo_b, a0 + 32 * j0), hi = min(hi_b, a0 + 32 * j1);
+        decode_piece<D, FP8, MG>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, lo, hi,
+                                 split, S, npre, out_part, lse_part, S_total, scale_log2, out, out_stride, tickets,
+                                 pre_bf16);
+        __syncthreads();  // the next piece reuses the LDS
+      }
+    }
+    if (++kvh == Hkv) {
+      kvh = 0;
+      ++b;
+    }
   }
 }
 
@@ -1052,6 +1140,30 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
     go(attn_decode_kernel<128, true, false, 32>, hf);
   else
     go(attn_decode_kernel<128, true, false, 16>, hf);
+  return hipGetLastError();
+}
+
+// Stream-K decode (attn_decode_sk_kernel): rows int32 [B + 1, 4] (the last row = plan), start int32 [nwg, 2].
+extern "C" hipError_t kafka_launch_attn_decode_sk(const bf16* q, int64_t q_stride, const void* k_cache,
+                                                 const void* v_cache, int fp8, int B, int Hkv, int G, int D,
+                                                 const int* block_tables, int bt_stride, const int* rows,
+                                                 const int* start, int nwg, float* out_part, float* lse_part,
+                                                 int S_total, float scale, bf16* out, int64_t out_stride,
+                                                 int* tickets, const bf16* pre_bf16, hipStream_t st) {
+  if (nwg == 0 || B == 0) return hipSuccess;
+  if (D != 128 || G > 8 || G < 1) return hipErrorInvalidValue;
+  if (out != nullptr && tickets == nullptr) return hipErrorInvalidValue;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  const auto* rw = reinterpret_cast<const int4*>(rows);
+  const auto* sp = reinterpret_cast<const int2*>(start);
+  if (fp8)
+    attn_decode_sk_kernel<128, true><<<nwg, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables,
+                                                          bt_stride, rw, sp, B, out_part, lse_part, S_total,
+                                                          scale_log2, out, out_stride, tickets, pre_bf16);
+  else
+    attn_decode_sk_kernel<128, false><<<nwg, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables,
+                                                           bt_stride, rw, sp, B, out_part, lse_part, S_total,
+                                                           scale_log2, out, out_stride, tickets, pre_bf16);
   return hipGetLastError();
 }
 

@@ -29,6 +29,11 @@ hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const void*
                                     const int* items, float* out_part, float* lse_part, int S_total, float scale,
                                     bf16* out, int64_t out_stride, int* tickets, const bf16* pre_bf16,
                                     hipStream_t st);
+hipError_t kafka_launch_attn_decode_sk(const bf16* q, int64_t q_stride, const void* k_cache, const void* v_cache,
+                                       int fp8, int B, int Hkv, int G, int D, const int* block_tables, int bt_stride,
+                                       const int* rows, const int* start, int nwg, float* out_part,
+                                       float* lse_part, int S_total, float scale, bf16* out, int64_t out_stride,
+                                       int* tickets, const bf16* pre_bf16, hipStream_t st);
 hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride,
                                      const void* k_cache, const void* v_cache, int fp8, int Hkv, int G, int D,
                                      const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
@@ -272,6 +277,57 @@ static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at
                                       Hq / Hkv, 128, block_tables.data_ptr<int>(), block_tables.stride(0),
                                       items.data_ptr<int>(), out_part.data_ptr<float>(), lse_part.data_ptr<float>(),
                                       S_total, scale, op, ostride, tp, pre, cur_stream()));
+}
+
+// Stream-K decode: rows int32 [B + 1, 4] (kv_lo, kv_hi, npre, cost start; last row = plan (T, F, total, 0)), start
+// int32 [nwg, 2] (first row, kv head of each workgroup's slice) — see attention.hip attn_decode_sk_kernel. Row /
+// slot values are device data; the kernel drops a piece whose row or slots fall outside the checked shapes.
+static void attn_decode_sk(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
+                           at::Tensor rows, at::Tensor start, at::Tensor out_part, at::Tensor lse_part, double scale, c10::optional<at::Tensor> out,
+                           c10::optional<at::Tensor> tickets, c10::optional<at::Tensor> pre_part) {
+  CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
+  CHECK_DT(block_tables, at::kInt); CHECK_DT(rows, at::kInt); CHECK_DT(start, at::kInt);
+  CHECK_DT(out_part, at::kFloat); CHECK_DT(lse_part, at::kFloat);
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == 128 && q.size(2) == 128, "q must be [B, Hq, 128]");
+  const int B = q.size(0), Hq = q.size(1), Hkv = k_cache.size(1);
+  TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 8, "decode kernel needs Hq/Hkv <= 8");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.stride(1) == 1, "block_tables");
+  TORCH_CHECK(rows.is_cuda() && rows.is_contiguous() && rows.dim() == 2 && rows.size(0) == B + 1 &&
+                  rows.size(1) == 4, "rows must be a device int32 [B + 1, 4]");
+  TORCH_CHECK(start.is_cuda() && start.is_contiguous() && start.dim() == 2 && start.size(1) == 2 &&
+                  start.size(0) <= 65535, "start must be a device int32 [nwg, 2]");
+  const int nwg = start.size(0);
+  TORCH_CHECK(out_part.is_contiguous() && out_part.dim() == 4 && out_part.size(0) >= B && out_part.size(1) == Hq &&
+                  out_part.size(3) == 128, "out_part must be [B, Hq, S_total, 128]");
+  const int S_total = out_part.size(2);
+  TORCH_CHECK(lse_part.is_contiguous() && lse_part.numel() >= (int64_t)B * Hq * S_total, "lse_part");
+  bf16* op = nullptr;
+  int64_t ostride = 0;
+  int* tp = nullptr;
+  if (out.has_value()) {
+    CHECK_DT(out.value(), at::kBFloat16);
+    TORCH_CHECK(out->dim() == 3 && out->size(0) >= B && out->size(1) == Hq && out->size(2) == 128 &&
+                    out->stride(2) == 1 && out->stride(1) == 128,
+                "attn_decode_sk: fused-merge out must be [B, Hq, 128]");
+    op = bptr(out.value());
+    ostride = out->stride(0);
+    TORCH_CHECK(tickets.has_value() && tickets->is_cuda() && tickets->scalar_type() == at::kInt &&
+                    tickets->numel() >= (int64_t)B * Hkv,
+                "attn_decode_sk: the fused merge needs an int32 ticket buffer of >= B * Hkv zeros");
+    tp = tickets->data_ptr<int>();
+  }
+  const bf16* pre = nullptr;
+  if (pre_part.has_value()) {
+    CHECK_DT(pre_part.value(), at::kBFloat16);
+    TORCH_CHECK(pre_part->is_contiguous() && pre_part->sizes() == out_part.sizes(),
+                "attn_decode_sk: pre_part must match out_part's shape");
+    pre = bptr(pre_part.value());
+  }
+  CHECK_HIP(kafka_launch_attn_decode_sk(bptr(q), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                         is_fp8_cache(k_cache) ? 1 : 0, B, Hkv, Hq / Hkv, 128,
+                                         block_tables.data_ptr<int>(), block_tables.stride(0), rows.data_ptr<int>(),
+                                         start.data_ptr<int>(), nwg, out_part.data_ptr<float>(), lse_part.data_ptr<float>(), S_total, scale, op,
+                                         ostride, tp, pre, cur_stream()));
 }
 
 static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
@@ -619,6 +675,23 @@ static void grouped_gemm(at::Tensor x, at::Tensor w, at::Tensor perm_tok, at::Te
                                       cur_stream()));
 }
 
+// ---- CU-masked streams (attention partition: the compute-bound cascade tile and the bandwidth-bound suffix decode
+// run side by side on disjoint CU sets). Returns the raw hipStream_t for torch.cuda.ExternalStream; the stream
+// lives for the process (one per partition, created once).
+static int64_t cu_mask_stream(std::vector<int64_t> mask_words) {
+  TORCH_CHECK(!mask_words.empty() && mask_words.size() <= 64, "cu_mask_stream: 1..64 mask words");
+  std::vector<uint32_t> m(mask_words.size());
+  for (size_t i = 0; i < m.size(); ++i) m[i] = (uint32_t)(mask_words[i] & 0xffffffffll);
+  hipStream_t st = nullptr;
+  CHECK_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data()));
+  return reinterpret_cast<int64_t>(st);
+}
+static std::vector<int64_t> stream_cu_mask(int64_t stream, int64_t words) {
+  std::vector<uint32_t> m((size_t)words, 0u);
+  CHECK_HIP(hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(stream), (uint32_t)words, m.data()));
+  return std::vector<int64_t>(m.begin(), m.end());
+}
+
 // ---- custom one-shot all-reduce (csrc/allreduce.hip): raw device allocations + IPC handles
 static int64_t car_alloc(int64_t bytes) {
   void* p = nullptr;
@@ -776,6 +849,9 @@ PYBIND11_MODULE(_kafka_ops, m) {
         py::arg("block_tables"), py::arg("q_limit"), py::arg("out"), py::arg("out_part"), py::arg("lse_part"),
         py::arg("scale"), py::arg("variant") = 0);
   m.def("attn_merge", &attn_merge);
+  m.def("attn_decode_sk", &attn_decode_sk, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
+        py::arg("block_tables"), py::arg("rows"), py::arg("start"), py::arg("out_part"), py::arg("lse_part"), py::arg("scale"), py::arg("out") = py::none(),
+        py::arg("tickets") = py::none(), py::arg("pre_part") = py::none());
   m.def("sample", &sample, py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"),
         py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none(), py::arg("nsplit") = 1);
   m.def("wstream_plan", &wstream_plan);
@@ -787,6 +863,8 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("slab_reduce", &slab_reduce);
   m.def("wstream_grouped", &wstream_grouped);
   m.def("moe_route", &moe_route);
+  m.def("cu_mask_stream", &cu_mask_stream);
+  m.def("stream_cu_mask", &stream_cu_mask);
   m.def("car_alloc", &car_alloc);
   m.def("car_ipc_handle", &car_ipc_handle);
   m.def("car_open", &car_open);
