@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--splits", default="2,3,4")
     ap.add_argument("--probe", action="store_true", help="time the cascade tile on CU-masked streams of known masks")
     ap.add_argument("--decode-study", action="store_true", help="decode kernel alone: merge / items / length law")
+    ap.add_argument("--sk-study", action="store_true", help="stream-K decode: partials only, F sweep, uniform rows")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     Hq, Hkv, D, G = 32, 8, 128, 4
@@ -112,6 +113,35 @@ def main():
     print(json.dumps({"case": "sequential", "cascade_chunks": nc, "decode_items": int(dit.shape[0]),
                       "us": round(t_seq, 1), "tile_us": round(t_tile, 1), "decode_us": round(t_seq - t_tile, 1),
                       "suffix_MB": round(suffix_bytes / 1e6, 1), "mean_suffix": round(sum(suf) / B)}), flush=True)
+
+    if args.sk_study:
+        u = sum(suf) // B // 32 * 32
+        for law, L in (("realistic", lens_np), ("uniform", np.full(B, P + u, dtype=np.int64))):
+            it = decode_items(L, np.full(B, P, dtype=np.int64), np.zeros(B, dtype=np.int64), Hkv, target=0)
+            st_i = int(it[:, 4].max())
+            dit2 = torch.tensor(it, dtype=torch.int32, device=dev)
+            part2 = torch.empty(B, Hq, max(st_i, 8), D, device=dev)
+            lse2 = torch.empty(B, Hq, max(st_i, 8), device=dev)
+            t_i = timeit(lambda: ops.attn_decode_items(q, k, v, bt, dit2, part2, lse2, scale))
+            print(json.dumps({"case": "sk_study", "law": law, "mode": "items_target0", "us": round(t_i, 1)}),
+                  flush=True)
+            for nwg in (512,):
+                for F in (0, 4, 16, 64):
+                    rows, start, sts = ops.decode_sk_plan(L, np.full(B, P), np.zeros(B, dtype=np.int64), Hkv,
+                                                          nwg=nwg, F=F)
+                    rows_d = torch.from_numpy(rows).to(dev)
+                    start_d = torch.from_numpy(start).to(dev)
+                    part3 = torch.empty(B, Hq, sts, D, device=dev)
+                    lse3 = torch.empty(B, Hq, sts, device=dev)
+                    o3 = torch.empty_like(out)
+                    t_p = timeit(lambda: ops.attn_decode_sk(q, k, v, bt, rows_d, start_d, part3, lse3, scale))
+                    t_f = timeit(lambda: ops.attn_decode_sk(q, k, v, bt, rows_d, start_d, part3, lse3, scale,
+                                                            out=o3))
+                    npieces = len(ops.decode_sk_items(rows, start, Hkv))
+                    print(json.dumps({"case": "sk_study", "law": law, "nwg": nwg, "F": F, "T": int(rows[-1, 0]),
+                                      "pieces": npieces, "partials_us": round(t_p, 1), "fused_us": round(t_f, 1)}),
+                          flush=True)
+        return
 
     if args.decode_study:
         for npre in (32, 0):

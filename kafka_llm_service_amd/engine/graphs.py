@@ -60,7 +60,7 @@ class DecodeGraphs:
 
     @staticmethod
     def key(h, sp) -> tuple:
-        return (h.B, h.n_dec_items, h.s_total, h.n_prefix_items, bool(h.cascade_prefix), h.i64.size, h.i32.size,
+        return (h.B, h.n_dec_items, h.dec_sk, h.s_total, h.n_prefix_items, bool(h.cascade_prefix), h.i64.size, h.i32.size,
                 h.n_late, h.late_off, sp.greedy)
 
     def eligible(self, h, sp) -> bool:

@@ -39,6 +39,7 @@ class HostStep:
     n_rows: int = 0
     s_total: int = 1        # partial slots per decode row (cascade prefix chunks + suffix pieces)
     n_dec_items: int = 0
+    dec_sk: int = 0         # stream-K decode workgroups (0: work-item decode); i32 holds rows [B + 1, 4] + start [dec_sk, 2]
     n_prefix_items: int = 0
     cascade_prefix: int = 0  # longest cascade prefix of the step (tokens; 0 = no cascade)
     n_items: int = 0
@@ -69,7 +70,7 @@ class SampleParams:
 
 
 _PLAN_SCALARS = ("B", "T", "nbt", "bt_w", "n_rows", "s_total", "n_dec_items", "n_prefix_items", "cascade_prefix",
-                 "n_items", "prefill_splits", "n_merge", "n_late", "late_off", "bt_need")
+                 "n_items", "prefill_splits", "n_merge", "n_late", "late_off", "bt_need", "dec_sk")
 PLAN_HDR = 32  # int64 header of a broadcast step plan
 
 
@@ -143,6 +144,9 @@ MIN_DECODE_KEYS = 256      # smallest key range of one decode work item
 DECODE_TARGET_ITEMS = int(os.environ.get("KAFKA_DECODE_TARGET", "768"))  # A/B: profiles/r02/decode_items_ab.jsonl
 MAX_PARTIALS = 64           # partial slots per row that the decode kernel's fused merge reads (one lane each)
 MAX_PREFIX_CHUNKS = 32
+# Decode attention as stream-K slices (ops.decode_sk_plan: every workgroup the same KV bytes + per-piece overhead)
+# instead of work items that the dispatcher runs in ~2 rounds of uneven length. KAFKA_DECODE_SK=0/1.
+DECODE_SK = os.environ.get("KAFKA_DECODE_SK", "0") == "1"
 
 
 def pad_step_rows(T: int) -> int:
@@ -464,15 +468,13 @@ class ModelRunner:
                     npre[r0:r0 + n] = nc
                     h.cascade_prefix = max(h.cascade_prefix, P)
                     r0 += n
-            ditems = decode_items(seq_lens, kv_start, npre, self.model.hkv)
-            if self.graphs is not None:  # fixed-size item list per bucket (graph replay); pads are dropped
-                cap = max(64, 1 << (int(ditems.shape[0]) - 1).bit_length())
-                pad = np.zeros((cap - ditems.shape[0], 8), dtype=np.int32)
-                pad[:, 3] = -1
-                ditems = np.concatenate([ditems, pad])
-            h.n_dec_items = int(ditems.shape[0])
-            h.s_total = int((npre[ditems[:, 0]] + ditems[:, 4]).max()) if B else 1
-            i32_parts.append(ditems.reshape(-1))
+            if DECODE_SK:
+                rows_sk, start_sk, h.s_total = ops.decode_sk_plan(seq_lens, kv_start, npre, self.model.hkv)
+                h.dec_sk = int(start_sk.shape[0])
+                i32_parts.append(rows_sk.reshape(-1))
+                i32_parts.append(start_sk.reshape(-1))
+            else:
+                self._plan_decode_items(h, seq_lens, kv_start, npre, i32_parts)
             if pit:
                 h.n_prefix_items = len(pit)
                 i32_parts.append(np.asarray(pit, dtype=np.int32).reshape(-1))
@@ -489,9 +491,21 @@ class ModelRunner:
         h.i64 = np.concatenate([tokens, positions, slots, np.asarray(logit_rows, dtype=np.int64)])
         h.i32 = np.concatenate(i32_parts)
         h.stats = {"B": B, "T": T, "cascade_prefix": h.cascade_prefix, "cascade_groups": len(groups),
-                   "decode_items": h.n_dec_items, "prefix_items": h.n_prefix_items, "s_total": h.s_total,
+                   "decode_items": h.n_dec_items, "decode_sk": h.dec_sk, "prefix_items": h.n_prefix_items, "s_total": h.s_total,
                    "prefill_splits": h.prefill_splits}
         return h, sample_seqs
+
+    def _plan_decode_items(self, h: HostStep, seq_lens: np.ndarray, kv_start: np.ndarray, npre: np.ndarray,
+                           i32_parts: list) -> None:
+        ditems = decode_items(seq_lens, kv_start, npre, self.model.hkv)
+        if self.graphs is not None:  # fixed-size item list per bucket (graph replay); pads are dropped
+            cap = max(64, 1 << (int(ditems.shape[0]) - 1).bit_length())
+            pad = np.zeros((cap - ditems.shape[0], 8), dtype=np.int32)
+            pad[:, 3] = -1
+            ditems = np.concatenate([ditems, pad])
+        h.n_dec_items = int(ditems.shape[0])
+        h.s_total = int((npre[ditems[:, 0]] + ditems[:, 4]).max()) if h.B else 1
+        i32_parts.append(ditems.reshape(-1))
 
     def to_device(self, h: HostStep) -> StepInput:
         """One H2D copy per packed buffer, then views into it (identical on every TP rank)."""
@@ -512,8 +526,14 @@ class ModelRunner:
         o += T
         Hq, D = self.model.hq, self.model.D
         if B:
-            meta.decode_items = d32[o:o + h.n_dec_items * 8].view(-1, 8)
-            o += h.n_dec_items * 8
+            if h.dec_sk:
+                meta.decode_sk_rows = d32[o:o + (B + 1) * 4].view(B + 1, 4)
+                o += (B + 1) * 4
+                meta.decode_sk_start = d32[o:o + h.dec_sk * 2].view(h.dec_sk, 2)
+                o += h.dec_sk * 2
+            else:
+                meta.decode_items = d32[o:o + h.n_dec_items * 8].view(-1, 8)
+                o += h.n_dec_items * 8
             if h.n_prefix_items:
                 meta.prefix_items = d32[o:o + h.n_prefix_items * 8].view(-1, 8)
                 o += h.n_prefix_items * 8

@@ -33,6 +33,8 @@ class AttnMeta:
     block_tables: torch.Tensor | None = None   # int32 [rows, W]; rows [0,B) decode seqs, then prefill seqs
     # decode
     decode_items: torch.Tensor | None = None   # int32 [n, 8] (b, lo, hi, split, nsplit, npre, 0, 0)
+    decode_sk_rows: torch.Tensor | None = None  # stream-K decode instead (ops.decode_sk_plan): int32 [B + 1, 4]
+    decode_sk_start: torch.Tensor | None = None  # int32 [nwg, 2]
     prefix_items: torch.Tensor | None = None   # int32 [m, 8] cascade prefix work items (rows = decode tokens)
     s_total: int = 1                           # partial slots per decode row
     part: torch.Tensor | None = None           # f32 [B, Hq, s_total, D]
@@ -100,8 +102,12 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                              meta.scale, out_part=meta.pre_part if meta.pre_part is not None else meta.part,
                              lse_part=meta.lse, variant=meta.variant)
         # the decode kernel merges each row's prefix partials and its own pieces and writes the final rows
-        ops.attn_decode_items(qd, k_cache, v_cache, meta.block_tables, meta.decode_items, meta.part, meta.lse,
-                              meta.scale, out=out[:B], pre_part=meta.pre_part)
+        if meta.decode_sk_rows is not None:
+            ops.attn_decode_sk(qd, k_cache, v_cache, meta.block_tables, meta.decode_sk_rows, meta.decode_sk_start,
+                               meta.part, meta.lse, meta.scale, out=out[:B], pre_part=meta.pre_part)
+        else:
+            ops.attn_decode_items(qd, k_cache, v_cache, meta.block_tables, meta.decode_items, meta.part, meta.lse,
+                                  meta.scale, out=out[:B], pre_part=meta.pre_part)
     if side is not None:
         torch.cuda.current_stream(q.device).wait_event(ev_done)
     elif has_prefill:

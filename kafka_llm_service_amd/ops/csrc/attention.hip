@@ -147,8 +147,17 @@ __device__ __forceinline__ void load_kv(KVFrag<D>& f, const bf16* __restrict__ k
   }
 }
 
+// Page ids of a decode piece staged in LDS: page i of the row at pages[i - pg0] (one ds_read instead of an L2 round
+// trip in front of every K/V block load — the decode loop is bound by that dependent chain per wave, not by HBM)
+struct LdsPages {
+  const int* p;
+  int pg0;
+  __device__ __forceinline__ int operator[](int i) const { return p[i - pg0]; }
+};
+
 // Pages holding keys [key0, key0 + 32) (key0 32-aligned); the second page is only dereferenced below `end`.
-__device__ __forceinline__ void block_pages(const int* __restrict__ bt, int key0, int end, int& p0, int& p1) {
+template <typename BT>
+__device__ __forceinline__ void block_pages(const BT& bt, int key0, int end, int& p0, int& p1) {
   p0 = bt[key0 >> 4];
   p1 = (key0 + 16 < end) ? bt[(key0 >> 4) + 1] : p0;
 }
@@ -247,9 +256,9 @@ __device__ __forceinline__ void attn_compute8(const KVFrag8<D>& f, int key0, int
 // Key blocks first, first+stride, ... < nblk (block b covers keys [base + 32 b, base + 32 b + 32)), software
 // pipelined one block deep. The prefetch of the block after the last one is clamped to the last block (pad, don't
 // branch: no divergent load, no extra waitcnt).
-template <int D, bool FP8>
+template <int D, bool FP8, typename BT = const int*>
 __device__ __forceinline__ void attn_blocks(const void* __restrict__ k_cache, const void* __restrict__ v_cache,
-                                            int Hkv, int kvh, const int* __restrict__ bt, int base, int first,
+                                            int Hkv, int kvh, const BT bt, int base, int first,
                                             int nblk, int stride, int end, int lo, int hi, int limit,
                                             const bf16x8 (&qf)[D / 16], float scale_log2, WaveAcc<D>& acc,
                                             int lane) {
@@ -319,8 +328,10 @@ struct DecodeItem {
 };
 
 // LDS of one decode piece (4 waves' partial results + the fused merge's per-split weights)
+constexpr int DEC_MAXPG = 2048;  // page ids of one decode piece staged in LDS (longer pieces read the table)
 template <int D>
 struct DecodeSmem {
+  int pages[DEC_MAXPG];
   float sO[4][8][D];
   float sM[4][8];
   float sL[4][8];
@@ -352,13 +363,24 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   const int nb = hi > lo ? (hi - a0 + 31) >> 5 : 0;
   const int* bt = block_tables + (int64_t)b * bt_stride;
 
+  // the piece's page ids -> LDS (pages covering [a0, hi))
+  const int pg0 = a0 >> 4;
+  const int npg = nb > 0 ? ((hi - 1) >> 4) - pg0 + 1 : 0;
+  const bool lds_pt = npg <= DEC_MAXPG;
+  if (lds_pt)
+    for (int i = threadIdx.x; i < npg; i += 256) sm.pages[i] = bt[pg0 + i];
+  __syncthreads();
   WaveAcc<D> acc;
   init_acc<D>(acc);
   if (w < nb) {
     bf16x8 qf[D / 16];
     load_q_frags<D>(qf, q + (int64_t)b * q_stride + (int64_t)(kvh * G + r) * D, r < G, h);
-    attn_blocks<D, FP8>(k_cache, v_cache, Hkv, kvh, bt, a0, w, nb, 4, hi, lo, hi, 0x7fffffff, qf, scale_log2, acc,
-                        lane);
+    if (lds_pt)
+      attn_blocks<D, FP8>(k_cache, v_cache, Hkv, kvh, LdsPages{sm.pages, pg0}, a0, w, nb, 4, hi, lo, hi, 0x7fffffff,
+                          qf, scale_log2, acc, lane);
+    else
+      attn_blocks<D, FP8>(k_cache, v_cache, Hkv, kvh, bt, a0, w, nb, 4, hi, lo, hi, 0x7fffffff, qf, scale_log2, acc,
+                          lane);
   }
   // cross-wave combine
   if (r < G) {
