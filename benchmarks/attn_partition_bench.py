@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--probe", action="store_true", help="time the cascade tile on CU-masked streams of known masks")
     ap.add_argument("--decode-study", action="store_true", help="decode kernel alone: merge / items / length law")
     ap.add_argument("--sk-study", action="store_true", help="stream-K decode: partials only, F sweep, uniform rows")
+    ap.add_argument("--seq-only", action="store_true", help="only the engine's sequential cascade + decode pair")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     Hq, Hkv, D, G = 32, 8, 128, 4
@@ -113,6 +114,8 @@ def main():
     print(json.dumps({"case": "sequential", "cascade_chunks": nc, "decode_items": int(dit.shape[0]),
                       "us": round(t_seq, 1), "tile_us": round(t_tile, 1), "decode_us": round(t_seq - t_tile, 1),
                       "suffix_MB": round(suffix_bytes / 1e6, 1), "mean_suffix": round(sum(suf) / B)}), flush=True)
+    if args.seq_only:
+        return
 
     if args.sk_study:
         u = sum(suf) // B // 32 * 32
