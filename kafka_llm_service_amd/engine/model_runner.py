@@ -147,6 +147,8 @@ MAX_PREFIX_CHUNKS = 32
 # Decode attention as stream-K slices (ops.decode_sk_plan: every workgroup the same KV bytes + per-piece overhead)
 # instead of work items that the dispatcher runs in ~2 rounds of uneven length. KAFKA_DECODE_SK=0/1.
 DECODE_SK = os.environ.get("KAFKA_DECODE_SK", "0") == "1"
+# one H2D copy per step for the plan + sampling parameters (KAFKA_BATCH_UPLOAD=0: one copy per array)
+BATCH_UPLOAD = os.environ.get("KAFKA_BATCH_UPLOAD", "1") == "1"
 
 
 def pad_step_rows(T: int) -> int:
@@ -301,6 +303,29 @@ class _Stager:
         ev = self.events[self.i]
         if ev is not None:
             ev.synchronize()  # normally long done: the arena's copies ran len(bufs) launches ago
+
+    def upload_many(self, arrays: list[np.ndarray]) -> list[torch.Tensor]:
+        """Several arrays staged back to back (256-B aligned) and moved by ONE async copy into one device buffer —
+        a step's plan and sampling parameters cost one copy launch instead of one each; returns device views."""
+        arrays = [np.ascontiguousarray(a) for a in arrays]
+        if self.device.type != "cuda":
+            return [torch.from_numpy(a) for a in arrays]
+        offs, off = [], 0
+        for a in arrays:
+            offs.append(off)
+            off = (off + a.nbytes + 255) & ~255
+        base = (self.off + 255) & ~255
+        buf = self.bufs[self.i]
+        if buf is None or base + off > buf.numel():
+            self.bufs[self.i] = buf = torch.empty(max(self.nbytes, 2 * (base + off)), dtype=torch.uint8,
+                                                  pin_memory=True)
+        host = buf.numpy()
+        for a, o in zip(arrays, offs):
+            host[base + o:base + o + a.nbytes] = a.reshape(-1).view(np.uint8)
+        self.off = base + off
+        dev = torch.empty(off, dtype=torch.uint8, device=self.device)
+        dev.copy_(buf[base:base + off], non_blocking=True)
+        return [dev[o:o + a.nbytes].view(_NP2TORCH[a.dtype]).view(a.shape) for a, o in zip(arrays, offs)]
 
     def upload(self, a: np.ndarray) -> torch.Tensor:
         a = np.ascontiguousarray(a)
@@ -507,9 +532,19 @@ class ModelRunner:
         h.s_total = int((npre[ditems[:, 0]] + ditems[:, 4]).max()) if h.B else 1
         i32_parts.append(ditems.reshape(-1))
 
-    def to_device(self, h: HostStep) -> StepInput:
-        """One H2D copy per packed buffer, then views into it (identical on every TP rank)."""
-        return self.views(self._h2d(h.i64), self._h2d(h.i32), h)
+    def to_device(self, h: HostStep, sp: "SampleParams | None" = None) -> StepInput:
+        """One H2D copy of the packed buffers (and of the step's sampling parameters when ``sp`` samples with
+        temperature: left in ``self._sp_dev`` for ``sample_device``), then views into it (identical on every TP
+        rank)."""
+        if not BATCH_UPLOAD:
+            return self.views(self._h2d(h.i64), self._h2d(h.i32), h)
+        if sp is not None and not sp.greedy and sp.temp.shape[0]:
+            d64, d32, f32, tk, sd = self.stager.upload_many([h.i64, h.i32, np.concatenate([sp.temp, sp.topp]), sp.topk,
+                                                             sp.seeds])
+            self._sp_dev = (sp, f32, tk, sd)
+        else:
+            d64, d32 = self.stager.upload_many([h.i64, h.i32])
+        return self.views(d64, d32, h)
 
     def views(self, d64: torch.Tensor, d32: torch.Tensor, h: HostStep) -> StepInput:
         """StepInput over packed device buffers laid out as ``h`` describes (only h's scalars are read, so a hipGraph
@@ -598,6 +633,10 @@ class ModelRunner:
         dev = logits.device
         if sp.greedy:
             return ops.sample(logits, torch.zeros(n, device=dev))
+        pre, self._sp_dev = getattr(self, "_sp_dev", None), None
+        if pre is not None and pre[0] is sp and pre[2].shape[0] == n:  # uploaded with the step's plan
+            _, f32, tk, sd = pre
+            return ops.sample(logits, f32[:n], f32[n:], tk, sd)
         f32 = self._h2d(np.concatenate([sp.temp, sp.topp]))
         return ops.sample(logits, f32[:n], f32[n:], self._h2d(sp.topk), self._h2d(sp.seeds))
 
@@ -717,7 +756,7 @@ class ModelRunner:
         if self.graphs is not None and self.graphs.eligible(host, sp):
             toks = self.graphs.run(host, sp)
         if toks is None:
-            inp = self.to_device(host)
+            inp = self.to_device(host, sp)
             logits = self.model.forward(inp, self.k_caches, self.v_caches)
             toks = self.sample_device(logits, sp)
             self.tok_buf[:toks.shape[0]].copy_(toks)
