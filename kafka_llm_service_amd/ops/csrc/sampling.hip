@@ -72,6 +72,24 @@ __device__ __forceinline__ float gumbel(uint64_t seed, uint64_t stream, uint64_t
   return -__logf(-__logf(fminf(u, 0.99999994f)));
 }
 
+// Plain-temperature rows: the per-element noise from a per-row 64-bit key (two splitmix64 rounds, once per thread)
+// and a 32-bit integer hash of the index (two lowbias32 rounds: 4 v_mul_lo_u32 instead of the ~16 32-bit multiplies
+// two 64-bit splitmix rounds cost per element) — the noise stream is still a pure function of (seed, step, index),
+// so every split of a row draws the same noise for an index and the token is the one-workgroup result.
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ float gumbel_fast(uint64_t key, uint32_t idx) {
+  const uint32_t h = lowbias32(lowbias32(idx + (uint32_t)key) ^ (uint32_t)(key >> 32));
+  const float u = ((float)(h >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
+  return -__logf(-__logf(fminf(u, 0.99999994f)));
+}
+
 template <typename T>
 __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logits, int64_t stride, int V,
                                                       const float* __restrict__ temperature,
@@ -97,6 +115,7 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
     const float inv_t = greedy ? 1.f : 1.f / temp;
     const uint64_t seed = seeds ? (uint64_t)seeds[row] : 0x1234ull;
     const uint64_t stream = (uint64_t)(step_ptr ? step_ptr[0] : 0) << 8;  // round 0 of the filtered path
+    const uint64_t key = mix64(seed ^ mix64(stream * 0x632BE59BD9B4E019ull));
     const int per = (nvec + nsplit - 1) / nsplit;
     const int v0 = sp * per, v1 = min(nvec, v0 + per);
     ArgMax a{-INFINITY, 0x7fffffff};
@@ -106,13 +125,13 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xv = v[j] * inv_t;
-        a = better(a, ArgMax{greedy ? xv : xv + gumbel(seed, stream, vi * 8 + j), vi * 8 + j});
+        a = better(a, ArgMax{greedy ? xv : xv + gumbel_fast(key, vi * 8 + j), vi * 8 + j});
       }
     }
     if (sp == nsplit - 1)
       for (int i = tail0 + threadIdx.x; i < V; i += SNT) {
         const float xv = (float)x[i] * inv_t;
-        a = better(a, ArgMax{greedy ? xv : xv + gumbel(seed, stream, i), i});
+        a = better(a, ArgMax{greedy ? xv : xv + gumbel_fast(key, i), i});
       }
     a = block_argmax(a, sv, si);
     if (threadIdx.x != 0) return;
