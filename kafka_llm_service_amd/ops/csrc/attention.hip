@@ -332,6 +332,7 @@ constexpr int DEC_MAXPG = 2048;  // page ids of one decode piece staged in LDS (
 template <int D>
 struct DecodeSmem {
   int pages[DEC_MAXPG];
+  bf16 qs[8][D];  // OCC3: the unit's G <= 8 query heads (B operand rows), read per block instead of held in VGPRs
   float sO[4][8][D];
   float sM[4][8];
   float sL[4][8];
@@ -343,7 +344,7 @@ struct DecodeSmem {
 // One decode piece: keys [lo, hi) of row b, kv head kvh, piece `split` of S, partial slots from split_offset. Every
 // thread of the workgroup calls it with the same arguments (it synchronises the workgroup); returns when the
 // piece's partial or final rows are written.
-template <int D, bool FP8, int MG>
+template <int D, bool FP8, int MG, bool OCC3 = false>
 __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __restrict__ q, int64_t q_stride,
                                              const void* __restrict__ k_cache, const void* __restrict__ v_cache,
                                              int Hkv, int G, const int* __restrict__ block_tables, int bt_stride,
@@ -369,10 +370,42 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   const bool lds_pt = npg <= DEC_MAXPG;
   if (lds_pt)
     for (int i = threadIdx.x; i < npg; i += 256) sm.pages[i] = bt[pg0 + i];
+  if constexpr (OCC3) {
+    for (int i = threadIdx.x; i < G * (D / 8); i += 256) {
+      const int g = i / (D / 8), c = i % (D / 8);
+      *reinterpret_cast<bf16x8*>(&sm.qs[g][8 * c]) = load_bf16x8(q + (int64_t)b * q_stride + (int64_t)(kvh * G + g) * D + 8 * c);
+    }
+  }
   __syncthreads();
   WaveAcc<D> acc;
   init_acc<D>(acc);
-  if (w < nb) {
+  if constexpr (OCC3) {
+    // Three waves per SIMD (VGPR budget 168): no Q fragments and no second K/V block in registers — each wave
+    // has its one block in flight at a time, and 12 waves per CU (3 workgroups) keep the memory system fed;
+    // more resident workgroups also cover each other's piece start / end.
+    if (w < nb && !FP8) {
+      const bool qrow = r < G;
+      for (int bk = w; bk < nb; bk += 4) {
+        const int key0 = a0 + 32 * bk;
+        int p0, p1;
+        if (lds_pt)
+          block_pages(LdsPages{sm.pages, pg0}, key0, hi, p0, p1);
+        else
+          block_pages(bt, key0, hi, p0, p1);
+        KVFrag<D> f;
+        load_kv<D>(f, static_cast<const bf16*>(k_cache), static_cast<const bf16*>(v_cache), Hkv, kvh, p0, p1, lane);
+        f32x16 sacc = {};
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) {
+          bf16x8 qv = *reinterpret_cast<const bf16x8*>(&sm.qs[qrow ? r : 0][16 * kk + 8 * h]);
+          if (!qrow) qv = bf16x8{};
+          sacc = mfma32(f.k[kk], qv, sacc);
+        }
+        const bool masked = (key0 < lo) | (key0 + 32 > hi);
+        softmax_pv<D>(sacc, masked, key0, lo, hi, 0x7fffffff, scale_log2, f.v, acc, lane);
+      }
+    }
+  } else if (w < nb) {
     bf16x8 qf[D / 16];
     load_q_frags<D>(qf, q + (int64_t)b * q_stride + (int64_t)(kvh * G + r) * D, r < G, h);
     if (lds_pt)
@@ -575,8 +608,8 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   }
 }
 
-template <int D, bool HEADS_FAST, bool FP8, int MG = 16>
-__global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
+template <int D, bool HEADS_FAST, bool FP8, int MG = 16, bool OCC3 = false>
+__global__ __launch_bounds__(256, OCC3 ? 3 : 2) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
                                                            const void* __restrict__ k_cache,
                                                            const void* __restrict__ v_cache, int Hkv, int G,
                                                            const int* __restrict__ block_tables, int bt_stride,
@@ -595,7 +628,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const bf16* __restr
   if (b < 0 || b >= B || split < 0 || split >= S || split_offset < 0 || split_offset + S > S_total ||
       (out != nullptr && split_offset + S > 64))
     return;
-  decode_piece<D, FP8, MG>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, it.lo, it.hi,
+  decode_piece<D, FP8, MG, OCC3>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, it.lo, it.hi,
                            split, S, split_offset, out_part, lse_part, S_total, scale_log2, out, out_stride, tickets,
                            pre_bf16);
 }
@@ -1151,6 +1184,12 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
     const int v = e ? atoi(e) : 32;
     return v == 8 || v == 16 ? v : 32;
   }();
+  // three workgroups per CU (Q in LDS, one K/V block per wave in flight; bench +0.9 %, profiles/r03/decode_occ3/);
+  // KAFKA_DECODE_OCC3=0: two per CU with a one-block register prefetch
+  static const bool occ3 = [] {
+    const char* e = getenv("KAFKA_DECODE_OCC3");
+    return e == nullptr || e[0] != '0';
+  }();
   const dim3 hf(Hkv, n_items), sf(n_items, Hkv);
   if (fp8)
     heads_fast ? go(attn_decode_kernel<128, true, true>, hf) : go(attn_decode_kernel<128, false, true>, sf);
@@ -1158,6 +1197,8 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
     go(attn_decode_kernel<128, false, false>, sf);
   else if (mg == 8)
     go(attn_decode_kernel<128, true, false, 8>, hf);
+  else if (mg == 32 && occ3)
+    go(attn_decode_kernel<128, true, false, 32, true>, hf);
   else if (mg == 32)
     go(attn_decode_kernel<128, true, false, 32>, hf);
   else
