@@ -141,9 +141,10 @@ class Launched:
 MIN_DECODE_KEYS = 256      # smallest key range of one decode work item
 # decode workgroups per launch (items x Hkv) the suffix pieces are sized for; 0 = one item per row (no split
 # unless a row alone would leave most CUs idle)
-# 1,152 with the decode kernel at three workgroups per CU (768 slots): +1.6 % over 768 same box
-# (profiles/r03/decode_occ3/decode_target_ab_*.jsonl; 768 was best at two per CU, profiles/r02/decode_items_ab.jsonl)
-DECODE_TARGET_ITEMS = int(os.environ.get("KAFKA_DECODE_TARGET", "1152"))
+# 1,344 with the decode kernel at three workgroups per CU (768 slots): 1,152 was +1.6 % over 768 and 1,344 another
+# +0.2-0.4 % over 1,152, same boxes (profiles/r03/decode_occ3/decode_target_ab_*.jsonl; 768 was best at two per CU,
+# profiles/r02/decode_items_ab.jsonl)
+DECODE_TARGET_ITEMS = int(os.environ.get("KAFKA_DECODE_TARGET", "1344"))
 MAX_PARTIALS = 64           # partial slots per row that the decode kernel's fused merge reads (one lane each)
 MAX_PREFIX_CHUNKS = 32
 # Decode attention as stream-K slices (ops.decode_sk_plan: every workgroup the same KV bytes + per-piece overhead)
