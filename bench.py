@@ -24,6 +24,11 @@ Workload (synthetic data, random-init Llama-3-8B weights — no checkpoints/data
     300-step one does;
   * ``--mixed-prefix F``: a fraction F of the slots use a different system prompt (threads created with their own
     system message, quirk Q4 of SURVEY.md §2.9) — the multi-group cascade case;
+  * ``--tool-frac F``: a fraction F of the slots decode under ``tool_choice="required"`` for their whole reply —
+    back-to-back grammar-constrained tool calls over the server's tool schemas (ToolCallLoop), so every one of their
+    tokens goes through the sampler's device-side grammar masks / forced tokens (engine/logits_proc.py) — and
+    ``--penalty-frac F`` slots carry presence / frequency penalties (device-side counts). Off in the headline;
+    the A/B that shows those threads no longer stall the batch (VERDICT r03 "Next round" #3);
   * DP: one engine replica per GPU (one process per GPU), 64 threads per replica (weak scaling).
 
 A "step" is one engine iteration (one continuous-batching forward over the mixed decode/prefill batch, sampling
@@ -68,6 +73,10 @@ def parse(argv=None):
     ap.add_argument("--prefix-tokens", type=int, default=18000, help="shared system prefix (0 = short prompt)")
     ap.add_argument("--mixed-prefix", type=float, default=0.0,
                     help="fraction of threads on a second system prompt (multi-group cascade)")
+    ap.add_argument("--tool-frac", type=float, default=0.0,
+                    help="fraction of threads decoding back-to-back grammar-constrained tool calls")
+    ap.add_argument("--penalty-frac", type=float, default=0.0,
+                    help="fraction of threads with presence / frequency penalties")
     ap.add_argument("--history-turns", type=int, default=4, help="mean earlier turns in front of a new turn")
     ap.add_argument("--user-tokens", type=int, default=64, help="mean user-message tokens")
     ap.add_argument("--min-out", type=int, default=128)
@@ -116,6 +125,48 @@ def spawn_ranks(n: int) -> int:
 
 
 # ---------------------------------------------------------------------------------------------------------------
+def bench_tools() -> list[dict]:
+    """The server's tool schemas (weather, counter, planner, shell, notebook; server/state.py)."""
+    from kafka_llm_service_amd.server_tools import NotebookTools, PlannerTools, ShellTools, count_tool, get_weather_tool
+
+    tools = [get_weather_tool, count_tool] + PlannerTools(None).tools + ShellTools(None).tools + \
+        NotebookTools(None).tools
+    return [t.definition for t in tools]
+
+
+class ToolCallLoop:
+    """allowed_tokens_fn of a ``--tool-frac`` thread: one ``tool_choice="required"`` tool call after another for the
+    whole reply (the same grammar the agent loop decodes tool calls with, engine/constrained.py), so the thread is
+    constrained at every token and keeps its reply length (no stop token)."""
+
+    def __init__(self, tok, tools):
+        from kafka_llm_service_amd.engine.constrained import ToolCallConstraint
+
+        self._mk = lambda: ToolCallConstraint(tok, tools, "required")
+        self.c = self._mk()
+        self.base = 0  # output index where the current call starts
+
+    def _cur(self, out):
+        if self.c.done:
+            self.base += self.c._n
+            self.c = self._mk()
+        return out[self.base:]
+
+    def __call__(self, out):
+        spec = self.c(self._cur(out))
+        if spec is None and self.c.done:  # the call just ended: the next token opens the next call
+            spec = self.c(self._cur(out))
+        return spec
+
+    def plan_state(self, out):
+        return self.c.plan_state(self._cur(out))
+
+    def rollback_at(self, out, slot):
+        if slot < self.base:
+            return False
+        return self.c.rollback_at(out[self.base:], slot - self.base)
+
+
 class ThreadSim:
     """One thread slot: the conversation's history token ids, its system prefix and the turn in flight."""
 
@@ -279,14 +330,26 @@ def main(argv=None):
     setup_s = time.perf_counter() - t_setup
 
     req_thread = {}
+    n_tool = int(round(args.tool_frac * args.threads))
+    n_pen = int(round(args.penalty_frac * args.threads))
+    tools = bench_tools() if n_tool else None
+    if n_tool:
+        from kafka_llm_service_amd.engine.tokenizer import tokenizer_for_model
+
+        tok = tokenizer_for_model(eng.model_cfg)
 
     def submit(th: ThreadSim, prompt: list[int] | None = None, n_left: int | None = None, resumed=False):
         rid = f"t{th.tid}-c{th.conv}-turn{th.turn}"
         if prompt is None:
             n_left, _ = th.reply_budget(stationary=False)
             prompt = th.next_prompt(0)
+        kw = {}
+        if th.tid < n_tool:
+            kw["allowed_tokens_fn"] = ToolCallLoop(tok, tools)
+        elif th.tid < n_tool + n_pen:
+            kw.update(presence_penalty=0.3, frequency_penalty=0.2)
         sp = SamplingParams(temperature=args.temperature, max_tokens=n_left, ignore_eos=True,
-                            seed=th.tid * 1000003 + th.conv * 1009 + th.turn)
+                            seed=th.tid * 1000003 + th.conv * 1009 + th.turn, **kw)
         seq = eng.add_request(rid, prompt, sp)
         req_thread[rid] = (th, seq, resumed)
 
@@ -397,7 +460,8 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
     p99 = ttfts[min(len(ttfts) - 1, int(len(ttfts) * 0.99))] * 1e3 if ttfts else None
     kv = eng.kv_stats()
     dp = world // args.tp
-    headline = (args.model, args.threads, args.prefix_tokens, args.tp) == ("llama3-8b", 64, 18000, 1)
+    headline = (args.model, args.threads, args.prefix_tokens, args.tp, args.tool_frac, args.penalty_frac) == \
+        ("llama3-8b", 64, 18000, 1, 0.0, 0.0)
     res = {
         "metric": METRIC if headline else
         f"output tok/s + p50 TTFT, {args.model}, {args.threads} concurrent threads per replica",
@@ -416,13 +480,15 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
                    "shared_prefix_tokens": args.prefix_tokens, "history_turns": args.history_turns,
                    "mixed_prefix": args.mixed_prefix, "max_out": [args.min_out, args.max_out],
                    "temperature": args.temperature, "cascade": not args.no_cascade, "graphs": eng.cfg.use_graphs,
-                   "kv_dtype": args.kv_dtype},
+                   "kv_dtype": args.kv_dtype, "tool_frac": args.tool_frac, "penalty_frac": args.penalty_frac},
         "ttft_p50_ms": round(p50, 2) if p50 else None, "ttft_p99_ms": round(p99, 2) if p99 else None,
         "ttft_samples": len(ttfts), "ttft_extra_steps": extra,
         "vs_baseline_basis": "derived 1-GPU bound 17k tok/s/GPU (BASELINE.md §3); reference publishes none",
         "setup_s": round(setup_s, 2),
         "prefix_hit_rate": round(kv["hit_tokens"] / max(1, kv["query_tokens"]), 4),
         "preemptions": eng.sched.num_preemptions,
+        "planned_ahead_frac": round(eng.stats.get("planned_ahead", 0) / max(1, eng.stats.get("steps", 1)), 4),
+        "grammar_rollbacks": eng.stats.get("grammar_rollbacks", 0),
     }
     if rank == 0:
         line = json.dumps(res)

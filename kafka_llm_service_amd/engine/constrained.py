@@ -129,6 +129,8 @@ class ToolCallConstraint:
         self._spec: Any = None
         self._n = 0
         self.done = False
+        self._guards: list[tuple[int, frozenset]] = []  # (slot, E): speculated "output_ids[slot] not in E"
+        self._reps: dict = {}
 
     def _mode(self, tc):
         if isinstance(tc, dict):
@@ -145,21 +147,99 @@ class ToolCallConstraint:
         raise ValueError(f"unsupported tool_choice: {tc!r}")
 
     # ---- runner protocol ----------------------------------------------------------------------------------------
-    def __call__(self, output_ids: list[int]):
+    # ``output_ids`` may end with ONE placeholder (< 0): the token being sampled by the step in flight (the engine
+    # plans step n+1 before step n's token lands). When the spec that token was drawn under makes the NEXT state
+    # depend only on whether the token falls in a small set E — a Mask (free string: E = the closing quote; digits,
+    # "none": E = its extra ids / nothing) or the first free token of "auto" (E = the tool-call start) — the
+    # program consumes a representative token outside E now and records the guard (slot, E). When the real token
+    # lands inside E the guess was wrong: the program is rebuilt from the landed tokens and the token sampled under
+    # the mis-predicted mask (slot + 1) is rolled back by the engine (``rollback_at``). Choice states (tool names,
+    # enums, booleans: the next state depends on WHICH token) cannot be predicted: ``plan_state`` -> "wait".
+    def _advance(self, t: int) -> None:
+        self._n += 1
+        if self._spec is _FREE_FOREVER:
+            return
+        try:
+            self._spec = self._gen.send(t)
+        except StopIteration:
+            self._spec = _FREE_FOREVER
+            self.done = True
+
+    def _start(self) -> None:
         if self._gen is None:
             self._gen = self._program()
             self._spec = next(self._gen)
+
+    def _class_of(self, spec):
+        """(representative token, E) for a spec whose successor state depends only on membership in E, else None."""
+        if spec is _FREE_FOREVER:
+            return 0, frozenset()
+        if spec is None:  # "auto" before the first token: only the tool-call start token changes the state
+            return (0 if self.start != 0 else 1), frozenset([self.start])
+        if isinstance(spec, Mask):
+            extra = frozenset(int(e) for e in spec.extra)
+            rep = self._reps.get(spec.key)
+            if rep is None:
+                cand = np.flatnonzero(spec.base)
+                rep = self._reps[spec.key] = next((int(c) for c in cand[:64] if int(c) not in extra), -1)
+            return (rep, extra) if rep >= 0 else None
+        return None
+
+    def _validate(self, output_ids: list[int]) -> int | None:
+        """Check every guard whose token has landed; on a violation rebuild the program from the landed tokens and
+        return the guarded slot (the token after it was drawn under a wrong mask)."""
+        bad = None
+        keep = []
+        for slot, extra in self._guards:
+            t = output_ids[slot] if slot < len(output_ids) else -1
+            if t < 0:
+                keep.append((slot, extra))
+            elif t in extra and bad is None:
+                bad = slot
+        self._guards = keep
+        if bad is None:
+            return None
+        self._gen, self._spec, self._n, self.done, self._guards = None, None, 0, False, []
+        self._start()
+        for t in output_ids[:bad + 1]:
+            self._advance(t)
+        return bad
+
+    def __call__(self, output_ids: list[int]):
+        self._start()
+        self._validate(output_ids)
         while self._n < len(output_ids):
             t = output_ids[self._n]
-            self._n += 1
-            if self._spec is _FREE_FOREVER:
-                return None
-            try:
-                self._spec = self._gen.send(t)
-            except StopIteration:
-                self._spec = _FREE_FOREVER
-                self.done = True
+            if t < 0:  # the in-flight token: speculate past it (plan_state said the spec allows it)
+                if self._n != len(output_ids) - 1:
+                    raise RuntimeError("constraint: only the last token may be pending")
+                cls = self._class_of(self._spec)
+                if cls is None:
+                    raise RuntimeError("constraint: cannot plan past a pending token drawn from a choice")
+                rep, extra = cls
+                if extra:
+                    self._guards.append((self._n, extra))
+                t = rep
+            self._advance(t)
         return None if self._spec is _FREE_FOREVER else self._spec
+
+    def plan_state(self, output_ids: list[int]) -> str:
+        """Can the row be planned while its last token is pending? "ok" | "wait" (choice state: sit this step
+        out) | "rollback" (a landed token broke a guess: the pending token was drawn under a wrong mask)."""
+        self._start()
+        if self._validate(output_ids) is not None:
+            return "rollback"
+        if not output_ids or output_ids[-1] >= 0:
+            return "ok"
+        if self._n < len(output_ids) - 1:  # consume the landed tokens first (no speculation involved)
+            self.__call__(output_ids[:-1])
+        return "ok" if self._n >= len(output_ids) or self._class_of(self._spec) is not None else "wait"
+
+    def rollback_at(self, output_ids: list[int], slot: int) -> bool:
+        """At the landing of ``output_ids[slot]``: True if it was drawn under a mis-predicted mask (the token before
+        it broke its guard) and must be discarded; the program is rebuilt from the landed tokens then."""
+        bad = self._validate(output_ids[:slot])
+        return bad is not None and bad == slot - 1
 
     # ---- grammar -------------------------------------------------------------------------------------------------
     def _program(self):

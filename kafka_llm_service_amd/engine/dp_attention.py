@@ -8,10 +8,13 @@ parallel/custom_allreduce.py or the library all-to-all). Versus the default tens
 all-reduce combine, every rank moves only its own tokens' rows and attention work and KV are split, not replicated.
 
 Lockstep: every layer's all-to-all needs every rank, so the group runs one forward per step on every rank
-(``LLMEngine.step_lockstep``): the ranks agree on (max tokens, any unfinished) with one host all-reduce per step —
-the largest step sets the all-to-all capacity — and a rank without tokens runs an expert-only step that serves the
-other ranks' rows. Scheduling is synchronous in this mode (one forward per ``step`` call keeps the collectives in
-line), and decode steps are not graph-captured.
+(``LLMEngine.step_lockstep``): the ranks agree on (max tokens, any unfinished, stop flag) once per step — the
+largest step sets the all-to-all capacity — and a rank without tokens runs an expert-only step that serves the
+other ranks' rows. The agreement goes through a shared-memory board (``runtime/csrc/group_board.cpp``: a few cache
+lines, microseconds; gloo all-reduce only if the board cannot be set up), and the engine plans ahead as in
+``LLMEngine.step``: step n+1 is planned, agreed and launched while step n still runs (one forward per call keeps the
+collectives in line; the host never waits on the GPU between steps). An idle group does not poll collectives: each
+rank sleeps on its request pipe and the board's wake counter, and the rank that receives a request wakes the others.
 
 Entry points: ``build_dpa_engine`` (inside a process of a torch.distributed world whose ranks form the EP groups),
 ``generate_lockstep`` (offline / bench), ``serve_pipe_lockstep`` (a replica of the API server's engine client).
@@ -39,16 +42,74 @@ def build_dpa_engine(cfg_dict: dict, ep: int):
     return LLMEngine(cfg), st
 
 
-def make_agree(st):
-    """(tokens, unfinished, flag) -> group maxima, over the EP group's gloo group (one 24-byte all-reduce per
-    step)."""
-    grp = st.ep_cpu_group
+_BOARDS: dict = {}
 
-    def agree(vals: tuple[int, ...]) -> tuple[int, ...]:
+
+def make_board(st):
+    """The EP group's shared-memory agreement board (collective over the group's gloo group: the group's first rank
+    creates the segment, every rank attaches, the name is unlinked once all have); None -> gloo agreement."""
+    key = (st.rank, st.ep)
+    if key in _BOARDS:
+        return _BOARDS[key]
+    import os
+    import uuid
+
+    from kafka_llm_service_amd.runtime import native
+
+    grp = st.ep_cpu_group
+    src = st.rank - st.ep_rank
+    name, board = None, None
+    if st.ep_rank == 0 and os.environ.get("KAFKA_DPA_BOARD", "1") == "1":
+        try:
+            name = f"/kafka_board_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+            board = native().GroupBoard(name, st.ep, 0, True)
+        except Exception:  # noqa: BLE001 - gloo fallback
+            log.exception("shared-memory agreement board unavailable")
+            name, board = None, None
+    box = [name]
+    dist.broadcast_object_list(box, src=src, group=grp)
+    ok = box[0] is not None
+    if ok and st.ep_rank != 0:
+        try:
+            board = native().GroupBoard(box[0], st.ep, st.ep_rank, False)
+        except Exception:  # noqa: BLE001
+            log.exception("could not attach the agreement board %s", box[0])
+            ok, board = False, None
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=grp)
+    if int(flag.item()) == 0:
+        if board is not None:
+            board.close()
+        board = None
+    elif st.ep_rank == 0:
+        board.unlink()  # every rank has attached: nothing outlives a killed group in /dev/shm
+    _BOARDS[key] = board
+    return board
+
+
+class Agree:
+    """(tokens, unfinished, flag[, ...]) -> group maxima: the shared-memory board's exchange, or one gloo all-reduce
+    of the EP group. ``board`` is exposed for the idle wait (wake counter)."""
+
+    def __init__(self, st, timeout_s: float | None = None):
+        import os
+
+        self.grp = st.ep_cpu_group
+        self.board = make_board(st)
+        self.timeout = float(os.environ.get("KAFKA_COLLECTIVE_TIMEOUT_S", "300")) if timeout_s is None else timeout_s
+
+    def __call__(self, vals: tuple[int, ...]) -> tuple[int, ...]:
+        if self.board is not None:
+            import numpy as np
+
+            return tuple(int(v) for v in self.board.exchange(np.asarray(vals, dtype=np.int64), self.timeout))
         t = torch.tensor(vals, dtype=torch.int64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=grp)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.grp)
         return tuple(int(v) for v in t)
-    return agree
+
+
+def make_agree(st) -> Agree:
+    return Agree(st)
 
 
 def generate_lockstep(eng, st, prompts: list[list[int]], params: SamplingParams) -> list[list[int]]:
@@ -60,30 +121,57 @@ def generate_lockstep(eng, st, prompts: list[list[int]], params: SamplingParams)
         eng.add_request(rid, p, params)
     out: dict[str, list[int]] = {rid: [] for rid in rids}
     while True:
-        outs, busy, _ = eng.step_lockstep(agree)
+        outs, busy, _, _ = eng.step_lockstep(agree)
         for o in outs:
             out[o.request_id].extend(o.new_token_ids)
         if not busy:
             return [out[r] for r in rids]
 
 
+def _idle_wait(conn, board, wake_seen: int, idle_since: float, hb_left: float) -> bool:
+    """An idle group. With the board: sleep until a request arrives on this rank's pipe or a peer bumps the wake
+    counter past ``wake_seen`` (the group's agreed reading before it went idle) -> True (step with the group), or
+    the heartbeat is due -> False (do NOT step: the peers are asleep). No collective is polled. Without a board:
+    one pipe poll backing off from 2 to 50 ms, then True (every wake-up is one gloo agreement of the group, which
+    the ranks reach on their own backoffs)."""
+    idle = time.monotonic() - idle_since
+    if board is None:
+        conn.poll(min(0.05, 0.002 * (1 + int(idle * 10))))
+        return True
+    t_end = time.monotonic() + hb_left
+    while True:
+        if conn.poll(0.0005 if idle < 1.0 else 0.002) or board.wake_count() > wake_seen:
+            return True
+        if time.monotonic() >= t_end:
+            return False
+        idle = time.monotonic() - idle_since
+
+
 def serve_pipe_lockstep(eng, st, conn) -> None:
     """The request loop of one DP-attention rank behind the API server's engine client: like engine/client.py
-    serve_pipe (same message protocol), but the rank steps whenever ANY rank of its group has work, and idles in
-    short polls so a new request on a peer starts its group step within ~2 ms."""
+    serve_pipe (same message protocol), but the rank steps whenever ANY rank of its group has work. While the whole
+    group is idle the ranks sleep on their pipes (``_idle_wait``); the rank that receives a request bumps the
+    agreement board's wake counter so its peers join the group step within about a millisecond (no
+    collective polling of an idle group)."""
     from kafka_llm_service_amd.engine.client import HEARTBEAT_S
 
     agree = make_agree(st)
+    board = agree.board
     pinned: list[int] | None = None
     last_hb = 0.0
     busy = 0
+    wake_seen = 0
+    idle_since = time.monotonic()
     while True:
         now = time.monotonic()
         if now - last_hb >= HEARTBEAT_S:
             conn.send(("hb", eng.stats["steps"]))
             last_hb = now
+        if not busy and not _idle_wait(conn, board, wake_seen, idle_since,
+                                       max(0.0, HEARTBEAT_S - (now - last_hb))):
+            continue  # heartbeat only
         stop = False
-        while conn.poll(0 if busy else 0.002):
+        while conn.poll(0):
             msg = conn.recv()
             kind = msg[0]
             if kind == "add":
@@ -110,10 +198,18 @@ def serve_pipe_lockstep(eng, st, conn) -> None:
             elif kind == "stop":
                 stop = True
                 break
+            if board is not None and not busy and (kind in ("add", "stop")):
+                board.wake()  # peers asleep in _idle_wait join the next group step
             busy = int(eng.has_unfinished())
         # every rank takes part in every agreement, busy or not; a stop seen by any rank stops the whole group
         # after the same step (nobody is left waiting in a collective for a peer that has exited)
-        outs, busy, stopping = eng.step_lockstep(agree, flag=int(stop))
+        wake_read = board.wake_count() if board is not None else 0
+        outs, busy, stopping, ext = eng.step_lockstep(agree, flag=int(stop), extra=(wake_read,))
+        wake_seen = ext[0]
+        if not busy:
+            idle_since = time.monotonic() if idle_since is None else idle_since
+        else:
+            idle_since = None
         if outs:
             conn.send(("out", [(o.request_id, o.new_token_ids, o.finished, o.finish_reason, o.num_prompt_tokens,
                                 o.num_output_tokens, o.num_cached_tokens) for o in outs], time.perf_counter()))

@@ -64,7 +64,7 @@ class EngineConfig:
     async_scheduling: bool = True       # plan step n+1 on the host while step n runs on the GPU
     # Mixtral data-parallel attention (engine/dp_attention.py): this rank serves its own sequences with whole
     # attention weights; experts are sharded over parallel.state's EP group and every step runs in lockstep with
-    # the group (step_lockstep; synchronous scheduling)
+    # the group (step_lockstep; planned ahead like step())
     dp_attention: bool = False
     eos_token_ids: list[int] = field(default_factory=list)
 
@@ -123,8 +123,7 @@ class LLMEngine:
 
             st = pstate.get()
             dpa = (st.ep, st.ep_rank)
-            cfg.async_scheduling = False  # one forward per step() call: the group's collectives line up
-            cfg.use_graphs = False
+            cfg.use_graphs = False  # idle (expert-only) steps interleave with decode steps; eager
         self.model = model or build_model(mc, self.device, tp=cfg.tp, tp_rank=cfg.tp_rank, seed=cfg.seed,
                                           weights=cfg.weights, max_positions=min(cfg.max_model_len,
                                                                                  mc.max_position_embeddings),
@@ -282,9 +281,11 @@ class LLMEngine:
         PENDING placeholder; the runner copies those ids device-side from n's sampler output, so the host never waits
         for a token before enqueueing the next forward. Rows planned for sequences that then finish at n (EOS, stop
         string, abort) compute one void token that is discarded; sequences that will finish by length are left out of
-        speculative plans up front. Steps whose sampling needs the landed tokens on the host (token-constrained tool
-        calls, penalties) launch after collecting n instead; a plan that would have to preempt is redone
-        synchronously. TP leaders plan ahead too: their followers sample the same ids on their own GPUs."""
+        speculative plans up front. Penalties and grammar masks run inside the sampler kernel (engine/logits_proc.py):
+        a grammar-constrained row whose next mask depends on a token still in flight sits out ONE plan-ahead step
+        (the others keep the pipeline); a token the grammar forces is known at launch and written at once. A plan
+        that would have to preempt is redone synchronously. TP leaders plan ahead too: their followers sample the
+        same ids on their own GPUs."""
         if self.fi.active:
             self.fi.on_step()
         cut: list[StepOutput] = []
@@ -315,37 +316,55 @@ class LLMEngine:
                 self._inflight = self._launch(plan.batch, plan.host, plan.sampled, None)
         return outs
 
-    def step_lockstep(self, agree, flag: int = 0) -> tuple[list[StepOutput], int, int]:
+    def step_lockstep(self, agree, flag: int = 0, extra: tuple = ()) -> tuple[list[StepOutput], int, int, tuple]:
         """One DP-attention group step: EXACTLY one forward on every rank of the group (an expert-only idle step on
-        a rank without tokens), so the per-layer all-to-alls line up. ``agree((tokens, unfinished, flag))``
+        a rank without tokens), so the per-layer all-to-alls line up. ``agree((tokens, unfinished, flag, *extra))``
         returns the group maxima; the largest step sets the all-to-all capacity. Returns (outputs, group max
-        unfinished — 0: every rank is idle, group max flag — e.g. a stop request seen by any rank)."""
-        batch = self.sched.schedule()
-        cut = self._cut_outputs(batch)
-        host = sampled = None
-        T = 0
-        if not batch.empty:
-            host, sampled = self.runner.build_host(batch)
-            T = host.T
-        t_max, busy, fl = agree((T, int(self.has_unfinished()), int(flag)))
-        if t_max == 0:
-            return cut, busy, fl
-        self.model.ep_t_cap = t_max
-        self.stats["group_steps"] = self.stats.get("group_steps", 0) + 1
-        if host is None:
-            with trace.span("dp_idle_step"):
-                self.model.dp_idle_step()
-            return cut, busy, fl
-        cur = self._launch(batch, host, sampled, None)
-        return cut + self._finish_step(cur), busy, fl
+        unfinished — 0: every rank is idle, group max flag — e.g. a stop request seen by any rank, group maxima of
+        ``extra``).
+
+        With ``async_scheduling`` (default) it pipelines like ``step``: the NEXT step is planned (speculatively, its
+        decode inputs PENDING), agreed and launched while the previous one is still on the GPU, then the previous
+        one is collected — the host never waits for the GPU between group steps, and the agreement itself is a
+        shared-memory exchange (engine/dp_attention.py)."""
+        cut: list[StepOutput] = []
+        batch = host = sampled = None
+        if self._inflight is None or not self.cfg.async_scheduling:
+            batch = self.sched.schedule()
+            cut = self._cut_outputs(batch)
+            if not batch.empty:
+                host, sampled = self.runner.build_host(batch)
+        else:
+            with trace.span("plan_ahead"):
+                plan = self._speculate()
+            if plan is not None:
+                batch, host, sampled = plan.batch, plan.host, plan.sampled
+        T = host.T if host is not None else 0
+        got = agree((T, int(self.has_unfinished()), int(flag)) + tuple(extra))
+        t_max, busy, fl, ext = got[0], got[1], got[2], tuple(got[3:])
+        cur, self._inflight = self._inflight, None
+        if t_max > 0:
+            self.model.ep_t_cap = t_max
+            self.stats["group_steps"] = self.stats.get("group_steps", 0) + 1
+            if host is None:
+                with trace.span("dp_idle_step"):
+                    self.model.dp_idle_step()
+            else:
+                if cur is not None:
+                    self.stats["planned_ahead"] += 1
+                self._inflight = self._launch(batch, host, sampled, cur)
+        outs = cut + (self._finish_step(cur) if cur is not None else [])
+        if not self.cfg.async_scheduling and self._inflight is not None:
+            nxt, self._inflight = self._inflight, None
+            outs += self._finish_step(nxt)
+        return outs, busy, fl, ext
 
     @staticmethod
     def _needs_landed(sampled: list[Sequence]) -> bool:
-        """True if a row's sampling reads the sequence's previous tokens on the host while one is still PENDING."""
+        """True if a row's grammar state would read a token that is still PENDING (the speculative scheduler leaves
+        such rows out, so this only guards the invariant; penalties are device-side and never need landed tokens)."""
         for s in sampled:
-            p = s.params
-            if (p.allowed_tokens_fn is not None or p.presence_penalty or p.frequency_penalty) and PENDING in \
-                    s.output_ids[-2:]:
+            if s.params.allowed_tokens_fn is not None and s.output_ids[-1:] == [PENDING]:
                 return True
         return False
 
@@ -364,9 +383,10 @@ class LLMEngine:
         for s, a, b in batch.prefill:
             self.kvm.commit(s.seq_id, s.num_computed)
         slots = []
-        for s in sampled:
+        known = launched.known or {}
+        for i, s in enumerate(sampled):
             slots.append(len(s.output_ids))
-            s.output_ids.append(PENDING)
+            s.output_ids.append(known.get(i, PENDING))  # a grammar-forced token is known now; others land later
         return _InFlight(sampled, slots, launched, t0)
 
     def _finish_step(self, cur: "_InFlight") -> list[StepOutput]:
@@ -378,6 +398,15 @@ class LLMEngine:
         outs: list[StepOutput] = []
         for s, idx, t in zip(cur.sampled, cur.slots, toks):
             if s.finished:  # ended (stop / abort) while this step was in flight: its row was void
+                continue
+            rb = getattr(s.params.allowed_tokens_fn, "rollback_at", None)
+            if rb is not None and rb(s.output_ids, idx):
+                # drawn under a grammar mask that was planned on a wrong guess about the previous (then pending)
+                # token: discard it and recompute the last position (its KV write was correct: the input token was
+                # the real one, gathered on the device)
+                del s.output_ids[idx:]
+                s.num_computed = s.total_len - 1
+                self.stats["grammar_rollbacks"] = self.stats.get("grammar_rollbacks", 0) + 1
                 continue
             s.output_ids[idx] = t
             self.kvm.append_token(s.seq_id, t)

@@ -8,11 +8,12 @@ cost drops from ~2 ms to ~20 us, which is what lets the host keep up with short 
 shards) and leaves the CPU free for the API loop.
 
 Layout key: (B, decode work items (padded to a power of two), partial slots, prefix work items, cascade on/off, packed-buffer sizes,
-greedy). Everything that changes from step to step — token ids, positions, KV slots, block tables, sequence lengths,
-cascade work items, sampling parameters and seeds — lives in STATIC device buffers that are refreshed (one async
-H2D each) before the replay; intermediates (activations, attention partials, logits) come from a graph memory pool
-shared by all captured layouts. Steps with prefill rows or host-side logits processing (penalties, tool grammars)
-run eagerly. Under tensor parallelism every rank captures the same layouts from the same broadcast plans: the graph
+greedy, logits processing on/off). Everything that changes from step to step — token ids, positions, KV slots, block
+tables, sequence lengths, cascade work items, sampling parameters, seeds and the rows' logits-processing entries
+(grammar mask rows / forced tokens / penalty slots, engine/logits_proc.py: the mask and count tables sit at fixed
+addresses) — lives in STATIC device buffers that are refreshed (one async H2D each) before the replay;
+intermediates (activations, attention partials, logits) come from a graph memory pool shared by all captured
+layouts. Steps with prefill rows run eagerly. Under tensor parallelism every rank captures the same layouts from the same broadcast plans: the graph
 ends with this rank's vocab shard of the logits (the layer seams' custom xGMI all-reduces are inside it — their call
 counters live in device memory), and the logit all-gather + sampler run eagerly after the replay.
 
@@ -45,7 +46,7 @@ class _FakeGraph:
 
 
 class _Entry:
-    __slots__ = ("graph", "s64", "s32", "f32", "topk", "seeds", "out", "layout", "local")
+    __slots__ = ("graph", "s64", "s32", "f32", "topk", "seeds", "out", "layout", "local", "proc")
 
 
 class DecodeGraphs:
@@ -61,11 +62,10 @@ class DecodeGraphs:
     @staticmethod
     def key(h, sp) -> tuple:
         return (h.B, h.n_dec_items, h.dec_sk, h.s_total, h.n_prefix_items, bool(h.cascade_prefix), h.i64.size, h.i32.size,
-                h.n_late, h.late_off, sp.greedy)
+                h.n_late, h.late_off, sp.greedy, sp.proc is not None)
 
     def eligible(self, h, sp) -> bool:
-        return (not self.disabled and h.B > 0 and h.T == h.B and h.n_items == 0 and not sp.procs
-                and not sp.leader_tokens)
+        return not self.disabled and h.B > 0 and h.T == h.B and h.n_items == 0
 
     # ------------------------------------------------------------------------------------------------------------
     def run(self, h, sp) -> torch.Tensor | None:
@@ -121,6 +121,8 @@ class DecodeGraphs:
             e.f32.copy_(r._h2d(np.concatenate([sp.temp, sp.topp])))
             e.topk.copy_(r._h2d(sp.topk))
             e.seeds.copy_(r._h2d(sp.seeds))
+        if sp.proc is not None:
+            e.proc.copy_(r._h2d(sp.proc))
 
     def _capture(self, k: tuple, h, sp) -> tuple[_Entry, torch.Tensor | None]:
         r = self.runner
@@ -133,6 +135,8 @@ class DecodeGraphs:
         e.topk = torch.empty(n, dtype=torch.int32, device=dev)
         e.seeds = torch.empty(n, dtype=torch.int64, device=dev)
         e.out = torch.empty(n, dtype=torch.int64, device=dev)
+        e.proc = torch.empty(n, 8, dtype=torch.int32, device=dev) if sp.proc is not None else None
+        kw = dict(r.proc_tables(sp), proc=e.proc) if sp.proc is not None else {}
         e.layout = copy.copy(h)
         e.layout.i64 = e.layout.i32 = None
         e.layout.patch = []
@@ -146,9 +150,9 @@ class DecodeGraphs:
                 return
             logits = r.model.forward(inp, r.k_caches, r.v_caches)
             if greedy:
-                toks = ops.sample(logits, torch.zeros(n, device=dev))
+                toks = ops.sample(logits, torch.zeros(n, device=dev), **kw)
             else:
-                toks = ops.sample(logits, e.f32[:n], e.f32[n:], e.topk, e.seeds)
+                toks = ops.sample(logits, e.f32[:n], e.f32[n:], e.topk, e.seeds, **kw)
             e.out.copy_(toks)
             r.tok_buf[:n].copy_(toks)  # input ids of the next step's late rows (ModelRunner.views)
 

@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from kafka_llm_service_amd import ops
+from kafka_llm_service_amd.engine.logits_proc import LogitsProcessor, ProcUpdates, spec_forced
 from kafka_llm_service_amd.engine.scheduler import ScheduledBatch
 from kafka_llm_service_amd.engine.sequence import Sequence
 from kafka_llm_service_amd.models.attention import AttnMeta
@@ -62,47 +63,54 @@ class SampleParams:
     topp: np.ndarray
     topk: np.ndarray
     seeds: np.ndarray
-    procs: list          # rows that need host-side logits processing (penalties / token constraints)
+    # per-row device logits processing (engine/logits_proc.py): int32 [n, 8] or None when no row needs it
+    proc: np.ndarray | None
     greedy: bool
-    # TP: the leader's step had host-processed rows, so every rank takes the leader's sampled ids (a device
-    # broadcast) instead of its own draw (followers cannot reproduce the host-side processing)
-    leader_tokens: bool = False
+    upd: ProcUpdates | None = None  # table writes (new grammar mask rows, penalty slots to clear) before sampling
+    known: dict | None = None       # row -> token fixed by the grammar (forced): the host knows it at launch
 
 
 _PLAN_SCALARS = ("B", "T", "nbt", "bt_w", "n_rows", "s_total", "n_dec_items", "n_prefix_items", "cascade_prefix",
                  "n_items", "prefill_splits", "n_merge", "n_late", "late_off", "bt_need", "dec_sk")
 PLAN_HDR = 32  # int64 header of a broadcast step plan
+PLAN_PAYLOAD_IDX = 1 + len(_PLAN_SCALARS) + 4  # header word holding the payload size (pack_plan)
 
 
 def pack_plan(h: HostStep, sp: SampleParams) -> tuple[np.ndarray, np.ndarray]:
     """A launched step as (int64 header [PLAN_HDR], uint8 payload): the fixed-layout wire format a TP leader sends its
     followers (two gloo tensor broadcasts per step; no pickling). Everything a follower needs to run the SAME step:
-    the layout scalars, the packed int64 / int32 buffers and the sampling parameters (every rank samples the
-    all-gathered logits itself, so its device copy of the sampled ids — the next step's late decode inputs — is
-    identical to the leader's)."""
+    the layout scalars, the packed int64 / int32 buffers and the sampling parameters with the logits-processing rows
+    and table updates (every rank samples the all-gathered logits itself with the same grammar masks and penalty
+    counts, so its device copy of the sampled ids — the next step's late decode inputs — is identical to the
+    leader's)."""
     n = sp.temp.shape[0]
     i32 = h.i32.astype(np.int32, copy=False)
     nbt_w = h.nbt * h.bt_w
     if 0 < h.bt_need < h.bt_w:  # ship only the block-table columns that hold pages (followers re-pad with zeros)
         bt = i32[:nbt_w].reshape(h.nbt, h.bt_w)[:, :h.bt_need]
         i32 = np.concatenate([bt.reshape(-1), i32[nbt_w:]])
+    upd = sp.upd if sp.upd is not None else ProcUpdates()
+    proc = sp.proc if sp.proc is not None else np.zeros((0, 8), np.int32)
     parts = [h.i64.astype(np.int64, copy=False), i32,
              sp.temp.astype(np.float32, copy=False), sp.topp.astype(np.float32, copy=False),
-             sp.topk.astype(np.int32, copy=False), sp.seeds.astype(np.int64, copy=False)]
+             sp.topk.astype(np.int32, copy=False), sp.seeds.astype(np.int64, copy=False),
+             proc.astype(np.int32, copy=False), upd.mask_rows.astype(np.int32, copy=False),
+             upd.mask_words.astype(np.int32, copy=False), upd.zero_slots.astype(np.int32, copy=False)]
     payload = np.concatenate([np.ascontiguousarray(a).reshape(-1).view(np.uint8) for a in parts])
     hdr = np.zeros(PLAN_HDR, dtype=np.int64)
     hdr[0] = 1
     k = len(_PLAN_SCALARS)
     hdr[1:1 + k] = [getattr(h, f) for f in _PLAN_SCALARS]
-    hdr[1 + k:1 + k + 6] = [h.i64.size, i32.size, n, int(sp.greedy), int(bool(sp.procs) or sp.leader_tokens),
-                            payload.size]
+    W = upd.mask_words.shape[1] if upd.mask_rows.size else 0
+    hdr[1 + k:1 + k + 9] = [h.i64.size, i32.size, n, int(sp.greedy), payload.size, proc.shape[0],
+                            upd.mask_rows.size, W, upd.zero_slots.size]
     return hdr, payload
 
 
 def unpack_plan(hdr: np.ndarray, payload: np.ndarray) -> tuple[HostStep, SampleParams]:
     k = len(_PLAN_SCALARS)
     h = HostStep(**{f: int(v) for f, v in zip(_PLAN_SCALARS, hdr[1:1 + k])})
-    n64, n32, n, greedy, lead, _ = (int(v) for v in hdr[1 + k:1 + k + 6])
+    n64, n32, n, greedy, _, n_proc, n_mask, W, n_zero = (int(v) for v in hdr[1 + k:1 + k + 9])
     o = 0
 
     def take(dt, cnt):
@@ -119,8 +127,13 @@ def unpack_plan(hdr: np.ndarray, payload: np.ndarray) -> tuple[HostStep, SampleP
         bt = np.zeros((h.nbt, h.bt_w), dtype=np.int32)
         bt[:, :h.bt_need] = h.i32[:nb].reshape(h.nbt, h.bt_need)
         h.i32 = np.concatenate([bt.reshape(-1), h.i32[nb:]])
-    sp = SampleParams(take(np.float32, n), take(np.float32, n), take(np.int32, n), take(np.int64, n), [],
-                      bool(greedy), bool(lead))
+    sp = SampleParams(take(np.float32, n), take(np.float32, n), take(np.int32, n), take(np.int64, n), None,
+                      bool(greedy))
+    proc = take(np.int32, n_proc * 8).reshape(n_proc, 8)
+    upd = ProcUpdates(take(np.int32, n_mask), take(np.int32, n_mask * W).reshape(n_mask, W),
+                      take(np.int32, n_zero))
+    sp.proc = proc if n_proc else None
+    sp.upd = None if upd.empty else upd
     return h, sp
 
 
@@ -136,6 +149,7 @@ class Launched:
     dev_tokens: torch.Tensor | None = None  # the sampler's device output (input ids of the next step's decode rows)
     rows: dict | None = None        # seq_id -> row of dev_tokens
     err_idx: int | None = None      # slot of ModelRunner._err_host holding the custom all-reduce error word
+    known: dict | None = None       # row -> token the grammar forced (known on the host at launch)
 
 
 MIN_DECODE_KEYS = 256      # smallest key range of one decode work item
@@ -390,6 +404,8 @@ class ModelRunner:
         # rows whose token was still being sampled at launch gather their input ids from it on the stream
         self.tok_buf = torch.zeros(max_num_seqs * 2 + 64, dtype=torch.int64, device=self.device)
         self.graphs = None  # engine/graphs.py DecodeGraphs when hipGraph decode is enabled
+        # grammar masks / forced tokens / penalties inside the sampler kernel (tables allocated on first use)
+        self.lp = LogitsProcessor(self.device, self.vocab, max_slots=max(256, max_num_seqs))
 
     # ------------------------------------------------------------------------------------------------------------
     def prepare(self, batch: ScheduledBatch) -> tuple[StepInput, list[Sequence]]:
@@ -541,13 +557,16 @@ class ModelRunner:
         rank)."""
         if not BATCH_UPLOAD:
             return self.views(self._h2d(h.i64), self._h2d(h.i32), h)
+        arrays = [h.i64, h.i32]
         if sp is not None and not sp.greedy and sp.temp.shape[0]:
-            d64, d32, f32, tk, sd = self.stager.upload_many([h.i64, h.i32, np.concatenate([sp.temp, sp.topp]), sp.topk,
-                                                             sp.seeds])
-            self._sp_dev = (sp, f32, tk, sd)
-        else:
-            d64, d32 = self.stager.upload_many([h.i64, h.i32])
-        return self.views(d64, d32, h)
+            arrays += [np.concatenate([sp.temp, sp.topp]), sp.topk, sp.seeds]
+        if sp is not None and sp.proc is not None:
+            arrays.append(sp.proc)
+        dev = self.stager.upload_many(arrays)
+        if len(dev) > 2:
+            has_t = not sp.greedy and sp.temp.shape[0]
+            self._sp_dev = (sp, *(dev[2:5] if has_t else (None, None, None)), dev[-1] if sp.proc is not None else None)
+        return self.views(dev[0], dev[1], h)
 
     def views(self, d64: torch.Tensor, d32: torch.Tensor, h: HostStep) -> StepInput:
         """StepInput over packed device buffers laid out as ``h`` describes (only h's scalars are read, so a hipGraph
@@ -611,12 +630,18 @@ class ModelRunner:
         return self.sample_device(logits, self.sample_params(seqs))
 
     def sample_params(self, seqs: list[Sequence]) -> "SampleParams":
+        """Per-row sampling parameters of a step; rows with a token constraint or penalties get a logits-processing
+        row (engine/logits_proc.py) that the sampler kernel applies on the device. A constrained row's spec is
+        computed from its landed tokens, or past a pending one when the grammar can guess its successor state
+        (engine/constrained.py: a wrong guess rolls the row back one token); a forced token is returned in
+        ``known`` so the engine writes it at launch."""
         n = len(seqs)
         temp = np.empty(n, dtype=np.float32)
         topp = np.empty(n, dtype=np.float32)
         topk = np.empty(n, dtype=np.int32)
         seeds = np.empty(n, dtype=np.int64)
-        procs = []  # (row, seq, allowed) for rows that need penalties or a token constraint
+        rows = []  # (row, seq, allowed) for rows that need penalties or a token constraint
+        known = None
         for i, s in enumerate(seqs):
             p = s.params
             temp[i] = p.temperature
@@ -624,57 +649,49 @@ class ModelRunner:
             topk[i] = p.top_k
             base = p.seed if p.seed is not None else (s.seq_id * 7919)
             seeds[i] = (base * 1000003 + len(s.output_ids)) & 0x7FFFFFFFFFFFFFFF
-            allowed = p.allowed_tokens_fn(s.output_ids) if p.allowed_tokens_fn is not None else None
+            allowed = None
+            if p.allowed_tokens_fn is not None:
+                # (a pending last token is speculated past by the constraint, ToolCallConstraint.__call__)
+                allowed = p.allowed_tokens_fn(s.output_ids)
+                f = spec_forced(allowed) if allowed is not None else None
+                if f is not None:
+                    known = known or {}
+                    known[i] = f
             if allowed is not None or p.presence_penalty or p.frequency_penalty:
-                procs.append((i, s, allowed))
-        return SampleParams(temp, topp, topk, seeds, procs, not temp.any())
+                rows.append((i, s, allowed))
+        proc = upd = None
+        if rows:
+            proc, upd = self.lp.build(rows, n)
+            upd = None if upd.empty else upd
+        return SampleParams(temp, topp, topk, seeds, proc, not temp.any(), upd, known)
+
+    def apply_proc_updates(self, sp: "SampleParams") -> None:
+        """The step's logits-processor table writes, stream-ordered before its sampler (every TP rank)."""
+        if sp.upd is not None:
+            self.lp.apply(sp.upd, self._h2d)
+
+    def proc_tables(self, sp: "SampleParams") -> dict:
+        if sp.proc is None:
+            return {}
+        mask_tab, counts = self.lp.tables()
+        return {"mask_tab": mask_tab, "counts": counts}
 
     def sample_device(self, logits: torch.Tensor, sp: "SampleParams") -> torch.Tensor:
-        if sp.procs:
-            logits = self._process_logits(logits, sp.procs)
         n = logits.shape[0]
         dev = logits.device
-        if sp.greedy:
-            return ops.sample(logits, torch.zeros(n, device=dev))
         pre, self._sp_dev = getattr(self, "_sp_dev", None), None
-        if pre is not None and pre[0] is sp and pre[2].shape[0] == n:  # uploaded with the step's plan
-            _, f32, tk, sd = pre
-            return ops.sample(logits, f32[:n], f32[n:], tk, sd)
+        if pre is not None and pre[0] is not sp:
+            pre = None
+        kw = self.proc_tables(sp)
+        if sp.proc is not None:
+            kw["proc"] = pre[4] if pre is not None and pre[4] is not None else self._h2d(sp.proc)
+        if sp.greedy:
+            return ops.sample(logits, torch.zeros(n, device=dev), **kw)
+        if pre is not None and pre[2] is not None and pre[2].shape[0] == n:  # uploaded with the step's plan
+            _, f32, tk, sd, _ = pre
+            return ops.sample(logits, f32[:n], f32[n:], tk, sd, **kw)
         f32 = self._h2d(np.concatenate([sp.temp, sp.topp]))
-        return ops.sample(logits, f32[:n], f32[n:], self._h2d(sp.topk), self._h2d(sp.seeds))
-
-    def _mask_tensor(self, m) -> torch.Tensor:
-        """Device copy of a constrained.Mask's base vocab mask (cached by key) with its extra ids allowed."""
-        cache = self.__dict__.setdefault("_masks", {})
-        base = cache.get(m.key)
-        if base is None or base.numel() != m.base.shape[0]:
-            base = cache[m.key] = torch.from_numpy(m.base).to(self.device)
-        if not m.extra:
-            return base
-        t = base.clone()
-        t[torch.as_tensor(m.extra, device=self.device, dtype=torch.long)] = True
-        return t
-
-    def _process_logits(self, logits: torch.Tensor, procs) -> torch.Tensor:
-        from kafka_llm_service_amd.engine.constrained import Mask
-
-        logits = logits.float().clone()
-        V = logits.shape[1]
-        for i, s, allowed in procs:
-            p = s.params
-            if (p.presence_penalty or p.frequency_penalty) and s.output_ids:
-                ids = torch.tensor(s.output_ids, device=logits.device)
-                cnt = torch.bincount(ids, minlength=V)[:V].float()
-                logits[i] -= p.frequency_penalty * cnt + p.presence_penalty * (cnt > 0).float()
-            if allowed is None:
-                continue
-            if isinstance(allowed, Mask):
-                keep = self._mask_tensor(allowed)[:V]
-            else:
-                keep = torch.zeros(V, dtype=torch.bool, device=logits.device)
-                keep[torch.as_tensor(allowed, device=logits.device, dtype=torch.long)] = True
-            logits[i].masked_fill_(~keep, float("-inf"))
-        return logits
+        return ops.sample(logits, f32[:n], f32[n:], self._h2d(sp.topk), self._h2d(sp.seeds), **kw)
 
     # ------------------------------------------------------------------------------------------------------------
     @torch.inference_mode()
@@ -715,7 +732,7 @@ class ModelRunner:
         toks = self._run(host, sp)
         rows = {s.seq_id: i for i, s in enumerate(sample_seqs)}
         if self.device.type != "cuda":
-            return Launched(toks.clone(), None, toks, rows)
+            return Launched(toks.clone(), None, toks, rows, known=sp.known)
         n = toks.shape[0]
         # a ring of pinned landing buffers: two steps can be in flight, each D2H needs its own
         ring = self._tok_host
@@ -733,15 +750,21 @@ class ModelRunner:
             car.error_async(self._err_host, err_idx)
         ev = torch.cuda.Event()
         ev.record()
-        return Launched(out, ev, toks, rows, err_idx)
+        return Launched(out, ev, toks, rows, err_idx, sp.known)
 
     def _custom_ar(self):
-        if self.model.tp == 1:
-            return None
+        """The IPC collective whose error word rides back with every step's ids: the TP group's custom all-reduce,
+        or — data-parallel attention (tp = 1) — the EP group's IPC all-to-all (a peer that stops arriving makes its
+        a2a waits time out; without this check the live ranks would stream tokens built from stale expert rows)."""
         if not hasattr(self, "_car"):
+            from kafka_llm_service_amd.parallel import comm
             from kafka_llm_service_amd.parallel import state as pstate
 
-            self._car = pstate.custom_ar()
+            self._car = None
+            if self.model.tp > 1:
+                self._car = pstate.custom_ar()
+            elif getattr(self.model, "dp_attention", False) and self.model.ep > 1 and self.device.type == "cuda":
+                self._car = comm.get_custom(pstate.get().ep_group)
         return self._car
 
     @torch.inference_mode()
@@ -756,6 +779,7 @@ class ModelRunner:
         """Forward + sampling of one step (hipGraph replay for eligible decode steps): the sampled ids on the device,
         also left in ``tok_buf`` for the next step's late decode rows."""
         toks = None
+        self.apply_proc_updates(sp)
         if self.graphs is not None and self.graphs.eligible(host, sp):
             toks = self.graphs.run(host, sp)
         if toks is None:
@@ -763,17 +787,12 @@ class ModelRunner:
             logits = self.model.forward(inp, self.k_caches, self.v_caches)
             toks = self.sample_device(logits, sp)
             self.tok_buf[:toks.shape[0]].copy_(toks)
-        if sp.leader_tokens or (sp.procs and self.model.tp > 1):
-            # host-processed rows: the leader's draw is the truth; followers overwrite theirs (stream-ordered)
-            from kafka_llm_service_amd.parallel import state as pstate
-
-            pstate.tp_broadcast_from_leader(toks)
-            self.tok_buf[:toks.shape[0]].copy_(toks)
         return toks
 
     def collect(self, h: "Launched") -> list[int]:
         if h.event is not None:
             h.event.synchronize()
         if h.err_idx is not None and int(self._err_host[h.err_idx]) != 0:
-            raise CollectiveError("custom all-reduce: a TP peer did not arrive within 2 s; failing the replica")
+            raise CollectiveError("custom all-reduce / all-to-all: a peer did not arrive within 2 s; failing the "
+                                  "replica")
         return h.tokens.tolist()

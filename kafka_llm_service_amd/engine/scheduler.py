@@ -19,7 +19,7 @@ import math
 from collections import deque
 from dataclasses import dataclass, field
 
-from kafka_llm_service_amd.engine.sequence import Sequence, SeqStatus
+from kafka_llm_service_amd.engine.sequence import PENDING, Sequence, SeqStatus
 
 
 @dataclass
@@ -127,6 +127,17 @@ class Scheduler:
         if self.kv.has_seq(seq.seq_id):
             self.kv.free_sequence(seq.seq_id)
 
+    @staticmethod
+    def _grammar_plannable(seq: Sequence) -> bool:
+        """May a grammar-constrained row be planned ahead of its in-flight token? Constraints that can speculate
+        past a pending token (``ToolCallConstraint.plan_state``: free strings, digits, the first token of "auto")
+        say so; any other allowed_tokens_fn waits while its last token is PENDING."""
+        fn = seq.params.allowed_tokens_fn
+        ps = getattr(fn, "plan_state", None)
+        if ps is None:
+            return seq.output_ids[-1:] != [PENDING]
+        return ps(seq.output_ids) == "ok"
+
     def _cost(self, start: int, end: int) -> float:
         """Token-equivalents of prefilling positions [start, end) (SchedulerConfig.prefill_cost_budget)."""
         n = end - start
@@ -134,8 +145,9 @@ class Scheduler:
 
     def schedule(self, speculative: bool = False) -> ScheduledBatch:
         """Build the next batch. ``speculative``: planned while the previous step is still on the GPU (its sampled
-        tokens are PENDING placeholders): sequences whose pending token is their last by length are left out, and a
-        plan that would need a preemption is abandoned (``NeedSync``) — the engine then plans after the step lands."""
+        tokens are PENDING placeholders): sequences whose pending token is their last by length, and grammar-constrained
+        sequences whose next mask depends on a pending token, are left out, and a plan that would need a preemption is
+        abandoned (``NeedSync``) — the engine then plans after the step lands."""
         cfg = self.cfg
         batch = ScheduledBatch()
         budget = cfg.max_num_batched_tokens
@@ -144,6 +156,11 @@ class Scheduler:
             if seq.status != SeqStatus.RUNNING or seq.remaining != 1:
                 continue
             if speculative and (len(seq.output_ids) >= seq.params.max_tokens or seq.total_len >= cfg.max_model_len):
+                continue
+            if speculative and seq.params.allowed_tokens_fn is not None and not self._grammar_plannable(seq):
+                # its grammar state (the mask of the next token) needs the token still being sampled (a choice:
+                # tool name / enum / boolean), or a landed token broke the grammar's guess: this row alone sits
+                # out the plan-ahead step and rejoins once the token has landed — the other rows keep the pipeline
                 continue
             while not self.kv.ensure_capacity(seq.seq_id, seq.total_len):
                 if speculative:

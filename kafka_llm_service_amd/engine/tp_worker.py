@@ -30,7 +30,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from kafka_llm_service_amd.engine.model_runner import _PLAN_SCALARS, PLAN_HDR, pack_plan, unpack_plan
+from kafka_llm_service_amd.engine.model_runner import PLAN_HDR, PLAN_PAYLOAD_IDX, pack_plan, unpack_plan
 from kafka_llm_service_amd.parallel import state as pstate
 
 log = logging.getLogger("kafka.tp")
@@ -42,7 +42,7 @@ def leader_src() -> int:
     return st.rank - st.tp_rank
 
 
-_HDR_BYTES = 1 + len(_PLAN_SCALARS) + 5  # header slot holding the payload size
+_HDR_BYTES = PLAN_PAYLOAD_IDX             # header slot holding the payload size
 _GLOO_MARK = 2                           # hdr[0]: the payload of this plan follows over gloo (larger than a slot)
 
 
@@ -94,6 +94,10 @@ class PlanTransport:
             if ch is not None:
                 ch.close()
             return None
+        if self.leader:
+            # every follower has attached: drop the name now (the mappings stay valid), so a group killed with
+            # SIGKILL by the stall monitor / respawn leaves nothing in /dev/shm
+            ch.unlink()
         return ch
 
     # --- leader ---------------------------------------------------------------------------------------------------
@@ -118,7 +122,9 @@ class PlanTransport:
     def recv(self) -> tuple[np.ndarray, np.ndarray] | None:
         """The next plan (header, payload), or None at exit. Views into the ring stay valid until ``done()``."""
         if self.ch is not None:
-            hdr, payload = self.ch.recv(self.timeout)
+            # no time limit while the leader process lives: an idle replica is not a dead one (the channel
+            # raises at once when the leader's pid is gone; in-step waits stay bounded by self.timeout)
+            hdr, payload = self.ch.recv(-1.0)
             if int(hdr[0]) == 0:
                 self.ch.ack()
                 return None

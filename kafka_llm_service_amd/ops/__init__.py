@@ -273,7 +273,11 @@ def _sample_ws(dev: torch.device, n: int) -> torch.Tensor:
     return t
 
 
-def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, step=None, out=None) -> torch.Tensor:
+def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, step=None, out=None, proc=None,
+           mask_tab=None, counts=None) -> torch.Tensor:
+    """Sampled ids [B] (int64). ``proc`` int32 [B, 8] turns on the per-row logits processing of the kernel (grammar
+    bitmask rows of ``mask_tab``, forced ids, presence / frequency penalties from ``counts``, which the sampler
+    updates with every drawn token; engine/logits_proc.py builds all three)."""
     B = logits.shape[0]
     if out is None:
         out = torch.empty(B, dtype=torch.long, device=logits.device)
@@ -281,9 +285,9 @@ def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, step=No
         V = logits.shape[1]
         nsplit = _SAMPLE_SPLIT if V >= 16384 else 1  # a row over 8 workgroups (greedy / plain temperature)
         ws = _sample_ws(logits.device, 65536 + 2 * B * nsplit) if nsplit > 1 else None
-        ext().sample(logits, temperature, top_p, top_k, seeds, step, out, ws, nsplit)
+        ext().sample(logits, temperature, top_p, top_k, seeds, step, out, ws, nsplit, proc, mask_tab, counts)
     else:
-        ref.sample(logits, temperature, top_p, top_k, seeds, step, out)
+        ref.sample(logits, temperature, top_p, top_k, seeds, step, out, proc, mask_tab, counts)
     return out
 
 

@@ -43,7 +43,8 @@ hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows
                              int64_t out_stride, float* lse_out, hipStream_t st);
 hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
                          const float* top_p, const int* top_k, const int64_t* seeds, const int64_t* step,
-                         int64_t* out_tokens, int* ws, int nsplit, hipStream_t st);
+                         int64_t* out_tokens, int* ws, int nsplit, const int* proc, const uint32_t* mask_tab,
+                         int64_t mask_ld, int* counts, int64_t cnt_ld, hipStream_t st);
 int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits);
 hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt, int kc,
                                      int splits, int nt, int kw, int glu, bf16* Y, int64_t ldy, float* P,
@@ -396,7 +397,8 @@ static void attn_merge(at::Tensor part, at::Tensor lse, at::Tensor out, c10::opt
 
 static void sample(at::Tensor logits, c10::optional<at::Tensor> temperature, c10::optional<at::Tensor> top_p,
                    c10::optional<at::Tensor> top_k, c10::optional<at::Tensor> seeds, c10::optional<at::Tensor> step,
-                   at::Tensor out, c10::optional<at::Tensor> ws, int64_t nsplit) {
+                   at::Tensor out, c10::optional<at::Tensor> ws, int64_t nsplit, c10::optional<at::Tensor> proc,
+                   c10::optional<at::Tensor> mask_tab, c10::optional<at::Tensor> counts) {
   CHECK_CUDA(logits); CHECK_DT(out, at::kLong);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [B, V]");
   const bool is_bf16 = logits.scalar_type() == at::kBFloat16;
@@ -421,11 +423,36 @@ static void sample(at::Tensor logits, c10::optional<at::Tensor> temperature, c10
                 "sample: workspace must be int32 [>= 65536 + 2 * B * nsplit]");
     wp = ws->data_ptr<int>();
   }
+  // logits processing: proc int32 [B, 8] (mode, mask row / forced id, penalty slot, presence, frequency), the
+  // bitmask table uint32-as-int32 [rows, >= V / 32] and the count table int32 [slots, >= V rounded to 8]. The
+  // kernel trusts the row / slot / forced-id values: the host builder (engine/logits_proc.py) range-checks them
+  // against these tables before the plan is uploaded
+  const int* pp = nullptr;
+  const uint32_t* mt = nullptr;
+  int* cp = nullptr;
+  int64_t mld = 0, cld = 0;
+  if (proc.has_value()) {
+    TORCH_CHECK(proc->is_cuda() && proc->scalar_type() == at::kInt && proc->is_contiguous() && proc->dim() == 2 &&
+                    proc->size(0) >= B && proc->size(1) == 8, "sample: proc must be int32 [>= B, 8] on the GPU");
+    TORCH_CHECK(mask_tab.has_value() && mask_tab->is_cuda() && mask_tab->scalar_type() == at::kInt &&
+                    mask_tab->is_contiguous() && mask_tab->dim() == 2 && mask_tab->size(1) * 32 >= V,
+                "sample: mask_tab must be int32 [rows, >= V / 32] on the GPU");
+    pp = proc->data_ptr<int>();
+    mt = reinterpret_cast<const uint32_t*>(mask_tab->data_ptr<int>());
+    mld = mask_tab->size(1);
+    if (counts.has_value()) {
+      TORCH_CHECK(counts->is_cuda() && counts->scalar_type() == at::kInt && counts->is_contiguous() &&
+                      counts->dim() == 2 && counts->size(1) >= ((V + 7) & ~7) && counts->size(1) % 8 == 0,
+                  "sample: counts must be int32 [slots, >= V rounded up to 8]");
+      cp = counts->data_ptr<int>();
+      cld = counts->size(1);
+    }
+  }
   CHECK_HIP(kafka_launch_sample(logits.data_ptr(), is_bf16, logits.stride(0), B, V,
                                  (const float*)fp(temperature, at::kFloat), (const float*)fp(top_p, at::kFloat),
                                  (const int*)fp(top_k, at::kInt), (const int64_t*)fp(seeds, at::kLong),
-                                 (const int64_t*)st, out.data_ptr<int64_t>(), wp, wp ? (int)nsplit : 1,
-                                 cur_stream()));
+                                 (const int64_t*)st, out.data_ptr<int64_t>(), wp, wp ? (int)nsplit : 1, pp, mt, mld,
+                                 cp, cld, cur_stream()));
 }
 
 // (mt, kc, splits) of the weight-streaming decode GEMM for a shape, or (0, 0, 0) if unsupported
@@ -853,7 +880,8 @@ PYBIND11_MODULE(_kafka_ops, m) {
         py::arg("block_tables"), py::arg("rows"), py::arg("start"), py::arg("out_part"), py::arg("lse_part"), py::arg("scale"), py::arg("out") = py::none(),
         py::arg("tickets") = py::none(), py::arg("pre_part") = py::none());
   m.def("sample", &sample, py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"),
-        py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none(), py::arg("nsplit") = 1);
+        py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none(), py::arg("nsplit") = 1,
+        py::arg("proc") = py::none(), py::arg("mask_tab") = py::none(), py::arg("counts") = py::none());
   m.def("wstream_plan", &wstream_plan);
   m.def("wstream_gemm", &wstream_gemm);
   m.def("skinny_plan", &skinny_plan);

@@ -90,18 +90,100 @@ __device__ __forceinline__ float gumbel_fast(uint64_t key, uint32_t idx) {
   return -__logf(-__logf(fminf(u, 0.99999994f)));
 }
 
-template <typename T>
+// Per-row logits processing on the device (PROC instantiation; VERDICT r03 "Next round" #3): proc[row] = int32 x 8
+//   [0] mode: 0 = none, 1 = vocab bitmask (row [1] of mask_tab), 2 = forced token ([1] is the id: no draw at all)
+//   [2] penalty slot: row of counts[slot][V] (the row's generated-token counts, -1 = none)
+//   [3] presence penalty, [4] frequency penalty (fp32 bits)
+// The logit of token i becomes  x_i - freq * c_i - (c_i > 0 ? pres : 0)  (OpenAI presence / frequency penalties,
+// before temperature), or -inf where the grammar mask has a zero bit; the sampler then runs unchanged over it, and
+// the thread that writes the row's token also bumps counts[slot][token] — the next step (stream-ordered) sees it, so
+// penalties need no landed tokens on the host and no per-row torch ops over the [B, V] logits.
+struct RowProc {
+  int mode, arg, slot;
+  float pres, freq;
+  const uint32_t* mask;
+  int* cnt;
+};
+
+template <bool PROC>
+__device__ __forceinline__ RowProc row_proc(const int* proc, const uint32_t* mask_tab, int64_t mask_ld, int* counts,
+                                            int64_t cnt_ld, int row) {
+  RowProc r{0, -1, -1, 0.f, 0.f, nullptr, nullptr};
+  if constexpr (PROC) {
+    const int* p = proc + (int64_t)row * 8;
+    r.mode = p[0];
+    r.arg = p[1];
+    r.slot = p[2];
+    r.pres = __int_as_float(p[3]);
+    r.freq = __int_as_float(p[4]);
+    if (r.mode == 1) r.mask = mask_tab + (int64_t)r.arg * mask_ld;
+    if (r.slot >= 0) r.cnt = counts + (int64_t)r.slot * cnt_ld;
+  }
+  return r;
+}
+
+// 8 logits starting at index i0 (a multiple of 8), processed
+template <typename T, bool PROC>
+__device__ __forceinline__ void load8p(const T* x, int i0, const RowProc& rp, float (&v)[8]) {
+  Vec8<T>::load(x + i0, v);
+  if constexpr (PROC) {
+    if (rp.cnt != nullptr) {
+      const int4 c0 = *reinterpret_cast<const int4*>(rp.cnt + i0);
+      const int4 c1 = *reinterpret_cast<const int4*>(rp.cnt + i0 + 4);
+      const int c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] -= rp.freq * (float)c[j] + (c[j] > 0 ? rp.pres : 0.f);
+    }
+    if (rp.mask != nullptr) {
+      const uint32_t bits = (rp.mask[i0 >> 5] >> (i0 & 31)) & 0xffu;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (!((bits >> j) & 1u)) v[j] = -INFINITY;
+    }
+  }
+}
+
+template <typename T, bool PROC>
+__device__ __forceinline__ float load1p(const T* x, int i, const RowProc& rp) {
+  float v = (float)x[i];
+  if constexpr (PROC) {
+    if (rp.cnt != nullptr) {
+      const int c = rp.cnt[i];
+      v -= rp.freq * (float)c + (c > 0 ? rp.pres : 0.f);
+    }
+    if (rp.mask != nullptr && !((rp.mask[i >> 5] >> (i & 31)) & 1u)) v = -INFINITY;
+  }
+  return v;
+}
+
+template <bool PROC>
+__device__ __forceinline__ void emit_token(int64_t* out_tokens, int row, int tok, int V, const RowProc& rp) {
+  tok = tok >= 0 && tok < V ? tok : 0;  // an all-NaN row (a broken upstream kernel) must not yield an id >= V
+  out_tokens[row] = tok;
+  if constexpr (PROC) {
+    if (rp.cnt != nullptr) rp.cnt[tok] += 1;  // the row's only writer this step (one row per sequence)
+  }
+}
+
+template <typename T, bool PROC>
 __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logits, int64_t stride, int V,
                                                       const float* __restrict__ temperature,
                                                       const float* __restrict__ top_p, const int* __restrict__ top_k,
                                                       const int64_t* __restrict__ seeds, const int64_t* __restrict__ step_ptr,
                                                       int64_t* __restrict__ out_tokens, int max_rounds,
-                                                      int* __restrict__ ws) {
+                                                      int* __restrict__ ws, const int* __restrict__ proc,
+                                                      const uint32_t* __restrict__ mask_tab, int64_t mask_ld,
+                                                      int* __restrict__ counts, int64_t cnt_ld) {
   __shared__ float sv[SNT / 64];
   __shared__ int si[SNT / 64];
   __shared__ float red[SNT / 64];
   const int row = blockIdx.x, sp = blockIdx.y, nsplit = gridDim.y;
   const T* x = logits + (int64_t)row * stride;
+  const RowProc rp = row_proc<PROC>(proc, mask_tab, mask_ld, counts, cnt_ld, row);
+  if (PROC && rp.mode == 2) {  // forced token (a fixed piece of a tool-call grammar): every split returns, no ticket
+    if (sp == 0 && threadIdx.x == 0) emit_token<PROC>(out_tokens, row, rp.arg, V, rp);
+    return;
+  }
   const float temp = temperature ? temperature[row] : 0.f;
   const int nvec = V >> 3;
   const int tail0 = nvec << 3;
@@ -121,7 +203,7 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
     ArgMax a{-INFINITY, 0x7fffffff};
     for (int vi = v0 + threadIdx.x; vi < v1; vi += SNT) {
       float v[8];
-      Vec8<T>::load(x + vi * 8, v);
+      load8p<T, PROC>(x, vi * 8, rp, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xv = v[j] * inv_t;
@@ -130,13 +212,13 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
     }
     if (sp == nsplit - 1)
       for (int i = tail0 + threadIdx.x; i < V; i += SNT) {
-        const float xv = (float)x[i] * inv_t;
+        const float xv = load1p<T, PROC>(x, i, rp) * inv_t;
         a = better(a, ArgMax{greedy ? xv : xv + gumbel_fast(key, i), i});
       }
     a = block_argmax(a, sv, si);
     if (threadIdx.x != 0) return;
     if (nsplit == 1) {
-      out_tokens[row] = a.i < V ? a.i : 0;  // an all-NaN row (a broken upstream kernel) must not yield an id >= V
+      emit_token<PROC>(out_tokens, row, a.i, V, rp);
       return;
     }
     // ws: tickets (zero, re-armed here) | [B][nsplit][2] (value bits, index)
@@ -152,7 +234,7 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
     for (int k = 0; k < nsplit; ++k)
       r = better(r, ArgMax{__int_as_float(__hip_atomic_load(p0 + 2 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
                            __hip_atomic_load(p0 + 2 * k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)});
-    out_tokens[row] = r.i < V ? r.i : 0;
+    emit_token<PROC>(out_tokens, row, r.i, V, rp);
     return;
   }
   if (sp != 0) return;  // top-k / top-p rows: one workgroup runs the whole-row rejection sampler
@@ -163,24 +245,22 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
   // pass 1: max of x (needed for the mass test only)
   float mx = -INFINITY;
   float z = 0.f;
-  if (filtered) {
-    for (int vi = threadIdx.x; vi < nvec; vi += SNT) {
-      float v[8];
-      Vec8<T>::load(x + vi * 8, v);
+  for (int vi = threadIdx.x; vi < nvec; vi += SNT) {
+    float v[8];
+    load8p<T, PROC>(x, vi * 8, rp, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) mx = fmaxf(mx, v[j] * inv_t);
-    }
-    for (int i = tail0 + threadIdx.x; i < V; i += SNT) mx = fmaxf(mx, (float)x[i] * inv_t);
-    mx = block_max<SNT>(mx, red);
-    for (int vi = threadIdx.x; vi < nvec; vi += SNT) {
-      float v[8];
-      Vec8<T>::load(x + vi * 8, v);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) z += __expf(v[j] * inv_t - mx);
-    }
-    for (int i = tail0 + threadIdx.x; i < V; i += SNT) z += __expf((float)x[i] * inv_t - mx);
-    z = block_sum<SNT>(z, red);
+    for (int j = 0; j < 8; ++j) mx = fmaxf(mx, v[j] * inv_t);
   }
+  for (int i = tail0 + threadIdx.x; i < V; i += SNT) mx = fmaxf(mx, load1p<T, PROC>(x, i, rp) * inv_t);
+  mx = block_max<SNT>(mx, red);
+  for (int vi = threadIdx.x; vi < nvec; vi += SNT) {
+    float v[8];
+    load8p<T, PROC>(x, vi * 8, rp, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z += __expf(v[j] * inv_t - mx);
+  }
+  for (int i = tail0 + threadIdx.x; i < V; i += SNT) z += __expf(load1p<T, PROC>(x, i, rp) * inv_t - mx);
+  z = block_sum<SNT>(z, red);
 
   float pivot = -INFINITY;
   int result = -1;
@@ -189,7 +269,7 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
     ArgMax a{-INFINITY, 0x7fffffff};
     for (int vi = threadIdx.x; vi < nvec; vi += SNT) {
       float v[8];
-      Vec8<T>::load(x + vi * 8, v);
+      load8p<T, PROC>(x, vi * 8, rp, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xv = v[j] * inv_t;
@@ -197,20 +277,16 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
       }
     }
     for (int i = tail0 + threadIdx.x; i < V; i += SNT) {
-      const float xv = (float)x[i] * inv_t;
+      const float xv = load1p<T, PROC>(x, i, rp) * inv_t;
       if (xv > pivot) a = better(a, ArgMax{xv + gumbel(seed, stream, i), i});
     }
     a = block_argmax(a, sv, si);
     if (a.i == 0x7fffffff) break;
-    if (!filtered) {
-      result = a.i;
-      break;
-    }
-    const float xc = (float)x[a.i] * inv_t;
+    const float xc = load1p<T, PROC>(x, a.i, rp) * inv_t;
     float mass = 0.f, cnt = 0.f;
     for (int vi = threadIdx.x; vi < nvec; vi += SNT) {
       float v[8];
-      Vec8<T>::load(x + vi * 8, v);
+      load8p<T, PROC>(x, vi * 8, rp, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xv = v[j] * inv_t;
@@ -221,7 +297,7 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
       }
     }
     for (int i = tail0 + threadIdx.x; i < V; i += SNT) {
-      const float xv = (float)x[i] * inv_t;
+      const float xv = load1p<T, PROC>(x, i, rp) * inv_t;
       if (xv > xc) {
         mass += __expf(xv - mx);
         cnt += 1.f;
@@ -241,32 +317,41 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
     ArgMax a{-INFINITY, 0x7fffffff};
     for (int vi = threadIdx.x; vi < nvec; vi += SNT) {
       float v[8];
-      Vec8<T>::load(x + vi * 8, v);
+      load8p<T, PROC>(x, vi * 8, rp, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) a = better(a, ArgMax{v[j], vi * 8 + j});
     }
-    for (int i = tail0 + threadIdx.x; i < V; i += SNT) a = better(a, ArgMax{(float)x[i], i});
+    for (int i = tail0 + threadIdx.x; i < V; i += SNT) a = better(a, ArgMax{load1p<T, PROC>(x, i, rp), i});
     a = block_argmax(a, sv, si);
     result = a.i;
   }
-  if (threadIdx.x == 0) out_tokens[row] = result >= 0 && result < V ? result : 0;
+  if (threadIdx.x == 0) emit_token<PROC>(out_tokens, row, result, V, rp);
 }
 
 // ws (optional): int32 workspace of >= SAMPLE_MAX_ROWS + 2 * B * nsplit entries whose first SAMPLE_MAX_ROWS are zero
-// (tickets, re-armed by the kernel); without it every row is one workgroup.
+// (tickets, re-armed by the kernel); without it every row is one workgroup. proc (optional, int32 [B, 8], see
+// RowProc) selects the logits-processing instantiation; mask_tab uint32 [rows, mask_ld] and counts int32
+// [slots, cnt_ld] (cnt_ld >= V rounded up to 8) are only read for rows that name them.
 extern "C" hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
                          const float* top_p, const int* top_k, const int64_t* seeds, const int64_t* step,
-                         int64_t* out_tokens, int* ws, int nsplit, hipStream_t st) {
+                         int64_t* out_tokens, int* ws, int nsplit, const int* proc, const uint32_t* mask_tab,
+                         int64_t mask_ld, int* counts, int64_t cnt_ld, hipStream_t st) {
   if (B == 0) return hipSuccess;
   if (ws == nullptr || nsplit < 1) nsplit = 1;
   if (B > SAMPLE_MAX_ROWS || nsplit > 64) return hipErrorInvalidValue;
+  if (proc != nullptr && (mask_ld * 32 < V || (counts != nullptr && cnt_ld < ((V + 7) & ~7))))
+    return hipErrorInvalidValue;
   const dim3 grid(B, nsplit);
-  if (is_bf16)
-    sample_kernel<bf16><<<grid, SNT, 0, st>>>(reinterpret_cast<const bf16*>(logits), stride, V, temperature, top_p,
-                                              top_k, seeds, step, out_tokens, 32, ws);
-  else
-    sample_kernel<float><<<grid, SNT, 0, st>>>(reinterpret_cast<const float*>(logits), stride, V, temperature, top_p,
-                                               top_k, seeds, step, out_tokens, 32, ws);
+#define KAFKA_SAMPLE(T_, P_)                                                                                       \
+  sample_kernel<T_, P_><<<grid, SNT, 0, st>>>(reinterpret_cast<const T_*>(logits), stride, V, temperature, top_p, \
+                                              top_k, seeds, step, out_tokens, 32, ws, proc, mask_tab, mask_ld,     \
+                                              counts, cnt_ld)
+  if (is_bf16) {
+    if (proc) KAFKA_SAMPLE(bf16, true); else KAFKA_SAMPLE(bf16, false);
+  } else {
+    if (proc) KAFKA_SAMPLE(float, true); else KAFKA_SAMPLE(float, false);
+  }
+#undef KAFKA_SAMPLE
   return hipGetLastError();
 }
 

@@ -332,12 +332,44 @@ def attn_merge(part, lse, out, lse_out=None):
                                                  torch.full_like(L[..., 0], float("-inf"))))
 
 
-def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, step=None, out=None):
+def process_logits(logits, proc, mask_tab, counts):
+    """The sampler's per-row logits processing (csrc/sampling.hip RowProc) in fp32: penalties from the row's token
+    counts, then the grammar bitmask (-inf where a bit is 0). Returns (processed fp32 logits, forced ids or -1)."""
+    B, V = logits.shape
+    x = logits.float().clone()
+    forced = torch.full((B,), -1, dtype=torch.long)
+    pr = proc[:B].cpu()
+    for b in range(B):
+        mode, arg, slot = int(pr[b, 0]), int(pr[b, 1]), int(pr[b, 2])
+        pres, freq = pr[b, 3:5].clone().view(torch.float32).tolist()
+        if mode == 2:
+            forced[b] = arg
+            continue
+        if slot >= 0:
+            c = counts[slot, :V].to(x.device).float()
+            x[b] -= freq * c + pres * (c > 0).float()
+        if mode == 1:
+            words = mask_tab[arg].to(torch.int64) & 0xFFFFFFFF
+            bits = (words[:, None] >> torch.arange(32)) & 1
+            keep = bits.reshape(-1)[:V].bool().to(x.device)
+            x[b].masked_fill_(~keep, float("-inf"))
+    return x, forced
+
+
+def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, step=None, out=None, proc=None,
+           mask_tab=None, counts=None):
     """CPU sampler with the same semantics (not the same random stream) as the HIP kernel."""
     B, V = logits.shape
-    x = logits.float()
+    forced = None
+    if proc is not None:
+        x, forced = process_logits(logits, proc, mask_tab, counts)
+    else:
+        x = logits.float()
     res = torch.empty(B, dtype=torch.long, device=logits.device)
     for b in range(B):
+        if forced is not None and int(forced[b]) >= 0:
+            res[b] = int(forced[b])
+            continue
         t = float(temperature[b]) if temperature is not None else 0.0
         if not t > 0:
             res[b] = int(torch.argmax(x[b]))
@@ -361,6 +393,11 @@ def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, step=No
         gen.manual_seed((seed * 1000003 + stepv) & 0x7FFFFFFFFFFFFFFF)
         idx = torch.multinomial(ps.cpu() / ps.sum().cpu(), 1, generator=gen)
         res[b] = order[idx.to(order.device)]
+    if proc is not None and counts is not None:
+        for b in range(B):
+            slot = int(proc[b, 2])
+            if slot >= 0:
+                counts[slot, int(res[b])] += 1
     if out is not None:
         out[:B].copy_(res)
         return out

@@ -422,11 +422,13 @@ class KVManager {
 
 namespace kafka {
 void register_plan_channel(py::module& m);  // plan_channel.cpp
+void register_group_board(py::module& m);   // group_board.cpp
 }
 
 PYBIND11_MODULE(_kafka_runtime, m) {
   m.doc() = "kafka_llm_service_amd native runtime: paged KV block manager + prefix cache + TP plan channel";
   kafka::register_plan_channel(m);
+  kafka::register_group_board(m);
   py::class_<kafka::KVManager>(m, "KVManager")
       .def(py::init<int, int, bool>(), py::arg("num_blocks"), py::arg("page") = 16, py::arg("prefix_cache") = true)
       .def_property_readonly("page", &kafka::KVManager::page)

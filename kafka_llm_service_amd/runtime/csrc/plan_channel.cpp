@@ -11,11 +11,18 @@
 //   * publish: wait until every follower has released slot seq % nslots (ack >= seq + 1 - nslots), memcpy, then
 //     seq = seq + 1 (release). recv: wait for seq > ack (acquire) and hand out zero-copy views of the slot; the
 //     follower acks once it has consumed the plan (uploaded it), so the leader may run up to nslots - 1 plans ahead;
-//   * every wait is bounded (a dead peer raises TimeoutError after `timeout_s`; the replica then fails and is
-//     respawned) and backs off from pause-spinning to yielding to short sleeps, so an idle
-//     follower does not burn a core.
+//   * every wait watches its peer's PROCESS: the leader's pid sits in the header and each follower's pid next to
+//     its ack word, and a waiter whose peer has exited raises at once ("peer process is gone"; the replica then
+//     fails and is respawned). A follower waiting for the next plan waits as long as its leader
+//     lives (timeout_s < 0: an idle replica is not a dead one — ADVICE r03); the leader's back-pressure wait for
+//     acks inside a step stays bounded by timeout_s. Waits back off from pause-spinning to yielding to short
+//     sleeps, so an idle follower does not burn a core;
+//   * the leader unlinks the segment name once every follower has attached (``unlink``): the mappings stay valid,
+//     and a group killed with SIGKILL leaves nothing behind in /dev/shm.
 // Single producer / single consumer per ack word: the only atomics needed are acquire/release loads and stores.
+#include <errno.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <sched.h>
@@ -43,15 +50,24 @@ struct alignas(64) ChanWord {
   char pad[64 - sizeof(std::atomic<uint64_t>)];
 };
 
+struct alignas(64) AckWord {
+  std::atomic<uint64_t> v;
+  std::atomic<int64_t> pid;  // the follower process (0 until it attaches)
+  char pad[64 - 2 * sizeof(std::atomic<uint64_t>)];
+};
+
 struct ChanHeader {
   uint64_t magic;
   uint64_t nslots;
   uint64_t slot_bytes;
   uint64_t nfollow;
-  char pad0[32];
+  int64_t leader_pid;
+  char pad0[24];
   ChanWord seq;
-  ChanWord acks[kMaxFollowers];
+  AckWord acks[kMaxFollowers];
 };
+
+static bool process_gone(int64_t pid) { return pid > 0 && kill((pid_t)pid, 0) != 0 && errno == ESRCH; }
 
 static_assert(sizeof(ChanHeader) % 64 == 0, "header lines");
 
@@ -74,8 +90,12 @@ class PlanChannel {
     hdr_->nslots = (uint64_t)nslots;
     hdr_->slot_bytes = (uint64_t)slot_bytes;
     hdr_->nfollow = (uint64_t)nfollow;
+    hdr_->leader_pid = (int64_t)getpid();
     hdr_->seq.v.store(0, std::memory_order_relaxed);
-    for (int i = 0; i < kMaxFollowers; ++i) hdr_->acks[i].v.store(0, std::memory_order_relaxed);
+    for (int i = 0; i < kMaxFollowers; ++i) {
+      hdr_->acks[i].v.store(0, std::memory_order_relaxed);
+      hdr_->acks[i].pid.store(0, std::memory_order_relaxed);
+    }
     std::atomic_thread_fence(std::memory_order_release);
     hdr_->magic = kChanMagic;
   }
@@ -93,6 +113,15 @@ class PlanChannel {
     map(fd);
     if (hdr_->magic != kChanMagic || idx < 0 || (uint64_t)idx >= hdr_->nfollow)
       throw std::runtime_error("PlanChannel: bad segment or follower index");
+    hdr_->acks[idx].pid.store((int64_t)getpid(), std::memory_order_release);
+  }
+
+  // leader: drop the segment's name (every follower has attached; the mappings stay valid)
+  void unlink() {
+    if (leader_ && !unlinked_) {
+      shm_unlink(name_.c_str());
+      unlinked_ = true;
+    }
   }
 
   ~PlanChannel() { close_(); }
@@ -121,7 +150,7 @@ class PlanChannel {
       py::gil_scoped_release nogil;
       for (uint64_t f = 0; f < hdr_->nfollow; ++f)
         wait_until([&] { return hdr_->acks[f].v.load(std::memory_order_acquire) >= need; }, timeout_s,
-                   "a follower stopped consuming plans");
+                   "a follower stopped consuming plans", &hdr_->acks[f].pid);
     }
     char* slot = slot_ptr(s);
     std::memcpy(slot, &hb, 8);
@@ -138,7 +167,7 @@ class PlanChannel {
     {
       py::gil_scoped_release nogil;
       wait_until([&] { return hdr_->seq.v.load(std::memory_order_acquire) > next; }, timeout_s,
-                 "the leader stopped publishing plans");
+                 "the leader stopped publishing plans", nullptr, hdr_->leader_pid);
     }
     char* slot = slot_ptr(next);
     uint64_t hb, pb;
@@ -176,10 +205,14 @@ class PlanChannel {
     return base_ + sizeof(ChanHeader) + (size_t)(s % hdr_->nslots) * (size_t)hdr_->slot_bytes;
   }
 
+  // timeout_s < 0: no time limit (only the peer's exit ends the wait); the peer is `peer_pid`, or the pid word
+  // `peer_word` (a follower that has not attached yet reads 0 = unknown)
   template <class Pred>
-  static void wait_until(Pred ready, double timeout_s, const char* what) {
+  static void wait_until(Pred ready, double timeout_s, const char* what, const std::atomic<int64_t>* peer_word = nullptr,
+                         int64_t peer_pid = 0) {
     if (ready()) return;
     const auto t0 = std::chrono::steady_clock::now();
+    double next_check = 0.5;
     for (uint64_t it = 1;; ++it) {
       if (ready()) return;
       if (it < 4096) {
@@ -189,7 +222,13 @@ class PlanChannel {
         continue;
       }
       const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      if (el > timeout_s) throw std::runtime_error(std::string("PlanChannel timeout: ") + what);
+      if (timeout_s >= 0 && el > timeout_s) throw std::runtime_error(std::string("PlanChannel timeout: ") + what);
+      if (el > next_check) {  // twice a second: is the peer process still there?
+        next_check = el + 0.5;
+        const int64_t pid = peer_word != nullptr ? peer_word->load(std::memory_order_acquire) : peer_pid;
+        if (process_gone(pid) && !ready())
+          throw std::runtime_error(std::string("PlanChannel: peer process is gone: ") + what);
+      }
       if (el < 1e-3) {
         sched_yield();
       } else {
@@ -217,6 +256,7 @@ void register_plan_channel(py::module& m) {
       .def("recv", &PlanChannel::recv, py::arg("timeout_s") = 300.0)
       .def("ack", &PlanChannel::ack)
       .def("close", &PlanChannel::close_)
+      .def("unlink", &PlanChannel::unlink)
       .def_property_readonly("published", &PlanChannel::published)
       .def_property_readonly("nslots", &PlanChannel::nslots)
       .def_property_readonly("slot_bytes", &PlanChannel::slot_bytes);

@@ -381,3 +381,57 @@ def test_dp_attention_mixtral_on_one_gpu(cuda, layout):
             for i, tok in enumerate(o):
                 row = lg[len(p) - 1 + i]
                 assert (row.max() - row[tok]).item() < 0.15
+
+
+def _dpa_skip_main(rank, world, port, q):
+    dev = rank % torch.cuda.device_count()
+    _env(rank, world, port, dev)
+    os.environ["KAFKA_TP_BACKEND"] = "gloo"
+    if rank == 1:  # this rank stops taking part in one expert all-to-all (a peer that never arrives)
+        os.environ["KAFKA_FI_CAR_SKIP_CALL"] = "12"
+    from kafka_llm_service_amd.engine import dp_attention
+    from kafka_llm_service_amd.engine.model_runner import CollectiveError
+    from kafka_llm_service_amd.engine.sequence import SamplingParams
+    from kafka_llm_service_amd.parallel import comm
+    from kafka_llm_service_amd.parallel import state as pstate
+    from kafka_llm_service_amd.utils import faults
+
+    faults.reset()
+    eng, st = dp_attention.build_dpa_engine(dict(CFG, model="tiny-mixtral", device=f"cuda:{dev}"), ep=world)
+    try:
+        assert comm.get_custom(st.ep_group) is not None
+        mine = [p for i, p in enumerate(_prompts(eng.model_cfg.vocab_size)) if i % world == rank]
+        sp = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
+        try:
+            dp_attention.generate_lockstep(eng, st, mine, sp)
+            q.put((rank, "finished without an error"))
+        except CollectiveError as e:
+            q.put((rank, f"raised: {e}"))
+        except Exception as e:  # noqa: BLE001 - e.g. the group's gloo agreement after the other rank failed
+            q.put((rank, f"other: {type(e).__name__}"))
+    finally:
+        os._exit(0)  # no collective teardown with a peer that may have failed
+
+
+@pytest.mark.timeout(300)
+def test_dp_attention_lost_peer_fails_the_step(cuda):
+    """with data-parallel attention (tp = 1) the EP group's IPC all-to-all error word must ride back
+    with the step's ids like the TP all-reduce's does — a peer that skips one expert all-to-all makes the other
+    rank raise CollectiveError instead of streaming tokens built from stale expert rows."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_dpa_skip_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        while 0 not in res:
+            m = q.get(timeout=240)
+            res[m[0]] = m[1]
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert res[0].startswith("raised"), res

@@ -30,7 +30,7 @@ def test_history_render_is_token_prefix(history, new_text):
 def test_generated_tokens_reused_verbatim():
     prompt_msgs = [Message(role="system", content="S"), Message(role="user", content="q")]
     p = TPL.render(prompt_msgs, TOOLS)
-    gen = [500, 70000, 91234, TOK.special_id("<|eot_id|>")]  # arbitrary ids incl. pseudo-words + eot
+    gen = [500, 70000, 91234, TOK.special_id("<|eot_id|>")]  # arbitrary ids + eot
     hist = prompt_msgs + [Message(role="assistant", content=TOK.decode(gen), token_ids=gen)]
     nxt = TPL.render(hist + [Message(role="user", content="more")], TOOLS)
     assert nxt[:len(p) + len(gen)] == p + gen
@@ -41,7 +41,7 @@ def test_special_tokens_and_roundtrip():
     assert TOK.decode(ids) == "Hello, MI355X world!"
     assert TOK.decode([TOK.special_id("<|eot_id|>")]) == ""
     assert TOK.decode([TOK.special_id("<|eot_id|>")], skip_special_tokens=False) == "<|eot_id|>"
-    assert TOK.decode([120000]).strip()  # unused id -> deterministic pseudo-word
+    assert TOK.decode([120000]).strip()  # a high regular id decodes to text
     d = IncrementalDetokenizer(TOK)
     s = "".join(d.add([i]) for i in TOK.encode("héllo wörld ✓ done"))
     assert s == "héllo wörld ✓ done"
@@ -106,3 +106,40 @@ def test_local_db_opens_a_reference_schema_database(tmp_path):
         assert (await db.get_thread_messages("t1"))[-1].content == "fifth"
         await db.close()
     asyncio.run(go())
+
+
+def test_tokenizer_compression_on_reference_prompt():
+    """Workload fidelity of the shipped BPE: trained on local text that is not the reference's
+    prompt (scripts/build_tokenizer.py), it must compress the held-out reference sections like a Llama-3-class
+    tokenizer (>= 3.8 chars/token; Llama-3 ~4.3) and render the served shared prefix — the reference's 13-section
+    system prompt (/root/reference/src/prompts/v1.py:73-117) + the server's tool schemas — in <= 19k tokens
+    (~18k)."""
+    import asyncio
+    from pathlib import Path
+
+    from kafka_llm_service_amd.kafka.v1 import KafkaV1Provider
+    from kafka_llm_service_amd.llm.stub import StubEchoProvider
+    from kafka_llm_service_amd.sandbox.local import LocalSandbox
+    from kafka_llm_service_amd.server_tools import NotebookTools, PlannerTools, ShellTools
+
+    assert TOK.n_base == 128000 and TOK.vocab_size == 128256
+    root = Path(__file__).resolve().parents[1] / "kafka_llm_service_amd/prompts/sections_reference"
+    chars = toks = 0
+    for f in sorted(root.rglob("*.md")):
+        t = f.read_text(encoding="utf-8")
+        chars += len(t)
+        toks += len(TOK.encode(t))
+        assert TOK.decode(TOK.encode(t)) == t
+    assert chars / toks >= 3.8, chars / toks
+
+    async def prefix():
+        sb = LocalSandbox("http://127.0.0.1:9")
+        kafka = KafkaV1Provider(StubEchoProvider(), tools=[get_weather_tool, count_tool] + PlannerTools(None).tools,
+                                sandbox_tools=ShellTools(sb).tools + NotebookTools(sb).tools, mcp_servers=[])
+        await kafka.initialize()
+        return kafka.system_prompt, await kafka.get_tools()
+
+    system, tools = asyncio.run(prefix())
+    assert len(system) == 70496  # the reference's rendered default prompt, byte for byte
+    ids = TPL.render([Message(role="system", content=system)], tools, add_generation_prompt=False)
+    assert 15000 <= len(ids) <= 19000, len(ids)

@@ -173,3 +173,55 @@ def test_plan_channel_ring_order_backpressure_and_timeout():
         f.close()
     lead.close()
     assert not os.path.exists(f"/dev/shm{name}")
+
+
+def test_plan_channel_idle_follower_waits_until_leader_exits():
+    """a follower waiting for the next plan must not time out while its leader is merely idle, and must
+    fail at once when the leader PROCESS is gone; the leader unlinks the name once the followers have attached
+    (a group killed with SIGKILL leaves nothing in /dev/shm)."""
+    import os
+    import subprocess
+    import sys
+    import threading
+    import time
+
+    import pytest
+
+    from kafka_llm_service_amd.runtime import native
+
+    rt = native()
+    name = f"/kafka_plan_idle_{os.getpid()}"
+    code = ("import sys, time; sys.path.insert(0, %r); from kafka_llm_service_amd.runtime import native; "
+            "ch = native().PlanChannel(%r, 3, 4096, 1); print('up', flush=True); sys.stdin.readline(); "
+            "ch.unlink(); print('unlinked', flush=True); time.sleep(600)") % (os.getcwd(), name)
+    lead = subprocess.Popen([sys.executable, "-c", code], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    try:
+        assert lead.stdout.readline().strip() == "up"
+        fol = rt.PlanChannel(name, 0)
+        lead.stdin.write("go\n")
+        lead.stdin.flush()
+        assert lead.stdout.readline().strip() == "unlinked"
+        assert not os.path.exists(f"/dev/shm{name}")  # attached mappings outlive the name
+        err = []
+
+        def wait():
+            try:
+                fol.recv(-1.0)
+            except RuntimeError as e:
+                err.append((time.monotonic(), str(e)))
+
+        t = threading.Thread(target=wait, daemon=True)
+        t.start()
+        time.sleep(1.5)  # idle leader: the follower keeps waiting (a bounded wait would have raised by now)
+        assert t.is_alive() and not err
+        t_kill = time.monotonic()
+        lead.kill()
+        lead.wait()
+        t.join(5)
+        assert err and "gone" in err[0][1] and err[0][0] - t_kill < 2.0
+        fol.close()
+    finally:
+        if lead.poll() is None:
+            lead.kill()
+    with pytest.raises(RuntimeError):
+        rt.PlanChannel(name, 0)  # nothing left to attach to

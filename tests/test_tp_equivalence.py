@@ -32,13 +32,16 @@ def _port() -> int:
 def _group_main(rank: int, world: int, port: int, q, extra: dict) -> None:
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(world),
                        "RANK": str(rank), "LOCAL_RANK": str(rank)})
+    extra = dict(extra)
+    os.environ.update(extra.pop("_env", {}))
+    proc = extra.pop("_proc", False)
     from kafka_llm_service_amd.engine import tp_worker
     from kafka_llm_service_amd.parallel import state as pstate
 
     eng, st = tp_worker.build_tp_engine(dict(CFG, **extra), tp=world)
     try:
         if st.is_tp_leader:
-            outs = eng.generate(_prompts(), GREEDY)
+            outs = eng.generate(_prompts(), _proc_params() if proc else GREEDY)
             tp_worker.release_followers()
             g = eng.runner.graphs
             q.put(("outs", outs, eng.num_blocks, eng.stats["planned_ahead"], g.stats if g is not None else None))
@@ -50,8 +53,23 @@ def _group_main(rank: int, world: int, port: int, q, extra: dict) -> None:
         pstate.destroy()
 
 
+TOOLS = [{"type": "function", "function": {"name": "get_weather", "parameters": {
+    "type": "object", "required": ["location"], "properties": {"location": {"type": "string"}}}}}]
+
+
+def _proc_params():
+    """Per-prompt params with device-side logits processing: a grammar-constrained tool call, penalties, plain."""
+    return [SamplingParams(temperature=0.0, max_tokens=60, ignore_eos=True,
+                           tool_grammar={"tools": TOOLS, "tool_choice": "required"}),
+            SamplingParams(temperature=0.0, max_tokens=5, ignore_eos=True, frequency_penalty=0.5,
+                           presence_penalty=0.5),
+            GREEDY]
+
+
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("extra", [{}, {"use_graphs": True}], ids=["eager", "graphs"])
+@pytest.mark.parametrize("extra", [{}, {"use_graphs": True}, {"_env": {"KAFKA_PLAN_CHANNEL": "gloo"}},
+                                   {"_env": {"KAFKA_PLAN_SLOT_BYTES": "1024"}}],
+                         ids=["eager", "graphs", "gloo_channel", "oversized_plans"])
 def test_tp2_generate_matches_tp1(extra):
     """Leader plans step n+1 while n runs (late decode inputs filled device-side on EVERY rank from its own sampler
     output); with ``use_graphs`` every rank captures and replays the decode layouts (fake graph backend on CPU:
@@ -168,8 +186,10 @@ def test_plan_wire_format_roundtrip():
                  n_items=1, prefill_splits=0, n_late=2, late_off=123)
     h.i64 = np.arange(125, dtype=np.int64)
     h.i32 = np.arange(4 * 32 + 77, dtype=np.int32)
+    from kafka_llm_service_amd.engine.logits_proc import ProcUpdates
+
     sp = SampleParams(np.array([0.7, 0, 1, 2], np.float32), np.ones(4, np.float32), np.array([0, 5, 0, 1], np.int32),
-                      np.array([1, 2, 3, 1 << 40], np.int64), [], False)
+                      np.array([1, 2, 3, 1 << 40], np.int64), None, False)
     hdr, payload = pack_plan(h, sp)
     h2, sp2 = unpack_plan(hdr, payload)
     for f in ("B", "T", "nbt", "bt_w", "n_rows", "s_total", "n_dec_items", "n_prefix_items", "cascade_prefix",
@@ -178,7 +198,17 @@ def test_plan_wire_format_roundtrip():
     assert (h2.i64 == h.i64).all() and (h2.i32 == h.i32).all()
     for f in ("temp", "topp", "topk", "seeds"):
         assert (getattr(sp2, f) == getattr(sp, f)).all()
-    assert sp2.greedy is False and sp2.leader_tokens is False
+    assert sp2.greedy is False and sp2.proc is None and sp2.upd is None
+    # with logits-processing rows and table updates (grammar mask rows + penalty slots to clear): every rank
+    # rebuilds the same device tables from the plan
+    proc = np.arange(32, dtype=np.int32).reshape(4, 8)
+    upd = ProcUpdates(np.array([3, 9], np.int32), np.arange(2 * 5, dtype=np.int32).reshape(2, 5) - 4,
+                      np.array([7], np.int32))
+    sp.proc, sp.upd = proc, upd
+    h3, sp3 = unpack_plan(*pack_plan(h, sp))
+    assert (h3.i32 == h.i32).all() and (sp3.seeds == sp.seeds).all()
+    assert (sp3.proc == proc).all() and (sp3.upd.mask_rows == upd.mask_rows).all()
+    assert (sp3.upd.mask_words == upd.mask_words).all() and (sp3.upd.zero_slots == upd.zero_slots).all()
 
 
 def test_ep_ops_roundtrip_equals_direct_moe_on_cpu():
@@ -226,10 +256,10 @@ def _dpa_owner(layout: str, i: int) -> int:
     return i % 2 if layout == "spread" else 0
 
 
-def _dpa_main(rank: int, world: int, port: int, q, layout) -> None:
+def _dpa_main(rank: int, world: int, port: int, q, layout, board: str = "1") -> None:
     """One rank of a DP-attention group: its own prompts (possibly none), experts sharded over the group."""
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(world),
-                       "RANK": str(rank), "LOCAL_RANK": str(rank)})
+                       "RANK": str(rank), "LOCAL_RANK": str(rank), "KAFKA_DPA_BOARD": board})
     from kafka_llm_service_amd.engine import dp_attention
     from kafka_llm_service_amd.parallel import state as pstate
 
@@ -239,23 +269,27 @@ def _dpa_main(rank: int, world: int, port: int, q, layout) -> None:
         assert eng.model.layers[0].w13.shape[0] == eng.model_cfg.num_experts // world
         mine = [p for i, p in enumerate(_prompts()) if _dpa_owner(layout, i) == rank]
         outs = dp_attention.generate_lockstep(eng, st, mine, GREEDY)
-        q.put((rank, outs, eng.stats["group_steps"]))
+        q.put((rank, outs, eng.stats["group_steps"], eng.stats["planned_ahead"],
+               dp_attention.make_board(st) is not None))
     finally:
         pstate.destroy()
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("layout", ["spread", "one_idle"])
-def test_dp_attention_mixtral_matches_single_rank(layout):
+@pytest.mark.parametrize("layout,board", [("spread", "1"), ("one_idle", "1"), ("spread", "0")],
+                         ids=["spread", "one_idle", "spread_gloo_agree"])
+def test_dp_attention_mixtral_matches_single_rank(layout, board):
     """Mixtral with data-parallel attention over 2 ranks (each rank its own sequences, whole attention weights,
     half the experts, device-side all-to-all dispatch/combine in lockstep): every greedy token is the EP=1 model's
-    argmax up to a small logit margin — also when one rank has no sequences at all and only serves its experts."""
+    argmax up to a small logit margin — also when one rank has no sequences at all and only serves its experts.
+    The group plans ahead (step n+1 agreed and launched before step n is collected) and agrees through the
+    shared-memory board (or gloo when the board is off)."""
     from kafka_llm_service_amd.models.oracle import dense_logits
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_dpa_main, args=(r, 2, port, q, layout)) for r in range(2)]
+    procs = [ctx.Process(target=_dpa_main, args=(r, 2, port, q, layout, board)) for r in range(2)]
     for p in procs:
         p.start()
     res = {m[0]: m[1:] for m in (q.get(timeout=240) for _ in range(2))}
@@ -263,6 +297,8 @@ def test_dp_attention_mixtral_matches_single_rank(layout):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[0][1] == res[1][1]  # lockstep: the same number of group steps on both ranks
+    assert res[0][2] > 0  # planned ahead
+    assert res[0][3] == res[1][3] == (board == "1")
     ref = LLMEngine(EngineConfig(**dict(CFG, model="tiny-mixtral")))
     prompts = _prompts()
     for r in (0, 1):
@@ -274,3 +310,32 @@ def test_dp_attention_mixtral_matches_single_rank(layout):
             for i, tok in enumerate(o):
                 row = lg[len(p) - 1 + i]
                 assert (row.max() - row[tok]).item() < 0.05
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("extra", [{"_proc": True}, {"_proc": True, "use_graphs": True},
+                                   {"_proc": True, "_env": {"KAFKA_PLAN_SLOT_BYTES": "1024"}}],
+                         ids=["eager", "graphs", "oversized_plans"])
+def test_tp2_logits_processing_matches_tp1(extra):
+    """Grammar masks / forced tokens / penalties under TP: the leader ships the proc rows and the table updates
+    (new mask rows of 16 KB: with 1 KB ring slots every such plan takes the oversized-plan gloo fallback) and every
+    rank samples identically — the group's tokens equal a TP = 1 engine's with the same parameters."""
+    from kafka_llm_service_amd.engine.chat_template import parse_tool_calls
+    from kafka_llm_service_amd.engine.tokenizer import get_tokenizer
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_group_main, args=(r, 2, port, q, extra)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((m[0], m[1:]) for m in (q.get(timeout=240) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    outs = res["outs"][0]
+    tok = get_tokenizer("llama3")
+    assert parse_tool_calls(tok.decode(outs[0])) and outs[0][-1] == tok.special_id("<|eom_id|>")
+    ref = LLMEngine(EngineConfig(**CFG)).generate(_prompts(), _proc_params())
+    assert ref[0] == outs[0]  # the grammar leaves few near-ties; forced tokens are exact
+    assert len(outs[1]) == len(ref[1]) == 5
