@@ -154,6 +154,11 @@ class Agent:
                 seen_usage = True
                 for k in total:
                     total[k] += getattr(usage, k, 0) or 0
+                # this LLM call's usage as a typed agent event (like tool_result: no ``choices``, so clients that
+                # index choices[0] of every chat.completion.chunk keep working): per-iteration prompt / cached tokens
+                # show each agent iteration re-using the previous one's KV
+                yield {"type": "usage", "id": cid, "iteration": iteration,
+                       "usage": {k: getattr(usage, k, 0) or 0 for k in total}}
             calls = [acc[i] for i in sorted(acc)]
             if not calls:
                 if emit_messages and content:

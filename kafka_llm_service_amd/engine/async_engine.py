@@ -160,7 +160,7 @@ class AsyncEngine:
                 "kv_free_pages": kv["free"] + kv["evictable"], "kv_total_pages": kv["num_blocks"],
                 "prefix_hit_tokens": kv["hit_tokens"], "prompt_tokens": kv["query_tokens"],
                 "output_tokens": eng.stats["output_tokens"], "steps": eng.stats["steps"],
-                "preemptions": eng.sched.num_preemptions}
+                "preemptions": eng.sched.num_preemptions, "perf": eng.perf_stats()}
 
     def shutdown(self) -> None:
         self._stop.set()

@@ -189,7 +189,8 @@ def _serve_pipe(eng, conn) -> None:
                 conn.send(("health", {"running": eng.num_running, "waiting": eng.num_waiting,
                                       "kv_free_pages": kv["free"] + kv["evictable"],
                                       "kv_total_pages": kv["num_blocks"], "prefix_hit_tokens": kv["hit_tokens"],
-                                      "output_tokens": eng.stats["output_tokens"], "steps": eng.stats["steps"]}))
+                                      "output_tokens": eng.stats["output_tokens"], "steps": eng.stats["steps"],
+                                      "perf": eng.perf_stats()}))
             elif kind == "stop":
                 conn.send(("stopped",))
                 return

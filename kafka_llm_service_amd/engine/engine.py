@@ -13,6 +13,7 @@ from __future__ import annotations
 import logging
 import os
 import time
+from collections import deque
 from dataclasses import dataclass, field, replace
 
 import torch
@@ -198,6 +199,9 @@ class LLMEngine:
         self.stats = {"steps": 0, "prompt_tokens": 0, "cached_tokens": 0, "output_tokens": 0, "step_time": 0.0,
                       "replans": 0, "planned_ahead": 0}
         self._inflight: _InFlight | None = None  # the step on the GPU that has not been collected yet
+        self.step_ms: deque = deque(maxlen=512)  # intervals between consecutive step completions (busy periods)
+        self._t_done = 0.0
+        self._coll_mark = (0, 0)  # (collective calls, steps) at the last perf_stats() read
         self._n_added = 0
         self.stop_checker_factory = None  # set by the frontend: (request params) -> incremental stop-string checker
         log.info("engine ready: %s tp=%d kv pages=%d (%s, %.1f GB) load %.1fs", mc.name, cfg.tp, nb, cfg.kv_dtype,
@@ -393,6 +397,9 @@ class LLMEngine:
         with trace.span("collect"):
             toks = self.runner.collect(cur.launched)
         now = time.perf_counter()
+        if now - self._t_done < 1.0:  # back-to-back steps: the interval is this GPU's step time
+            self.step_ms.append((now - self._t_done) * 1e3)
+        self._t_done = now
         self.stats["step_time"] += now - cur.t0
         self.stats["steps"] += 1
         outs: list[StepOutput] = []
@@ -485,6 +492,32 @@ class LLMEngine:
         if sid is not None and self.kvm.has_seq(sid):
             self.kvm.free_sequence(sid)
         self._pinned = None
+
+    def perf_stats(self) -> dict:
+        """Per-GPU step time (quantiles over the last <= 512 busy steps) and, with an IPC collective (TP custom
+        all-reduce / DP-attention all-to-all), its time per call and per step (the kernels' own
+        clock stamps: graph replays included)."""
+        d: dict = {"device": str(self.device), "steps": self.stats["steps"]}
+        if self.step_ms:
+            xs = sorted(self.step_ms)
+            q = lambda f: xs[min(len(xs) - 1, int(f * len(xs)))]  # noqa: E731
+            d.update(step_ms_mean=round(sum(xs) / len(xs), 3), step_ms_p50=round(q(0.5), 3),
+                     step_ms_p99=round(q(0.99), 3))
+        car = self.runner._custom_ar() if self.device.type == "cuda" else None
+        if car is not None:
+            try:
+                us, calls = car.timing()
+            except Exception:  # noqa: BLE001 - diagnostics only
+                us, calls = None, 0
+            if us is not None and len(us):
+                c0, s0 = self._coll_mark
+                steps = self.stats["steps"]
+                per_step = (calls - c0) / (steps - s0) if steps > s0 else 0.0
+                self._coll_mark = (calls, steps)
+                d.update(collective_calls=calls, collective_us_per_call=round(float(us.mean()), 2),
+                         collective_calls_per_step=round(per_step, 2),
+                         collective_ms_per_step=round(float(us.mean()) * per_step / 1e3, 3))
+        return d
 
     def kv_stats(self) -> dict:
         d = dict(self.kvm.stats())

@@ -45,6 +45,20 @@ class EngineLLMProvider(LLMProvider):
         self._pin: list[int] | None = None
         self._pin_key = None
 
+    def _choice(self, tool_choice: Any, messages: list[Message]) -> Any:
+        """The request's tool_choice, else the server default; a LIST default is a per-iteration script: entry i for
+        the i-th LLM call of the turn (i = assistant tool-call messages after the last user message)."""
+        tc = tool_choice or self.tool_choice
+        if isinstance(tc, list):
+            i = 0
+            for m in reversed(messages):
+                if m.role == "user":
+                    break
+                if m.role == "assistant" and m.tool_calls:
+                    i += 1
+            tc = tc[min(i, len(tc) - 1)] if tc else "auto"
+        return tc
+
     def render(self, messages: list[Message], tools: list[dict] | None) -> list[int]:
         return self.template.render(messages, tools)
 
@@ -107,7 +121,7 @@ class EngineLLMProvider(LLMProvider):
                                 frequency_penalty=float(frequency_penalty or 0.0),
                                 presence_penalty=float(presence_penalty or 0.0), seed=seed,
                                 ignore_eos=self.ignore_eos,
-                                tool_grammar=({"tools": tools, "tool_choice": tool_choice or self.tool_choice}
+                                tool_grammar=({"tools": tools, "tool_choice": self._choice(tool_choice, messages)}
                                               if tools and self.constrain_tools else None))
         stops = [s for s in (stop or []) if s]
         hold = max((len(s) for s in stops), default=1) - 1

@@ -37,7 +37,12 @@ constexpr int AR_MAX_RANKS = 8;
 constexpr int AR_MAX_BLOCKS = 128;
 constexpr int AR_ERR_OFF = AR_MAX_RANKS * AR_MAX_BLOCKS * 4;  // 4096
 constexpr int AR_EPOCH_OFF = AR_ERR_OFF + 256;
+// collective timing ring (SURVEY §5.5 "all-reduce time"): block 0 of every call stamps the 100 MHz constant clock at
+// entry and exit into slot (epoch & 127) — [start, end] uint64 pairs, read by the host on /metrics requests only
+constexpr int AR_TIME_OFF = 5120;
+constexpr int AR_TIME_SLOTS = 128;
 constexpr int AR_HEADER = 8192;
+static_assert(AR_EPOCH_OFF + AR_MAX_BLOCKS * 4 <= AR_TIME_OFF && AR_TIME_OFF + AR_TIME_SLOTS * 16 <= AR_HEADER, "hdr");
 
 struct ARPtrs {
   char* base[AR_MAX_RANKS];  // every rank's allocation, mapped into this process (base[rank] = own)
@@ -61,9 +66,21 @@ __device__ __forceinline__ int ar_epoch(const ARPtrs& ptrs, int rank, int* s_e) 
     const int e = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
     __hip_atomic_store(ep, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *s_e = e;
+    if (blockIdx.x == 0) {
+      uint64_t* ts = reinterpret_cast<uint64_t*>(ptrs.base[rank] + AR_TIME_OFF) + (e & (AR_TIME_SLOTS - 1)) * 2;
+      __hip_atomic_store(ts, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   __syncthreads();
   return *s_e;
+}
+
+// Exit stamp of the call's timing slot (block 0, thread 0; vector store like the epoch update)
+__device__ __forceinline__ void ar_stamp_end(const ARPtrs& ptrs, int rank, int e) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint64_t* ts = reinterpret_cast<uint64_t*>(ptrs.base[rank] + AR_TIME_OFF) + (e & (AR_TIME_SLOTS - 1)) * 2 + 1;
+    __hip_atomic_store(ts, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Steps 2 + 3: publish this block's staged slice to every peer and wait for theirs.
@@ -145,6 +162,7 @@ __global__ __launch_bounds__(256) void allreduce_oneshot_kernel(ARPtrs ptrs, int
     for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
     store_bf16x8(y + c * 8, o);
   }
+  ar_stamp_end(ptrs, rank, e);
 }
 
 // Fused: rows r of [T, d] are owned by block r % nblocks (d <= 8 * 256 * CPT). Per row: s = bf16(allreduce(x) +
@@ -198,6 +216,7 @@ __global__ __launch_bounds__(256) void allreduce_add_rmsnorm_kernel(ARPtrs ptrs,
       }
     }
   }
+  ar_stamp_end(ptrs, rank, e);
 }
 
 extern "C" hipError_t kafka_car_alloc(int64_t bytes, void** out) {
@@ -207,6 +226,20 @@ extern "C" hipError_t kafka_car_alloc(int64_t bytes, void** out) {
 }
 
 extern "C" int64_t kafka_car_header_bytes() { return AR_HEADER; }
+
+// Host copy of the timing ring ([AR_TIME_SLOTS][2] uint64 = 2 KB) and of block 0's epoch (the call count), on a
+// private stream so a /metrics request never waits behind the engine's queued steps.
+extern "C" hipError_t kafka_car_timing(const void* own, uint64_t* ring_out, int* epoch_out) {
+  hipStream_t s;
+  hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  if (e != hipSuccess) return e;
+  const char* b = static_cast<const char*>(own);
+  e = hipMemcpyAsync(ring_out, b + AR_TIME_OFF, AR_TIME_SLOTS * 16, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(epoch_out, b + AR_EPOCH_OFF, sizeof(int), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  hipStreamDestroy(s);
+  return e;
+}
 
 extern "C" hipError_t kafka_car_ipc_handle(void* p, hipIpcMemHandle_t* h) { return hipIpcGetMemHandle(h, p); }
 
@@ -307,6 +340,7 @@ __global__ __launch_bounds__(256) void a2a_pull_kernel(ARPtrs ptrs, int rank, co
         if (cc < z) recv[p * bpd16 + (cc - lo)] = v[p][u];
       }
   }
+  ar_stamp_end(ptrs, rank, e);
 }
 
 extern "C" hipError_t kafka_launch_car_a2a(char* const* bases, int nranks, int rank, const void* send, int64_t nbytes,

@@ -67,6 +67,7 @@ hipError_t kafka_launch_grouped_gemm(const bf16* X, int64_t ldx, const bf16* W, 
                                      int64_t ldo, hipStream_t st);
 hipError_t kafka_car_alloc(int64_t bytes, void** out);
 int64_t kafka_car_header_bytes();
+hipError_t kafka_car_timing(const void* own, uint64_t* ring_out, int* epoch_out);
 hipError_t kafka_car_ipc_handle(void* p, hipIpcMemHandle_t* h);
 hipError_t kafka_car_open(const hipIpcMemHandle_t* h, void** out);
 hipError_t kafka_car_close(void* p);
@@ -754,6 +755,14 @@ static void car_error_async(int64_t own, at::Tensor out, int64_t idx) {
   CHECK_HIP(hipMemcpyAsync(out.data_ptr<int>() + idx, reinterpret_cast<char*>(own) + 8 * 128 * 4, sizeof(int),
                            hipMemcpyDeviceToHost, cur_stream()));
 }
+// (timing ring [128, 2] of 100 MHz clock stamps, block 0's call counter): SURVEY §5.5 collective time in /metrics
+static std::tuple<at::Tensor, int64_t> car_timing(int64_t own) {
+  at::Tensor ring = at::empty({128, 2}, at::TensorOptions().dtype(at::kLong));
+  int epoch = 0;
+  CHECK_HIP(kafka_car_timing(reinterpret_cast<const void*>(own), reinterpret_cast<uint64_t*>(ring.data_ptr<int64_t>()),
+                             &epoch));
+  return {ring, (int64_t)epoch};
+}
 static std::vector<char*> car_bases(const std::vector<int64_t>& bases) {
   std::vector<char*> b(bases.size());
   for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<char*>(bases[i]);
@@ -900,6 +909,7 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("car_free", &car_free);
   m.def("car_error", &car_error);
   m.def("car_error_async", &car_error_async);
+  m.def("car_timing", &car_timing);
   m.def("car_all_reduce", &car_all_reduce);
   m.def("car_all_reduce_add_rmsnorm", &car_all_reduce_add_rmsnorm);
   m.def("car_a2a", &car_a2a);

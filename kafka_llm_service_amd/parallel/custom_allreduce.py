@@ -131,6 +131,20 @@ class CustomAllReduce:
         if ext().car_error(self.own):
             raise RuntimeError("custom all-reduce: a peer did not arrive within 2 s")
 
+    def timing(self) -> tuple:
+        """(call durations in us of the last <= 128 calls, oldest first, this rank's call count): block 0's entry /
+        exit stamps of the 100 MHz constant clock (csrc/allreduce.hip AR_TIME_OFF). Synchronises with a private
+        stream only: for /metrics, never the step path."""
+        import numpy as np
+
+        ring, epoch = ext().car_timing(self.own)
+        r = ring.numpy().view(np.uint64)
+        n = min(int(epoch), r.shape[0])
+        slots = [(int(epoch) - k) & (r.shape[0] - 1) for k in range(n - 1, -1, -1)]
+        st, en = r[slots, 0].astype(np.int64), r[slots, 1].astype(np.int64)
+        ok = (en >= st) & (st > 0)
+        return (en[ok] - st[ok]) / 100.0, int(epoch)
+
     def error_async(self, out: torch.Tensor, idx: int) -> None:
         """Stream-ordered copy of the error word into ``out[idx]`` (pinned int32): read it once the stream passed."""
         ext().car_error_async(self.own, out, int(idx))

@@ -39,8 +39,13 @@ class ServerConfig:
     max_model_len: int = 131072
     default_max_tokens: int = 1024
     # default tool_choice of engine-backed generations ("auto" | "required" | "none" | a JSON function object);
-    # "required" makes random-init models drive the agent/tool loop with well-formed calls (BASELINE config 4)
+    # "required" makes random-init models drive the agent/tool loop with well-formed calls (BASELINE config 4). A
+    # LIST is a per-iteration script: agent iteration i of a turn (i = assistant tool-call messages since the last
+    # user message) uses entry min(i, len - 1), e.g. create_shell, then shell_exec, then get_weather
     tool_choice: Any = "auto"
+    # JSON-schema overrides of tool parameters by tool name (KAFKA_TOOL_OVERRIDES, a JSON object): e.g. enum values
+    # that pin a random-init model's constrained arguments to a working call ({"shell_id": {"enum": ["main"]}})
+    tool_overrides: dict[str, Any] = field(default_factory=dict)
     # subset of the Kafka v1 prompt sections (None = all 13: the reference's 70,496-character prompt, or ~47k with
     # KAFKA_PROMPT=compact); small engines / CPU tests use a few
     prompt_sections: list[str] | None = None
@@ -68,6 +73,7 @@ class ServerConfig:
                             max_model_len=int(e.get("KAFKA_MAX_MODEL_LEN", "131072")),
                             default_max_tokens=int(e.get("KAFKA_DEFAULT_MAX_TOKENS", "1024")),
                             tool_choice=_tool_choice(e.get("KAFKA_TOOL_CHOICE", "auto")),
+                            tool_overrides=json.loads(e.get("KAFKA_TOOL_OVERRIDES", "{}")),
                             ignore_eos=e.get("KAFKA_IGNORE_EOS", "0") == "1",
                             warm_prefix=e.get("KAFKA_WARM_PREFIX", "1") == "1",
                             engine_process=_engine_process(e.get("KAFKA_ENGINE_PROCESS", "auto")),
@@ -102,9 +108,28 @@ def _engine_process(v: str) -> bool:
     return v == "1"
 
 
+def apply_tool_overrides(tools: list, overrides: dict[str, Any]) -> list:
+    """Tools with ``overrides[name]`` ({property: JSON schema}) merged into their parameters' properties — copies,
+    so module-level tool singletons stay untouched."""
+    if not overrides:
+        return list(tools)
+    import copy
+
+    out = []
+    for t in tools:
+        ov = overrides.get(t.name)
+        if ov:
+            t = copy.copy(t)
+            params = copy.deepcopy(t.parameters)
+            params.setdefault("properties", {}).update(copy.deepcopy(ov))
+            t._parameters = params
+        out.append(t)
+    return out
+
+
 def _tool_choice(v: str) -> Any:
     v = v.strip()
-    return json.loads(v) if v.startswith("{") else v
+    return json.loads(v) if v.startswith(("{", "[")) else v
 
 
 class ServerState:
@@ -149,7 +174,8 @@ class ServerState:
                 SharedURLProvisioner(cfg.sandbox_url)
             warm = HTTPWarmSandboxFactory() if os.environ.get("WARM_SANDBOX_SERVICE_URL") else None
             self.sandbox_manager = SandboxManager(self.db, self.provisioner, warm)
-        tools = [get_weather_tool, count_tool] + PlannerTools(None).tools
+        tools = apply_tool_overrides([get_weather_tool, count_tool] + PlannerTools(None).tools, cfg.tool_overrides)
+        sandbox_tools = apply_tool_overrides(sandbox_tools, cfg.tool_overrides)
         self.kafka = KafkaV1Provider(self.llm, tools=tools, sandbox_tools=sandbox_tools,
                                      mcp_servers=DEFAULT_MCP_SERVERS if cfg.mcp else [],
                                      prompt_sections=cfg.prompt_sections, max_iterations=cfg.agent_max_iterations)
@@ -234,9 +260,12 @@ class ServerState:
                 self.sandbox_manager.ensure_sandbox_background(thread_id)
                 sb = LazySandbox(thread_id, self.sandbox_manager, timeout=120.0)
             sandbox_tools = ShellTools(sb).tools + NotebookTools(sb).tools
+        ov = self.config.tool_overrides
         agent = KafkaV1Provider(self.llm, thread_id=thread_id, db_client=self.db,
-                                tools=[get_weather_tool, count_tool] + PlannerTools(thread_id).tools,
-                                sandbox_tools=sandbox_tools, prompt_sections=self.config.prompt_sections,
+                                tools=apply_tool_overrides([get_weather_tool, count_tool] + PlannerTools(thread_id).tools,
+                                                           ov),
+                                sandbox_tools=apply_tool_overrides(sandbox_tools, ov),
+                                prompt_sections=self.config.prompt_sections,
                                 max_iterations=self.config.agent_max_iterations)
         await agent.initialize()
         try:

@@ -150,58 +150,13 @@ def test_agent_iterations_hit_the_prefix_cache(monkeypatch):
             (cur.num_cached, len(prev.prompt_ids), len(prev.output_ids))
 
 
-def test_thread_agent_run_forced_shell_exec_against_sandbox_service(tmp_path):
-    """Config 4's tool path on CPU (tiny model): /v1/threads/{id}/agent/run, generation constrained to a shell_exec
-    call, executed by the shipped sandbox service over HTTP, streamed back as tool_result frames, loop ended by
-    max_iterations, tool turns persisted. tests/test_server_gpu.py runs the same flow on a TP=2 group on the GPU."""
-    import os
-    import socket
-    import subprocess
-    import sys
-    import time
+def test_thread_agent_run_working_tools_against_sandbox_service(tmp_path):
+    """Config 4's tool loop on CPU (tiny model): /v1/threads/{id}/agent/run with a per-iteration tool_choice script
+    and enum schema overrides (tests/config4_flow.py) — create_shell, then ``ls`` in the shipped sandbox service
+    listing a planted file, then the weather tool's offline fixture; the second LLM call hits the prefix cache; the
+    tool turns are persisted. tests/test_server_gpu.py runs the same flow on a TP = 2 group on the GPU."""
+    import config4_flow
 
-    import httpx
-    from fastapi.testclient import TestClient
-
-    from kafka_llm_service_amd.db.local import MemoryDBClient
-    from kafka_llm_service_amd.server.app import create_app
-    from kafka_llm_service_amd.server.state import ServerConfig, ServerState
-
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    work = tmp_path / "sbx"
-    work.mkdir()
-    sbx = subprocess.Popen([sys.executable, "-m", "kafka_llm_service_amd.sandbox.service", "--port", str(port),
-                            "--workdir", str(work)], env=dict(os.environ, HOME=str(tmp_path)))
-    try:
-        for _ in range(300):
-            try:
-                if httpx.get(f"http://127.0.0.1:{port}/health", timeout=1).status_code == 200:
-                    break
-            except httpx.HTTPError:
-                time.sleep(0.1)
-        cfg = ServerConfig(backend="engine", model="tiny-llama", sandbox="shared",
-                           sandbox_url=f"http://127.0.0.1:{port}", max_model_len=32768, default_max_tokens=64,
-                           tool_choice={"type": "function", "function": {"name": "shell_exec"}},
-                           prompt_sections=["intro"], agent_max_iterations=2, warm_prefix=False,
-                           engine_kwargs={"device": "cpu", "num_kv_blocks": 4096})
-        st = ServerState(cfg, db=MemoryDBClient())
-        with TestClient(create_app(state=st)) as c:
-            tid = c.post("/v1/threads").json()["thread_id"]
-            text = c.post(f"/v1/threads/{tid}/agent/run",
-                          json={"messages": [{"role": "user", "content": "list files"}], "max_tokens": 64}).text
-            msgs = c.get(f"/v1/threads/{tid}/messages").json()["messages"]
-    finally:
-        sbx.terminate()
-        sbx.wait(timeout=30)
-    frames = [json.loads(b[6:]) for b in text.split("\n\n") if b.startswith("data: {")]
-    assert text.rstrip().endswith("data: [DONE]")
-    tr = [f for f in frames if f.get("type") == "tool_result"]
-    assert tr and all(f["tool_name"] == "shell_exec" for f in tr) and any(f["is_complete"] for f in tr), tr[:2]
-    done = [f for f in frames if f.get("type") == "agent_done"]
-    assert done and done[-1]["reason"] == "max_iterations"
-    roles = [m["role"] for m in msgs]
-    assert roles[0] == "user" and roles.count("tool") == 2 and roles.count("assistant") == 2, roles
-    call = next(m for m in msgs if m["role"] == "assistant")["tool_calls"][0]["function"]
-    assert call["name"] == "shell_exec" and isinstance(json.loads(call["arguments"]), dict)
+    text, frames, msgs = config4_flow.run(tmp_path, "tiny-llama", {"device": "cpu", "num_kv_blocks": 4096},
+                                          max_model_len=32768, default_max_tokens=96, warm_prefix=False)
+    config4_flow.check(text, frames, msgs)

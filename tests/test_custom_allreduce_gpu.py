@@ -208,7 +208,7 @@ def _tp_main(rank, world, port, q, graphs, model):
             tp_worker.release_followers()
             g = eng.runner.graphs
             q.put(("leader", outs, [s.numpy() for s in seen], g.stats if g is not None else None,
-                   eng.stats["planned_ahead"], a2a_calls[0]))
+                   eng.stats["planned_ahead"], a2a_calls[0], eng.perf_stats()))
         else:
             n = tp_worker.follower_loop(eng)
             q.put(("follower", n, a2a_calls[0]))
@@ -243,8 +243,10 @@ def test_tp2_engine_on_one_gpu_matches_tp1(cuda, model, graphs):
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    outs, seen, gstats, ahead, a2a_lead = res["leader"]
+    outs, seen, gstats, ahead, a2a_lead, perf = res["leader"]
     assert res["follower"][0] >= 6 and ahead > 0
+    if os.environ.get("KAFKA_CUSTOM_AR", "1") == "1":  # collective time from the kernels' clock stamps
+        assert perf.get("collective_us_per_call", 0) > 0 and perf.get("collective_calls_per_step", 0) > 0, perf
     if graphs:
         assert gstats["replays"] >= 1
     if model.endswith(("+a2a", "+overlap")):  # eager MoE calls under sync-debug "error" / overlapped seams ran

@@ -77,3 +77,29 @@ def test_server_cli_flags_map_to_config(monkeypatch):
     monkeypatch.setenv("KAFKA_PROMPT_SECTIONS", "intro,core_tools")
     cfg = ServerConfig.from_env()
     assert cfg.model == "tiny-llama" and cfg.dp == 2 and cfg.prompt_sections == ["intro", "core_tools"]
+
+
+def test_metrics_per_gpu_step_time():
+    """/metrics carries each replica's GPU step time (and collective time when the replica has an IPC
+    collective; the GPU TP tests cover that path) labelled by replica and device."""
+    import re
+
+    from fastapi.testclient import TestClient
+
+    from kafka_llm_service_amd.db.local import MemoryDBClient
+    from kafka_llm_service_amd.server.app import create_app
+    from kafka_llm_service_amd.server.state import ServerConfig, ServerState
+
+    cfg = ServerConfig(backend="engine", model="tiny-llama", sandbox="none", max_model_len=4096, warm_prefix=False,
+                       prompt_sections=["intro"], ignore_eos=True, engine_kwargs={"device": "cpu", "num_kv_blocks": 512})
+    st = ServerState(cfg, db=MemoryDBClient())
+    with TestClient(create_app(state=st)) as c:
+        c.post("/v1/chat/completions", json={"model": "m", "messages": [{"role": "user", "content": "x"}],
+                                             "max_tokens": 12, "temperature": 0})
+        m = ""
+        for _ in range(50):
+            m = c.get("/metrics").text
+            if "kafka_gpu_step_ms" in m:
+                break
+    v = re.search(r'kafka_gpu_step_ms\{replica="0",device="cpu",stat="p50"\} ([0-9.]+)', m)
+    assert v and float(v.group(1)) > 0, m[-2000:]
