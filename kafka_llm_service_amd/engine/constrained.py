@@ -130,7 +130,6 @@ class ToolCallConstraint:
         self._n = 0
         self.done = False
         self._guards: list[tuple[int, frozenset]] = []  # (slot, E): speculated "output_ids[slot] not in E"
-        self._reps: dict = {}
 
     def _mode(self, tc):
         if isinstance(tc, dict):
@@ -165,6 +164,14 @@ class ToolCallConstraint:
             self._spec = _FREE_FOREVER
             self.done = True
 
+    def _enc(self, text: str) -> list[int]:
+        """Token ids of a grammar segment, cached per tokenizer (the same keys / names / punctuation every call)."""
+        cache = self.tok.__dict__.setdefault("_grammar_enc", {})
+        ids = cache.get(text)
+        if ids is None:
+            ids = cache[text] = self.tok.encode(text)
+        return ids
+
     def _start(self) -> None:
         if self._gen is None:
             self._gen = self._program()
@@ -178,10 +185,11 @@ class ToolCallConstraint:
             return (0 if self.start != 0 else 1), frozenset([self.start])
         if isinstance(spec, Mask):
             extra = frozenset(int(e) for e in spec.extra)
-            rep = self._reps.get(spec.key)
+            k = (id(spec.base), spec.key, extra)
+            rep = _REPS.get(k)
             if rep is None:
-                cand = np.flatnonzero(spec.base)
-                rep = self._reps[spec.key] = next((int(c) for c in cand[:64] if int(c) not in extra), -1)
+                cand = np.flatnonzero(spec.base[:4096]) if spec.base[:4096].any() else np.flatnonzero(spec.base)
+                rep = _REPS[k] = next((int(c) for c in cand[:64] if int(c) not in extra), -1)
             return (rep, extra) if rep >= 0 else None
         return None
 
@@ -264,12 +272,12 @@ class ToolCallConstraint:
         self.done = True
 
     def _forced(self, text: str):
-        for i in self.tok.encode(text):
+        for i in self._enc(text):
             yield [i]
 
     def _choice(self, alts: list[str]):
         """Trie walk over the tokenizations of ``alts``; returns the chosen alternative."""
-        seqs = [(a, self.tok.encode(a)) for a in alts]
+        seqs = [(a, self._enc(a)) for a in alts]
         pos = 0
         while True:
             live = [(a, s) for a, s in seqs if len(s) > pos]
@@ -308,7 +316,7 @@ class ToolCallConstraint:
             # "minimum" / "maximum" restrict the choice to tokens whose value is in range
             lo, hi = schema.get("minimum"), schema.get("maximum")
             if lo is None and hi is None:
-                yield Mask("digits_nz", self.cls.digits_nz, self.tok.encode("0")[:1])
+                yield Mask("digits_nz", self.cls.digits_nz, self._enc("0")[:1])
                 return
             m = self.cls.digit_range(self.tok, lo, hi)
             if m.any():
@@ -320,7 +328,7 @@ class ToolCallConstraint:
         elif typ == "null":
             yield from self._forced("null")
         else:  # string (and anything unrecognised): 1..MAX_STR_TOKENS string-safe tokens, then the closing quote
-            q = self.tok.encode('"')
+            q = self._enc('"')
             yield from self._forced('"')
             yield Mask("str", self.cls.str_safe, [])
             for _ in range(MAX_STR_TOKENS - 1):
@@ -333,3 +341,4 @@ class ToolCallConstraint:
 
 
 _FREE_FOREVER = object()
+_REPS: dict = {}  # (id(mask base), key, extras) -> a representative token outside the extras

@@ -201,6 +201,12 @@ def plan_prefill_items(tiles: list[tuple[int, int, int, int, int]], hkv: int, ta
         ck = min(max(min_chunk, -(-total // (target_wgs * 32)) * 32), max_keys)
         if longest < 3 * ck // 2 and longest <= max_keys:
             ck = max_keys  # nothing long enough for a split to shorten the launch by much
+        elif all(t[3] > ck for t in tiles):
+            # every tile is split (new turns against a long cached context): keep the launch to ONE round of
+            # workgroups — per-tile rounding up can overshoot target_wgs by a few, and a second round of a handful
+            # of workgroups doubles the launch (r03 trace: 272 workgroups for a new turn, 125 us vs ~60)
+            while ck < max_keys and sum(-(-t[3] // ck) for t in tiles) * hkv > target_wgs:
+                ck += 32
     items, splits, ranges = [], 0, []
     for q0, cnt, btr, ext, hi in tiles:
         if ext <= ck:

@@ -35,17 +35,24 @@ from kafka_llm_service_amd.parallel import state as pstate
 FUSE_QKV_ROPE = os.environ.get("KAFKA_FUSE_QKV_ROPE", "0") == "1"
 
 # TP decode seam overlap (KAFKA_TP_OVERLAP=1): the row-parallel O / down projection of a decode-sized step is
-# computed in two column halves; half 0's all-reduce runs on a second HIP stream while half 1's GEMM streams its
-# weights on the main one, then half 1's all-reduce, the join and the residual add + RMSNorm. Unlike a split of the
-# batch into two micro-batches it reads every weight once (decode GEMMs are weight-bound), and the per-element sums
-# are those of the one-shot all-reduce. Captured hipGraphs record the fork/join. Off by default: the gain needs
-# TP over xGMI to measure (ranks sharing one GPU overlap nothing), and the seam loses its fused AR + RMSNorm launch.
+# computed in two column halves; half 0's all-reduce runs on a second HIP stream (into a persistent buffer) while half
+# 1's GEMM streams its weights on the main one, then ONE launch on the main stream all-reduces half 1, joins half 0
+# (read in place: no concatenation), adds the residual and applies the next RMSNorm (csrc/allreduce.hip, the fused
+# kernel's ``pre`` columns). Unlike a split of the batch into two micro-batches it reads every weight once (decode
+# GEMMs are weight-bound), and the per-element sums are those of the one-shot all-reduce. Captured hipGraphs record
+# the fork/join. Off by default: the gain needs TP over xGMI to measure (ranks sharing one GPU overlap nothing).
 TP_OVERLAP = os.environ.get("KAFKA_TP_OVERLAP", "0") == "1"
 
 # Projections of 129..256-row steps (decode + a new turn's prefill) that run on the skinny MFMA GEMM
 # (ops.linear_skinny, csrc/skinny_gemm.hip) instead of hipBLASLt: env KAFKA_SKINNY, a comma list of qkv / o / down
 # ("" = none; "+" also separates). gate_up stays on hipBLASLt (faster there). Same-box A/B, 2 interleaved rounds:
 # 7,857 (none) -> 7,924 tok/s (o+down or all three), profiles/r03/skinny_gemm/bench_ab_wired.jsonl.
+# Prefill-sized TP seams whose message exceeds the custom all-reduce's buffer (RCCL): the row-parallel GEMM and the
+# all-reduce are pipelined over row blocks of at least PIPE_ROWS tokens, at most PIPE_CHUNKS blocks
+# (comm.pipelined_linear_all_reduce; env KAFKA_TP_PIPE_CHUNKS, 1 = off). At Llama-3-70B TP = 8 a 2k-token chunk has
+# 160 such seams of 32 MiB each; with the pipeline only the last block's all-reduce is left exposed.
+PIPE_CHUNKS = max(1, int(os.environ.get("KAFKA_TP_PIPE_CHUNKS", "4")))
+PIPE_ROWS = 256
 SKINNY = frozenset(p for p in os.environ.get("KAFKA_SKINNY", "qkv,o,down").replace("+", ",").split(",")
                    if p in ("qkv", "o", "down"))
 _OVL: dict = {}
@@ -250,6 +257,9 @@ class TransformerLM:
             paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out)
             if tp and self._can_overlap(T, lw.o_t):
                 self._overlapped_seam(attn_out.view(T, -1), lw.o_t, residual, lw.post_norm, eps, x)
+            elif tp and self._can_pipe(T, lw.o, lw.o_t):
+                o = pstate.tp_linear_all_reduce(attn_out.view(T, -1), self._dense(lw.o, lw.o_t), self._pipe_chunks(T))
+                ops.fused_add_rmsnorm(o, residual, lw.post_norm, eps, out=x)
             else:
                 o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t, kind="o")
                 if tp:
@@ -268,6 +278,9 @@ class TransformerLM:
                     # the next layer's input RMSNorm is the seam's normalisation: delta is consumed here
                     self._overlapped_seam(a, lw.down_t, residual, self.layers[i + 1].input_norm, eps, x)
                     delta, pending = _SEAM_DONE, False
+                elif tp and self._can_pipe(T, lw.down, lw.down_t):
+                    delta = pstate.tp_linear_all_reduce(a, self._dense(lw.down, lw.down_t), self._pipe_chunks(T))
+                    pending = False  # already reduced: the next seam is a plain add + RMSNorm
                 else:
                     delta = self._linear(a, lw.down, lw.down_t, kind="down")
                     pending = tp
@@ -284,6 +297,18 @@ class TransformerLM:
             logits = pstate.tp_all_gather_lastdim(logits)
         return logits[:, :cfg.vocab_size]
 
+    def _can_pipe(self, T: int, w: torch.Tensor | None, wt: torch.Tensor | None) -> bool:
+        """A prefill-sized seam that goes to the library all-reduce (beyond the custom all-reduce's buffer) and is
+        long enough to pipeline its GEMM against it."""
+        if PIPE_CHUNKS < 2 or T < 2 * PIPE_ROWS or (self.stream and T <= self.stream_max_m):
+            return False
+        car = pstate.custom_ar()
+        n = (w.shape[0] if w is not None else wt.shape[0] * 32)
+        return car is None or T * n * 2 > car.max_bytes
+
+    def _pipe_chunks(self, T: int) -> int:
+        return max(2, min(PIPE_CHUNKS, T // PIPE_ROWS))
+
     def _can_overlap(self, T: int, wt: torch.Tensor | None) -> bool:
         if not (TP_OVERLAP and self.stream and wt is not None and 0 < T <= self.stream_max_m and self.device.type == "cuda"):
             return False
@@ -293,26 +318,26 @@ class TransformerLM:
     def _overlapped_seam(self, a: torch.Tensor, wt: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor,
                          eps: float, out: torch.Tensor) -> None:
         """residual += allreduce(a @ W^T); out = rmsnorm(residual) * norm_w, with W's two column halves pipelined
-        against their all-reduces (TP_OVERLAP above)."""
+        against their all-reduces (TP_OVERLAP above): half 0 reduced on the side stream into a persistent buffer,
+        half 1 reduced + joined + residual + RMSNorm in one fused launch."""
         car = pstate.custom_ar()
         side, (ev_in, ev1, ev_done) = _overlap_stream(a.device)
         main = torch.cuda.current_stream(a.device)
         nb = wt.shape[0] // 2
         T = a.shape[0]
-        halves = [torch.empty(T, nb * 32, dtype=self.dtype, device=a.device) for _ in range(2)]
+        key = (a.device, T, nb * 32)
+        h0 = _OVL.get(key)
+        if h0 is None:  # persistent (a graph capture records a fixed address; stream order keeps uses apart)
+            h0 = _OVL[key] = torch.empty(T, nb * 32, dtype=self.dtype, device=a.device)
         y0 = ops.linear_stream(a, wt[:nb])
         ev_in.record(main)
         with torch.cuda.stream(side):
             side.wait_event(ev_in)
-            car.all_reduce(y0, out=halves[0])  # overlaps the second half's GEMM below
-        y1 = ops.linear_stream(a, wt[nb:])
-        ev1.record(main)
-        with torch.cuda.stream(side):
-            side.wait_event(ev1)
-            car.all_reduce(y1, out=halves[1])
+            car.all_reduce(y0, out=h0)  # overlaps the second half's GEMM below
             ev_done.record(side)
-        main.wait_event(ev_done)  # joined: every buffer the side stream read is released after it on main
-        ops.fused_add_rmsnorm(torch.cat(halves, 1), residual, norm_w, eps, out=out)
+        y1 = ops.linear_stream(a, wt[nb:])
+        main.wait_event(ev_done)  # joined: half 0 is reduced (and every buffer the side stream read is released)
+        car.all_reduce_add_rmsnorm(y1, residual, norm_w, eps, out, pre=h0)
 
     def _embed(self, tokens: torch.Tensor) -> torch.Tensor:
         if self.tp == 1:

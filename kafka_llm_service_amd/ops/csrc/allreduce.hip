@@ -167,6 +167,10 @@ __global__ __launch_bounds__(256) void allreduce_oneshot_kernel(ARPtrs ptrs, int
 
 // Fused: rows r of [T, d] are owned by block r % nblocks (d <= 8 * 256 * CPT). Per row: s = bf16(allreduce(x) +
 // resid); resid = s; out = bf16(s * rsqrt(mean(s^2) + eps) * w) — the fused_add_rmsnorm of the same inputs.
+// With `pre` (dpre > 0 columns): the row's first dpre columns are ALREADY all-reduced (bf16 [T, dpre], row stride
+// pre_s: the first column half of an overlapped TP seam, reduced on a side stream while the second half's GEMM
+// streamed) and only the last d - dpre columns (x: [T, d - dpre] or its slabs) go through this exchange — the
+// half's all-reduce, the join, the residual add and the RMSNorm of the full row in one launch, no concatenation.
 template <int NR, int CPT>
 __global__ __launch_bounds__(256) void allreduce_add_rmsnorm_kernel(ARPtrs ptrs, int rank, const bf16* x,
                                                                      const float* __restrict__ xp, int S,
@@ -174,15 +178,16 @@ __global__ __launch_bounds__(256) void allreduce_add_rmsnorm_kernel(ARPtrs ptrs,
                                                                      bf16* __restrict__ resid, int64_t rs,
                                                                      const bf16* __restrict__ w, float eps,
                                                                      bf16* __restrict__ out, int64_t os,
-                                                                     int64_t max_bytes) {
+                                                                     int64_t max_bytes, const bf16* __restrict__ pre,
+                                                                     int64_t pre_s, int dpre) {
   __shared__ int s_e;
   __shared__ float red[4];
   const int e = ar_epoch(ptrs, rank, &s_e);
   const int64_t half = (int64_t)(e & 1) * max_bytes;
   bf16* mine = reinterpret_cast<bf16*>(ptrs.base[rank] + AR_HEADER + half);
-  const int n8 = d >> 3;
+  const int n8 = d >> 3, np8 = dpre >> 3, nx8 = n8 - np8;  // chunks per row: all / pre-reduced / exchanged
   for (int r = blockIdx.x; r < T; r += gridDim.x)
-    for (int c = threadIdx.x; c < n8; c += 256) stage8(mine, x, xp, S, ps, (int64_t)r * n8 + c);
+    for (int c = threadIdx.x; c < nx8; c += 256) stage8(mine, x, xp, S, ps, (int64_t)r * nx8 + c);
   ar_exchange<NR>(ptrs, rank, e);
   for (int r = blockIdx.x; r < T; r += gridDim.x) {  // block-uniform
     float v[CPT][8];
@@ -191,7 +196,13 @@ __global__ __launch_bounds__(256) void allreduce_add_rmsnorm_kernel(ARPtrs ptrs,
     for (int i = 0; i < CPT; ++i) {
       const int c = threadIdx.x + 256 * i;
       if (c < n8) {
-        ar_sum8<NR>(ptrs, half, (int64_t)r * n8 + c, v[i]);
+        if (c < np8) {
+          const bf16x8 pv = load_bf16x8(pre + (int64_t)r * pre_s + c * 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[i][j] = (float)pv[j];
+        } else {
+          ar_sum8<NR>(ptrs, half, (int64_t)r * nx8 + (c - np8), v[i]);
+        }
         const bf16x8 rv = load_bf16x8(resid + (int64_t)r * rs + c * 8);
         bf16x8 sv;
 #pragma unroll
@@ -274,16 +285,18 @@ extern "C" hipError_t kafka_launch_car_allreduce_add_rmsnorm(char* const* bases,
                                                             const bf16* x, const float* xp, int S, int64_t ps,
                                                             int T, int d, bf16* resid, int64_t rs, const bf16* w,
                                                             float eps, bf16* out, int64_t os, int64_t max_bytes,
-                                                            int nblocks, hipStream_t st) {
+                                                            int nblocks, const bf16* pre, int64_t pre_s, int dpre,
+                                                            hipStream_t st) {
   if (nranks < 2 || nranks > AR_MAX_RANKS || nblocks < 1 || nblocks > AR_MAX_BLOCKS || d % 8 != 0 ||
-      (int64_t)T * d * 2 > max_bytes || (x == nullptr) == (xp == nullptr))
+      dpre % 8 != 0 || dpre < 0 || dpre >= d || (dpre > 0) != (pre != nullptr) ||
+      (int64_t)T * (d - dpre) * 2 > max_bytes || (x == nullptr) == (xp == nullptr))
     return hipErrorInvalidValue;
   const int cpt = (d / 8 + 255) / 256;
   ARPtrs p{};
   for (int i = 0; i < nranks; ++i) p.base[i] = bases[i];
 #define KAFKA_CARN(NR_, CPT_)                                                                                    \
   allreduce_add_rmsnorm_kernel<NR_, CPT_><<<nblocks, 256, 0, st>>>(p, rank, x, xp, S, ps, T, d, resid, rs, w, eps, \
-                                                                   out, os, max_bytes)
+                                                                   out, os, max_bytes, pre, pre_s, dpre)
 #define KAFKA_CARN_R(CPT_)                          \
   switch (nranks) {                                 \
     case 2: KAFKA_CARN(2, CPT_); break;             \

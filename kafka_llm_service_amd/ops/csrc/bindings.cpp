@@ -89,7 +89,7 @@ hipError_t kafka_launch_skinny_gemm(const bf16* X, int64_t ldx, const bf16* Wt, 
 hipError_t kafka_launch_car_allreduce_add_rmsnorm(char* const* bases, int nranks, int rank, const bf16* x,
                                                   const float* xp, int S, int64_t ps, int T, int d, bf16* resid,
                                                   int64_t rs, const bf16* w, float eps, bf16* out, int64_t os,
-                                                  int64_t max_bytes, int nblocks, hipStream_t st);
+                                                  int64_t max_bytes, int nblocks, const bf16* pre, int64_t pre_s, int dpre, hipStream_t st);
 }  // extern "C"
 
 #define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
@@ -790,24 +790,38 @@ static void car_all_reduce(at::Tensor x, c10::optional<at::Tensor> y, std::vecto
 }
 
 // residual <- allreduce(x) + residual; out = rmsnorm(residual) * w  (x: bf16 [T, d] or slab [S, T, d])
+// pre (optional): bf16 [T, dpre] columns 0 .. dpre-1 of the row, already all-reduced; x then holds only the remaining
+// d - dpre columns (the second half of an overlapped TP seam)
 static void car_all_reduce_add_rmsnorm(at::Tensor x, at::Tensor residual, at::Tensor w, double eps, at::Tensor out,
                                        std::vector<int64_t> bases, int64_t rank, int64_t max_bytes,
-                                       int64_t nblocks) {
+                                       int64_t nblocks, c10::optional<at::Tensor> pre) {
   CHECK_CUDA(x); CHECK_DT(residual, at::kBFloat16); CHECK_DT(w, at::kBFloat16); CHECK_DT(out, at::kBFloat16);
   const bool slab = is_slab(x);
   if (slab) check_slab(x); else CHECK_DT(x, at::kBFloat16);
   TORCH_CHECK(x.is_contiguous() && (slab || x.dim() == 2), "car_all_reduce_add_rmsnorm: x [T, d] or slab");
-  const int T = x.size(slab ? 1 : 0), d = x.size(slab ? 2 : 1);
+  const int T = x.size(slab ? 1 : 0), dx = x.size(slab ? 2 : 1);
+  int dpre = 0;
+  int64_t pre_s = 0;
+  const bf16* pp = nullptr;
+  if (pre.has_value()) {
+    CHECK_CUDA(*pre); CHECK_DT(*pre, at::kBFloat16);
+    TORCH_CHECK(pre->dim() == 2 && pre->size(0) == T && pre->stride(1) == 1 && pre->size(1) % 8 == 0 &&
+                    pre->stride(0) % 8 == 0, "car_all_reduce_add_rmsnorm: pre [T, dpre] bf16");
+    dpre = pre->size(1);
+    pre_s = pre->stride(0);
+    pp = bptr(*pre);
+  }
+  const int d = dpre + dx;
   TORCH_CHECK(residual.dim() == 2 && residual.size(0) == T && residual.size(1) == d && residual.stride(1) == 1 &&
                   out.dim() == 2 && out.size(0) == T && out.size(1) == d && out.stride(1) == 1 &&
-                  w.is_contiguous() && w.numel() == d && d % 8 == 0 && d <= 16384,
+                  w.is_contiguous() && w.numel() == d && d % 8 == 0 && dx % 8 == 0 && d <= 16384,
               "car_all_reduce_add_rmsnorm: shapes");
-  TORCH_CHECK((int64_t)T * d * 2 <= max_bytes, "car_all_reduce_add_rmsnorm: message larger than the buffer");
+  TORCH_CHECK((int64_t)T * dx * 2 <= max_bytes, "car_all_reduce_add_rmsnorm: message larger than the buffer");
   auto b = car_bases(bases);
   CHECK_HIP(kafka_launch_car_allreduce_add_rmsnorm(
       b.data(), (int)b.size(), (int)rank, slab ? nullptr : bptr(x), slab ? x.data_ptr<float>() : nullptr,
-      slab ? x.size(0) : 0, slab ? (int64_t)T * d : 0, T, d, bptr(residual), residual.stride(0), bptr(w), (float)eps,
-      bptr(out), out.stride(0), max_bytes, (int)nblocks, cur_stream()));
+      slab ? x.size(0) : 0, slab ? (int64_t)T * dx : 0, T, d, bptr(residual), residual.stride(0), bptr(w),
+      (float)eps, bptr(out), out.stride(0), max_bytes, (int)nblocks, pp, pre_s, dpre, cur_stream()));
 }
 
 // Expert-parallel all-to-all (bcast = false: part q of `send` [nranks * bpd bytes] goes to rank q) or all-gather
@@ -911,7 +925,9 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("car_error_async", &car_error_async);
   m.def("car_timing", &car_timing);
   m.def("car_all_reduce", &car_all_reduce);
-  m.def("car_all_reduce_add_rmsnorm", &car_all_reduce_add_rmsnorm);
+  m.def("car_all_reduce_add_rmsnorm", &car_all_reduce_add_rmsnorm, py::arg("x"), py::arg("residual"), py::arg("w"),
+        py::arg("eps"), py::arg("out"), py::arg("bases"), py::arg("rank"), py::arg("max_bytes"), py::arg("nblocks"),
+        py::arg("pre") = py::none());
   m.def("car_a2a", &car_a2a);
   m.def("ep_dispatch", &ep_dispatch);
   m.def("ep_recv_route", &ep_recv_route);

@@ -64,6 +64,30 @@ def all_reduce_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Ten
     return ops.fused_add_rmsnorm(all_reduce(x, group), residual, w, eps, out=out)
 
 
+def pipelined_linear_all_reduce(x: torch.Tensor, w: torch.Tensor, group, chunks: int) -> torch.Tensor:
+    """sum over ``group`` of x @ w^T for a prefill-sized row-parallel seam, with the GEMM and the library all-reduce
+    pipelined over ``chunks`` row blocks: block i's all-reduce is issued asynchronously (RCCL runs it on its own HIP
+    stream, ordered after the block's GEMM) while block i+1's GEMM runs on the compute stream; the compute stream
+    waits for every block only at the end. The weight is re-read per block (a prefill GEMM is compute-bound) and the
+    per-element sums are the library all-reduce's, so the result equals the unchunked seam's."""
+    T = x.shape[0]
+    y = torch.empty(T, w.shape[0], dtype=x.dtype, device=x.device)
+    bounds = [T * i // chunks for i in range(chunks + 1)]
+    works = []
+    host = x.is_cuda and _is_gloo(group)  # several ranks on one GPU (tests): through host memory, serially
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        if b <= a:
+            continue
+        torch.matmul(x[a:b], w.t(), out=y[a:b])
+        if host:
+            _host_all_reduce(y[a:b], group)
+        else:
+            works.append(dist.all_reduce(y[a:b], group=group, async_op=True))
+    for wk in works:
+        wk.wait()
+    return y
+
+
 def all_gather_lastdim(x: torch.Tensor, world: int, group) -> torch.Tensor:
     x = x.contiguous()
     if x.is_cuda and _is_gloo(group):

@@ -101,10 +101,12 @@ class CustomAllReduce:
         return x if out is None else out
 
     def all_reduce_add_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
-                               out: torch.Tensor) -> torch.Tensor:
+                               out: torch.Tensor, pre: torch.Tensor | None = None) -> torch.Tensor:
+        """residual += allreduce(x); out = rmsnorm(residual) * w — one launch. ``pre``: the row's first columns,
+        already all-reduced (bf16 [T, dpre]); x then holds only the remaining columns (overlapped TP seam)."""
         if not self._skip():
             ext().car_all_reduce_add_rmsnorm(x, residual, w, float(eps), out, self.bases, self.rank, self.max_bytes,
-                                             self.nblocks)
+                                             self.nblocks, pre)
         return out
 
     def fits_bytes(self, nbytes: int) -> bool:

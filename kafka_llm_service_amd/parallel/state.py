@@ -178,6 +178,14 @@ def tp_all_reduce_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.
     return comm.all_reduce_add_rmsnorm(x, residual, w, eps, out, _STATE.tp_group)
 
 
+def tp_linear_all_reduce(x: torch.Tensor, w: torch.Tensor, chunks: int) -> torch.Tensor:
+    """allreduce(x @ w^T) over the TP group, GEMM blocks pipelined against the library all-reduce
+    (comm.pipelined_linear_all_reduce)."""
+    from . import comm
+
+    return comm.pipelined_linear_all_reduce(x, w, _STATE.tp_group, chunks)
+
+
 def tp_all_gather_lastdim(x: torch.Tensor) -> torch.Tensor:
     st = _STATE
     if st.tp == 1:

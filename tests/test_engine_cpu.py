@@ -371,7 +371,11 @@ def test_plan_prefill_items_balances_causal_tiles():
     # a new turn: 2 tiles against a 20k context -> ~target_wgs workgroups in total
     turn = [(0, 64, 0, 20000, 20064), (64, 40, 0, 20104, 20104)]
     items, splits, ranges = plan_prefill_items(turn, 8, 256, 256)
-    assert 200 <= len(items) * 8 <= 320 and ranges == [(0, 104)]
+    assert 200 <= len(items) * 8 <= 256 and ranges == [(0, 104)]
+    # several new turns in one step (tiles of mixed lengths, all long): still ONE round of <= 256 workgroups
+    burst = [(64 * i, 64, i // 2, 19000 + 300 * i, 19100 + 300 * i) for i in range(5)]
+    items, splits, ranges = plan_prefill_items(burst, 8, 256, 256)
+    assert 200 <= len(items) * 8 <= 256, len(items) * 8
 
 
 def test_padded_mixed_steps_match_unpadded(base_engine):

@@ -17,9 +17,9 @@ CFG = dict(model="tiny-llama", device="cpu", num_kv_blocks=256, max_model_len=20
 GREEDY = SamplingParams(temperature=0.0, max_tokens=5, ignore_eos=True)
 
 
-def _prompts():
+def _prompts(long: bool = False):
     g = torch.Generator().manual_seed(11)
-    pre = torch.randint(0, 5000, (48,), generator=g).tolist()
+    pre = torch.randint(0, 5000, (700 if long else 48,), generator=g).tolist()
     return [pre + torch.randint(0, 5000, (n,), generator=g).tolist() for n in (3, 21, 40)]
 
 
@@ -35,13 +35,14 @@ def _group_main(rank: int, world: int, port: int, q, extra: dict) -> None:
     extra = dict(extra)
     os.environ.update(extra.pop("_env", {}))
     proc = extra.pop("_proc", False)
+    long = extra.pop("_long", False)
     from kafka_llm_service_amd.engine import tp_worker
     from kafka_llm_service_amd.parallel import state as pstate
 
     eng, st = tp_worker.build_tp_engine(dict(CFG, **extra), tp=world)
     try:
         if st.is_tp_leader:
-            outs = eng.generate(_prompts(), _proc_params() if proc else GREEDY)
+            outs = eng.generate(_prompts(long), _proc_params() if proc else GREEDY)
             tp_worker.release_followers()
             g = eng.runner.graphs
             q.put(("outs", outs, eng.num_blocks, eng.stats["planned_ahead"], g.stats if g is not None else None))
@@ -68,8 +69,8 @@ def _proc_params():
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("extra", [{}, {"use_graphs": True}, {"_env": {"KAFKA_PLAN_CHANNEL": "gloo"}},
-                                   {"_env": {"KAFKA_PLAN_SLOT_BYTES": "1024"}}],
-                         ids=["eager", "graphs", "gloo_channel", "oversized_plans"])
+                                   {"_env": {"KAFKA_PLAN_SLOT_BYTES": "1024"}}, {"_long": True}],
+                         ids=["eager", "graphs", "gloo_channel", "oversized_plans", "pipelined_prefill_seams"])
 def test_tp2_generate_matches_tp1(extra):
     """Leader plans step n+1 while n runs (late decode inputs filled device-side on EVERY rank from its own sampler
     output); with ``use_graphs`` every rank captures and replays the decode layouts (fake graph backend on CPU:
@@ -90,7 +91,7 @@ def test_tp2_generate_matches_tp1(extra):
     if extra.get("use_graphs"):
         assert gstats["replays"] >= 1 and res["follower_steps"][1]["replays"] == gstats["replays"]
     ref = LLMEngine(EngineConfig(**CFG))
-    prompts = _prompts()
+    prompts = _prompts(extra.get("_long", False))  # _long: a 2 x 700-token prefill step -> GEMM || all-reduce blocks
     # TP=2 reduces in a different order (bf16): tokens must be the TP=1 model's argmax up to a small logit margin
     for p, o in zip(prompts, outs):
         lg = dense_logits(ref.model, p + o)
