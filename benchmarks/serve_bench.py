@@ -105,11 +105,12 @@ def _system_message(chars: int) -> str | None:
     return " ".join(out)
 
 
-# The reference's 13 prompt sections (src/prompts/sections/*.md, 70,568 characters) encode to 36,364 tokens with the
-# engine's tokenizer (engine/tokenizer.py; measured once, the reference is not read at run time). Our own re-worded
-# sections are 47,002 characters / 19,571 tokens (PARITY.md #18). ``--system-tokens ref`` serves a shared prefix of
-# the reference prompt's size so the HTTP numbers compare like for like.
-REFERENCE_PROMPT_TOKENS = 36364
+# The reference's 13 prompt sections (rendered: 70,496 characters) encode to 17,032 tokens with the engine's
+# Llama-3-class BPE (engine/tokenizer.py, round 4; 18,151 with the server's tool schemas — the round-3 toy BPE made
+# that 37.4k). ``--system-tokens ref`` serves a synthetic shared prefix of the reference prompt's size (+ schemas);
+# ``--system-tokens 18000`` the headline bench's 18k shared prefix, so the API-path tax on the engine metric is
+# measured like for like.
+REFERENCE_PROMPT_TOKENS = 18151
 
 
 @functools.lru_cache(maxsize=4)

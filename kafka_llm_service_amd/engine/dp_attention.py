@@ -128,38 +128,43 @@ def generate_lockstep(eng, st, prompts: list[list[int]], params: SamplingParams)
             return [out[r] for r in rids]
 
 
-def _idle_wait(conn, board, wake_seen: int, idle_since: float, hb_left: float) -> bool:
-    """An idle group. With the board: sleep until a request arrives on this rank's pipe or a peer bumps the wake
-    counter past ``wake_seen`` (the group's agreed reading before it went idle) -> True (step with the group), or
-    the heartbeat is due -> False (do NOT step: the peers are asleep). No collective is polled. Without a board:
-    one pipe poll backing off from 2 to 50 ms, then True (every wake-up is one gloo agreement of the group, which
-    the ranks reach on their own backoffs)."""
+def _idle_wait(conn, board, wake_seen: int, idle_since: float, hb_left: float) -> str | None:
+    """An idle group. With the board: sleep until a message arrives on this rank's pipe ("msg") or a peer bumps the
+    wake counter past ``wake_seen`` — the group's agreed reading before it went idle — ("wake": that peer is entering
+    a group step, join it), or the heartbeat is due (None: do NOT step, the peers are asleep). No collective is
+    polled. Without a board: one pipe poll backing off from 2 to 50 ms, then "msg" (every wake-up is one gloo
+    agreement of the group, which the ranks reach on their own backoffs)."""
     idle = time.monotonic() - idle_since
     if board is None:
         conn.poll(min(0.05, 0.002 * (1 + int(idle * 10))))
-        return True
+        return "msg"
     t_end = time.monotonic() + hb_left
     while True:
-        if conn.poll(0.0005 if idle < 1.0 else 0.002) or board.wake_count() > wake_seen:
-            return True
+        if board.wake_count() > wake_seen:
+            return "wake"
+        if conn.poll(0.0005 if idle < 1.0 else 0.002):
+            return "msg"
         if time.monotonic() >= t_end:
-            return False
+            return None
         idle = time.monotonic() - idle_since
 
 
 def serve_pipe_lockstep(eng, st, conn) -> None:
     """The request loop of one DP-attention rank behind the API server's engine client: like engine/client.py
     serve_pipe (same message protocol), but the rank steps whenever ANY rank of its group has work. While the whole
-    group is idle the ranks sleep on their pipes (``_idle_wait``); the rank that receives a request bumps the
-    agreement board's wake counter so its peers join the group step within about a millisecond (no
-    collective polling of an idle group)."""
+    group is idle the ranks sleep on their pipes (``_idle_wait``, ADVICE r03: no collective polling of an idle
+    group). Protocol (shared-memory board): an idle rank enters a group step only if it has work of its own or a
+    stop (then it first bumps the board's wake counter) or a peer woke it; a message that brings no work (health,
+    pin, abort) is answered without stepping. Every bump is made by a rank that is about to step, so a woken rank
+    always finds its peer in the agreement; the wake reading is part of each agreement, so a bump is never missed
+    or double-counted across idle periods."""
     from kafka_llm_service_amd.engine.client import HEARTBEAT_S
 
     agree = make_agree(st)
     board = agree.board
     pinned: list[int] | None = None
     last_hb = 0.0
-    busy = 0
+    busy = 0  # the group's busy flag, as last agreed
     wake_seen = 0
     idle_since = time.monotonic()
     while True:
@@ -167,9 +172,12 @@ def serve_pipe_lockstep(eng, st, conn) -> None:
         if now - last_hb >= HEARTBEAT_S:
             conn.send(("hb", eng.stats["steps"]))
             last_hb = now
-        if not busy and not _idle_wait(conn, board, wake_seen, idle_since,
-                                       max(0.0, HEARTBEAT_S - (now - last_hb))):
-            continue  # heartbeat only
+        woke = False
+        if not busy:
+            r = _idle_wait(conn, board, wake_seen, idle_since, max(0.0, HEARTBEAT_S - (now - last_hb)))
+            if r is None:
+                continue  # heartbeat only
+            woke = r == "wake"
         stop = False
         while conn.poll(0):
             msg = conn.recv()
@@ -199,9 +207,12 @@ def serve_pipe_lockstep(eng, st, conn) -> None:
             elif kind == "stop":
                 stop = True
                 break
-            if board is not None and not busy and (kind in ("add", "stop")):
-                board.wake()  # peers asleep in _idle_wait join the next group step
-            busy = int(eng.has_unfinished())
+        mine = eng.has_unfinished()
+        if board is not None and not busy:
+            if not (mine or stop or woke):
+                continue  # nothing for the group (health / pin / abort): the peers stay asleep
+            if mine or stop:
+                board.wake()  # peers asleep in _idle_wait join this group step
         # every rank takes part in every agreement, busy or not; a stop seen by any rank stops the whole group
         # after the same step (nobody is left waiting in a collective for a peer that has exited)
         wake_read = board.wake_count() if board is not None else 0

@@ -124,7 +124,6 @@ class LLMEngine:
 
             st = pstate.get()
             dpa = (st.ep, st.ep_rank)
-            cfg.use_graphs = False  # idle (expert-only) steps interleave with decode steps; eager
         self.model = model or build_model(mc, self.device, tp=cfg.tp, tp_rank=cfg.tp_rank, seed=cfg.seed,
                                           weights=cfg.weights, max_positions=min(cfg.max_model_len,
                                                                                  mc.max_position_embeddings),
@@ -348,7 +347,9 @@ class LLMEngine:
         t_max, busy, fl, ext = got[0], got[1], got[2], tuple(got[3:])
         cur, self._inflight = self._inflight, None
         if t_max > 0:
-            self.model.ep_t_cap = t_max
+            # the all-to-all capacity: the group's largest step, bucketed to a power of two so captured decode graphs
+            # (keyed by it) are reused across steps; every rank derives the same value from the agreed maximum
+            self.model.ep_t_cap = 1 << max(3, (t_max - 1).bit_length())
             self.stats["group_steps"] = self.stats.get("group_steps", 0) + 1
             if host is None:
                 with trace.span("dp_idle_step"):

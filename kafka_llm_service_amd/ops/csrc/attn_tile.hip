@@ -130,7 +130,37 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
     valid[rb] = tok < it.q_count;
     token[rb] = it.q_start + tok;
     head[rb] = kvh * G + R % G;
-    limit[rb] = valid[rb] ? q_limit[token[rb]] : -1;
+  }
+  // prologue loads that depend only on the work item go out TOGETHER (one round trip instead of a chain of three):
+  // the item's page ids, the causal limits and the Q fragments (B operand of S^T = K . Q^T: lane (r, h) holds
+  // Q[row r][16 kk + 8 h + j])
+  const int lo0 = it.kv_lo;
+  const int pg00 = (lo0 & ~63) >> 4;
+  const int npg_all0 = ((it.kv_hi + 15) >> 4) - pg00;
+  const int npg0 = min(npg_all0, 2048);
+  const int* bt0 = block_tables + (int64_t)it.bt_row * bt_stride;
+  constexpr int PPT = 2048 / (512 / RB);  // page ids per thread (MAXPG / threads)
+  int pgv[PPT];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int i = tid + k * (512 / RB);
+    pgv[k] = i < npg0 ? bt0[pg00 + i] : 0;
+  }
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) limit[rb] = valid[rb] ? q_limit[token[rb]] : -1;
+  bf16x8 qf[RB][D / 16];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const bf16* qrow = q + (int64_t)token[rb] * q_stride + (int64_t)head[rb] * D + 8 * h;
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) {
+      if (valid[rb]) {
+        qf[rb][kk] = load_bf16x8(qrow + 16 * kk);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[rb][kk][j] = (bf16)0.f;
+      }
+    }
   }
   // per-block wave-uniform bounds: keys past hi_b are masked for every row of the block, keys <= wmin_b for none
   int hi_b[2], wmin_b[2];  // (RB == 1: block 1 mirrors block 0)
@@ -156,8 +186,11 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
   const int pg0 = base >> 4;
   const int npg_all = ((it.kv_hi + 15) >> 4) - pg0;
   const int npg = min(npg_all, MAXPG);
-  const int* bt = block_tables + (int64_t)it.bt_row * bt_stride;
-  for (int i = tid; i < npg; i += 256) s_pages[i] = bt[pg0 + i];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int i = tid + k * (512 / RB);
+    if (i < npg) s_pages[i] = pgv[k];
+  }
   if (lane == 0) s_hi[w] = max(hi_b[0], hi_b[1]);
   __syncthreads();
   int hi_wg = s_hi[0];
@@ -192,21 +225,6 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
   for (int j = 0; j < NSLOT - 1; ++j)
     if (j < ntiles) issue(j);
 
-  // ---- Q fragments (B operand of S^T = K . Q^T): lane (r, h) holds Q[row r][16 kk + 8 h + j]
-  bf16x8 qf[RB][D / 16];
-#pragma unroll
-  for (int rb = 0; rb < RB; ++rb) {
-    const bf16* qrow = q + (int64_t)token[rb] * q_stride + (int64_t)head[rb] * D + 8 * h;
-#pragma unroll
-    for (int kk = 0; kk < D / 16; ++kk) {
-      if (valid[rb]) {
-        qf[rb][kk] = load_bf16x8(qrow + 16 * kk);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[rb][kk][j] = (bf16)0.f;
-      }
-    }
-  }
   // Running state per row block: O^T accumulators; row sums `ls` as an MFMA accumulator (every register of a lane
   // holds its column's sum ones . P: 8 MFMAs per tile instead of 64 adds); the running max m (exp2 domain).
   // (Folding -m into the QK^T accumulator init would save the per-score FMA too, but needs Q prescaled by

@@ -318,7 +318,7 @@ def test_tp2_custom_allreduce_lost_peer_fails_the_step(cuda):
     assert res["leader"].startswith("raised"), res["leader"]
 
 
-def _dpa_gpu_main(rank, world, port, q, layout):
+def _dpa_gpu_main(rank, world, port, q, layout, graphs=False):
     dev = rank % torch.cuda.device_count()
     _env(rank, world, port, dev)
     os.environ["KAFKA_TP_BACKEND"] = "gloo"
@@ -340,7 +340,8 @@ def _dpa_gpu_main(rank, world, port, q, layout):
                 torch.cuda.set_sync_debug_mode("default")
                 calls[0] += 1
         setattr(MoEBlock, name, checked)
-    eng, st = dp_attention.build_dpa_engine(dict(CFG, model="tiny-mixtral", device=f"cuda:{dev}"), ep=world)
+    eng, st = dp_attention.build_dpa_engine(dict(CFG, model="tiny-mixtral", device=f"cuda:{dev}", use_graphs=graphs),
+                                            ep=world)
     try:
         assert comm.get_custom(st.ep_group) is not None, "IPC all-to-all not registered on the EP group"
         mine = [p for i, p in enumerate(_prompts(eng.model_cfg.vocab_size))
@@ -348,14 +349,17 @@ def _dpa_gpu_main(rank, world, port, q, layout):
         sp = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
         outs = dp_attention.generate_lockstep(eng, st, mine, sp)
         comm.get_custom(st.ep_group).check()
-        q.put((rank, outs, eng.stats["group_steps"], calls[0]))
+        g = eng.runner.graphs
+        q.put((rank, outs, eng.stats["group_steps"], calls[0], g.stats["replays"] if g is not None else 0,
+               eng.stats["planned_ahead"]))
     finally:
         pstate.destroy()
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("layout", ["spread", "one_idle"])
-def test_dp_attention_mixtral_on_one_gpu(cuda, layout):
+@pytest.mark.parametrize("layout,graphs", [("spread", False), ("one_idle", False), ("spread", True)],
+                         ids=["spread", "one_idle", "spread_graphs"])
+def test_dp_attention_mixtral_on_one_gpu(cuda, layout, graphs):
     """Mixtral with data-parallel attention, EP = 2 over two processes on one GPU: each rank decodes its own
     sequences (or none), every MoE layer exchanges rows through the device-side dispatch + IPC all-to-all without
     a host sync, and every greedy token is the EP = 1 model's argmax up to bf16 rounding."""
@@ -365,7 +369,7 @@ def test_dp_attention_mixtral_on_one_gpu(cuda, layout):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_dpa_gpu_main, args=(r, 2, port, q, layout)) for r in range(2)]
+    ps = [ctx.Process(target=_dpa_gpu_main, args=(r, 2, port, q, layout, graphs)) for r in range(2)]
     for p in ps:
         p.start()
     res = {m[0]: m[1:] for m in (q.get(timeout=240) for _ in range(2))}
@@ -373,6 +377,9 @@ def test_dp_attention_mixtral_on_one_gpu(cuda, layout):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[0][1] == res[1][1] and res[0][2] > 0 and res[1][2] > 0
+    assert res[0][4] > 0  # the group planned ahead (pipelined lockstep)
+    if graphs:
+        assert res[0][3] > 0 and res[1][3] > 0  # decode steps replayed from captured graphs on both ranks
     ref = LLMEngine(EngineConfig(**dict(CFG, model="tiny-mixtral", device="cuda:0")))
     prompts = _prompts(ref.model_cfg.vocab_size)
     for r in (0, 1):

@@ -220,3 +220,8 @@ def test_dp_attention_group_serves_threads_over_http():
                        json={"model": "m", "messages": [{"role": "user", "content": f"hi {i}"}], "stream": False,
                              "max_tokens": 6})
             assert r.status_code == 200 and r.json()["usage"]["completion_tokens"] == 6
+            # health / metrics requests reach ONE rank of the idle group at a time: answered without a group
+            # step (a lone rank entering the agreement would wait for peers that sleep on their pipes)
+            for _ in range(3):
+                assert c.get("/metrics").status_code == 200
+                time.sleep(0.05)

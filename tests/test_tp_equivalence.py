@@ -257,29 +257,31 @@ def _dpa_owner(layout: str, i: int) -> int:
     return i % 2 if layout == "spread" else 0
 
 
-def _dpa_main(rank: int, world: int, port: int, q, layout, board: str = "1") -> None:
+def _dpa_main(rank: int, world: int, port: int, q, layout, board: str = "1", graphs: bool = False) -> None:
     """One rank of a DP-attention group: its own prompts (possibly none), experts sharded over the group."""
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(world),
                        "RANK": str(rank), "LOCAL_RANK": str(rank), "KAFKA_DPA_BOARD": board})
     from kafka_llm_service_amd.engine import dp_attention
     from kafka_llm_service_amd.parallel import state as pstate
 
-    eng, st = dp_attention.build_dpa_engine(dict(CFG, model="tiny-mixtral"), ep=world)
+    eng, st = dp_attention.build_dpa_engine(dict(CFG, model="tiny-mixtral", use_graphs=graphs), ep=world)
     try:
         assert eng.model.dp_attention and eng.model.ep == world and eng.model.tp == 1
         assert eng.model.layers[0].w13.shape[0] == eng.model_cfg.num_experts // world
         mine = [p for i, p in enumerate(_prompts()) if _dpa_owner(layout, i) == rank]
         outs = dp_attention.generate_lockstep(eng, st, mine, GREEDY)
+        g = eng.runner.graphs
         q.put((rank, outs, eng.stats["group_steps"], eng.stats["planned_ahead"],
-               dp_attention.make_board(st) is not None))
+               dp_attention.make_board(st) is not None, g.stats["replays"] if g is not None else 0))
     finally:
         pstate.destroy()
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("layout,board", [("spread", "1"), ("one_idle", "1"), ("spread", "0")],
-                         ids=["spread", "one_idle", "spread_gloo_agree"])
-def test_dp_attention_mixtral_matches_single_rank(layout, board):
+@pytest.mark.parametrize("layout,board,graphs", [("spread", "1", False), ("one_idle", "1", False),
+                                                 ("spread", "0", False), ("spread", "1", True)],
+                         ids=["spread", "one_idle", "spread_gloo_agree", "spread_graphs"])
+def test_dp_attention_mixtral_matches_single_rank(layout, board, graphs):
     """Mixtral with data-parallel attention over 2 ranks (each rank its own sequences, whole attention weights,
     half the experts, device-side all-to-all dispatch/combine in lockstep): every greedy token is the EP=1 model's
     argmax up to a small logit margin — also when one rank has no sequences at all and only serves its experts.
@@ -290,7 +292,7 @@ def test_dp_attention_mixtral_matches_single_rank(layout, board):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_dpa_main, args=(r, 2, port, q, layout, board)) for r in range(2)]
+    procs = [ctx.Process(target=_dpa_main, args=(r, 2, port, q, layout, board, graphs)) for r in range(2)]
     for p in procs:
         p.start()
     res = {m[0]: m[1:] for m in (q.get(timeout=240) for _ in range(2))}
@@ -300,6 +302,8 @@ def test_dp_attention_mixtral_matches_single_rank(layout, board):
     assert res[0][1] == res[1][1]  # lockstep: the same number of group steps on both ranks
     assert res[0][2] > 0  # planned ahead
     assert res[0][3] == res[1][3] == (board == "1")
+    if graphs:  # decode steps replayed from captured layouts (fake graph backend on CPU: static buffers only)
+        assert res[0][4] > 0 and res[1][4] > 0
     ref = LLMEngine(EngineConfig(**dict(CFG, model="tiny-mixtral")))
     prompts = _prompts()
     for r in (0, 1):
