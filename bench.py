@@ -488,6 +488,7 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
         "prefix_hit_rate": round(kv["hit_tokens"] / max(1, kv["query_tokens"]), 4),
         "preemptions": eng.sched.num_preemptions,
         "planned_ahead_frac": round(eng.stats.get("planned_ahead", 0) / max(1, eng.stats.get("steps", 1)), 4),
+        "planned_late_frac": round(eng.stats.get("planned_late", 0) / max(1, eng.stats.get("steps", 1)), 4),
         "grammar_rollbacks": eng.stats.get("grammar_rollbacks", 0),
     }
     if rank == 0:

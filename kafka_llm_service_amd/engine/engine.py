@@ -196,7 +196,7 @@ class LLMEngine:
             self.runner.graphs = DecodeGraphs(self.runner)
         self.requests: dict[str, Sequence] = {}
         self.stats = {"steps": 0, "prompt_tokens": 0, "cached_tokens": 0, "output_tokens": 0, "step_time": 0.0,
-                      "replans": 0, "planned_ahead": 0}
+                      "replans": 0, "planned_ahead": 0, "planned_late": 0}
         self._inflight: _InFlight | None = None  # the step on the GPU that has not been collected yet
         self.step_ms: deque = deque(maxlen=512)  # intervals between consecutive step completions (busy periods)
         self._t_done = 0.0
@@ -314,8 +314,8 @@ class LLMEngine:
         if plan is not None:
             if plan.n_added != self._n_added or any(s.finished for s in plan.seqs):
                 self.stats["replans"] += 1  # dropped: the next call plans again with the landed tokens
-            else:
-                self.stats["planned_ahead"] += 1
+            else:  # planned while n ran, launched after it landed: the GPU idles for the launch
+                self.stats["planned_late"] += 1
                 self._inflight = self._launch(plan.batch, plan.host, plan.sampled, None)
         return outs
 
@@ -366,10 +366,11 @@ class LLMEngine:
 
     @staticmethod
     def _needs_landed(sampled: list[Sequence]) -> bool:
-        """True if a row's grammar state would read a token that is still PENDING (the speculative scheduler leaves
-        such rows out, so this only guards the invariant; penalties are device-side and never need landed tokens)."""
+        """True if a row's grammar state would read a token that is still PENDING and cannot be speculated past (the
+        speculative scheduler leaves such rows out by the same predicate, so this only guards the invariant;
+        penalties are device-side and never need landed tokens)."""
         for s in sampled:
-            if s.params.allowed_tokens_fn is not None and s.output_ids[-1:] == [PENDING]:
+            if s.params.allowed_tokens_fn is not None and not Scheduler._grammar_plannable(s):
                 return True
         return False
 

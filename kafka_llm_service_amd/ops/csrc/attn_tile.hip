@@ -76,6 +76,15 @@ __device__ __forceinline__ uint64_t t3_stamp() {
   return t;
 }
 
+// diagnostic-build stamp (ABL == 8): the 100 MHz constant clock, comparable across CUs and XCDs
+__device__ __forceinline__ uint64_t t3_rt() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
 // s_waitcnt vmcnt(n * DPT) for a wave-uniform n in [0, 2] (the count is an immediate)
 template <int DPT>
 __device__ __forceinline__ void t3_wait_tiles(int n) {
@@ -88,7 +97,9 @@ __device__ __forceinline__ void t3_wait_tiles(int n) {
 }
 
 // ABL (timing-only ablations, wrong outputs; KAFKA_TILE_ABL): 1 = no DMA inside the tile loop, 2 = no exp2,
-// 3 = no wait / barrier in the loop, 9 = per-phase shader-clock stamps of the interior loop written over out_part
+// 3 = no wait / barrier in the loop, 8 = workgroup phase stamps (100 MHz clock; the full kernel runs, lse_part is
+// overwritten with u64 [entry, prologue done, first tile landed, loop done, epilogue done, 0, 0, 0] per workgroup
+// blockIdx.y * Hkv + blockIdx.x), 9 = per-phase shader-clock stamps of the interior loop written over out_part
 // (wave (blockIdx.y * Hkv + blockIdx.x) * 4 + w: u64 [wait + barrier, DMA issue, QK^T + max, rescale + exp + PV,
 // tiles, 0, 0, 0])
 // RB = 32-row MFMA blocks per wave: 2 -> 4 waves (one per SIMD, 512 registers each); 1 -> 8 waves (two per SIMD,
@@ -112,6 +123,8 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
   int* s_pages = reinterpret_cast<int*>(smem + NSLOT * SLOT);
   int* s_hi = s_pages + MAXPG;
 
+  uint64_t ph[5] = {0, 0, 0, 0, 0};
+  if constexpr (ABL == 8) ph[0] = t3_rt();
   const TileItem it = items[blockIdx.y];
   const int kvh = blockIdx.x;
   const int tid = threadIdx.x;
@@ -193,6 +206,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
   }
   if (lane == 0) s_hi[w] = max(hi_b[0], hi_b[1]);
   __syncthreads();
+  if constexpr (ABL == 8) ph[1] = t3_rt();
   int hi_wg = s_hi[0];
 #pragma unroll
   for (int i = 1; i < NW; ++i) hi_wg = max(hi_wg, s_hi[i]);
@@ -375,6 +389,8 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
   for (int i = 0; i < n_int; ++i) {
     if constexpr (ABL == 9) stamp_mark(0);
     step(i);
+    if constexpr (ABL == 8)
+      if (i == 0) ph[2] = t3_rt();
     tile_body(std::false_type{}, i, base + TK * tile_of(i));
     if constexpr (ABL == 9) stamp_mark(4);
   }
@@ -400,6 +416,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
     }
     return;
   }
+  if constexpr (ABL == 8) ph[3] = t3_rt();
   // ---- epilogue: through a per-wave LDS transpose (slot ntiles % NSLOT is idle: its last tile was read before the
   // barrier every wave passed NSLOT - 1 tiles ago), so every store instruction writes whole 128-B lines
   const bool part = it.split >= 0;
@@ -410,7 +427,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
     if (!__any(valid[rb])) continue;  // wave-uniform
     const float ll = fits ? ls[rb][0] : __builtin_nanf("");
     const float inv = ll > 0.f ? 1.f / ll : (fits ? 0.f : ll);
-    if (part && valid[rb] && h == 0)
+    if (ABL != 8 && part && valid[rb] && h == 0)
       lse_part[((int64_t)token[rb] * Hq + head[rb]) * S_total + it.split] =
           ll > 0.f ? m[rb] + log2f(ll) : (fits ? -INFINITY : ll);
     const int R0 = 32 * RB * w + 32 * rb;
@@ -462,6 +479,16 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
       }
     }
   }
+  if constexpr (ABL == 8) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ph[4] = t3_rt();
+    if (tid == 0) {
+      uint64_t* dst = reinterpret_cast<uint64_t*>(lse_part) + ((int64_t)blockIdx.y * Hkv + blockIdx.x) * 8;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) dst[k] = ph[k];
+    }
+  }
 }
 
 // Host launcher (bf16 KV only; the fp8 cache keeps tile variant 0). Items: int32 [n, 8] as attn_prefill_kernel.
@@ -489,6 +516,7 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
                       : (slots == 4 ? attn_tile_kernel<1, 4> : attn_tile_kernel<1, 3>);
   if (abl == 1) kern = rb == 2 ? attn_tile_kernel<2, 3, 1> : attn_tile_kernel<1, 3, 1>;
   if (abl == 2) kern = rb == 2 ? attn_tile_kernel<2, 3, 2> : attn_tile_kernel<1, 3, 2>;
+  if (abl == 8) kern = rb == 2 ? attn_tile_kernel<2, 3, 8> : attn_tile_kernel<1, 3, 8>;
   if (abl == 9) kern = rb == 2 ? attn_tile_kernel<2, 3, 9> : attn_tile_kernel<1, 3, 9>;
   kern<<<dim3(Hkv, n_items), 512 / rb, 0, st>>>(
       reinterpret_cast<const TileItem*>(items), q, q_stride, static_cast<const bf16*>(k_cache),

@@ -18,6 +18,7 @@ for mode in ${MODES:-burst stagger}; do
   [[ $rc == 0 ]] || { echo "serve failed rc=$rc"; tail -30 gpurun_out/serve_$tag.log; exit 1; }
   tail -1 gpurun_out/serve_$tag.log
   python scripts/ttft_breakdown.py "/tmp/ktr.*.json" | tee gpurun_out/ttft_breakdown_$tag.txt
-  [[ -n "$KEEP_TRACES" ]] && mkdir -p gpurun_out/traces_$tag && cp /tmp/ktr.*.json gpurun_out/traces_$tag/
+  if [[ -n "$KEEP_TRACES" ]]; then mkdir -p gpurun_out/traces_$tag && cp /tmp/ktr.*.json gpurun_out/traces_$tag/; fi
 done
 done
+exit 0
