@@ -82,9 +82,13 @@ def _prefill_part(q, k_cache, v_cache, meta: AttnMeta, out: torch.Tensor) -> Non
 
 
 def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, meta: AttnMeta,
-                    out: torch.Tensor) -> torch.Tensor:
-    """q [T, Hq, D] (post-RoPE) -> out [T, Hq, D] bf16."""
+                    out: torch.Tensor, gates=None) -> int:
+    """q [T, Hq, D] (post-RoPE) -> out [T, Hq, D] bf16. ``gates`` = (ops.GateSet, gate id the q / KV writer arrives
+    on) on an early-launched decode-only step (models/llama.py EARLY): the cascade streams its prefix K/V before q is
+    ready, the suffix decode runs beside it and waits for its partials only before the merge. Returns the gate the
+    decode arrives on (-1: none)."""
     B = meta.num_decode
+    gs, g_in = gates if gates is not None else (None, -1)
     has_prefill = meta.prefill_items is not None and meta.num_tokens > B
     side = None
     if has_prefill and B > 0 and PREFILL_STREAM and q.is_cuda and not torch.cuda.is_current_stream_capturing():
@@ -95,24 +99,32 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
             side.wait_event(ev_q)
             _prefill_part(q, k_cache, v_cache, meta, out)
             ev_done.record(side)
+    g_out = -1
     if B > 0:
         qd = q[:B]
+        g_pre = -1
         if meta.prefix_items is not None:
+            if gs is not None:
+                g_pre = gs.new()
             ops.attn_prefill(meta.prefix_items, qd, k_cache, v_cache, meta.block_tables, meta.q_limit,
                              meta.scale, out_part=meta.pre_part if meta.pre_part is not None else meta.part,
-                             lse_part=meta.lse, variant=meta.variant)
+                             lse_part=meta.lse, variant=meta.variant,
+                             gates=gs.args(wait=g_in, sig=g_pre) if gs is not None else None)
         # the decode kernel merges each row's prefix partials and its own pieces and writes the final rows
         if meta.decode_sk_rows is not None:
             ops.attn_decode_sk(qd, k_cache, v_cache, meta.block_tables, meta.decode_sk_rows, meta.decode_sk_start,
                                meta.part, meta.lse, meta.scale, out=out[:B], pre_part=meta.pre_part)
         else:
+            if gs is not None:
+                g_out = gs.new()
             ops.attn_decode_items(qd, k_cache, v_cache, meta.block_tables, meta.decode_items, meta.part, meta.lse,
-                                  meta.scale, out=out[:B], pre_part=meta.pre_part)
+                                  meta.scale, out=out[:B], pre_part=meta.pre_part,
+                                  gates=gs.args(wait=g_in, sig=g_out, wait2=g_pre) if gs is not None else None)
     if side is not None:
         torch.cuda.current_stream(q.device).wait_event(ev_done)
     elif has_prefill:
         _prefill_part(q, k_cache, v_cache, meta, out)
-    return out
+    return g_out
 
 
 def default_scale(head_dim: int) -> float:

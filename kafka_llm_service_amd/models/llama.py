@@ -55,6 +55,15 @@ PIPE_CHUNKS = max(1, int(os.environ.get("KAFKA_TP_PIPE_CHUNKS", "4")))
 PIPE_ROWS = 256
 SKINNY = frozenset(p for p in os.environ.get("KAFKA_SKINNY", "qkv,o,down").replace("+", ",").split(",")
                    if p in ("qkv", "o", "down"))
+# Early-launched decode layers (env KAFKA_EARLY; ops.GateSet, csrc/common.h Gates). On a decode-only step of the
+# weight-streaming path every kernel of a layer after its input RMSNorm — QKV projection, RoPE/KV write, cascade,
+# suffix decode, O projection, gate_up, down — is launched without the AQL barrier bit: it is dispatched while its
+# predecessor's last workgroups still run, does the part of its work that does not depend on them (a projection's
+# first weight chunk, the cascade's page table and first prefix K/V tiles) and then waits on a device gate the
+# predecessor's workgroups arrive on. The suffix decode even runs BESIDE the cascade (both read only q / the KV cache)
+# and waits for the cascade's partials only before its merge. The two post-attention / post-MLP RMSNorms stay ordinary
+# launches (full barriers), so each chain is short and every gate waits on the kernel launched right before it.
+EARLY = os.environ.get("KAFKA_EARLY", "0") == "1"
 _OVL: dict = {}
 _SEAM_DONE = object()  # forward(): the previous layer's overlapped seam already produced this layer's input
 
@@ -119,6 +128,8 @@ class TransformerLM:
         self.stream = False  # decode GEMMs on the weight-streaming kernel (enable_stream_weights)
         self.tiled_only = False  # row-major dense weights dropped (enable_stream_weights(tiled_only=True))
         self.stream_max_m = ops.STREAM_MAX_M  # rows up to which a step's projections stream
+        self.early = EARLY  # early-launched decode layers (see EARLY)
+        self._gates: ops.GateSet | None = None
 
     def enable_dp_attention(self, ep: int, ep_rank: int) -> None:
         """Data-parallel attention for a MoE model (call before the weights are created): attention, norms and the
@@ -200,16 +211,32 @@ class TransformerLM:
         return added
 
     def _linear(self, x: torch.Tensor, w: torch.Tensor, wt: torch.Tensor | None, max_splits: int = 8,
-                kind: str = ""):
+                kind: str = "", gates=None):
         """x @ w^T: the weight-streaming kernel for decode-sized x (bf16 or a split-K slab out), the skinny MFMA GEMM
-        for 129..256 rows of the projections in SKINNY, else hipBLASLt."""
+        for 129..256 rows of the projections in SKINNY, else hipBLASLt. ``gates``: streaming path only."""
         M = x.shape[0]
         if self.stream and wt is not None:
             if 0 < M <= self.stream_max_m:
-                return ops.linear_stream(x, wt, max_splits)
+                return ops.linear_stream(x, wt, max_splits, gates=gates)
             if kind in SKINNY and ops.skinny_plan(M, wt.shape[0] * 32, x.shape[1], max_splits):
                 return ops.linear_skinny(x, wt, max_splits)
         return F.linear(x, self._dense(w, wt))
+
+    def _gateset(self, T: int, inp: StepInput, k_cache: torch.Tensor, fuse_rope: bool) -> "ops.GateSet | None":
+        """The forward's device gates when this step runs early-launched layers (EARLY), else None."""
+        m = inp.attn
+        if not (self.early and self.stream and self.tp == 1 and self.moe is None and self.device.type == "cuda"):
+            return None
+        if fuse_rope or not (0 < T <= min(128, self.stream_max_m)) or m.num_decode != T or m.prefill_items is not None:
+            return None
+        if k_cache.dtype != torch.bfloat16 or m.decode_sk_rows is not None or m.decode_items is None:
+            return None
+        if (m.prefix_items is not None and m.variant != 3) or torch.cuda.is_current_stream_capturing():
+            return None
+        if self._gates is None:
+            self._gates = ops.GateSet(self.device, 8 * len(self.layers) + 8)
+        self._gates.begin()
+        return self._gates
 
     @staticmethod
     def _dense(w: torch.Tensor | None, wt: torch.Tensor | None, glu: bool = False) -> torch.Tensor:
@@ -237,7 +264,19 @@ class TransformerLM:
         delta, pending = None, False
         fuse_rope = (self.stream and FUSE_QKV_ROPE and 0 < T <= min(128, self.stream_max_m) and self.layers[0].qkv_t is not None
                      and ops.qkv_rope_fusable(k_caches[0], self.D))
+        gs = self._gateset(T, inp, k_caches[0], fuse_rope)
+        # gate_up + down gated only with the one-split (fused SwiGLU) plan: a split plan puts silu_mul between them
+        glu_gated = gs is not None and self.layers[0].glu and \
+            (ops.stream_plan(T, self.layers[0].gate_up_t.shape[0] * 32, cfg.hidden_size) or (0, 0, 0))[2] == 1
+
+        def G(wait: int = -1, sig: int = -1, wait2: int = -1):
+            return gs.args(wait=wait, sig=sig, wait2=wait2) if gs is not None else None
+
+        def new() -> int:
+            return gs.new() if gs is not None else -1
+
         for i, lw in enumerate(self.layers):
+            g_in = -1  # gate the input RMSNorm arrives on (-1: the QKV projection is an ordinary launch)
             if delta is _SEAM_DONE:
                 pass  # the previous layer's overlapped down seam already wrote residual and x
             elif delta is None:
@@ -246,16 +285,25 @@ class TransformerLM:
             elif pending:
                 pstate.tp_all_reduce_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x)
             else:
-                ops.fused_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x)
+                g_in = new()
+                ops.fused_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x, gates=G(sig=g_in))
+            g_rope = -1  # gate the RoPE / KV write arrives on (the attention kernels' input)
             if fuse_rope:  # RoPE + KV write in the streaming QKV GEMM's epilogue (no rope_kv launch)
                 ops.linear_stream_rope(x, lw.qkv_t, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i],
                                        inp.slot_mapping, self.hq, self.hkv)
             else:
-                qkv = self._linear(x, lw.qkv, lw.qkv_t, kind="qkv")
+                g_qkv = new()
+                qkv = self._linear(x, lw.qkv, lw.qkv_t, kind="qkv", gates=G(wait=g_in, sig=g_qkv))
+                g_rope = new()
                 ops.rope_kv_write(qkv, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i], inp.slot_mapping,
-                                  self.hq, self.hkv)
-            paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out)
-            if tp and self._can_overlap(T, lw.o_t):
+                                  self.hq, self.hkv, gates=G(wait=g_qkv, sig=g_rope))
+            g_attn = paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out,
+                                     gates=(gs, g_rope) if gs is not None else None)
+            if gs is not None:  # the O projection streams its first weight chunk beside the decode's tail
+                o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t, kind="o", gates=G(wait=g_attn))
+                g_post = new() if glu_gated else -1
+                ops.fused_add_rmsnorm(o, residual, lw.post_norm, eps, out=x, gates=G(sig=g_post))
+            elif tp and self._can_overlap(T, lw.o_t):
                 self._overlapped_seam(attn_out.view(T, -1), lw.o_t, residual, lw.post_norm, eps, x)
             elif tp and self._can_pipe(T, lw.o, lw.o_t):
                 o = pstate.tp_linear_all_reduce(attn_out.view(T, -1), self._dense(lw.o, lw.o_t), self._pipe_chunks(T))
@@ -269,6 +317,11 @@ class TransformerLM:
             if lw.router is not None:
                 delta = self.moe(x, lw)
                 pending = tp and not self.moe.reduced
+            elif glu_gated:
+                g_gu = new()
+                a = ops.linear_glu(x, lw.gate_up_t, gates=G(wait=g_post, sig=g_gu))
+                delta = self._linear(a, lw.down, lw.down_t, kind="down", gates=G(wait=g_gu))
+                pending = False
             else:
                 if self.stream and lw.glu and 0 < T <= self.stream_max_m:
                     a = ops.linear_glu(x, lw.gate_up_t)  # SwiGLU in the GEMM epilogue (or on its slabs)

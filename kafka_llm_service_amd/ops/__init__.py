@@ -49,16 +49,61 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | No
     return out
 
 
+class GateSet:
+    """Device gates of one forward (csrc/common.h ``Gates``): a consumer kernel launched without the AQL barrier bit
+    runs its producer-independent prologue (a projection's first weight chunk, the cascade's prefix K/V tiles) while
+    its producer's tail still runs, and waits on the gate the producer's workgroups arrive on before it reads their
+    outputs. ``begin`` zeroes the gates (an ordinary launch: it waits for everything before it) at the start of a
+    forward; ``new`` hands out gate ids in launch order. The caller's rules: a gated consumer waits on the kernel
+    launched immediately before it and writes nothing before its wait (gates chain transitively, so the caching
+    allocator's stream-order reuse stays safe)."""
+
+    INTS = 16  # GATE_INTS: 8 shard counters + the error word (a wait that timed out after 2 s)
+
+    def __init__(self, device: torch.device, n: int):
+        self.n = n
+        self.buf = torch.zeros(n * self.INTS, dtype=torch.int32, device=device)
+        self.used = 0
+
+    def begin(self) -> None:
+        self.buf.zero_()
+        self.used = 0
+
+    def new(self) -> int:
+        if self.used >= self.n:
+            raise RuntimeError("GateSet: out of gates")
+        self.used += 1
+        return self.used - 1
+
+    def args(self, wait: int = -1, expect: int = 0, sig: int = -1, wait2: int = -1, expect2: int = 0):
+        """The (buffer, args) pair the gated ops take."""
+        return self.buf, [int(wait), int(expect), int(sig), int(wait2), int(expect2)]
+
+    def timed_out(self) -> bool:
+        """Whether any wait of the last forward gave up (host sync: tests and diagnostics)."""
+        return bool(self.buf.view(-1, self.INTS)[:, 8].any().item())
+
+    def arrivals(self, g: int) -> int:
+        return int(self.buf.view(-1, self.INTS)[g, :8].sum().item())
+
+
+def _gk(gates) -> dict:
+    """Binding kwargs of an optional (GateSet buffer, args) pair."""
+    return {} if gates is None else {"gates": gates[0], "gate_args": gates[1]}
+
+
 def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
-                      out: torch.Tensor | None = None) -> torch.Tensor:
+                      out: torch.Tensor | None = None, gates=None) -> torch.Tensor:
     """residual <- x + residual (in place); returns rmsnorm(residual) * w (into ``out`` or a new tensor).
-    ``x`` may be a split-K slab [S, T, d] (summed in fp32 before the add)."""
+    ``x`` may be a split-K slab [S, T, d] (summed in fp32 before the add). ``gates``: GateSet.args (the kernel
+    arrives on ``sig`` once per row)."""
     slab = is_slab(x)
     if out is None:
         out = torch.empty(residual.shape, dtype=residual.dtype, device=x.device)
     if _gpu(x):
         xa = x if slab else x.reshape(-1, x.shape[-1])
-        ext().fused_add_rmsnorm(out.view(-1, x.shape[-1]), xa, residual.view(-1, x.shape[-1]), w, float(eps))
+        ext().fused_add_rmsnorm(out.view(-1, x.shape[-1]), xa, residual.view(-1, x.shape[-1]), w, float(eps),
+                                **_gk(gates))
     else:
         y, s = ref.fused_add_rmsnorm(x.sum(0) if slab else x, residual, w, eps)
         residual.copy_(s)
@@ -80,10 +125,13 @@ def silu_mul(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     return out
 
 
-def rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq: int, Hkv: int) -> None:
-    """RoPE on q/k + paged KV write; ``qkv`` is bf16 [T, W] or a split-K slab [S, T, W]."""
+def rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq: int, Hkv: int,
+                  gates=None) -> None:
+    """RoPE on q/k + paged KV write; ``qkv`` is bf16 [T, W] or a split-K slab [S, T, W]. ``gates``: bf16 cache
+    only (the kernel waits on ``wait`` and arrives on ``sig`` once per workgroup)."""
     if _gpu(qkv):
-        ext().rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, int(Hq), int(Hkv))
+        ext().rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, int(Hq), int(Hkv),
+                            **_gk(gates))
     else:
         ref.rope_kv_write(qkv.sum(0) if is_slab(qkv) else qkv, positions, cos_sin, q_out, k_cache, v_cache,
                           slot_mapping, Hq, Hkv)
@@ -106,7 +154,7 @@ DECODE_ITEM = 8  # int32 fields of a decode work item: (b, lo, hi, split, nsplit
 
 
 def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale: float, out=None,
-                      pre_part=None) -> None:
+                      pre_part=None, gates=None) -> None:
     """Paged decode attention over work items (int32 [n, 8]: row b, key range [lo, hi), piece ``split`` of
     ``nsplit``, ``npre`` prefix partials in front). Each item writes its (O, lse2) partial to slot npre + split of
     [B, Hq, S_total, D]; with ``out`` (npre + nsplit <= 64 per row) the rows are instead merged with their prefix
@@ -116,7 +164,7 @@ def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_pa
     if _gpu(q):
         tk = _tickets(q.device, q.shape[0] * k_cache.shape[1]) if out is not None else None
         ext().attn_decode(q, k_cache, v_cache, block_tables, items, out_part, lse_part, float(scale), out, tk,
-                          pre_part)
+                          pre_part, **_gk(gates))
         return
     ref.attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale, out, pre_part)
 
@@ -238,12 +286,13 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part,
 
 
 def attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, scale: float, out=None, out_part=None,
-                 lse_part=None, variant: int = 0) -> None:
+                 lse_part=None, variant: int = 0, gates=None) -> None:
     """Work-item paged attention (chunked prefill / cascade prefix). ``items`` is int32 [n, 8]:
-    (q_start, q_count, bt_row, kv_lo, kv_hi, split, 0, 0)."""
+    (q_start, q_count, bt_row, kv_lo, kv_hi, split, 0, 0). ``gates`` (tile variant 3, cascade only: the key range
+    must not be written by this step) early-launch it: the prefix K/V streams in before q is ready."""
     if _gpu(q):
         ext().attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, out, out_part, lse_part, float(scale),
-                           int(variant))
+                           int(variant), **_gk(gates))
     else:
         ref.attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale, out, out_part, lse_part)
 
@@ -373,7 +422,7 @@ def linear_skinny(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, glu: b
 
 
 def linear_stream(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, nt: bool = True,
-                  glu: bool = False) -> torch.Tensor:
+                  glu: bool = False, gates=None) -> torch.Tensor:
     """y = x @ W^T for decode-sized M (<= 128) from the wave-tiled weight ``wt``: the weight-streaming MFMA kernel.
     Returns bf16 [M, N] when the plan has one split, else the fp32 split-K slabs [S, M, N] (a slab; the consumer
     kernels sum it while loading). ``glu`` (wt tiled with glu=True): a one-split plan returns the ACTIVATED
@@ -387,10 +436,10 @@ def linear_stream(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, nt: bo
     if _gpu(x):
         if S == 1:
             y = torch.empty(M, N // 2 if glu else N, dtype=x.dtype, device=x.device)
-            ext().wstream_gemm(x, wt, y, None, int(max_splits), bool(nt), bool(glu))
+            ext().wstream_gemm(x, wt, y, None, int(max_splits), bool(nt), bool(glu), **_gk(gates))
             return y
         p = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
-        ext().wstream_gemm(x, wt, None, p, int(max_splits), bool(nt), bool(glu))
+        ext().wstream_gemm(x, wt, None, p, int(max_splits), bool(nt), bool(glu), **_gk(gates))
         return p
     w = untile_weight(wt, glu).float()
     xf = x.float()
@@ -409,7 +458,7 @@ def qkv_rope_fusable(k_cache: torch.Tensor, D: int) -> bool:
 
 
 def linear_stream_rope(x, wt, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq: int, Hkv: int,
-                       max_splits: int = 8) -> None:
+                       max_splits: int = 8, gates=None) -> None:
     """QKV projection of a decode-sized step (wave-tiled weight ``wt``, N = (Hq + 2 Hkv) * 128) with RoPE and the
     paged KV write fused into the streaming GEMM's epilogue: the same results as ``linear_stream`` followed by
     ``rope_kv_write``, without the rope_kv launch (the last split-K workgroup of each head tile finishes it)."""
@@ -422,18 +471,21 @@ def linear_stream_rope(x, wt, positions, cos_sin, q_out, k_cache, v_cache, slot_
         S = plan[2]
         p = torch.empty(S, M, N, dtype=torch.float32, device=x.device) if S > 1 else None
         ext().wstream_qkv_rope(x, wt, p, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, int(Hq),
-                               int(Hkv), _tickets(x.device, N // 128, pool="qkv_rope"), int(max_splits))
+                               int(Hkv), _tickets(x.device, N // 128, pool="qkv_rope"), int(max_splits),
+                               **_gk(gates))
         return
     rope_kv_write(linear_stream(x, wt, max_splits), positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq,
                   Hkv)
 
 
-def linear_glu(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8) -> torch.Tensor:
+def linear_glu(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, gates=None) -> torch.Tensor:
     """silu(x @ Wg^T) * (x @ Wu^T) from GLU-tiled gate_up weights: fused into the GEMM epilogue when the plan has one
-    split, else the GEMM's slabs go through silu_mul."""
+    split, else the GEMM's slabs go through silu_mul (``gates`` only with one split: ``glu_fused``)."""
     N = wt.shape[0] * 32
     plan = stream_plan(x.shape[0], N, x.shape[1], max_splits)
-    y = linear_stream(x, wt, max_splits, glu=True)
+    if gates is not None and not (plan is not None and plan[2] == 1):
+        raise ValueError("linear_glu: gates need the one-split (fused SwiGLU) plan")
+    y = linear_stream(x, wt, max_splits, glu=True, gates=gates)
     return y if plan is not None and plan[2] == 1 else silu_mul(y)
 
 

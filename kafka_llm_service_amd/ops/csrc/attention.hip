@@ -351,7 +351,8 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
                                              int b, int kvh, int lo, int hi, int split, int S, int split_offset,
                                              float* __restrict__ out_part, float* __restrict__ lse_part, int S_total,
                                              float scale_log2, bf16* __restrict__ out, int64_t out_stride,
-                                             int* __restrict__ tickets, const bf16* __restrict__ pre_bf16) {
+                                             int* __restrict__ tickets, const bf16* __restrict__ pre_bf16,
+                                             const Gates& gt = Gates{}, int gt_total = 0) {
   auto& sO = sm.sO;
   auto& sM = sm.sM;
   auto& sL = sm.sL;
@@ -437,6 +438,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     // Phase 1: wave w owns heads w, w + 4: lanes load the prefix lse values in parallel, wave-reduce the max and
     // the weight sum, and publish per-split weights in LDS. Phase 2: thread (g, 4 dims) sums weight x partial over
     // the splits with all loads of a group of 8 in flight.
+    gate_wait(gt.wait2, gt.expect2);  // early-launched beside the cascade: its partials are complete
     for (int g = w; g < G; g += 4) {
       float Ms = -INFINITY;
 #pragma unroll
@@ -513,6 +515,10 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
       for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc4[j] * inv);
       *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
     }
+    if (gt.sig != nullptr) {  // one arrival per merged (row, kv head)
+      __syncthreads();
+      if (threadIdx.x == 0) gate_arrive(gt.sig, gt_total);
+    }
     return;
   }
   for (int idx = threadIdx.x; idx < G * D; idx += 256) {
@@ -555,6 +561,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   }
   __syncthreads();
   if (!sm.s_last) return;
+  gate_wait(gt.wait2, gt.expect2);
   auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   // 16-B agent-coherent loads (sc1: not served from this XCD's possibly stale L2); inline asm, so the group below
   // waits for them itself
@@ -606,6 +613,10 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc4[j] * inv);
     *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
   }
+  if (gt.sig != nullptr) {  // one arrival per merged (row, kv head)
+    __syncthreads();
+    if (threadIdx.x == 0) gate_arrive(gt.sig, gt_total);
+  }
 }
 
 template <int D, bool HEADS_FAST, bool FP8, int MG = 16, bool OCC3 = false>
@@ -618,7 +629,7 @@ __global__ __launch_bounds__(256, OCC3 ? 3 : 2) void attn_decode_kernel(const bf
                                                            int S_total, float scale_log2,
                                                            bf16* __restrict__ out, int64_t out_stride,
                                                            int* __restrict__ tickets,
-                                                           const bf16* __restrict__ pre_bf16) {
+                                                           const bf16* __restrict__ pre_bf16, Gates gt) {
   __shared__ DecodeSmem<D> sm;
   // HEADS_FAST: consecutive workgroups are the Hkv heads of one item (grid (Hkv, items)), else the items of one
   // head (grid (items, Hkv)) — a placement choice only (which XCD's L2 sees which pages)
@@ -628,9 +639,10 @@ __global__ __launch_bounds__(256, OCC3 ? 3 : 2) void attn_decode_kernel(const bf
   if (b < 0 || b >= B || split < 0 || split >= S || split_offset < 0 || split_offset + S > S_total ||
       (out != nullptr && split_offset + S > 64))
     return;
+  gate_wait(gt.wait, gt.expect);  // early-launched: q and this step's K/V rows are written
   decode_piece<D, FP8, MG, OCC3>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, it.lo, it.hi,
                            split, S, split_offset, out_part, lse_part, S_total, scale_log2, out, out_stride, tickets,
-                           pre_bf16);
+                           pre_bf16, gt, B * Hkv);
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -1163,7 +1175,7 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
                                               const int* block_tables, int bt_stride, const int* items,
                                               float* out_part, float* lse_part, int S_total, float scale, bf16* out,
                                               int64_t out_stride, int* tickets, const bf16* pre_bf16,
-                                              hipStream_t st) {
+                                              Gates gt, hipStream_t st) {
   if (n_items == 0) return hipSuccess;
   if (D != 128 || G > 8 || G < 1) return hipErrorInvalidValue;
   if (out != nullptr && tickets == nullptr) return hipErrorInvalidValue;
@@ -1174,8 +1186,9 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
   }();
   const auto* di = reinterpret_cast<const DecodeItem*>(items);
   auto go = [&](auto kern, dim3 grid) {
-    kern<<<grid, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, di, B, out_part,
-                               lse_part, S_total, scale_log2, out, out_stride, tickets, pre_bf16);
+    launch_maybe_early(kern, grid, dim3(256), st, gt.wait != nullptr || gt.wait2 != nullptr, q, q_stride, k_cache, v_cache, Hkv, G,
+                       block_tables, bt_stride, di, B, out_part, lse_part, S_total, scale_log2, out, out_stride,
+                       tickets, pre_bf16, gt);
   };
   // prefix partials per load round trip in the fused merge (env KAFKA_DECODE_MERGE_GROUP = 8 / 16 / 32; bench A/B
   // profiles/r02/decode_merge_group_ab.jsonl: 7,491 / 7,489 / 7,505 tok/s — the epilogue is not on the critical path)
@@ -1253,21 +1266,21 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
                                             const void* k_cache, const void* v_cache, int Hkv, int G, int D,
                                             const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
                                             int64_t out_stride, float* out_part, float* lse_part, int S_total,
-                                            float scale, int part_bf16, hipStream_t st);
+                                            float scale, int part_bf16, Gates gt, hipStream_t st);
 
 extern "C" hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride,
                                                const void* k_cache, const void* v_cache, int fp8, int Hkv, int G,
                                                int D, const int* block_tables, int bt_stride, const int* q_limit,
                                                bf16* out, int64_t out_stride, float* out_part, float* lse_part,
-                                               int S_total, float scale, int variant, int part_bf16,
+                                               int S_total, float scale, int variant, int part_bf16, Gates gt,
                                                hipStream_t st) {
   if (n_items == 0) return hipSuccess;
   if (variant == 3) {  // LDS-DMA ring, one wave per SIMD, 256 rows (attn_tile.hip); bf16 pages only
     if (fp8) return hipErrorInvalidValue;
     return kafka_launch_attn_tile(items, n_items, q, q_stride, k_cache, v_cache, Hkv, G, D, block_tables, bt_stride,
-                                  q_limit, out, out_stride, out_part, lse_part, S_total, scale, part_bf16, st);
+                                  q_limit, out, out_stride, out_part, lse_part, S_total, scale, part_bf16, gt, st);
   }
-  if (part_bf16) return hipErrorInvalidValue;  // bf16 partials: tile v3 only
+  if (part_bf16 || gt.wait != nullptr || gt.sig != nullptr) return hipErrorInvalidValue;  // tile v3 only
   if (D != 128 || G < 1 || G > 32 || (128 % G) != 0 || n_items > 65535) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
   const auto* it = reinterpret_cast<const AttnWorkItem*>(items);

@@ -113,7 +113,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
                                                            const int* __restrict__ q_limit, bf16* __restrict__ out,
                                                            int64_t out_stride, float* __restrict__ out_part,
                                                            float* __restrict__ lse_part, int S_total,
-                                                           float scale_log2, int part_bf16) {
+                                                           float scale_log2, int part_bf16, Gates gt) {
   using namespace tile3;
   static_assert(NSLOT == 3 || NSLOT == 4, "ring depth");
   static_assert(RB == 1 || RB == 2, "row blocks per wave");
@@ -162,19 +162,24 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) limit[rb] = valid[rb] ? q_limit[token[rb]] : -1;
   bf16x8 qf[RB][D / 16];
+  auto load_q = [&]() {
 #pragma unroll
-  for (int rb = 0; rb < RB; ++rb) {
-    const bf16* qrow = q + (int64_t)token[rb] * q_stride + (int64_t)head[rb] * D + 8 * h;
+    for (int rb = 0; rb < RB; ++rb) {
+      const bf16* qrow = q + (int64_t)token[rb] * q_stride + (int64_t)head[rb] * D + 8 * h;
 #pragma unroll
-    for (int kk = 0; kk < D / 16; ++kk) {
-      if (valid[rb]) {
-        qf[rb][kk] = load_bf16x8(qrow + 16 * kk);
-      } else {
+      for (int kk = 0; kk < D / 16; ++kk) {
+        if (valid[rb]) {
+          qf[rb][kk] = load_bf16x8(qrow + 16 * kk);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) qf[rb][kk][j] = (bf16)0.f;
+          for (int j = 0; j < 8; ++j) qf[rb][kk][j] = (bf16)0.f;
+        }
       }
     }
-  }
+  };
+  // early-launched cascade (common.h Gates): the prefix K/V (written by earlier steps) streams in before q exists
+  const bool gated = gt.wait != nullptr;
+  if (!gated) load_q();
   // per-block wave-uniform bounds: keys past hi_b are masked for every row of the block, keys <= wmin_b for none
   int hi_b[2], wmin_b[2];  // (RB == 1: block 1 mirrors block 0)
 #pragma unroll
@@ -238,6 +243,10 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
 #pragma unroll
   for (int j = 0; j < NSLOT - 1; ++j)
     if (j < ntiles) issue(j);
+  if (gated) {
+    gate_wait(gt.wait, gt.expect);
+    load_q();
+  }
 
   // Running state per row block: O^T accumulators; row sums `ls` as an MFMA accumulator (every register of a lane
   // holds its column's sum ones . P: 8 MFMAs per tile instead of 64 adds); the running max m (exp2 domain).
@@ -479,6 +488,10 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
       }
     }
   }
+  if (gt.sig != nullptr) {  // one arrival per workgroup
+    __syncthreads();
+    if (tid == 0) gate_arrive(gt.sig, (int)(gridDim.x * gridDim.y));
+  }
   if constexpr (ABL == 8) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -496,7 +509,7 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
                                             const void* k_cache, const void* v_cache, int Hkv, int G, int D,
                                             const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
                                             int64_t out_stride, float* out_part, float* lse_part, int S_total,
-                                            float scale, int part_bf16, hipStream_t st) {
+                                            float scale, int part_bf16, Gates gt, hipStream_t st) {
   if (n_items == 0) return hipSuccess;
   if (D != 128 || G < 1 || G > 32 || (256 % G) != 0 || n_items > 65535) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
@@ -518,10 +531,10 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
   if (abl == 2) kern = rb == 2 ? attn_tile_kernel<2, 3, 2> : attn_tile_kernel<1, 3, 2>;
   if (abl == 8) kern = rb == 2 ? attn_tile_kernel<2, 3, 8> : attn_tile_kernel<1, 3, 8>;
   if (abl == 9) kern = rb == 2 ? attn_tile_kernel<2, 3, 9> : attn_tile_kernel<1, 3, 9>;
-  kern<<<dim3(Hkv, n_items), 512 / rb, 0, st>>>(
-      reinterpret_cast<const TileItem*>(items), q, q_stride, static_cast<const bf16*>(k_cache),
-      static_cast<const bf16*>(v_cache), Hkv, G, block_tables, bt_stride, q_limit, out, out_stride, out_part,
-      lse_part, S_total, scale_log2, part_bf16);
+  launch_maybe_early(kern, dim3(Hkv, n_items), dim3(512 / rb), st, gt.wait != nullptr,
+                     reinterpret_cast<const TileItem*>(items), q, q_stride, static_cast<const bf16*>(k_cache),
+                     static_cast<const bf16*>(v_cache), Hkv, G, block_tables, bt_stride, q_limit, out, out_stride,
+                     out_part, lse_part, S_total, scale_log2, part_bf16, gt);
   return hipGetLastError();
 }
 

@@ -7,19 +7,30 @@
 
 typedef unsigned short bf16;  // raw bf16 storage on the host side
 
+// device gates of early-launched consumers (layout of `Gates` in csrc/common.h)
+struct Gates {
+  int* wait = nullptr;
+  int expect = 0;
+  int* sig = nullptr;
+  int* wait2 = nullptr;
+  int expect2 = 0;
+};
+constexpr int GATE_INTS = 16;
+
 extern "C" {
 hipError_t kafka_launch_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs, const bf16* w, int T, int d, float eps,
                           hipStream_t st);
 hipError_t kafka_launch_fused_add_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs, bf16* resid, int64_t rs,
-                                    const bf16* w, int T, int d, float eps, hipStream_t st);
+                                    const bf16* w, int T, int d, float eps, Gates gt, hipStream_t st);
 hipError_t kafka_launch_fused_add_rmsnorm_slab(bf16* out, int64_t os, const float* xp, int S, int64_t ps, bf16* resid,
-                                               int64_t rs, const bf16* w, int T, int d, float eps, hipStream_t st);
+                                               int64_t rs, const bf16* w, int T, int d, float eps, Gates gt,
+                                               hipStream_t st);
 hipError_t kafka_launch_silu_mul(bf16* out, const bf16* x, int64_t xs, int T, int F, hipStream_t st);
 hipError_t kafka_launch_silu_mul_slab(bf16* out, const float* xp, int S, int64_t ps, int T, int F, hipStream_t st);
 hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int S, int64_t ps, int64_t qkv_stride,
                                 const int64_t* positions, const float* cos_sin, bf16* q_out, int64_t q_stride,
                                 bf16* k_cache, bf16* v_cache, const int64_t* slot_mapping, int T, int Hq, int Hkv,
-                                int D, int block_size, hipStream_t st);
+                                int D, int block_size, Gates gt, hipStream_t st);
 hipError_t kafka_launch_rope_kv_fp8(const bf16* qkv, const float* qp, int S, int64_t ps, int64_t qkv_stride,
                                     const int64_t* positions, const float* cos_sin, bf16* q_out, int64_t q_stride,
                                     uint8_t* k_cache, uint8_t* v_cache, const int64_t* slot_mapping, int T, int Hq,
@@ -28,7 +39,7 @@ hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const void*
                                     int n_items, int B, int Hkv, int G, int D, const int* block_tables, int bt_stride,
                                     const int* items, float* out_part, float* lse_part, int S_total, float scale,
                                     bf16* out, int64_t out_stride, int* tickets, const bf16* pre_bf16,
-                                    hipStream_t st);
+                                    Gates gt, hipStream_t st);
 hipError_t kafka_launch_attn_decode_sk(const bf16* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                                        int fp8, int B, int Hkv, int G, int D, const int* block_tables, int bt_stride,
                                        const int* rows, const int* start, int nwg, float* out_part,
@@ -38,7 +49,7 @@ hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16*
                                      const void* k_cache, const void* v_cache, int fp8, int Hkv, int G, int D,
                                      const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
                                      int64_t out_stride, float* out_part, float* lse_part, int S_total, float scale,
-                                     int variant, int part_bf16, hipStream_t st);
+                                     int variant, int part_bf16, Gates gt, hipStream_t st);
 hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows, int Hq, int S, int D, bf16* out,
                              int64_t out_stride, float* lse_out, hipStream_t st);
 hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
@@ -48,12 +59,13 @@ hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride,
 int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits);
 hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt, int kc,
                                      int splits, int nt, int kw, int glu, bf16* Y, int64_t ldy, float* P,
-                                     hipStream_t st);
+                                     Gates gt, hipStream_t st);
 hipError_t kafka_launch_slab_reduce(const float* P, int S, int M, int N, bf16* Y, int64_t ldy, hipStream_t st);
 hipError_t kafka_launch_wstream_qkv_rope(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt,
                                          int kc, int splits, float* P, const int64_t* positions, const float* cos_sin,
                                          bf16* q_out, int64_t q_stride, bf16* k_cache, bf16* v_cache,
-                                         const int64_t* slots, int Hq, int Hkv, int* tickets, hipStream_t st);
+                                         const int64_t* slots, int Hq, int Hkv, int* tickets, Gates gt,
+                                         hipStream_t st);
 hipError_t kafka_launch_wstream_grouped(const bf16* X, int64_t ldx, const bf16* Wt, int e_local, int N, int K,
                                         const int* perm_tok, const float* perm_w, const int* expert_off, int e_lo,
                                         int max_rows, int gather, bf16* Y, int64_t ldy, float* out, int64_t ldo,
@@ -115,6 +127,27 @@ static void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
                                   cur_stream()));
 }
 
+// gates: int32 buffer of GATE_INTS words per gate (ops.GateSet); args: [wait, expect, sig, wait2, expect2] with gate
+// ids (-1: none). Missing buffer or args: no gates (an ordinary launch).
+static Gates make_gates(const c10::optional<at::Tensor>& buf, const std::vector<int64_t>& a) {
+  Gates g;
+  if (!buf.has_value() || a.empty()) return g;
+  TORCH_CHECK(buf->scalar_type() == at::kInt && buf->is_contiguous() && buf->is_cuda(), "gates: int32 device buffer");
+  const int64_t n = buf->numel() / GATE_INTS;
+  int* base = buf->data_ptr<int>();
+  auto at_ = [&](size_t i) -> int* {
+    if (i >= a.size() || a[i] < 0) return nullptr;
+    TORCH_CHECK(a[i] < n, "gates: gate id out of range");
+    return base + a[i] * GATE_INTS;
+  };
+  g.wait = at_(0);
+  g.expect = a.size() > 1 ? (int)a[1] : 0;
+  g.sig = at_(2);
+  g.wait2 = at_(3);
+  g.expect2 = a.size() > 4 ? (int)a[4] : 0;
+  return g;  // expect <= 0: the producer's published arrival count
+}
+
 // A split-K slab is an fp32 contiguous [S, T, n] tensor (wstream_gemm output); kernels that accept one sum it on load.
 static bool is_slab(const at::Tensor& x) { return x.scalar_type() == at::kFloat && x.dim() == 3; }
 static void check_slab(const at::Tensor& x) {
@@ -122,7 +155,9 @@ static void check_slab(const at::Tensor& x) {
 }
 
 // x: bf16 [T, d] or slab [S, T, d]
-static void fused_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor residual, at::Tensor w, double eps) {
+static void fused_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor residual, at::Tensor w, double eps,
+                              c10::optional<at::Tensor> gates, std::vector<int64_t> gate_args) {
+  const Gates gt = make_gates(gates, gate_args);
   CHECK_CUDA(x); CHECK_DT(residual, at::kBFloat16); CHECK_DT(w, at::kBFloat16);
   CHECK_DT(out, at::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out); CHECK_LASTDIM(residual);
@@ -138,10 +173,10 @@ static void fused_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor residual,
   if (slab)
     CHECK_HIP(kafka_launch_fused_add_rmsnorm_slab(bptr(out), out.stride(0), x.data_ptr<float>(), x.size(0),
                                                   T * d, bptr(residual), residual.stride(0), bptr(w), T, d, eps,
-                                                  cur_stream()));
+                                                  gt, cur_stream()));
   else
     CHECK_HIP(kafka_launch_fused_add_rmsnorm(bptr(out), out.stride(0), bptr(x), x.stride(0), bptr(residual),
-                                              residual.stride(0), bptr(w), T, d, eps, cur_stream()));
+                                              residual.stride(0), bptr(w), T, d, eps, gt, cur_stream()));
 }
 
 // x: bf16 [T, 2F] or slab [S, T, 2F]
@@ -184,7 +219,8 @@ static void check_cache_pair(const at::Tensor& k_cache, const at::Tensor& v_cach
 
 static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin, at::Tensor q_out,
                           at::Tensor k_cache, at::Tensor v_cache, c10::optional<at::Tensor> slot_mapping, int64_t Hq,
-                          int64_t Hkv) {
+                          int64_t Hkv, c10::optional<at::Tensor> gates, std::vector<int64_t> gate_args) {
+  const Gates gt = make_gates(gates, gate_args);
   CHECK_CUDA(qkv); CHECK_DT(q_out, at::kBFloat16);
   const bool slab = is_slab(qkv);
   if (slab) check_slab(qkv); else CHECK_DT(qkv, at::kBFloat16);
@@ -192,6 +228,7 @@ static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_s
   TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && cos_sin.is_contiguous() &&
                   positions.is_contiguous(), "rope_kv_write: caches/positions/cos_sin must be contiguous");
   const bool fp8 = is_fp8_cache(k_cache);
+  TORCH_CHECK(!fp8 || (gt.wait == nullptr && gt.sig == nullptr), "rope_kv_write: gates need a bf16 cache");
   int D, bs = 16;
   if (fp8) {
     check_cache_pair(k_cache, v_cache);
@@ -229,7 +266,7 @@ static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_s
     CHECK_HIP(kafka_launch_rope_kv(slab ? nullptr : bptr(qkv), slab ? qkv.data_ptr<float>() : nullptr,
                                     slab ? qkv.size(0) : 0, slab ? (int64_t)T * W : 0, slab ? W : qkv.stride(0),
                                     positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), bptr(q_out),
-                                    q_out.stride(0), bptr(k_cache), bptr(v_cache), sm, T, Hq, Hkv, D, bs,
+                                    q_out.stride(0), bptr(k_cache), bptr(v_cache), sm, T, Hq, Hkv, D, bs, gt,
                                     cur_stream()));
 }
 
@@ -238,7 +275,9 @@ static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_s
 static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
                         at::Tensor items, at::Tensor out_part, at::Tensor lse_part, double scale,
                         c10::optional<at::Tensor> out, c10::optional<at::Tensor> tickets,
-                        c10::optional<at::Tensor> pre_part) {
+                        c10::optional<at::Tensor> pre_part, c10::optional<at::Tensor> gates,
+                        std::vector<int64_t> gate_args) {
+  const Gates gt = make_gates(gates, gate_args);
   CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
   CHECK_DT(block_tables, at::kInt); CHECK_DT(items, at::kInt); CHECK_DT(out_part, at::kFloat);
   CHECK_DT(lse_part, at::kFloat);
@@ -278,7 +317,7 @@ static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at
                                       is_fp8_cache(k_cache) ? 1 : 0, items.size(0), B, Hkv,
                                       Hq / Hkv, 128, block_tables.data_ptr<int>(), block_tables.stride(0),
                                       items.data_ptr<int>(), out_part.data_ptr<float>(), lse_part.data_ptr<float>(),
-                                      S_total, scale, op, ostride, tp, pre, cur_stream()));
+                                      S_total, scale, op, ostride, tp, pre, gt, cur_stream()));
 }
 
 // Stream-K decode: rows int32 [B + 1, 4] (kv_lo, kv_hi, npre, cost start; last row = plan (T, F, total, 0)), start
@@ -335,7 +374,9 @@ static void attn_decode_sk(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
 static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                          at::Tensor block_tables, at::Tensor q_limit, c10::optional<at::Tensor> out,
                          c10::optional<at::Tensor> out_part, c10::optional<at::Tensor> lse_part, double scale,
-                         int64_t variant) {
+                         int64_t variant, c10::optional<at::Tensor> gates, std::vector<int64_t> gate_args) {
+  const Gates gt = make_gates(gates, gate_args);
+  TORCH_CHECK((gt.wait == nullptr && gt.sig == nullptr) || variant == 3, "attn_prefill: gates need tile variant 3");
   CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
   CHECK_DT(items, at::kInt); CHECK_DT(block_tables, at::kInt); CHECK_DT(q_limit, at::kInt);
   TORCH_CHECK(items.is_contiguous() && items.dim() == 2 && items.size(1) == 8, "items must be [n, 8] int32");
@@ -376,7 +417,7 @@ static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at:
   CHECK_HIP(kafka_launch_attn_prefill(items.data_ptr<int>(), items.size(0), bptr(q), q.stride(0), k_cache.data_ptr(),
                                        v_cache.data_ptr(), is_fp8_cache(k_cache) ? 1 : 0, Hkv, G, 128, block_tables.data_ptr<int>(),
                                        block_tables.stride(0), q_limit.data_ptr<int>(), op, os, pp, lp, S_total,
-                                       scale, (int)variant, part_bf16, cur_stream()));
+                                       scale, (int)variant, part_bf16, gt, cur_stream()));
 }
 
 static void attn_merge(at::Tensor part, at::Tensor lse, at::Tensor out, c10::optional<at::Tensor> lse_out) {
@@ -466,7 +507,9 @@ static std::vector<int64_t> wstream_plan(int64_t M, int64_t N, int64_t K, int64_
 // x [M, K] bf16 . W^T with W given wave-tiled as wt [N/32, K/16, 64, 8] (ops.tile_weight). Writes bf16 y [M, N]
 // (splits == 1) or fp32 slabs p [splits, M, N].
 static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y, c10::optional<at::Tensor> p,
-                         int64_t max_splits, bool nt, bool glu) {
+                         int64_t max_splits, bool nt, bool glu, c10::optional<at::Tensor> gates,
+                         std::vector<int64_t> gate_args) {
+  const Gates gt = make_gates(gates, gate_args);
   CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0, "wstream_gemm: x must be [M, K] with 16-B rows");
   TORCH_CHECK(wt.dim() == 4 && wt.is_contiguous() && wt.size(2) == 64 && wt.size(3) == 8,
@@ -494,7 +537,7 @@ static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> 
     pp = p->data_ptr<float>();
   }
   CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, nt ? 1 : 0, 1, glu ? 1 : 0,
-                                      yp, ldy, pp, cur_stream()));
+                                      yp, ldy, pp, gt, cur_stream()));
 }
 
 // Skinny MFMA GEMM (csrc/skinny_gemm.hip) for 129..256 rows on the wave-tiled weights: y bf16 for one split
@@ -538,7 +581,8 @@ static void skinny_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y
 static void wstream_qkv_rope(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> p, at::Tensor positions,
                              at::Tensor cos_sin, at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache,
                              c10::optional<at::Tensor> slot_mapping, int64_t Hq, int64_t Hkv, at::Tensor tickets,
-                             int64_t max_splits) {
+                             int64_t max_splits, c10::optional<at::Tensor> gates, std::vector<int64_t> gate_args) {
+  const Gates gt = make_gates(gates, gate_args);
   CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
   CHECK_DT(positions, at::kLong); CHECK_DT(cos_sin, at::kFloat); CHECK_DT(q_out, at::kBFloat16);
   CHECK_DT(k_cache, at::kBFloat16); CHECK_DT(v_cache, at::kBFloat16); CHECK_DT(tickets, at::kInt);
@@ -573,7 +617,7 @@ static void wstream_qkv_rope(at::Tensor x, at::Tensor wt, c10::optional<at::Tens
   CHECK_HIP(kafka_launch_wstream_qkv_rope(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, pp,
                                           positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), bptr(q_out),
                                           q_out.stride(0), bptr(k_cache), bptr(v_cache), sm, (int)Hq, (int)Hkv,
-                                          tickets.data_ptr<int>(), cur_stream()));
+                                          tickets.data_ptr<int>(), gt, cur_stream()));
 }
 
 // explicit-configuration variant (microbenchmark sweeps): (mt, kc, splits) as given, no planning
@@ -593,7 +637,7 @@ static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tens
   CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, (int)mt, (int)kc, (int)s, nt ? 1 : 0,
                                       (int)kw, 0,
                                       s == 1 ? bptr(y.value()) : nullptr, s == 1 ? y->stride(0) : 0,
-                                      s == 1 ? nullptr : p->data_ptr<float>(), cur_stream()));
+                                      s == 1 ? nullptr : p->data_ptr<float>(), Gates{}, cur_stream()));
 }
 
 // Expert MLP halves on wave-tiled expert weights wt [E_local, N/32, K/16, 64, 8] (ops.tile_experts). glu: gate_up
@@ -889,15 +933,20 @@ static void ep_combine(at::Tensor back, at::Tensor slot_map, at::Tensor topk_w, 
 PYBIND11_MODULE(_kafka_ops, m) {
   m.doc() = "kafka_llm_service_amd CDNA4 (gfx950) HIP kernels";
   m.def("rmsnorm", &rmsnorm);
-  m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
+  m.def("fused_add_rmsnorm", &fused_add_rmsnorm, py::arg("out"), py::arg("x"), py::arg("residual"), py::arg("w"),
+        py::arg("eps"), py::arg("gates") = py::none(), py::arg("gate_args") = std::vector<int64_t>{});
   m.def("silu_mul", &silu_mul);
-  m.def("rope_kv_write", &rope_kv_write);
+  m.def("rope_kv_write", &rope_kv_write, py::arg("qkv"), py::arg("positions"), py::arg("cos_sin"), py::arg("q_out"),
+        py::arg("k_cache"), py::arg("v_cache"), py::arg("slot_mapping"), py::arg("Hq"), py::arg("Hkv"),
+        py::arg("gates") = py::none(), py::arg("gate_args") = std::vector<int64_t>{});
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("items"), py::arg("out_part"), py::arg("lse_part"), py::arg("scale"), py::arg("out"),
-        py::arg("tickets"), py::arg("pre_part") = py::none());
+        py::arg("tickets"), py::arg("pre_part") = py::none(), py::arg("gates") = py::none(),
+        py::arg("gate_args") = std::vector<int64_t>{});
   m.def("attn_prefill", &attn_prefill, py::arg("items"), py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("block_tables"), py::arg("q_limit"), py::arg("out"), py::arg("out_part"), py::arg("lse_part"),
-        py::arg("scale"), py::arg("variant") = 0);
+        py::arg("scale"), py::arg("variant") = 0, py::arg("gates") = py::none(),
+        py::arg("gate_args") = std::vector<int64_t>{});
   m.def("attn_merge", &attn_merge);
   m.def("attn_decode_sk", &attn_decode_sk, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("block_tables"), py::arg("rows"), py::arg("start"), py::arg("out_part"), py::arg("lse_part"), py::arg("scale"), py::arg("out") = py::none(),
@@ -906,10 +955,15 @@ PYBIND11_MODULE(_kafka_ops, m) {
         py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none(), py::arg("nsplit") = 1,
         py::arg("proc") = py::none(), py::arg("mask_tab") = py::none(), py::arg("counts") = py::none());
   m.def("wstream_plan", &wstream_plan);
-  m.def("wstream_gemm", &wstream_gemm);
+  m.def("wstream_gemm", &wstream_gemm, py::arg("x"), py::arg("wt"), py::arg("y"), py::arg("p"),
+        py::arg("max_splits"), py::arg("nt"), py::arg("glu"), py::arg("gates") = py::none(),
+        py::arg("gate_args") = std::vector<int64_t>{});
   m.def("skinny_plan", &skinny_plan);
   m.def("skinny_gemm", &skinny_gemm);
-  m.def("wstream_qkv_rope", &wstream_qkv_rope);
+  m.def("wstream_qkv_rope", &wstream_qkv_rope, py::arg("x"), py::arg("wt"), py::arg("p"), py::arg("positions"),
+        py::arg("cos_sin"), py::arg("q_out"), py::arg("k_cache"), py::arg("v_cache"), py::arg("slot_mapping"),
+        py::arg("Hq"), py::arg("Hkv"), py::arg("tickets"), py::arg("max_splits"), py::arg("gates") = py::none(),
+        py::arg("gate_args") = std::vector<int64_t>{});
   m.def("wstream_gemm_cfg", &wstream_gemm_cfg);
   m.def("slab_reduce", &slab_reduce);
   m.def("wstream_grouped", &wstream_grouped);

@@ -9,6 +9,7 @@
 //       B: lane l holds B[k = 8*(l>>5) + j][col l&31]
 //       C/D: lane l, reg i -> row (i&3) + 8*(i>>2) + 4*(l>>5), col l&31
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -113,6 +114,73 @@ __device__ __forceinline__ void load_in8(float (&v)[8], const bf16* __restrict__
 
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// ---- device gates: early-launched consumers ---------------------------------------------------------------------
+// A consumer kernel launched WITHOUT the AQL barrier bit (hipExtAnyOrderLaunch) is dispatched as soon as its
+// predecessor's last workgroup has been dispatched, so it runs its producer-independent prologue (the weight stream
+// of a projection, page tables, first K/V tiles) while the producer's tail still runs, then waits on a gate: GATE_INTS
+// int32 per gate, shards [0, 8) bumped once per arriving producer workgroup (shard = workgroup id & 7: arrivals of
+// different XCDs hit different lines), word 8 = error flag (a wait that timed out), word 9 = the producer's arrival
+// count (published by every arriving workgroup, so the host never mirrors launch geometry). The producer's arrival is an
+// agent-scope release after a workgroup barrier; the consumer's wait ends with an agent-scope acquire, so its later
+// loads see the producer's writes from any XCD. Dispatch order within a queue guarantees every producer workgroup is
+// resident before any consumer workgroup, so a waiting consumer can never starve its producer.
+// Rule for callers (ops.gates / models): a gated consumer writes nothing to global memory before its wait, and it
+// waits on the kernel launched immediately before it (gates then chain transitively, and the caching allocator's
+// stream-order reuse stays safe).
+constexpr int GATE_INTS = 16;
+struct Gates {
+  int* wait = nullptr;   // wait until the shards of this gate sum to `expect` (<= 0: the producer's published count)
+  int expect = 0;
+  int* sig = nullptr;    // arrive on this gate when the workgroup's outputs are written (nullptr: none)
+  int* wait2 = nullptr;  // a second gate (decode attention: the cascade partials, before the merge)
+  int expect2 = 0;
+};
+
+// ONE thread per workgroup, after a __syncthreads() that follows every global write the consumer will read; `total`:
+// how many workgroups of this launch arrive (the same value from every one)
+__device__ __forceinline__ void gate_arrive(int* sig, int total) {
+  if (sig == nullptr) return;
+  const int shard = (int)((blockIdx.x + blockIdx.y * 7u + blockIdx.z * 3u) & 7u);
+  __hip_atomic_store(sig + 9, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(sig + shard, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// every thread of the workgroup (workgroup-uniform arguments); bounded: after 2 s the error word is raised and the
+// wait gives up (the host fails the step instead of hanging the GPU)
+__device__ __forceinline__ void gate_wait(int* g, int expect) {
+  if (g == nullptr) return;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+      // lanes 0..7: the shards, lane 8: the published count (monotonic: a stale read only delays the release)
+      int v = lane < 9 ? __hip_atomic_load(g + (lane < 8 ? lane : 9), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      const int target = expect > 0 ? expect : __shfl(v, 8, 64);
+      if (lane >= 8) v = 0;
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if (target > 0 && __shfl(v, 0, 64) >= target) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+        if (lane == 0) __hip_atomic_store(g + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// Launch `kernel`; `early`: without the AQL barrier bit (the kernel waits on a gate before reading its inputs)
+template <typename F, typename... Args>
+inline void launch_maybe_early(F kernel, dim3 grid, dim3 block, hipStream_t st, bool early, Args... args) {
+  if (early)
+    hipExtLaunchKernelGGL(kernel, grid, block, 0, st, nullptr, nullptr, hipExtAnyOrderLaunch, args...);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
 }
 
 // Counter-based RNG (splitmix64 finaliser): deterministic given (seed, stream, index).

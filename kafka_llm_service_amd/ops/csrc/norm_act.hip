@@ -19,7 +19,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int
                                                        const bf16* __restrict__ x, const float* __restrict__ xp,
                                                        int S, int64_t ps, int64_t x_stride,
                                                        bf16* __restrict__ resid, int64_t r_stride,
-                                                       const bf16* __restrict__ w, int d, float eps) {
+                                                       const bf16* __restrict__ w, int d, float eps, Gates gt) {
   __shared__ float red[NT / 64];
   const int64_t row = blockIdx.x;
   const int nvec = d >> 3;
@@ -63,6 +63,10 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int
       store_bf16x8(out + row * out_stride + vi * 8, o);
     }
   }
+  if (gt.sig != nullptr) {  // one arrival per row (common.h Gates)
+    __syncthreads();
+    if (threadIdx.x == 0) gate_arrive(gt.sig, (int)gridDim.x);
+  }
 }
 
 // out[t, :] = silu(x[t, :F]) * x[t, F:]   (x: [T, 2F] row stride xs (bf16 or slabs), out: [T, F] contiguous)
@@ -85,21 +89,21 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(bf16* __restrict__ out, c
 template <bool RESID>
 static hipError_t launch_rmsnorm_t(bf16* out, int64_t os, const bf16* x, const float* xp, int S, int64_t ps,
                                    int64_t xs, bf16* r, int64_t rs, const bf16* w, int T, int d, float eps,
-                                   hipStream_t st) {
+                                   hipStream_t st, Gates gt = Gates{}) {
   const int nvec = d / 8;
   const int nv = (nvec + 255) / 256;
   dim3 grid(T), block(256);
   if (T == 0) return hipSuccess;
   if (nvec <= 512 && nvec > 256) {  // e.g. d = 4096: one 16-B vector per thread, twice the loads in flight per row
-    rmsnorm_kernel<1, RESID, 512><<<grid, 512, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps);
+    rmsnorm_kernel<1, RESID, 512><<<grid, 512, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt);
     return hipGetLastError();
   }
   switch (nv) {
-    case 1: rmsnorm_kernel<1, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
-    case 2: rmsnorm_kernel<2, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
+    case 1: rmsnorm_kernel<1, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt); break;
+    case 2: rmsnorm_kernel<2, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt); break;
     case 3:
-    case 4: rmsnorm_kernel<4, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
-    default: rmsnorm_kernel<8, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
+    case 4: rmsnorm_kernel<4, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt); break;
+    default: rmsnorm_kernel<8, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt); break;
   }
   return hipGetLastError();
 }
@@ -110,15 +114,15 @@ extern "C" hipError_t kafka_launch_rmsnorm(bf16* out, int64_t os, const bf16* x,
 }
 
 extern "C" hipError_t kafka_launch_fused_add_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs, bf16* resid, int64_t rs,
-                                    const bf16* w, int T, int d, float eps, hipStream_t st) {
-  return launch_rmsnorm_t<true>(out, os, x, nullptr, 0, 0, xs, resid, rs, w, T, d, eps, st);
+                                    const bf16* w, int T, int d, float eps, Gates gt, hipStream_t st) {
+  return launch_rmsnorm_t<true>(out, os, x, nullptr, 0, 0, xs, resid, rs, w, T, d, eps, st, gt);
 }
 
 // fused add + RMSNorm whose x input is S fp32 split-K slabs [S][T][d] (row stride d, slab stride ps)
 extern "C" hipError_t kafka_launch_fused_add_rmsnorm_slab(bf16* out, int64_t os, const float* xp, int S, int64_t ps,
                                                          bf16* resid, int64_t rs, const bf16* w, int T, int d,
-                                                         float eps, hipStream_t st) {
-  return launch_rmsnorm_t<true>(out, os, nullptr, xp, S, ps, d, resid, rs, w, T, d, eps, st);
+                                                         float eps, Gates gt, hipStream_t st) {
+  return launch_rmsnorm_t<true>(out, os, nullptr, xp, S, ps, d, resid, rs, w, T, d, eps, st, gt);
 }
 
 extern "C" hipError_t kafka_launch_silu_mul(bf16* out, const bf16* x, int64_t xs, int T, int F, hipStream_t st) {

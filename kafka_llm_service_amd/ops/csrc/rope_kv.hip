@@ -43,10 +43,11 @@ __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ 
                                                        bf16* __restrict__ q_out, int64_t q_stride,
                                                        bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
                                                        const int64_t* __restrict__ slot_mapping, int Hq, int Hkv,
-                                                       int block_size) {
+                                                       int block_size, Gates gt) {
   constexpr int HALF = D / 2;
   constexpr int RU = HALF / 8;  // rope units (8 rotation pairs each) per head
   constexpr int VU = D / 8;     // v copy units (8 elements) per head
+  gate_wait(gt.wait, gt.expect);  // early-launched (common.h Gates): the QKV projection's slabs are complete
   const int64_t t = blockIdx.x;
   const int64_t pos = positions[t];
   const int64_t slot = slot_mapping ? slot_mapping[t] : -1;
@@ -96,6 +97,10 @@ __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) dst[(int64_t)(c + j) * block_size] = (bf16)x[j];
     }
+  }
+  if (gt.sig != nullptr) {  // one arrival per workgroup
+    __syncthreads();
+    if (threadIdx.x == 0) gate_arrive(gt.sig, (int)(gridDim.x * gridDim.y));
   }
 }
 
@@ -241,7 +246,7 @@ extern "C" hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int
                                           const int64_t* positions, const float* cos_sin, bf16* q_out,
                                           int64_t q_stride, bf16* k_cache, bf16* v_cache,
                                           const int64_t* slot_mapping, int T, int Hq, int Hkv, int D,
-                                          int block_size, hipStream_t st) {
+                                          int block_size, Gates gt, hipStream_t st) {
   if (T == 0) return hipSuccess;
   if (D != 128 && D != 64) return hipErrorInvalidValue;
   // one thread per work unit (8 rotation pairs of a Q/K head, or 8 V elements), so a token's whole row is one
@@ -262,12 +267,13 @@ extern "C" hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int
     ny = (units + nt - 1) / nt;
   }
   const dim3 grid(T, ny);
+  const bool early = gt.wait != nullptr;
   if (D == 128)
-    rope_kv_kernel<128><<<grid, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
-                                          v_cache, slot_mapping, Hq, Hkv, block_size);
+    launch_maybe_early(rope_kv_kernel<128>, grid, dim3(nt), st, early, qkv, qp, S, ps, qkv_stride, positions, cos_sin,
+                       q_out, q_stride, k_cache, v_cache, slot_mapping, Hq, Hkv, block_size, gt);
   else
-    rope_kv_kernel<64><<<grid, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
-                                         v_cache, slot_mapping, Hq, Hkv, block_size);
+    launch_maybe_early(rope_kv_kernel<64>, grid, dim3(nt), st, early, qkv, qp, S, ps, qkv_stride, positions, cos_sin,
+                       q_out, q_stride, k_cache, v_cache, slot_mapping, Hq, Hkv, block_size, gt);
   return hipGetLastError();
 }
 

@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
                                                                  const bf16x8* __restrict__ Wt, int M, int N, int K,
                                                                  int ks, bf16* __restrict__ Y, int64_t ldy,
                                                                  float* __restrict__ P, int glu, RopeKV ra,
-                                                                 int row_tiles) {
+                                                                 int row_tiles, Gates gt) {
   constexpr int NTH = 256 * KW;
   constexpr int ROWS = 32 * MT;
   constexpr int CPR = KC / 8;             // 16-B chunks per X row of one K chunk
@@ -124,8 +124,14 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
   };
 
   bf16x8 wa[KSW], wb[KSW];
-  load_x(0);
   load_w(wa, 0);
+  if (gt.wait != nullptr) {
+    // early-launched (common.h Gates): the first K chunk of this workgroup's weight slice is in flight while the
+    // producer of X finishes; X is read only after the gate
+    asm volatile("" ::: "memory");
+    gate_wait(gt.wait, gt.expect);
+  }
+  load_x(0);
   store_x(0);
   __syncthreads();
   // steady state: two chunks per trip, both prefetches in range (no conditional loads inside the trip)
@@ -254,6 +260,10 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
           }
         }
       }
+    if (gt.sig != nullptr) {  // one arrival per head tile (the last split's)
+      __syncthreads();
+      if (tid == 0) gate_arrive(gt.sig, (int)gridDim.x);
+    }
     return;
   }
   if (glu && P == nullptr) {
@@ -269,35 +279,39 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
         for (int i = 0; i < 16; ++i) red[(((ct >> 1) * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
     }
     __syncthreads();
-    if (!active || kh != 0 || (ct & 1)) return;
-    const int n = (nb >> 1) * 32 + r;
+    if (active && kh == 0 && !(ct & 1)) {
+      const int n = (nb >> 1) * 32 + r;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (m < M) {
+            const float g = acc[mt][i], u = red[(((ct >> 1) * MT + mt) * 16 + i) * 64 + lane];
+            Y[(int64_t)m * ldy + n] = (bf16)(g / (1.0f + __expf(-g)) * u);
+          }
+        }
+    }
+  } else if (active && kh == 0) {
+    // GLU-interleaved tiles written un-split: tile 2j -> gate columns [32j, +32), tile 2j+1 -> up columns N/2 + 32j
+    const int n = glu ? ((nb & 1) ? (N >> 1) : 0) + (nb >> 1) * 32 + r : nb * 32 + r;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
         if (m < M) {
-          const float g = acc[mt][i], u = red[(((ct >> 1) * MT + mt) * 16 + i) * 64 + lane];
-          Y[(int64_t)m * ldy + n] = (bf16)(g / (1.0f + __expf(-g)) * u);
+          if (P)
+            P[((int64_t)blockIdx.y * Mtot + m) * N + n] = acc[mt][i];
+          else
+            Y[(int64_t)m * ldy + n] = (bf16)acc[mt][i];
         }
       }
-    return;
   }
-  if (!active || kh != 0) return;
-  // GLU-interleaved tiles written un-split: tile 2j -> gate columns [32j, +32), tile 2j+1 -> up columns N/2 + 32j
-  const int n = glu ? ((nb & 1) ? (N >> 1) : 0) + (nb >> 1) * 32 + r : nb * 32 + r;
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-      if (m < M) {
-        if (P)
-          P[((int64_t)blockIdx.y * Mtot + m) * N + n] = acc[mt][i];
-        else
-          Y[(int64_t)m * ldy + n] = (bf16)acc[mt][i];
-      }
-    }
+  if (gt.sig != nullptr) {  // one arrival per workgroup
+    __syncthreads();
+    if (tid == 0) gate_arrive(gt.sig, (int)(gridDim.x * gridDim.y));
+  }
 }
 
 // Grouped (MoE) variant: one weight stream per expert over wave-tiled expert weights Wt[E_local][N/32][K/16][64][8].
@@ -487,7 +501,7 @@ extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, 
 
 extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K,
                                                int mt, int kc, int splits, int nt, int kw, int glu, bf16* Y,
-                                               int64_t ldy, float* P, hipStream_t st) {
+                                               int64_t ldy, float* P, Gates gt, hipStream_t st) {
   if (M < 1) return hipSuccess;
   if (glu && (N % 64 != 0 || kw != 1)) return hipErrorInvalidValue;
   if (K % (kc * splits) != 0 || (splits > 1 && P == nullptr) || (splits == 1 && P == nullptr && Y == nullptr))
@@ -497,14 +511,15 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   const int ks = K / splits;
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   float* p = splits > 1 ? P : nullptr;
-#define KAFKA_WS(MT_, KC_, KW_)                                                                             \
-  do {                                                                                                     \
-    if (nt)                                                                                                \
-      wstream_gemm_kernel<MT_, KC_, true, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, \
-                                                                           RopeKV{}, rt);                           \
-    else                                                                                                   \
-      wstream_gemm_kernel<MT_, KC_, false, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, \
-                                                                            RopeKV{}, rt);                          \
+  const bool early = gt.wait != nullptr;
+#define KAFKA_WS(MT_, KC_, KW_)                                                                                \
+  do {                                                                                                        \
+    if (nt)                                                                                                   \
+      launch_maybe_early(wstream_gemm_kernel<MT_, KC_, true, KW_>, grid, dim3(256 * KW_), st, early, X, ldx, wt, M, \
+                         N, K, ks, Y, ldy, p, glu, RopeKV{}, rt, gt);                                         \
+    else                                                                                                      \
+      launch_maybe_early(wstream_gemm_kernel<MT_, KC_, false, KW_>, grid, dim3(256 * KW_), st, early, X, ldx, wt, \
+                         M, N, K, ks, Y, ldy, p, glu, RopeKV{}, rt, gt);                                      \
   } while (0)
   if (mt == 1 && kc == 256 && kw == 1) KAFKA_WS(1, 256, 1);
   else if (mt == 1 && kc == 256 && kw == 2) KAFKA_WS(1, 256, 2);
@@ -526,7 +541,7 @@ extern "C" hipError_t kafka_launch_wstream_qkv_rope(const bf16* X, int64_t ldx, 
                                                    int mt, int kc, int splits, float* P, const int64_t* positions,
                                                    const float* cos_sin, bf16* q_out, int64_t q_stride,
                                                    bf16* k_cache, bf16* v_cache, const int64_t* slots, int Hq,
-                                                   int Hkv, int* tickets, hipStream_t st) {
+                                                   int Hkv, int* tickets, Gates gt, hipStream_t st) {
   if (M < 1) return hipSuccess;
   if (M > 128 || N != (Hq + 2 * Hkv) * 128 || K % (kc * splits) != 0 ||
       (splits > 1 && (P == nullptr || tickets == nullptr)))
@@ -535,12 +550,17 @@ extern "C" hipError_t kafka_launch_wstream_qkv_rope(const bf16* X, int64_t ldx, 
   const int ks = K / splits;
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   const RopeKV ra{positions, cos_sin, q_out, q_stride, k_cache, v_cache, slots, Hq, Hkv, tickets};
+  const bool early = gt.wait != nullptr;
+  bf16* const ny = nullptr;
   if (mt == 1 && kc == 256)
-    wstream_gemm_kernel<1, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1);
+    launch_maybe_early(wstream_gemm_kernel<1, 256, true, 1, true>, grid, dim3(256), st, early, X, ldx, wt, M, N, K, ks,
+                       ny, (int64_t)0, P, 0, ra, 1, gt);
   else if (mt == 2 && kc == 256)
-    wstream_gemm_kernel<2, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1);
+    launch_maybe_early(wstream_gemm_kernel<2, 256, true, 1, true>, grid, dim3(256), st, early, X, ldx, wt, M, N, K, ks,
+                       ny, (int64_t)0, P, 0, ra, 1, gt);
   else if (mt == 4 && kc == 128)
-    wstream_gemm_kernel<4, 128, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1);
+    launch_maybe_early(wstream_gemm_kernel<4, 128, true, 1, true>, grid, dim3(256), st, early, X, ldx, wt, M, N, K, ks,
+                       ny, (int64_t)0, P, 0, ra, 1, gt);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

@@ -101,3 +101,46 @@ def test_engine_on_poisoned_memory(cuda, model):
     outs = e.generate(prompts, GREEDY)
     assert seen and all(seen)
     _oracle_ok(e.model, prompts, outs)
+
+
+def _run_logits(e, prompts, sps):
+    seen = []
+    orig = e.runner.sample_device
+
+    def keep(logits, sp):
+        seen.append(logits.float().cpu())
+        return orig(logits, sp)
+
+    e.runner.sample_device = keep
+    try:
+        outs = e.generate(prompts, sps)
+    finally:
+        e.runner.sample_device = orig
+    return outs, seen
+
+
+def test_early_launched_layers_match_ordinary(eng):
+    """Early-launched decode layers (models/llama.py EARLY: kernels launched without the AQL barrier bit behind
+    device gates, the suffix decode beside the cascade) compute exactly what ordinary launches do: bitwise-equal
+    logits on every step (cascade + split rows, greedy and seeded sampling), every gate released by its producer."""
+    prompts = _prompts(9, 1200, (3, 40, 77, 500))
+    eng.generate([prompts[0][:1200] + [1]], GREEDY)  # cache the shared prefix: decode steps run the cascade
+    sps = [SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True),
+           SamplingParams(temperature=0.8, max_tokens=12, ignore_eos=True, seed=3),
+           SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True),
+           SamplingParams(temperature=0.7, top_p=0.9, max_tokens=12, ignore_eos=True, seed=4)]
+    m = eng.model
+    m.early = False
+    ref_outs, ref_logits = _run_logits(eng, prompts, sps)
+    m.early = True
+    try:
+        outs, logits = _run_logits(eng, prompts, sps)
+        gs = m._gates
+        assert gs is not None and gs.used > 0, "no step ran early-launched layers"
+        assert not gs.timed_out(), "a gate wait timed out"
+    finally:
+        m.early = False
+    assert outs == ref_outs
+    assert len(logits) == len(ref_logits)
+    for a, b in zip(logits, ref_logits):
+        assert torch.equal(a, b)
