@@ -234,7 +234,7 @@ class TransformerLM:
         if (m.prefix_items is not None and m.variant != 3) or torch.cuda.is_current_stream_capturing():
             return None
         if self._gates is None:
-            self._gates = ops.GateSet(self.device, 8 * len(self.layers) + 8)
+            self._gates = ops.GateSet(self.device, 12 * len(self.layers) + 8)
         self._gates.begin()
         return self._gates
 
@@ -275,8 +275,10 @@ class TransformerLM:
         def new() -> int:
             return gs.new() if gs is not None else -1
 
+        g_down = -1
         for i, lw in enumerate(self.layers):
             g_in = -1  # gate the input RMSNorm arrives on (-1: the QKV projection is an ordinary launch)
+            g_prev, g_down = (g_down if gs is not None and i > 0 else -1), -1
             if delta is _SEAM_DONE:
                 pass  # the previous layer's overlapped down seam already wrote residual and x
             elif delta is None:
@@ -286,7 +288,7 @@ class TransformerLM:
                 pstate.tp_all_reduce_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x)
             else:
                 g_in = new()
-                ops.fused_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x, gates=G(sig=g_in))
+                ops.fused_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x, gates=G(wait=g_prev, sig=g_in))
             g_rope = -1  # gate the RoPE / KV write arrives on (the attention kernels' input)
             if fuse_rope:  # RoPE + KV write in the streaming QKV GEMM's epilogue (no rope_kv launch)
                 ops.linear_stream_rope(x, lw.qkv_t, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i],
@@ -300,9 +302,10 @@ class TransformerLM:
             g_attn = paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out,
                                      gates=(gs, g_rope) if gs is not None else None)
             if gs is not None:  # the O projection streams its first weight chunk beside the decode's tail
-                o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t, kind="o", gates=G(wait=g_attn))
+                g_o = new()
+                o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t, kind="o", gates=G(wait=g_attn, sig=g_o))
                 g_post = new() if glu_gated else -1
-                ops.fused_add_rmsnorm(o, residual, lw.post_norm, eps, out=x, gates=G(sig=g_post))
+                ops.fused_add_rmsnorm(o, residual, lw.post_norm, eps, out=x, gates=G(wait=g_o, sig=g_post))
             elif tp and self._can_overlap(T, lw.o_t):
                 self._overlapped_seam(attn_out.view(T, -1), lw.o_t, residual, lw.post_norm, eps, x)
             elif tp and self._can_pipe(T, lw.o, lw.o_t):
@@ -320,7 +323,8 @@ class TransformerLM:
             elif glu_gated:
                 g_gu = new()
                 a = ops.linear_glu(x, lw.gate_up_t, gates=G(wait=g_post, sig=g_gu))
-                delta = self._linear(a, lw.down, lw.down_t, kind="down", gates=G(wait=g_gu))
+                g_down = new() if i + 1 < len(self.layers) else -1  # the next input RMSNorm waits on it
+                delta = self._linear(a, lw.down, lw.down_t, kind="down", gates=G(wait=g_gu, sig=g_down))
                 pending = False
             else:
                 if self.stream and lw.glu and 0 < T <= self.stream_max_m:

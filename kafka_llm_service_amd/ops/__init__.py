@@ -64,10 +64,12 @@ class GateSet:
         self.n = n
         self.buf = torch.zeros(n * self.INTS, dtype=torch.int32, device=device)
         self.used = 0
+        self.forwards = 0  # forwards that ran gated (stats, tests)
 
     def begin(self) -> None:
         self.buf.zero_()
         self.used = 0
+        self.forwards += 1
 
     def new(self) -> int:
         if self.used >= self.n:

@@ -14,6 +14,7 @@ struct Gates {
   int* sig = nullptr;
   int* wait2 = nullptr;
   int expect2 = 0;
+  int mode = 0;
 };
 constexpr int GATE_INTS = 16;
 
@@ -145,6 +146,12 @@ static Gates make_gates(const c10::optional<at::Tensor>& buf, const std::vector<
   g.sig = at_(2);
   g.wait2 = at_(3);
   g.expect2 = a.size() > 4 ? (int)a[4] : 0;
+  static const int mode = [] {  // diagnostics only (csrc/common.h Gates::mode)
+    const char* e = getenv("KAFKA_GATE_MODE");
+    const char* sl = getenv("KAFKA_GATE_SLEEP");
+    return (e && (e[0] == '1' || e[0] == '3') ? 1 : 0) | ((sl ? atoi(sl) : 0) << 4);
+  }();
+  g.mode = mode;
   return g;  // expect <= 0: the producer's published arrival count
 }
 

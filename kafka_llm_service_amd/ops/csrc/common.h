@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 typedef __bf16 bf16;
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -136,20 +138,25 @@ struct Gates {
   int* sig = nullptr;    // arrive on this gate when the workgroup's outputs are written (nullptr: none)
   int* wait2 = nullptr;  // a second gate (decode attention: the cascade partials, before the merge)
   int expect2 = 0;
+  int mode = 0;          // diagnostics: bit 0 (KAFKA_GATE_MODE=1/3) = no release / acquire (timing only: unordered
+                         // reads); bits 4.. (KAFKA_GATE_SLEEP) = poll back-off level
 };
 
 // ONE thread per workgroup, after a __syncthreads() that follows every global write the consumer will read; `total`:
 // how many workgroups of this launch arrive (the same value from every one)
-__device__ __forceinline__ void gate_arrive(int* sig, int total) {
+__device__ __forceinline__ void gate_arrive(int* sig, int total, int mode = 0) {
   if (sig == nullptr) return;
   const int shard = (int)((blockIdx.x + blockIdx.y * 7u + blockIdx.z * 3u) & 7u);
   __hip_atomic_store(sig + 9, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_fetch_add(sig + shard, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (mode & 1)
+    __hip_atomic_fetch_add(sig + shard, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    __hip_atomic_fetch_add(sig + shard, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // every thread of the workgroup (workgroup-uniform arguments); bounded: after 2 s the error word is raised and the
 // wait gives up (the host fails the step instead of hanging the GPU)
-__device__ __forceinline__ void gate_wait(int* g, int expect) {
+__device__ __forceinline__ void gate_wait(int* g, int expect, int mode = 0) {
   if (g == nullptr) return;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
@@ -167,17 +174,25 @@ __device__ __forceinline__ void gate_wait(int* g, int expect) {
         if (lane == 0) __hip_atomic_store(g + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
+      switch (mode >> 4) {  // uniform
+        case 0: __builtin_amdgcn_s_sleep(1); break;
+        case 1: __builtin_amdgcn_s_sleep(8); break;
+        default: __builtin_amdgcn_s_sleep(32); break;
+      }
     }
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (!(mode & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 // Launch `kernel`; `early`: without the AQL barrier bit (the kernel waits on a gate before reading its inputs)
 template <typename F, typename... Args>
 inline void launch_maybe_early(F kernel, dim3 grid, dim3 block, hipStream_t st, bool early, Args... args) {
-  if (early)
+  static const bool ordered = [] {  // diagnostics: KAFKA_GATE_MODE=2 keeps the barrier bit (gates without overlap)
+    const char* e = getenv("KAFKA_GATE_MODE");
+    return e && (e[0] == '2' || e[0] == '3');
+  }();
+  if (early && !ordered)
     hipExtLaunchKernelGGL(kernel, grid, block, 0, st, nullptr, nullptr, hipExtAnyOrderLaunch, args...);
   else
     hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);

@@ -32,6 +32,10 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int
     const int vi = threadIdx.x + i * NT;
     if (vi < nvec) wv[i] = load_bf16x8(w + vi * 8);
   }
+  if (gt.wait != nullptr) {  // early-launched (common.h Gates): the producer of x has finished
+    asm volatile("" ::: "memory");
+    gate_wait(gt.wait, gt.expect, gt.mode);
+  }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int vi = threadIdx.x + i * NT;
@@ -65,7 +69,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int
   }
   if (gt.sig != nullptr) {  // one arrival per row (common.h Gates)
     __syncthreads();
-    if (threadIdx.x == 0) gate_arrive(gt.sig, (int)gridDim.x);
+    if (threadIdx.x == 0) gate_arrive(gt.sig, (int)gridDim.x, gt.mode);
   }
 }
 
@@ -95,15 +99,20 @@ static hipError_t launch_rmsnorm_t(bf16* out, int64_t os, const bf16* x, const f
   dim3 grid(T), block(256);
   if (T == 0) return hipSuccess;
   if (nvec <= 512 && nvec > 256) {  // e.g. d = 4096: one 16-B vector per thread, twice the loads in flight per row
-    rmsnorm_kernel<1, RESID, 512><<<grid, 512, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt);
+    launch_maybe_early(rmsnorm_kernel<1, RESID, 512>, grid, dim3(512), st, gt.wait != nullptr, out, os, x, xp, S, ps,
+                       xs, r, rs, w, d, eps, gt);
     return hipGetLastError();
   }
   switch (nv) {
-    case 1: rmsnorm_kernel<1, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt); break;
-    case 2: rmsnorm_kernel<2, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt); break;
+#define KAFKA_RMS(NV_) \
+  launch_maybe_early(rmsnorm_kernel<NV_, RESID>, grid, block, st, gt.wait != nullptr, out, os, x, xp, S, ps, xs, r, rs, \
+                     w, d, eps, gt)
+    case 1: KAFKA_RMS(1); break;
+    case 2: KAFKA_RMS(2); break;
     case 3:
-    case 4: rmsnorm_kernel<4, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt); break;
-    default: rmsnorm_kernel<8, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt); break;
+    case 4: KAFKA_RMS(4); break;
+    default: KAFKA_RMS(8); break;
+#undef KAFKA_RMS
   }
   return hipGetLastError();
 }

@@ -124,18 +124,37 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
   };
 
   bf16x8 wa[KSW], wb[KSW];
+  int ch = 0;
   load_w(wa, 0);
   if (gt.wait != nullptr) {
-    // early-launched (common.h Gates): the first K chunk of this workgroup's weight slice is in flight while the
-    // producer of X finishes; X is read only after the gate
+    // early-launched (common.h Gates): the first two K chunks of this workgroup's weight slice are in flight while
+    // the producer of X finishes; X is read only after the gate. The first trip is peeled (chunk 1 is loaded).
+    const bool two = nchunks > 2;  // workgroup-uniform
+    if (two) load_w(wb, 1);
     asm volatile("" ::: "memory");
-    gate_wait(gt.wait, gt.expect);
+    gate_wait(gt.wait, gt.expect, gt.mode);
+    load_x(0);
+    store_x(0);
+    __syncthreads();
+    if (two) {
+      load_x(1);
+      compute(0, wa);
+      store_x(1);
+      __syncthreads();
+      load_x(2);
+      load_w(wa, 2);
+      compute(1, wb);
+      store_x(0);
+      __syncthreads();
+      ch = 2;
+    }
+  } else {
+    load_x(0);
+    store_x(0);
+    __syncthreads();
   }
-  load_x(0);
-  store_x(0);
-  __syncthreads();
-  // steady state: two chunks per trip, both prefetches in range (no conditional loads inside the trip)
-  int ch = 0;
+  // steady state: two chunks per trip, both prefetches in range (no conditional loads inside the trip); chunk ch is
+  // in buffer 0 / wa
   for (; ch + 2 < nchunks; ch += 2) {
     load_x(ch + 1);
     load_w(wb, ch + 1);
@@ -262,7 +281,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
       }
     if (gt.sig != nullptr) {  // one arrival per head tile (the last split's)
       __syncthreads();
-      if (tid == 0) gate_arrive(gt.sig, (int)gridDim.x);
+      if (tid == 0) gate_arrive(gt.sig, (int)gridDim.x, gt.mode);
     }
     return;
   }
@@ -310,7 +329,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
   }
   if (gt.sig != nullptr) {  // one arrival per workgroup
     __syncthreads();
-    if (tid == 0) gate_arrive(gt.sig, (int)(gridDim.x * gridDim.y));
+    if (tid == 0) gate_arrive(gt.sig, (int)(gridDim.x * gridDim.y), gt.mode);
   }
 }
 

@@ -122,24 +122,33 @@ def _run_logits(e, prompts, sps):
 def test_early_launched_layers_match_ordinary(eng):
     """Early-launched decode layers (models/llama.py EARLY: kernels launched without the AQL barrier bit behind
     device gates, the suffix decode beside the cascade) compute exactly what ordinary launches do: bitwise-equal
-    logits on every step (cascade + split rows, greedy and seeded sampling), every gate released by its producer."""
+    logits on every step (cascade + split rows, greedy and seeded sampling), every gate released by its producer.
+    Two fresh engines over the same weights, so both runs schedule identical steps."""
     prompts = _prompts(9, 1200, (3, 40, 77, 500))
-    eng.generate([prompts[0][:1200] + [1]], GREEDY)  # cache the shared prefix: decode steps run the cascade
     sps = [SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True),
            SamplingParams(temperature=0.8, max_tokens=12, ignore_eos=True, seed=3),
            SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True),
            SamplingParams(temperature=0.7, top_p=0.9, max_tokens=12, ignore_eos=True, seed=4)]
     m = eng.model
-    m.early = False
-    ref_outs, ref_logits = _run_logits(eng, prompts, sps)
-    m.early = True
-    try:
-        outs, logits = _run_logits(eng, prompts, sps)
-        gs = m._gates
-        assert gs is not None and gs.used > 0, "no step ran early-launched layers"
-        assert not gs.timed_out(), "a gate wait timed out"
-    finally:
-        m.early = False
+
+    def run(early: bool):
+        e = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", num_kv_blocks=4096, max_model_len=8192,
+                                   cascade_min_prefix=64, prefill_kv_chunk=256), model=m)
+        m.early = early
+        try:
+            e.generate([prompts[0][:1200] + [1]], GREEDY)  # cache the shared prefix: decode steps run the cascade
+            n0 = m._gates.forwards if m._gates is not None else 0
+            outs, logits = _run_logits(e, prompts, sps)
+            gated = (m._gates.forwards - n0) if m._gates is not None else 0
+            timed_out = m._gates.timed_out() if m._gates is not None else False
+        finally:
+            m.early = False
+        return outs, logits, gated, timed_out
+
+    ref_outs, ref_logits, _, _ = run(False)
+    outs, logits, gated, timed_out = run(True)
+    assert gated >= 8, f"only {gated} forwards ran early-launched layers"
+    assert not timed_out, "a gate wait timed out"
     assert outs == ref_outs
     assert len(logits) == len(ref_logits)
     for a, b in zip(logits, ref_logits):
