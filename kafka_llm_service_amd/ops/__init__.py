@@ -58,7 +58,7 @@ class GateSet:
     launched immediately before it and writes nothing before its wait (gates chain transitively, so the caching
     allocator's stream-order reuse stays safe)."""
 
-    INTS = 16  # GATE_INTS: 8 shard counters + the error word (a wait that timed out after 2 s)
+    INTS = 17 * 16  # GATE_INTS: 8 arrival-counter lines, the top counter (+ error word), 8 per-XCD done flags
 
     def __init__(self, device: torch.device, n: int):
         self.n = n
@@ -83,10 +83,13 @@ class GateSet:
 
     def timed_out(self) -> bool:
         """Whether any wait of the last forward gave up (host sync: tests and diagnostics)."""
-        return bool(self.buf.view(-1, self.INTS)[:, 8].any().item())
+        return bool(self.buf.view(-1, self.INTS)[:, 8 * 16 + 1].any().item())
 
     def arrivals(self, g: int) -> int:
-        return int(self.buf.view(-1, self.INTS)[g, :8].sum().item())
+        return int(self.buf.view(-1, self.INTS)[g, 0:8 * 16:16].sum().item())
+
+    def released(self, g: int) -> bool:
+        return bool(self.buf.view(-1, self.INTS)[g, 9 * 16:17 * 16:16].all().item())
 
 
 def _gk(gates) -> dict:

@@ -438,7 +438,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     // Phase 1: wave w owns heads w, w + 4: lanes load the prefix lse values in parallel, wave-reduce the max and
     // the weight sum, and publish per-split weights in LDS. Phase 2: thread (g, 4 dims) sums weight x partial over
     // the splits with all loads of a group of 8 in flight.
-    gate_wait(gt.wait2, gt.expect2, gt.mode);  // early-launched beside the cascade: its partials are complete
+    gate_wait(gt.wait2, gt.mode);  // early-launched beside the cascade: its partials are complete
     for (int g = w; g < G; g += 4) {
       float Ms = -INFINITY;
 #pragma unroll
@@ -517,7 +517,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     }
     if (gt.sig != nullptr) {  // one arrival per merged (row, kv head)
       __syncthreads();
-      if (threadIdx.x == 0) gate_arrive(gt.sig, gt_total, gt.mode);
+      if (threadIdx.x == 0) gate_arrive(gt.sig, b * Hkv + kvh, gt_total, gt.mode);
     }
     return;
   }
@@ -561,7 +561,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   }
   __syncthreads();
   if (!sm.s_last) return;
-  gate_wait(gt.wait2, gt.expect2, gt.mode);
+  gate_wait(gt.wait2, gt.mode);
   auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   // 16-B agent-coherent loads (sc1: not served from this XCD's possibly stale L2); inline asm, so the group below
   // waits for them itself
@@ -615,7 +615,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   }
   if (gt.sig != nullptr) {  // one arrival per merged (row, kv head)
     __syncthreads();
-    if (threadIdx.x == 0) gate_arrive(gt.sig, gt_total, gt.mode);
+    if (threadIdx.x == 0) gate_arrive(gt.sig, b * Hkv + kvh, gt_total, gt.mode);
   }
 }
 
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(256, OCC3 ? 3 : 2) void attn_decode_kernel(const bf
   if (b < 0 || b >= B || split < 0 || split >= S || split_offset < 0 || split_offset + S > S_total ||
       (out != nullptr && split_offset + S > 64))
     return;
-  gate_wait(gt.wait, gt.expect, gt.mode);  // early-launched: q and this step's K/V rows are written
+  gate_wait(gt.wait, gt.mode);  // early-launched: q and this step's K/V rows are written
   decode_piece<D, FP8, MG, OCC3>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, it.lo, it.hi,
                            split, S, split_offset, out_part, lse_part, S_total, scale_log2, out, out_stride, tickets,
                            pre_bf16, gt, B * Hkv);

@@ -244,7 +244,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
   for (int j = 0; j < NSLOT - 1; ++j)
     if (j < ntiles) issue(j);
   if (gated) {
-    gate_wait(gt.wait, gt.expect, gt.mode);
+    gate_wait(gt.wait, gt.mode);
     load_q();
   }
 
@@ -490,7 +490,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
   }
   if (gt.sig != nullptr) {  // one arrival per workgroup
     __syncthreads();
-    if (tid == 0) gate_arrive(gt.sig, (int)(gridDim.x * gridDim.y), gt.mode);
+    if (tid == 0) gate_arrive(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y), gt.mode);
   }
   if constexpr (ABL == 8) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -16,7 +16,7 @@ struct Gates {
   int expect2 = 0;
   int mode = 0;
 };
-constexpr int GATE_INTS = 16;
+constexpr int GATE_INTS = 17 * 16;  // csrc/common.h
 
 extern "C" {
 hipError_t kafka_launch_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs, const bf16* w, int T, int d, float eps,

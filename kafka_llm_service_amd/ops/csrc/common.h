@@ -121,57 +121,67 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
 // ---- device gates: early-launched consumers ---------------------------------------------------------------------
 // A consumer kernel launched WITHOUT the AQL barrier bit (hipExtAnyOrderLaunch) is dispatched as soon as its
 // predecessor's last workgroup has been dispatched, so it runs its producer-independent prologue (the weight stream
-// of a projection, page tables, first K/V tiles) while the producer's tail still runs, then waits on a gate: GATE_INTS
-// int32 per gate, shards [0, 8) bumped once per arriving producer workgroup (shard = workgroup id & 7: arrivals of
-// different XCDs hit different lines), word 8 = error flag (a wait that timed out), word 9 = the producer's arrival
-// count (published by every arriving workgroup, so the host never mirrors launch geometry). The producer's arrival is an
-// agent-scope release after a workgroup barrier; the consumer's wait ends with an agent-scope acquire, so its later
-// loads see the producer's writes from any XCD. Dispatch order within a queue guarantees every producer workgroup is
-// resident before any consumer workgroup, so a waiting consumer can never starve its producer.
-// Rule for callers (ops.gates / models): a gated consumer writes nothing to global memory before its wait, and it
+// of a projection, page tables, first K/V tiles) while the producer's tail still runs, then waits on a gate. Dispatch
+// order within a queue guarantees every producer workgroup is resident before any consumer workgroup, so a waiting
+// consumer can never starve its producer.
+// A gate is 17 cache lines (no line is hot): lines 0..7 are arrival counters (a producer unit u arrives on line
+// u & 7), line 8 the top counter (+ error word), lines 9..16 per-XCD "done" flags. The last arrival of a line bumps
+// the top counter; the last of those raises all 8 flags. A consumer workgroup polls ONE flag (line 9 + its id & 7),
+// so each line sees a handful of same-address accesses instead of every workgroup of both kernels.
+// The producer's arrivals are agent-scope acq_rel RMWs after a workgroup barrier (release cumulativity carries the
+// whole workgroup's writes), the flags release stores, the consumer's wait ends with an agent-scope acquire.
+// Rule for callers (ops.GateSet / models): a gated consumer writes nothing to global memory before its wait, and it
 // waits on the kernel launched immediately before it (gates then chain transitively, and the caching allocator's
 // stream-order reuse stays safe).
-constexpr int GATE_INTS = 16;
+constexpr int GATE_LINE = 16;                // int32 per 64-B line
+constexpr int GATE_INTS = 17 * GATE_LINE;
 struct Gates {
-  int* wait = nullptr;   // wait until the shards of this gate sum to `expect` (<= 0: the producer's published count)
-  int expect = 0;
-  int* sig = nullptr;    // arrive on this gate when the workgroup's outputs are written (nullptr: none)
+  int* wait = nullptr;   // wait until this gate's producer has fully arrived (nullptr: no wait)
+  int expect = 0;        // (unused: the producer counts its own arrivals)
+  int* sig = nullptr;    // arrive on this gate when the unit's outputs are written (nullptr: none)
   int* wait2 = nullptr;  // a second gate (decode attention: the cascade partials, before the merge)
   int expect2 = 0;
   int mode = 0;          // diagnostics: bit 0 (KAFKA_GATE_MODE=1/3) = no release / acquire (timing only: unordered
                          // reads); bits 4.. (KAFKA_GATE_SLEEP) = poll back-off level
 };
 
-// ONE thread per workgroup, after a __syncthreads() that follows every global write the consumer will read; `total`:
-// how many workgroups of this launch arrive (the same value from every one)
-__device__ __forceinline__ void gate_arrive(int* sig, int total, int mode = 0) {
-  if (sig == nullptr) return;
-  const int shard = (int)((blockIdx.x + blockIdx.y * 7u + blockIdx.z * 3u) & 7u);
-  __hip_atomic_store(sig + 9, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (mode & 1)
-    __hip_atomic_fetch_add(sig + shard, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    __hip_atomic_fetch_add(sig + shard, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ int gate_block_id() {
+  return (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+}
+
+// ONE thread, after a __syncthreads() that follows every global write of arrival unit `unit` (0 <= unit < total; a
+// launch arrives `total` times, each unit once)
+__device__ __forceinline__ void gate_arrive(int* g, int unit, int total, int mode = 0) {
+  if (g == nullptr) return;
+  const int s = unit & 7;
+  const int n_s = total / 8 + (s < total % 8 ? 1 : 0);
+  const int lines = total < 8 ? total : 8;
+  const bool rlx = mode & 1;
+  const int old = rlx ? __hip_atomic_fetch_add(g + s * GATE_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : __hip_atomic_fetch_add(g + s * GATE_LINE, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (old != n_s - 1) return;
+  const int top = rlx ? __hip_atomic_fetch_add(g + 8 * GATE_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : __hip_atomic_fetch_add(g + 8 * GATE_LINE, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (top != lines - 1) return;
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    if (rlx)
+      __hip_atomic_store(g + (9 + x) * GATE_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      __hip_atomic_store(g + (9 + x) * GATE_LINE, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // every thread of the workgroup (workgroup-uniform arguments); bounded: after 2 s the error word is raised and the
 // wait gives up (the host fails the step instead of hanging the GPU)
-__device__ __forceinline__ void gate_wait(int* g, int expect, int mode = 0) {
+__device__ __forceinline__ void gate_wait(int* g, int mode = 0) {
   if (g == nullptr) return;
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
+  if (threadIdx.x == 0) {
+    const int* flag = g + (9 + (gate_block_id() & 7)) * GATE_LINE;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (true) {
-      // lanes 0..7: the shards, lane 8: the published count (monotonic: a stale read only delays the release)
-      int v = lane < 9 ? __hip_atomic_load(g + (lane < 8 ? lane : 9), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-      const int target = expect > 0 ? expect : __shfl(v, 8, 64);
-      if (lane >= 8) v = 0;
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      if (target > 0 && __shfl(v, 0, 64) >= target) break;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
-        if (lane == 0) __hip_atomic_store(g + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(g + 8 * GATE_LINE + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       switch (mode >> 4) {  // uniform

@@ -34,7 +34,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int
   }
   if (gt.wait != nullptr) {  // early-launched (common.h Gates): the producer of x has finished
     asm volatile("" ::: "memory");
-    gate_wait(gt.wait, gt.expect, gt.mode);
+    gate_wait(gt.wait, gt.mode);
   }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int
   }
   if (gt.sig != nullptr) {  // one arrival per row (common.h Gates)
     __syncthreads();
-    if (threadIdx.x == 0) gate_arrive(gt.sig, (int)gridDim.x, gt.mode);
+    if (threadIdx.x == 0) gate_arrive(gt.sig, (int)blockIdx.x, (int)gridDim.x, gt.mode);
   }
 }
 

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ 
   constexpr int HALF = D / 2;
   constexpr int RU = HALF / 8;  // rope units (8 rotation pairs each) per head
   constexpr int VU = D / 8;     // v copy units (8 elements) per head
-  gate_wait(gt.wait, gt.expect, gt.mode);  // early-launched (common.h Gates): the QKV projection's slabs are complete
+  gate_wait(gt.wait, gt.mode);  // early-launched (common.h Gates): the QKV projection's slabs are complete
   const int64_t t = blockIdx.x;
   const int64_t pos = positions[t];
   const int64_t slot = slot_mapping ? slot_mapping[t] : -1;
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ 
   }
   if (gt.sig != nullptr) {  // one arrival per workgroup
     __syncthreads();
-    if (threadIdx.x == 0) gate_arrive(gt.sig, (int)(gridDim.x * gridDim.y), gt.mode);
+    if (threadIdx.x == 0) gate_arrive(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y), gt.mode);
   }
 }
 

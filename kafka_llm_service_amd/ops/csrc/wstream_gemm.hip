@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
     const bool two = nchunks > 2;  // workgroup-uniform
     if (two) load_w(wb, 1);
     asm volatile("" ::: "memory");
-    gate_wait(gt.wait, gt.expect, gt.mode);
+    gate_wait(gt.wait, gt.mode);
     load_x(0);
     store_x(0);
     __syncthreads();
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
       }
     if (gt.sig != nullptr) {  // one arrival per head tile (the last split's)
       __syncthreads();
-      if (tid == 0) gate_arrive(gt.sig, (int)gridDim.x, gt.mode);
+      if (tid == 0) gate_arrive(gt.sig, (int)blockIdx.x, (int)gridDim.x, gt.mode);
     }
     return;
   }
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
   }
   if (gt.sig != nullptr) {  // one arrival per workgroup
     __syncthreads();
-    if (tid == 0) gate_arrive(gt.sig, (int)(gridDim.x * gridDim.y), gt.mode);
+    if (tid == 0) gate_arrive(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y), gt.mode);
   }
 }
 
