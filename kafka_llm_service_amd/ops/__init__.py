@@ -372,6 +372,9 @@ STREAM_MAX_M = max(1, min(256, int(os.environ.get("KAFKA_STREAM_MAX_M", "128")))
 STREAM_KERNEL_MAX_M = 256
 
 
+_WSTREAM_TARGET = int(os.environ.get("KAFKA_WSTREAM_TARGET", "0"))  # A/B override of the split target (both sides)
+
+
 def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, int] | None:
     """(row tiles, K chunk, splits) of the decode GEMM for a shape, None if unsupported (same rule as
     kafka_wstream_plan in csrc/wstream_gemm.hip, mirrored so CPU runs take the same split decisions)."""
@@ -382,7 +385,7 @@ def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, 
     if K % kc or K <= 0:
         return None
     nx, chunks, s = (N + 127) // 128 * ((M + 127) // 128), K // kc, 1
-    target = 256 if mt == 4 else 192
+    target = _WSTREAM_TARGET or (256 if mt == 4 else 192)
     while s * 2 <= max_splits and s * 2 <= 8 and chunks % (s * 2) == 0 and nx * s < target:
         s *= 2
     return mt, kc, s

@@ -23,6 +23,8 @@
 // 128-B row segments.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace kafka {
 
 // QKV-projection epilogue (ROPE instantiations): rotate-half RoPE on the q / k heads, q to q_out, k / v straight
@@ -509,7 +511,11 @@ extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, 
   // split until the grid reaches ~192 (MT <= 2) / 256 (MT = 4) workgroups: measured on MI355X
   // (benchmarks/wstream_sweep.py, profiles/wstream_sweep_r01.log) — every extra split adds 2 x M x N x 4 B of slab
   // traffic, so e.g. gate_up (N = 28672) at M = 64 runs fastest unsplit and qkv (N = 6144) with S = 4
-  const int target = MT == 4 ? 256 : 192;
+  static const int target_env = [] {  // KAFKA_WSTREAM_TARGET (A/B only; mirrored by ops.stream_plan)
+    const char* e = getenv("KAFKA_WSTREAM_TARGET");
+    return e ? atoi(e) : 0;
+  }();
+  const int target = target_env > 0 ? target_env : (MT == 4 ? 256 : 192);
   int s = 1;
   while (s * 2 <= max_splits && s * 2 <= 8 && chunks % (s * 2) == 0 && nx * s < target) s *= 2;
   *mt = MT;
