@@ -344,7 +344,7 @@ struct DecodeSmem {
 // One decode piece: keys [lo, hi) of row b, kv head kvh, piece `split` of S, partial slots from split_offset. Every
 // thread of the workgroup calls it with the same arguments (it synchronises the workgroup); returns when the
 // piece's partial or final rows are written.
-template <int D, bool FP8, int MG, bool OCC3 = false>
+template <int D, bool FP8, int MG, bool OCC3 = false, bool GATED = false>
 __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __restrict__ q, int64_t q_stride,
                                              const void* __restrict__ k_cache, const void* __restrict__ v_cache,
                                              int Hkv, int G, const int* __restrict__ block_tables, int bt_stride,
@@ -438,7 +438,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     // Phase 1: wave w owns heads w, w + 4: lanes load the prefix lse values in parallel, wave-reduce the max and
     // the weight sum, and publish per-split weights in LDS. Phase 2: thread (g, 4 dims) sums weight x partial over
     // the splits with all loads of a group of 8 in flight.
-    gate_wait(gt.wait2, gt.mode);  // early-launched beside the cascade: its partials are complete
+    if constexpr (GATED) gate_wait(gt.wait2, gt.mode);  // early-launched beside the cascade: its partials are in
     for (int g = w; g < G; g += 4) {
       float Ms = -INFINITY;
 #pragma unroll
@@ -515,7 +515,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
       for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc4[j] * inv);
       *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
     }
-    if (gt.sig != nullptr) {  // one arrival per merged (row, kv head)
+    if constexpr (GATED) {  // one arrival per merged (row, kv head)
       __syncthreads();
       if (threadIdx.x == 0) gate_arrive(gt.sig, b * Hkv + kvh, gt_total, gt.mode);
     }
@@ -561,7 +561,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   }
   __syncthreads();
   if (!sm.s_last) return;
-  gate_wait(gt.wait2, gt.mode);
+  if constexpr (GATED) gate_wait(gt.wait2, gt.mode);
   auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   // 16-B agent-coherent loads (sc1: not served from this XCD's possibly stale L2); inline asm, so the group below
   // waits for them itself
@@ -613,13 +613,13 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc4[j] * inv);
     *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
   }
-  if (gt.sig != nullptr) {  // one arrival per merged (row, kv head)
+  if constexpr (GATED) {  // one arrival per merged (row, kv head)
     __syncthreads();
     if (threadIdx.x == 0) gate_arrive(gt.sig, b * Hkv + kvh, gt_total, gt.mode);
   }
 }
 
-template <int D, bool HEADS_FAST, bool FP8, int MG = 16, bool OCC3 = false>
+template <int D, bool HEADS_FAST, bool FP8, int MG = 16, bool OCC3 = false, bool GATED = false>
 __global__ __launch_bounds__(256, OCC3 ? 3 : 2) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
                                                            const void* __restrict__ k_cache,
                                                            const void* __restrict__ v_cache, int Hkv, int G,
@@ -639,8 +639,8 @@ __global__ __launch_bounds__(256, OCC3 ? 3 : 2) void attn_decode_kernel(const bf
   if (b < 0 || b >= B || split < 0 || split >= S || split_offset < 0 || split_offset + S > S_total ||
       (out != nullptr && split_offset + S > 64))
     return;
-  gate_wait(gt.wait, gt.mode);  // early-launched: q and this step's K/V rows are written
-  decode_piece<D, FP8, MG, OCC3>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, it.lo, it.hi,
+  if constexpr (GATED) gate_wait(gt.wait, gt.mode);  // early-launched: q and this step's K/V rows are written
+  decode_piece<D, FP8, MG, OCC3, GATED>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, it.lo, it.hi,
                            split, S, split_offset, out_part, lse_part, S_total, scale_log2, out, out_stride, tickets,
                            pre_bf16, gt, B * Hkv);
 }
@@ -1204,6 +1204,11 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
     return e == nullptr || e[0] != '0';
   }();
   const dim3 hf(Hkv, n_items), sf(n_items, Hkv);
+  if (gt.wait != nullptr || gt.wait2 != nullptr || gt.sig != nullptr) {  // gated: its own instantiation
+    if (fp8 || !heads_fast || mg != 32 || !occ3) return hipErrorInvalidValue;
+    go(attn_decode_kernel<128, true, false, 32, true, true>, hf);
+    return hipGetLastError();
+  }
   if (fp8)
     heads_fast ? go(attn_decode_kernel<128, true, true>, hf) : go(attn_decode_kernel<128, false, true>, sf);
   else if (!heads_fast)

@@ -104,7 +104,7 @@ __device__ __forceinline__ void t3_wait_tiles(int n) {
 // tiles, 0, 0, 0])
 // RB = 32-row MFMA blocks per wave: 2 -> 4 waves (one per SIMD, 512 registers each); 1 -> 8 waves (two per SIMD,
 // 256 registers each: the partner wave's MFMAs run beside this wave's softmax VALU). Rows per workgroup: 256.
-template <int RB, int NSLOT, int ABL = 0>
+template <int RB, int NSLOT, int ABL = 0, bool GATED = false>
 __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(const TileItem* __restrict__ items,
                                                            const bf16* __restrict__ q, int64_t q_stride,
                                                            const bf16* __restrict__ k_cache,
@@ -178,8 +178,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
     }
   };
   // early-launched cascade (common.h Gates): the prefix K/V (written by earlier steps) streams in before q exists
-  const bool gated = gt.wait != nullptr;
-  if (!gated) load_q();
+  if constexpr (!GATED) load_q();
   // per-block wave-uniform bounds: keys past hi_b are masked for every row of the block, keys <= wmin_b for none
   int hi_b[2], wmin_b[2];  // (RB == 1: block 1 mirrors block 0)
 #pragma unroll
@@ -243,7 +242,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
 #pragma unroll
   for (int j = 0; j < NSLOT - 1; ++j)
     if (j < ntiles) issue(j);
-  if (gated) {
+  if constexpr (GATED) {
     gate_wait(gt.wait, gt.mode);
     load_q();
   }
@@ -488,7 +487,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
       }
     }
   }
-  if (gt.sig != nullptr) {  // one arrival per workgroup
+  if constexpr (GATED) {  // one arrival per workgroup
     __syncthreads();
     if (tid == 0) gate_arrive(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y), gt.mode);
   }
@@ -531,6 +530,10 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
   if (abl == 2) kern = rb == 2 ? attn_tile_kernel<2, 3, 2> : attn_tile_kernel<1, 3, 2>;
   if (abl == 8) kern = rb == 2 ? attn_tile_kernel<2, 3, 8> : attn_tile_kernel<1, 3, 8>;
   if (abl == 9) kern = rb == 2 ? attn_tile_kernel<2, 3, 9> : attn_tile_kernel<1, 3, 9>;
+  if (gt.wait != nullptr || gt.sig != nullptr) {  // early-launched cascade: its own instantiation (default shape)
+    if (rb != 1 || slots != 3 || abl != 0) return hipErrorInvalidValue;
+    kern = attn_tile_kernel<1, 3, 0, true>;
+  }
   launch_maybe_early(kern, dim3(Hkv, n_items), dim3(512 / rb), st, gt.wait != nullptr,
                      reinterpret_cast<const TileItem*>(items), q, q_stride, static_cast<const bf16*>(k_cache),
                      static_cast<const bf16*>(v_cache), Hkv, G, block_tables, bt_stride, q_limit, out, out_stride,

@@ -14,7 +14,7 @@ namespace kafka {
 
 // y = x * rsqrt(mean(x^2) + eps) * w     (x: [T, d] with row stride, out: [T, d] contiguous)
 // If RESID: r = x + r (rounded to bf16, written back to r), y = norm(r) * w.
-template <int NV, bool RESID, int NT = 256>
+template <int NV, bool RESID, int NT = 256, bool GATED = false>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int64_t out_stride,
                                                        const bf16* __restrict__ x, const float* __restrict__ xp,
                                                        int S, int64_t ps, int64_t x_stride,
@@ -32,7 +32,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int
     const int vi = threadIdx.x + i * NT;
     if (vi < nvec) wv[i] = load_bf16x8(w + vi * 8);
   }
-  if (gt.wait != nullptr) {  // early-launched (common.h Gates): the producer of x has finished
+  if constexpr (GATED) {  // early-launched (common.h Gates): the producer of x has finished
     asm volatile("" ::: "memory");
     gate_wait(gt.wait, gt.mode);
   }
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int
       store_bf16x8(out + row * out_stride + vi * 8, o);
     }
   }
-  if (gt.sig != nullptr) {  // one arrival per row (common.h Gates)
+  if constexpr (GATED) {  // one arrival per row (common.h Gates)
     __syncthreads();
     if (threadIdx.x == 0) gate_arrive(gt.sig, (int)blockIdx.x, (int)gridDim.x, gt.mode);
   }
@@ -98,15 +98,24 @@ static hipError_t launch_rmsnorm_t(bf16* out, int64_t os, const bf16* x, const f
   const int nv = (nvec + 255) / 256;
   dim3 grid(T), block(256);
   if (T == 0) return hipSuccess;
+  const bool gated = gt.wait != nullptr || gt.sig != nullptr;  // (the gated code is its own instantiation)
   if (nvec <= 512 && nvec > 256) {  // e.g. d = 4096: one 16-B vector per thread, twice the loads in flight per row
-    launch_maybe_early(rmsnorm_kernel<1, RESID, 512>, grid, dim3(512), st, gt.wait != nullptr, out, os, x, xp, S, ps,
-                       xs, r, rs, w, d, eps, gt);
+    if (gated)
+      launch_maybe_early(rmsnorm_kernel<1, RESID, 512, true>, grid, dim3(512), st, gt.wait != nullptr, out, os, x, xp,
+                         S, ps, xs, r, rs, w, d, eps, gt);
+    else
+      rmsnorm_kernel<1, RESID, 512><<<grid, 512, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt);
     return hipGetLastError();
   }
   switch (nv) {
-#define KAFKA_RMS(NV_) \
-  launch_maybe_early(rmsnorm_kernel<NV_, RESID>, grid, block, st, gt.wait != nullptr, out, os, x, xp, S, ps, xs, r, rs, \
-                     w, d, eps, gt)
+#define KAFKA_RMS(NV_)                                                                                          \
+  do {                                                                                                         \
+    if (gated)                                                                                                 \
+      launch_maybe_early(rmsnorm_kernel<NV_, RESID, 256, true>, grid, block, st, gt.wait != nullptr, out, os, x, xp, \
+                         S, ps, xs, r, rs, w, d, eps, gt);                                                    \
+    else                                                                                                       \
+      rmsnorm_kernel<NV_, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt);       \
+  } while (0)
     case 1: KAFKA_RMS(1); break;
     case 2: KAFKA_RMS(2); break;
     case 3:

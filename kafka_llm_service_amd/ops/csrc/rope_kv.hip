@@ -35,7 +35,7 @@ namespace kafka {
 
 __device__ __forceinline__ int vt_pos(int o) { return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1); }
 
-template <int D>
+template <int D, bool GATED = false>
 __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ qkv, const float* __restrict__ qp,
                                                        int S, int64_t ps, int64_t qkv_stride,
                                                        const int64_t* __restrict__ positions,
@@ -47,7 +47,7 @@ __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ 
   constexpr int HALF = D / 2;
   constexpr int RU = HALF / 8;  // rope units (8 rotation pairs each) per head
   constexpr int VU = D / 8;     // v copy units (8 elements) per head
-  gate_wait(gt.wait, gt.mode);  // early-launched (common.h Gates): the QKV projection's slabs are complete
+  if constexpr (GATED) gate_wait(gt.wait, gt.mode);  // early-launched (common.h Gates): the QKV slabs are complete
   const int64_t t = blockIdx.x;
   const int64_t pos = positions[t];
   const int64_t slot = slot_mapping ? slot_mapping[t] : -1;
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ 
       for (int j = 0; j < 8; ++j) dst[(int64_t)(c + j) * block_size] = (bf16)x[j];
     }
   }
-  if (gt.sig != nullptr) {  // one arrival per workgroup
+  if constexpr (GATED) {  // one arrival per workgroup
     __syncthreads();
     if (threadIdx.x == 0) gate_arrive(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y), gt.mode);
   }
@@ -268,12 +268,20 @@ extern "C" hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int
   }
   const dim3 grid(T, ny);
   const bool early = gt.wait != nullptr;
-  if (D == 128)
-    launch_maybe_early(rope_kv_kernel<128>, grid, dim3(nt), st, early, qkv, qp, S, ps, qkv_stride, positions, cos_sin,
-                       q_out, q_stride, k_cache, v_cache, slot_mapping, Hq, Hkv, block_size, gt);
-  else
-    launch_maybe_early(rope_kv_kernel<64>, grid, dim3(nt), st, early, qkv, qp, S, ps, qkv_stride, positions, cos_sin,
-                       q_out, q_stride, k_cache, v_cache, slot_mapping, Hq, Hkv, block_size, gt);
+  if (gt.wait != nullptr || gt.sig != nullptr) {  // (the gated code is its own instantiation)
+    if (D == 128)
+      launch_maybe_early(rope_kv_kernel<128, true>, grid, dim3(nt), st, early, qkv, qp, S, ps, qkv_stride, positions,
+                         cos_sin, q_out, q_stride, k_cache, v_cache, slot_mapping, Hq, Hkv, block_size, gt);
+    else
+      launch_maybe_early(rope_kv_kernel<64, true>, grid, dim3(nt), st, early, qkv, qp, S, ps, qkv_stride, positions,
+                         cos_sin, q_out, q_stride, k_cache, v_cache, slot_mapping, Hq, Hkv, block_size, gt);
+  } else if (D == 128) {
+    rope_kv_kernel<128><<<grid, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
+                                          v_cache, slot_mapping, Hq, Hkv, block_size, gt);
+  } else {
+    rope_kv_kernel<64><<<grid, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
+                                         v_cache, slot_mapping, Hq, Hkv, block_size, gt);
+  }
   return hipGetLastError();
 }
 

@@ -47,7 +47,7 @@ struct RopeKV {
 
 __device__ __forceinline__ int rope_vt_pos(int o) { return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1); }
 
-template <int MT, int KC, bool NT, int KW, bool ROPE = false>
+template <int MT, int KC, bool NT, int KW, bool ROPE = false, bool EARLY = false>
 __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                                  const bf16x8* __restrict__ Wt, int M, int N, int K,
                                                                  int ks, bf16* __restrict__ Y, int64_t ldy,
@@ -127,8 +127,14 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
 
   bf16x8 wa[KSW], wb[KSW];
   int ch = 0;
-  load_w(wa, 0);
-  if (gt.wait != nullptr) {
+  if (!EARLY || gt.wait == nullptr) {  // (EARLY: the gated instantiation, common.h Gates)
+    // X first: its LDS image is written while the first weight chunk is still in flight (loads return in order)
+    load_x(0);
+    load_w(wa, 0);
+    store_x(0);
+    __syncthreads();
+  } else {
+    load_w(wa, 0);
     // early-launched (common.h Gates): the first two K chunks of this workgroup's weight slice are in flight while
     // the producer of X finishes; X is read only after the gate. The first trip is peeled (chunk 1 is loaded).
     const bool two = nchunks > 2;  // workgroup-uniform
@@ -150,10 +156,6 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
       __syncthreads();
       ch = 2;
     }
-  } else {
-    load_x(0);
-    store_x(0);
-    __syncthreads();
   }
   // steady state: two chunks per trip, both prefetches in range (no conditional loads inside the trip); chunk ch is
   // in buffer 0 / wa
@@ -281,9 +283,11 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
           }
         }
       }
-    if (gt.sig != nullptr) {  // one arrival per head tile (the last split's)
-      __syncthreads();
-      if (tid == 0) gate_arrive(gt.sig, (int)blockIdx.x, (int)gridDim.x, gt.mode);
+    if constexpr (EARLY) {  // one arrival per head tile (the last split's)
+      if (gt.sig != nullptr) {
+        __syncthreads();
+        if (tid == 0) gate_arrive(gt.sig, (int)blockIdx.x, (int)gridDim.x, gt.mode);
+      }
     }
     return;
   }
@@ -329,9 +333,11 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
         }
       }
   }
-  if (gt.sig != nullptr) {  // one arrival per workgroup
-    __syncthreads();
-    if (tid == 0) gate_arrive(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y), gt.mode);
+  if constexpr (EARLY) {  // one arrival per workgroup
+    if (gt.sig != nullptr) {
+      __syncthreads();
+      if (tid == 0) gate_arrive(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y), gt.mode);
+    }
   }
 }
 
@@ -536,15 +542,21 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   const int ks = K / splits;
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   float* p = splits > 1 ? P : nullptr;
-  const bool early = gt.wait != nullptr;
+  const bool early = gt.wait != nullptr, gated = early || gt.sig != nullptr;
+  // (gated launches use their own instantiation, EARLY: the ordinary kernel is exactly the ungated code)
 #define KAFKA_WS(MT_, KC_, KW_)                                                                                \
   do {                                                                                                        \
-    if (nt)                                                                                                   \
-      launch_maybe_early(wstream_gemm_kernel<MT_, KC_, true, KW_>, grid, dim3(256 * KW_), st, early, X, ldx, wt, M, \
-                         N, K, ks, Y, ldy, p, glu, RopeKV{}, rt, gt);                                         \
+    if (gated && nt && KW_ == 1)                                                                              \
+      launch_maybe_early(wstream_gemm_kernel<MT_, KC_, true, KW_, false, true>, grid, dim3(256 * KW_), st, early, \
+                         X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, RopeKV{}, rt, gt);                          \
+    else if (gated)                                                                                           \
+      return hipErrorInvalidValue;                                                                            \
+    else if (nt)                                                                                              \
+      wstream_gemm_kernel<MT_, KC_, true, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, \
+                                                                           RopeKV{}, rt, gt);                \
     else                                                                                                      \
-      launch_maybe_early(wstream_gemm_kernel<MT_, KC_, false, KW_>, grid, dim3(256 * KW_), st, early, X, ldx, wt, \
-                         M, N, K, ks, Y, ldy, p, glu, RopeKV{}, rt, gt);                                      \
+      wstream_gemm_kernel<MT_, KC_, false, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p,   \
+                                                                            glu, RopeKV{}, rt, gt);           \
   } while (0)
   if (mt == 1 && kc == 256 && kw == 1) KAFKA_WS(1, 256, 1);
   else if (mt == 1 && kc == 256 && kw == 2) KAFKA_WS(1, 256, 2);
@@ -575,17 +587,13 @@ extern "C" hipError_t kafka_launch_wstream_qkv_rope(const bf16* X, int64_t ldx, 
   const int ks = K / splits;
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   const RopeKV ra{positions, cos_sin, q_out, q_stride, k_cache, v_cache, slots, Hq, Hkv, tickets};
-  const bool early = gt.wait != nullptr;
-  bf16* const ny = nullptr;
+  if (gt.wait != nullptr || gt.sig != nullptr) return hipErrorInvalidValue;  // the fused QKV + RoPE kernel: never gated
   if (mt == 1 && kc == 256)
-    launch_maybe_early(wstream_gemm_kernel<1, 256, true, 1, true>, grid, dim3(256), st, early, X, ldx, wt, M, N, K, ks,
-                       ny, (int64_t)0, P, 0, ra, 1, gt);
+    wstream_gemm_kernel<1, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1, gt);
   else if (mt == 2 && kc == 256)
-    launch_maybe_early(wstream_gemm_kernel<2, 256, true, 1, true>, grid, dim3(256), st, early, X, ldx, wt, M, N, K, ks,
-                       ny, (int64_t)0, P, 0, ra, 1, gt);
+    wstream_gemm_kernel<2, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1, gt);
   else if (mt == 4 && kc == 128)
-    launch_maybe_early(wstream_gemm_kernel<4, 128, true, 1, true>, grid, dim3(256), st, early, X, ldx, wt, M, N, K, ks,
-                       ny, (int64_t)0, P, 0, ra, 1, gt);
+    wstream_gemm_kernel<4, 128, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1, gt);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

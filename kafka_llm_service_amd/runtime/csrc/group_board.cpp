@@ -140,11 +140,12 @@ class GroupBoard {
     return out;
   }
 
-  void wake() { h_->wake.fetch_add(1, std::memory_order_acq_rel); }
-  uint64_t wake_count() const { return h_->wake.load(std::memory_order_acquire); }
+  void wake() { live().wake.fetch_add(1, std::memory_order_acq_rel); }
+  uint64_t wake_count() const { return live().wake.load(std::memory_order_acquire); }
 
   // sleep until the wake counter differs from `seen` or `timeout_s` passed; returns the counter
   uint64_t wait_wake(uint64_t seen, double timeout_s) {
+    live();
     py::gil_scoped_release nogil;
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
@@ -158,9 +159,14 @@ class GroupBoard {
   }
 
   int rank() const { return rank_; }
-  int nranks() const { return (int)h_->nranks; }
+  int nranks() const { return (int)live().nranks; }
 
  private:
+  BoardHeader& live() const {
+    if (h_ == nullptr) throw std::runtime_error("GroupBoard: closed");
+    return *h_;
+  }
+
   template <class Pred>
   static void wait(Pred ready, double timeout_s, const std::atomic<int64_t>* pid, const char* what) {
     if (ready()) return;

@@ -14,5 +14,7 @@ done
 for v in 3 4; do
   KAFKA_TILE_SLOTS=$v timeout -k 10 200 python -u benchmarks/attn_tile_anatomy.py --variants 3 --keys 576,1152 2>&1 | grep keys_per | sed "s/^/slots$v /" || exit 1
 done
-KAFKA_TILE_SLOTS=4 KAFKA_EARLY=1 timeout -k 10 300 python bench.py --steps 200 --warmup 20 > gpurun_out/bench_slots4.log 2>&1 || { tail -20 gpurun_out/bench_slots4.log; exit 1; }
-tail -1 gpurun_out/bench_slots4.log | cut -c1-150
+for cfg in "KAFKA_TILE_SLOTS=4 KAFKA_EARLY=1" "KAFKA_CASCADE_WGS=128 KAFKA_EARLY=1" "KAFKA_CASCADE_WGS=192 KAFKA_EARLY=1" "KAFKA_CASCADE_WGS=128 KAFKA_EARLY=0"; do
+  env $cfg timeout -k 10 300 python bench.py --steps 200 --warmup 20 > gpurun_out/bench_cfg.log 2>&1 || { tail -20 gpurun_out/bench_cfg.log; exit 1; }
+  echo "$cfg $(tail -1 gpurun_out/bench_cfg.log | cut -c1-150)"
+done
