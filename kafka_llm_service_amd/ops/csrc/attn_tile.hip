@@ -251,17 +251,24 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
   // holds its column's sum ones . P: 8 MFMAs per tile instead of 64 adds); the running max m (exp2 domain).
   // (Folding -m into the QK^T accumulator init would save the per-score FMA too, but needs Q prescaled by
   // scale * log2(e) in bf16: +0.4 % relative score error, 0.037 abs on a peaked row vs 0.02 tolerance — rejected.)
+  // HALF (RB == 2, one wave per SIMD with 64 rows): the 512-register budget has no room for both 32-key halves'
+  // scores and an MFMA row-sum accumulator per block (the straight port spilled 122 VGPRs), so each half runs its own
+  // online-softmax step and the row sums are VALU adds (one float per row block).
+  constexpr bool HALF = RB == 2;
   f32x16 o[RB][D / 32], ls[RB];
-  float m[RB];
+  float m[RB], lsum[RB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
     for (int t = 0; t < D / 32; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) o[rb][t][i] = 0.f;
+    if constexpr (!HALF) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) ls[rb][i] = 0.f;
+      for (int i = 0; i < 16; ++i) ls[rb][i] = 0.f;
+    }
     m[rb] = -INFINITY;
+    lsum[rb] = 0.f;
   }
   bf16x8 ones;
 #pragma unroll
@@ -281,11 +288,95 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
     st_last = t;
   };
 
+  // ---- HALF: one 32-key half (kb) of a tile as its own online-softmax step
+  auto half_body = [&](auto masked_c, const char* Ks, const char* Vs, int kb, int key0) {
+    constexpr bool MASKED = decltype(masked_c)::value;
+    f32x16 s[RB];
+    {
+      bf16x8 kf[D / 16];
+#pragma unroll
+      for (int kk = 0; kk < D / 16; ++kk)
+        kf[kk] = *reinterpret_cast<const bf16x8*>(Ks + (2 * kb + (r >> 4)) * 4096 + ((2 * kk + h) * 16 + (r & 15)) * 16);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        f32x16 acc = {};
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) acc = mfma32(kf[kk], qf[rb][kk], acc);
+        s[rb] = acc;
+      }
+    }
+    if constexpr (MASKED) {
+      const int k0 = key0 + 32 * kb;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+        if ((k0 < lo) | (k0 + 32 > hi_b[rb]) | (k0 + 31 > wmin_b[rb])) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = k0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (!((key >= lo) & (key < hi_b[rb]) & (key <= limit[rb]))) s[rb][i] = -INFINITY;
+          }
+        }
+    }
+    float smax[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      float mx = s[rb][0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[rb][i]);
+      smax[rb] = t3_xor32_max(mx) * scale_log2;
+    }
+    bool need = false;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) need = need | !(smax[rb] <= m[rb] + THR);
+    if (__any(need)) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        const float mn = fmaxf(m[rb], smax[rb]);
+        const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m[rb] - mn);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) o[rb][t] *= alpha;
+        lsum[rb] *= alpha;
+        m[rb] = mn;
+      }
+    }
+    bf16x8 vf[2][D / 32];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int t = 0; t < D / 32; ++t) {
+        const int d = 32 * t + r;
+        vf[s2][t] = *reinterpret_cast<const bf16x8*>(Vs + (2 * kb + s2) * 4096 + d * 32 + 16 * (h ^ ((d >> 3) & 1)));
+      }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const float mu = (m[rb] == -INFINITY) ? 0.f : m[rb];
+      bf16x8 pf[2];
+      float psum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float x = fmaf(s[rb][i], scale_log2, -mu);
+        const bf16 p = (bf16)(ABL == 2 ? x : exp2f(x));
+        pf[i >> 3][i & 7] = p;
+        psum += (float)p;  // the rounded value the PV product uses
+      }
+      lsum[rb] += t3_xor32_sum(psum);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) o[rb][t] = mfma32(vf[s2][t], pf[s2], o[rb][t]);
+    }
+  };
+
   // ---- one 64-key tile (processing index j) from ring slot j % NSLOT
   auto tile_body = [&](auto masked_c, int j, int key0) {
     constexpr bool MASKED = decltype(masked_c)::value;
     const char* Ks = smem + (j % NSLOT) * SLOT;  // [page 4][plane 16][key 16][16 B]
     const char* Vs = Ks + KBYTES;                // [page 4][d 128][2 x 16 B] (halves swapped on rows 8..15 of 16)
+    if constexpr (HALF) {
+      half_body(masked_c, Ks, Vs, 0, key0);
+      half_body(masked_c, Ks, Vs, 1, key0);
+      return;
+    }
     // S^T = K . Q^T for both 32-key halves (kb) and both row blocks
     f32x16 s[RB][2];
 #pragma unroll
@@ -433,7 +524,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     if (!__any(valid[rb])) continue;  // wave-uniform
-    const float ll = fits ? ls[rb][0] : __builtin_nanf("");
+    const float ll = fits ? (HALF ? lsum[rb] : ls[rb][0]) : __builtin_nanf("");
     const float inv = ll > 0.f ? 1.f / ll : (fits ? 0.f : ll);
     if (ABL != 8 && part && valid[rb] && h == 0)
       lse_part[((int64_t)token[rb] * Hq + head[rb]) * S_total + it.split] =
