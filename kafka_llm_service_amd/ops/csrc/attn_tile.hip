@@ -144,9 +144,9 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
     token[rb] = it.q_start + tok;
     head[rb] = kvh * G + R % G;
   }
-  // prologue loads that depend only on the work item go out TOGETHER (one round trip instead of a chain of three):
-  // the item's page ids, the causal limits and the Q fragments (B operand of S^T = K . Q^T: lane (r, h) holds
-  // Q[row r][16 kk + 8 h + j])
+  // prologue loads that depend only on the work item go out together (one round trip): the item's page ids and the
+  // causal limits; Q fragments (B operand of S^T = K . Q^T: lane (r, h) holds Q[row r][16 kk + 8 h + j]) follow the
+  // first DMAs
   const int lo0 = it.kv_lo;
   const int pg00 = (lo0 & ~63) >> 4;
   const int npg_all0 = ((it.kv_hi + 15) >> 4) - pg00;
@@ -177,8 +177,9 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
       }
     }
   };
-  // early-launched cascade (common.h Gates): the prefix K/V (written by earlier steps) streams in before q exists
-  if constexpr (!GATED) load_q();
+  // (Q fragments are loaded after the first K/V tiles' DMAs are issued: those are the critical path — Q loads issued
+  // ahead of them delayed the first tile, -0.6 % on the headline, profiles/r04/bench_ab_tile_prologue.jsonl; the
+  // early-launched cascade (common.h Gates) additionally waits for q's producer first)
   // per-block wave-uniform bounds: keys past hi_b are masked for every row of the block, keys <= wmin_b for none
   int hi_b[2], wmin_b[2];  // (RB == 1: block 1 mirrors block 0)
 #pragma unroll
@@ -242,10 +243,8 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
 #pragma unroll
   for (int j = 0; j < NSLOT - 1; ++j)
     if (j < ntiles) issue(j);
-  if constexpr (GATED) {
-    gate_wait(gt.wait, gt.mode);
-    load_q();
-  }
+  if constexpr (GATED) gate_wait(gt.wait, gt.mode);
+  load_q();
 
   // Running state per row block: O^T accumulators; row sums `ls` as an MFMA accumulator (every register of a lane
   // holds its column's sum ones . P: 8 MFMAs per tile instead of 64 adds); the running max m (exp2 domain).
@@ -289,7 +288,8 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
   };
 
   // ---- HALF: one 32-key half (kb) of a tile as its own online-softmax step
-  auto half_body = [&](auto masked_c, const char* Ks, const char* Vs, int kb, int key0) {
+  // (always inlined: a call would put the closure's register arrays — o, q, m — in scratch memory)
+  auto half_body = [&](auto masked_c, const char* Ks, const char* Vs, int kb, int key0) __attribute__((always_inline)) {
     constexpr bool MASKED = decltype(masked_c)::value;
     f32x16 s[RB];
     {
