@@ -283,7 +283,9 @@ class TransformerLM:
                 pass  # the previous layer's overlapped down seam already wrote residual and x
             elif delta is None:
                 ops.rmsnorm(h, lw.input_norm, eps, out=x)
-                residual = h.clone()
+                # the embedding is a fresh tensor at TP = 1 (the residual stream can own it); under TP it may be the
+                # all-reduce's persistent buffer
+                residual = h if self.tp == 1 else h.clone()
             elif pending:
                 pstate.tp_all_reduce_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x)
             else:
