@@ -373,6 +373,7 @@ STREAM_KERNEL_MAX_M = 256
 
 
 _WSTREAM_TARGET = int(os.environ.get("KAFKA_WSTREAM_TARGET", "0"))  # A/B override of the split target (both sides)
+_WSTREAM_MT3 = os.environ.get("KAFKA_WSTREAM_MT3", "1") != "0"  # 65..96 rows on three row tiles (csrc mt3_off)
 
 
 def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, int] | None:
@@ -380,7 +381,7 @@ def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, 
     kafka_wstream_plan in csrc/wstream_gemm.hip, mirrored so CPU runs take the same split decisions)."""
     if M < 1 or M > STREAM_KERNEL_MAX_M or N % 32 or N <= 0:
         return None
-    mt = 1 if M <= 32 else (2 if M <= 64 else 4)
+    mt = 1 if M <= 32 else (2 if M <= 64 else (3 if M <= 96 and _WSTREAM_MT3 else 4))
     kc = 128 if mt == 4 else 256
     if K % kc or K <= 0:
         return None

@@ -426,7 +426,7 @@ def test_wstream_grouped(cuda, T, d, F, E, e_lo, e_n):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("M", [1, 7, 32, 33, 64, 65, 128, 129, 200, 256])
+@pytest.mark.parametrize("M", [1, 7, 32, 33, 64, 65, 80, 96, 97, 128, 129, 200, 256])
 @pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1280, 8192), (16032, 1024), (96, 512)])
 def test_wstream_gemm(cuda, M, N, K):
     """Weight-streaming decode GEMM on wave-tiled weights (bf16 direct and split-K slabs) vs fp32 matmul."""
@@ -447,7 +447,7 @@ def test_wstream_gemm(cuda, M, N, K):
         torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("M", [1, 40, 64, 100, 168, 256])
+@pytest.mark.parametrize("M", [1, 40, 64, 80, 100, 168, 256])
 @pytest.mark.parametrize("N,K", [(28672, 4096), (7168, 8192), (2048, 1024)])
 def test_wstream_glu(cuda, M, N, K):
     """GLU-tiled gate_up: fused silu(gate) * up epilogue (one split) and de-interleaved gate | up slabs (split plans)
@@ -568,7 +568,8 @@ def test_attn_merge_ignores_unwritten_slots(cuda):
     _close(out, ref_out, atol=0.02, msg="merge with unwritten slots")
 
 
-@pytest.mark.parametrize("M,Hq,Hkv,K", [(1, 32, 8, 4096), (17, 32, 8, 4096), (64, 32, 8, 4096), (100, 32, 8, 4096),
+@pytest.mark.parametrize("M,Hq,Hkv,K", [(1, 32, 8, 4096), (17, 32, 8, 4096), (64, 32, 8, 4096), (90, 32, 8, 4096),
+                                        (100, 32, 8, 4096),
                                         (128, 32, 8, 4096), (48, 8, 1, 1024)])
 def test_wstream_qkv_rope(cuda, M, Hq, Hkv, K):
     """QKV streaming GEMM with RoPE + the paged KV write in its epilogue (split-K tickets) vs the fp32 reference of
