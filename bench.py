@@ -489,6 +489,7 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
         "preemptions": eng.sched.num_preemptions,
         "planned_ahead_frac": round(eng.stats.get("planned_ahead", 0) / max(1, eng.stats.get("steps", 1)), 4),
         "planned_late_frac": round(eng.stats.get("planned_late", 0) / max(1, eng.stats.get("steps", 1)), 4),
+        "step_rows_hist": dict(zip(("<=64", "65-96", "97-128", "129-256", ">256"), eng.runner.rows_hist)),
         "grammar_rollbacks": eng.stats.get("grammar_rollbacks", 0),
     }
     if rank == 0:

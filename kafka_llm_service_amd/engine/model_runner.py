@@ -9,6 +9,8 @@ batches run eagerly.
 """
 from __future__ import annotations
 
+import bisect
+
 import math
 import os
 from collections import deque
@@ -158,6 +160,7 @@ MIN_DECODE_KEYS = 256      # smallest key range of one decode work item
 # 1,344 with the decode kernel at three workgroups per CU (768 slots): 1,152 was +1.6 % over 768 and 1,344 another
 # +0.2-0.4 % over 1,152, same boxes (profiles/r03/decode_occ3/decode_target_ab_*.jsonl; 768 was best at two per CU,
 # profiles/r02/decode_items_ab.jsonl)
+ROWS_BUCKETS = (64, 96, 128, 256, 1 << 30)  # step-size histogram buckets (decode GEMM row-tile plans, skinny, BLAS)
 DECODE_TARGET_ITEMS = int(os.environ.get("KAFKA_DECODE_TARGET", "1344"))
 MAX_PARTIALS = 64           # partial slots per row that the decode kernel's fused merge reads (one lane each)
 MAX_PREFIX_CHUNKS = 32
@@ -402,6 +405,7 @@ class ModelRunner:
         self._pin = pin
         self.last_stats: dict = {}
         self.recent_stats: deque = deque(maxlen=16)  # stats of the last launched steps (two can be in flight)
+        self.rows_hist = [0] * len(ROWS_BUCKETS)  # launched steps by token rows (ROWS_BUCKETS upper bounds)
         self.broadcast = None  # set on a TP leader: callable(HostStep, SampleParams) (engine/tp_worker.py)
         self._tok_host = None  # pinned landing buffers of the sampled ids
         self._err_host = None  # pinned landing slots of the custom all-reduce error word (TP)
@@ -731,6 +735,7 @@ class ModelRunner:
             host.i64 = np.concatenate([host.i64, np.asarray(late_dst + late_src, dtype=np.int64)])
         self.last_stats = host.stats
         self.recent_stats.append(host.stats)
+        self.rows_hist[bisect.bisect_left(ROWS_BUCKETS, host.T)] += 1
         sp = self.sample_params(sample_seqs)
         self.stager.begin()
         if self.broadcast is not None:  # TP leader: followers run the same step on their shards
