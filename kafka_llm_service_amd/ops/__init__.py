@@ -374,6 +374,7 @@ STREAM_KERNEL_MAX_M = 256
 
 _WSTREAM_TARGET = int(os.environ.get("KAFKA_WSTREAM_TARGET", "0"))  # A/B override of the split target (both sides)
 _WSTREAM_MT3 = os.environ.get("KAFKA_WSTREAM_MT3", "1") != "0"  # 65..96 rows on three row tiles (csrc mt3_off)
+_WSTREAM_MT4_KC256 = os.environ.get("KAFKA_WSTREAM_MT4_KC", "") == "256"  # A/B (csrc mt4_kc256)
 
 
 def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, int] | None:
@@ -382,7 +383,7 @@ def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, 
     if M < 1 or M > STREAM_KERNEL_MAX_M or N % 32 or N <= 0:
         return None
     mt = 1 if M <= 32 else (2 if M <= 64 else (3 if M <= 96 and _WSTREAM_MT3 else 4))
-    kc = 128 if mt == 4 else 256
+    kc = 128 if mt == 4 and not _WSTREAM_MT4_KC256 else 256
     if K % kc or K <= 0:
         return None
     nx, chunks, s = (N + 127) // 128 * ((M + 127) // 128), K // kc, 1

@@ -515,12 +515,20 @@ static bool mt3_off() {  // KAFKA_WSTREAM_MT3=0: 65..96 rows on the four-tile ke
   return off;
 }
 
+static bool mt4_kc256() {  // KAFKA_WSTREAM_MT4_KC=256: four row tiles on 256-deep chunks (128 KB X stage; A/B)
+  static const bool on = [] {
+    const char* e = getenv("KAFKA_WSTREAM_MT4_KC");
+    return e != nullptr && atoi(e) == 256;
+  }();
+  return on;
+}
+
 extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits) {
   if (M < 1 || M > 256 || N % 32 != 0 || N <= 0) return 1;
   // 65..96 rows (a decode batch plus a short new-turn chunk): three 32-row tiles on 256-deep chunks (96 KB X stage)
   // instead of four on 128-deep ones
   const int MT = M <= 32 ? 1 : (M <= 64 ? 2 : (M <= 96 && !mt3_off() ? 3 : 4));
-  const int KC = MT == 4 ? 128 : 256;
+  const int KC = MT == 4 && !mt4_kc256() ? 128 : 256;
   if (K % KC != 0 || K <= 0) return 2;
   const int nx = (N + 127) / 128 * ((M + 127) / 128);  // workgroups per split (row tiles beyond 128 rows)
   const int chunks = K / KC;
@@ -576,6 +584,7 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   else if (mt == 2 && kc == 256 && kw == 1) KAFKA_WS(2, 256, 1);
   else if (mt == 2 && kc == 256 && kw == 2) KAFKA_WS(2, 256, 2);
   else if (mt == 3 && kc == 256 && kw == 1) KAFKA_WS(3, 256, 1);
+  else if (mt == 4 && kc == 256 && kw == 1) KAFKA_WS(4, 256, 1);
   else if (mt == 4 && kc == 128 && kw == 1) KAFKA_WS(4, 128, 1);
   else if (mt == 4 && kc == 128 && kw == 2) KAFKA_WS(4, 128, 2);
   else return hipErrorInvalidValue;
@@ -605,6 +614,8 @@ extern "C" hipError_t kafka_launch_wstream_qkv_rope(const bf16* X, int64_t ldx, 
     wstream_gemm_kernel<2, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1, gt);
   else if (mt == 3 && kc == 256)
     wstream_gemm_kernel<3, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1, gt);
+  else if (mt == 4 && kc == 256)
+    wstream_gemm_kernel<4, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1, gt);
   else if (mt == 4 && kc == 128)
     wstream_gemm_kernel<4, 128, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1, gt);
   else
