@@ -328,6 +328,7 @@ def main(argv=None):
     if dev.startswith("cuda"):
         torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
+    eng.runner.rows_hist = [0] * len(eng.runner.rows_hist)  # the histogram covers the warm-up + timed steps only
 
     req_thread = {}
     n_tool = int(round(args.tool_frac * args.threads))
