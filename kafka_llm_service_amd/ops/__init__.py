@@ -375,6 +375,7 @@ STREAM_KERNEL_MAX_M = 256
 _WSTREAM_TARGET = int(os.environ.get("KAFKA_WSTREAM_TARGET", "0"))  # A/B override of the split target (both sides)
 _WSTREAM_MT3 = os.environ.get("KAFKA_WSTREAM_MT3", "1") != "0"  # 65..96 rows on three row tiles (csrc mt3_off)
 _WSTREAM_MT4_KC256 = os.environ.get("KAFKA_WSTREAM_MT4_KC", "") == "256"  # A/B (csrc mt4_kc256)
+_WSTREAM_ROWSPLIT = os.environ.get("KAFKA_WSTREAM_ROWSPLIT", "0") == "1"  # 64-row tiles sharing L2 (csrc rowsplit_on)
 
 
 def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, int] | None:
@@ -382,11 +383,12 @@ def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, 
     kafka_wstream_plan in csrc/wstream_gemm.hip, mirrored so CPU runs take the same split decisions)."""
     if M < 1 or M > STREAM_KERNEL_MAX_M or N % 32 or N <= 0:
         return None
-    mt = 1 if M <= 32 else (2 if M <= 64 else (3 if M <= 96 and _WSTREAM_MT3 else 4))
+    mt = 2 if _WSTREAM_ROWSPLIT and M > 64 else \
+        (1 if M <= 32 else (2 if M <= 64 else (3 if M <= 96 and _WSTREAM_MT3 else 4)))
     kc = 128 if mt == 4 and not _WSTREAM_MT4_KC256 else 256
     if K % kc or K <= 0:
         return None
-    nx, chunks, s = (N + 127) // 128 * ((M + 127) // 128), K // kc, 1
+    nx, chunks, s = (N + 127) // 128 * ((M + 32 * mt - 1) // (32 * mt)), K // kc, 1
     target = _WSTREAM_TARGET or (256 if mt == 4 else 192)
     while s * 2 <= max_splits and s * 2 <= 8 and chunks % (s * 2) == 0 and nx * s < target:
         s *= 2

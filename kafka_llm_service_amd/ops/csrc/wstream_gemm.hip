@@ -65,9 +65,24 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ct = w & 3, kh = w >> 2;  // column tile of the workgroup, K part of the chunk
   const int r = lane & 31, h = lane >> 5;
-  // row tiles (M > 32 MT): the row_tiles workgroups of one weight slice are consecutive in dispatch order, so the
+  // row tiles (M > 32 MT): the row_tiles workgroups of one weight slice are placed on ONE XCD — workgroups b, b + 8,
+  // ... under round-robin placement (blockIdx.x % 8 picks the XCD) — so the slice streams from HBM once and the other
+  // row tiles read it from that XCD's L2 (the launch pads the column blocks to a multiple of 8; padding workgroups
+  // exit). Previously consecutive in dispatch order (one weight slice on 2 XCDs, shared through the MALL); so the
   // slice is fetched from HBM once and the other row tiles read it back from the MALL; P stays [S][M_total][N]
-  const int cb = blockIdx.x / row_tiles, row0 = (blockIdx.x % row_tiles) * ROWS;
+  int cb = blockIdx.x, rti = 0;
+  if (row_tiles > 1) {
+    const int grp = blockIdx.x / (8 * row_tiles), rem = blockIdx.x % (8 * row_tiles);
+    cb = grp * 8 + rem % 8;
+    rti = rem / 8;
+    if (cb >= (N + 127) / 128) {  // padding workgroup (workgroup-uniform): no work, but a gated launch counts it
+      if constexpr (EARLY) {
+        if (gt.sig != nullptr && threadIdx.x == 0) gate_arrive(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y), gt.mode);
+      }
+      return;
+    }
+  }
+  const int row0 = rti * ROWS;
   const int Mtot = M;
   M = min(ROWS, Mtot - row0);
   X += (int64_t)row0 * ldx;
@@ -515,6 +530,14 @@ static bool mt3_off() {  // KAFKA_WSTREAM_MT3=0: 65..96 rows on the four-tile ke
   return off;
 }
 
+static bool rowsplit_on() {  // mirrored by ops.stream_plan
+  static const bool on = [] {
+    const char* e = getenv("KAFKA_WSTREAM_ROWSPLIT");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 static bool mt4_kc256() {  // KAFKA_WSTREAM_MT4_KC=256: four row tiles on 256-deep chunks (128 KB X stage; A/B)
   static const bool on = [] {
     const char* e = getenv("KAFKA_WSTREAM_MT4_KC");
@@ -527,10 +550,11 @@ extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, 
   if (M < 1 || M > 256 || N % 32 != 0 || N <= 0) return 1;
   // 65..96 rows (a decode batch plus a short new-turn chunk): three 32-row tiles on 256-deep chunks (96 KB X stage)
   // instead of four on 128-deep ones
-  const int MT = M <= 32 ? 1 : (M <= 64 ? 2 : (M <= 96 && !mt3_off() ? 3 : 4));
+  // KAFKA_WSTREAM_ROWSPLIT=1: beyond 64 rows, 64-row tiles whose workgroups share each weight slice in one XCD's L2
+  const int MT = rowsplit_on() && M > 64 ? 2 : (M <= 32 ? 1 : (M <= 64 ? 2 : (M <= 96 && !mt3_off() ? 3 : 4)));
   const int KC = MT == 4 && !mt4_kc256() ? 128 : 256;
   if (K % KC != 0 || K <= 0) return 2;
-  const int nx = (N + 127) / 128 * ((M + 127) / 128);  // workgroups per split (row tiles beyond 128 rows)
+  const int nx = (N + 127) / 128 * ((M + 32 * MT - 1) / (32 * MT));  // workgroups per split (x row tiles)
   const int chunks = K / KC;
   // split until the grid reaches ~192 (MT <= 2) / 256 (MT = 4) workgroups: measured on MI355X
   // (benchmarks/wstream_sweep.py, profiles/wstream_sweep_r01.log) — every extra split adds 2 x M x N x 4 B of slab
@@ -555,8 +579,9 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   if (glu && (N % 64 != 0 || kw != 1)) return hipErrorInvalidValue;
   if (K % (kc * splits) != 0 || (splits > 1 && P == nullptr) || (splits == 1 && P == nullptr && Y == nullptr))
     return hipErrorInvalidValue;
-  const int rt = (M + 32 * mt - 1) / (32 * mt);  // row tiles of 32 * mt rows (M > 128: 2 tiles of 128)
-  const dim3 grid((N + 127) / 128 * rt, splits);
+  const int rt = (M + 32 * mt - 1) / (32 * mt);  // row tiles of 32 * mt rows
+  const int nblk = (N + 127) / 128;
+  const dim3 grid((rt > 1 ? (nblk + 7) / 8 * 8 : nblk) * rt, splits);  // (row tiles: column blocks padded to 8)
   const int ks = K / splits;
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   float* p = splits > 1 ? P : nullptr;
