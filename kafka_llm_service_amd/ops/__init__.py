@@ -378,12 +378,13 @@ _WSTREAM_MT4_KC256 = os.environ.get("KAFKA_WSTREAM_MT4_KC", "") == "256"  # A/B 
 _WSTREAM_ROWSPLIT = os.environ.get("KAFKA_WSTREAM_ROWSPLIT", "0") == "1"  # 64-row tiles sharing L2 (csrc rowsplit_on)
 
 
-def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, int] | None:
+def stream_plan(M: int, N: int, K: int, max_splits: int = 8, one_tile: bool = False) -> tuple[int, int, int] | None:
     """(row tiles, K chunk, splits) of the decode GEMM for a shape, None if unsupported (same rule as
-    kafka_wstream_plan in csrc/wstream_gemm.hip, mirrored so CPU runs take the same split decisions)."""
+    kafka_wstream_plan in csrc/wstream_gemm.hip, mirrored so CPU runs take the same split decisions). ``one_tile``:
+    all rows in one row tile (the fused QKV + RoPE kernel), so the row-split plan does not apply."""
     if M < 1 or M > STREAM_KERNEL_MAX_M or N % 32 or N <= 0:
         return None
-    mt = 2 if _WSTREAM_ROWSPLIT and M > 64 else \
+    mt = 2 if _WSTREAM_ROWSPLIT and not one_tile and M > 64 else \
         (1 if M <= 32 else (2 if M <= 64 else (3 if M <= 96 and _WSTREAM_MT3 else 4)))
     kc = 128 if mt == 4 and not _WSTREAM_MT4_KC256 else 256
     if K % kc or K <= 0:
@@ -476,7 +477,7 @@ def linear_stream_rope(x, wt, positions, cos_sin, q_out, k_cache, v_cache, slot_
     ``rope_kv_write``, without the rope_kv launch (the last split-K workgroup of each head tile finishes it)."""
     M, K = x.shape
     N = wt.shape[0] * 32
-    plan = stream_plan(M, N, K, max_splits)
+    plan = stream_plan(M, N, K, max_splits, one_tile=True)
     if plan is None or N != (Hq + 2 * Hkv) * 128:
         raise ValueError(f"linear_stream_rope: unsupported shape M={M} N={N} K={K}")
     if _gpu(x):

@@ -57,7 +57,7 @@ hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride,
                          const float* top_p, const int* top_k, const int64_t* seeds, const int64_t* step,
                          int64_t* out_tokens, int* ws, int nsplit, const int* proc, const uint32_t* mask_tab,
                          int64_t mask_ld, int* counts, int64_t cnt_ld, hipStream_t st);
-int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits);
+int kafka_wstream_plan(int M, int N, int K, int max_splits, int one_tile, int* mt, int* kc, int* splits);
 hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt, int kc,
                                      int splits, int nt, int kw, int glu, bf16* Y, int64_t ldy, float* P,
                                      Gates gt, hipStream_t st);
@@ -507,7 +507,7 @@ static void sample(at::Tensor logits, c10::optional<at::Tensor> temperature, c10
 // (mt, kc, splits) of the weight-streaming decode GEMM for a shape, or (0, 0, 0) if unsupported
 static std::vector<int64_t> wstream_plan(int64_t M, int64_t N, int64_t K, int64_t max_splits) {
   int mt = 0, kc = 0, s = 0;
-  if (kafka_wstream_plan((int)M, (int)N, (int)K, (int)max_splits, &mt, &kc, &s) != 0) return {0, 0, 0};
+  if (kafka_wstream_plan((int)M, (int)N, (int)K, (int)max_splits, 0, &mt, &kc, &s) != 0) return {0, 0, 0};
   return {mt, kc, s};
 }
 
@@ -525,7 +525,7 @@ static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> 
   TORCH_CHECK(wt.size(1) * 16 == K, "wstream_gemm: K mismatch");
   TORCH_CHECK(!glu || N % 64 == 0, "wstream_gemm: GLU weights need N % 64 == 0");
   int mt = 0, kc = 0, s = 0;
-  TORCH_CHECK(kafka_wstream_plan(M, N, K, (int)max_splits, &mt, &kc, &s) == 0, "wstream_gemm: unsupported shape");
+  TORCH_CHECK(kafka_wstream_plan(M, N, K, (int)max_splits, 0, &mt, &kc, &s) == 0, "wstream_gemm: unsupported shape");
   bf16* yp = nullptr;
   int64_t ldy = 0;
   float* pp = nullptr;
@@ -613,7 +613,7 @@ static void wstream_qkv_rope(at::Tensor x, at::Tensor wt, c10::optional<at::Tens
     sm = slot_mapping->data_ptr<int64_t>();
   }
   int mt = 0, kc = 0, s = 0;
-  TORCH_CHECK(kafka_wstream_plan(M, N, K, (int)max_splits, &mt, &kc, &s) == 0, "wstream_qkv_rope: unsupported shape");
+  TORCH_CHECK(kafka_wstream_plan(M, N, K, (int)max_splits, 1, &mt, &kc, &s) == 0, "wstream_qkv_rope: unsupported shape");
   float* pp = nullptr;
   if (s > 1) {
     TORCH_CHECK(p.has_value(), "wstream_qkv_rope: scratch required for a split plan");

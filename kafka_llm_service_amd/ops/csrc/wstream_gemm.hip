@@ -68,8 +68,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
   // row tiles (M > 32 MT): the row_tiles workgroups of one weight slice are placed on ONE XCD — workgroups b, b + 8,
   // ... under round-robin placement (blockIdx.x % 8 picks the XCD) — so the slice streams from HBM once and the other
   // row tiles read it from that XCD's L2 (the launch pads the column blocks to a multiple of 8; padding workgroups
-  // exit). Previously consecutive in dispatch order (one weight slice on 2 XCDs, shared through the MALL); so the
-  // slice is fetched from HBM once and the other row tiles read it back from the MALL; P stays [S][M_total][N]
+  // exit); P stays [S][M_total][N]
   int cb = blockIdx.x, rti = 0;
   if (row_tiles > 1) {
     const int grp = blockIdx.x / (8 * row_tiles), rem = blockIdx.x % (8 * row_tiles);
@@ -546,12 +545,14 @@ static bool mt4_kc256() {  // KAFKA_WSTREAM_MT4_KC=256: four row tiles on 256-de
   return on;
 }
 
-extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits) {
+// one_tile: the plan must cover all M rows with one row tile (the fused QKV + RoPE kernel: its epilogue's per-head
+// tickets count split-K workgroups of ONE row tile), so KAFKA_WSTREAM_ROWSPLIT does not apply
+extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int one_tile, int* mt, int* kc, int* splits) {
   if (M < 1 || M > 256 || N % 32 != 0 || N <= 0) return 1;
   // 65..96 rows (a decode batch plus a short new-turn chunk): three 32-row tiles on 256-deep chunks (96 KB X stage)
   // instead of four on 128-deep ones
   // KAFKA_WSTREAM_ROWSPLIT=1: beyond 64 rows, 64-row tiles whose workgroups share each weight slice in one XCD's L2
-  const int MT = rowsplit_on() && M > 64 ? 2 : (M <= 32 ? 1 : (M <= 64 ? 2 : (M <= 96 && !mt3_off() ? 3 : 4)));
+  const int MT = rowsplit_on() && !one_tile && M > 64 ? 2 : (M <= 32 ? 1 : (M <= 64 ? 2 : (M <= 96 && !mt3_off() ? 3 : 4)));
   const int KC = MT == 4 && !mt4_kc256() ? 128 : 256;
   if (K % KC != 0 || K <= 0) return 2;
   const int nx = (N + 127) / 128 * ((M + 32 * MT - 1) / (32 * MT));  // workgroups per split (x row tiles)
@@ -625,7 +626,7 @@ extern "C" hipError_t kafka_launch_wstream_qkv_rope(const bf16* X, int64_t ldx, 
                                                    bf16* k_cache, bf16* v_cache, const int64_t* slots, int Hq,
                                                    int Hkv, int* tickets, Gates gt, hipStream_t st) {
   if (M < 1) return hipSuccess;
-  if (M > 128 || N != (Hq + 2 * Hkv) * 128 || K % (kc * splits) != 0 ||
+  if (M > 128 || M > 32 * mt || N != (Hq + 2 * Hkv) * 128 || K % (kc * splits) != 0 ||
       (splits > 1 && (P == nullptr || tickets == nullptr)))
     return hipErrorInvalidValue;
   const dim3 grid(N / 128, splits);
