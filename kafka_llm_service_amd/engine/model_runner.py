@@ -398,6 +398,8 @@ class ModelRunner:
         self.cascade_bf16 = self.variant == 3 and os.environ.get("KAFKA_CASCADE_BF16", "1") != "0"
         self.cascade_min_prefix = cascade_min_prefix
         self.target_wgs = int(os.environ.get("KAFKA_CASCADE_WGS", target_wgs))
+        # workgroups of the cascade's prefix pass alone (KAFKA_PREFIX_WGS; fewer leave CUs to an overlapped decode)
+        self.prefix_wgs = int(os.environ.get("KAFKA_PREFIX_WGS", self.target_wgs))
         self.prefill_kv_chunk = int(os.environ.get("KAFKA_PREFILL_KV_CHUNK", prefill_kv_chunk))
         self.use_cascade = use_cascade
         self.vocab = model.cfg.vocab_size
@@ -505,7 +507,7 @@ class ModelRunner:
             if groups:
                 # key chunks sized so the prefix pass launches ~target_wgs workgroups over all groups together
                 work = sum(-(-n // self.tile) * p * PAGE for n, p in groups)
-                want = max(1, self.target_wgs // self.model.hkv)
+                want = max(1, self.prefix_wgs // self.model.hkv)
                 chunk = min(MAX_ITEM_KEYS, max(256, -(-work // (want * 32)) * 32))
                 r0 = 0
                 for n, p in groups:

@@ -86,7 +86,8 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     """q [T, Hq, D] (post-RoPE) -> out [T, Hq, D] bf16. ``gates`` = (ops.GateSet, gate id the q / KV writer arrives
     on) on an early-launched decode-only step (models/llama.py EARLY): the cascade streams its prefix K/V before q is
     ready, the suffix decode runs beside it and waits for its partials only before the merge. Returns the gate the
-    decode arrives on (-1: none)."""
+    decode arrives on (-1: none). With ``(GateSet, -1)`` (models/llama.py ATTN_OVERLAP) only the decode is launched
+    early: it runs beside the cascade and waits for the cascade's partials before its merge."""
     B = meta.num_decode
     gs, g_in = gates if gates is not None else (None, -1)
     has_prefill = meta.prefill_items is not None and meta.num_tokens > B
@@ -115,7 +116,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
             ops.attn_decode_sk(qd, k_cache, v_cache, meta.block_tables, meta.decode_sk_rows, meta.decode_sk_start,
                                meta.part, meta.lse, meta.scale, out=out[:B], pre_part=meta.pre_part)
         else:
-            if gs is not None:
+            if gs is not None and g_in >= 0:  # (g_in = -1: only the cascade -> decode overlap is gated)
                 g_out = gs.new()
             ops.attn_decode_items(qd, k_cache, v_cache, meta.block_tables, meta.decode_items, meta.part, meta.lse,
                                   meta.scale, out=out[:B], pre_part=meta.pre_part,

@@ -64,6 +64,14 @@ SKINNY = frozenset(p for p in os.environ.get("KAFKA_SKINNY", "qkv,o,down").repla
 # and waits for the cascade's partials only before its merge. The two post-attention / post-MLP RMSNorms stay ordinary
 # launches (full barriers), so each chain is short and every gate waits on the kernel launched right before it.
 EARLY = os.environ.get("KAFKA_EARLY", "0") == "1"
+# Overlapped attention (env KAFKA_ATTN_OVERLAP): only the suffix decode is launched without the barrier bit, so its
+# workgroups take the CUs the cascade's ~256 tile workgroups leave free (and each CU a tile workgroup finishes)
+# instead of waiting for the cascade's last one; it waits for the cascade's partials (a write-through hand-off:
+# no release / acquire fences, csrc/common.h st_wt16) only before its merge.
+ATTN_OVERLAP = os.environ.get("KAFKA_ATTN_OVERLAP", "0") == "1"
+# gate_up of steps up to this many rows on the streaming kernel (two XCD-shared row tiles beyond 128) instead of
+# hipBLASLt + silu_mul (env KAFKA_STREAM_GU_MAX_M; 0 = the model's stream_max_m)
+STREAM_GU_MAX_M = min(256, int(os.environ.get("KAFKA_STREAM_GU_MAX_M", "0")))
 _OVL: dict = {}
 _SEAM_DONE = object()  # forward(): the previous layer's overlapped seam already produced this layer's input
 
@@ -130,6 +138,8 @@ class TransformerLM:
         self.stream_max_m = ops.STREAM_MAX_M  # rows up to which a step's projections stream
         self.early = EARLY  # early-launched decode layers (see EARLY)
         self._gates: ops.GateSet | None = None
+        self.attn_overlap = ATTN_OVERLAP
+        self._agates: ops.GateSet | None = None  # the overlapped attention's gates (one per layer)
 
     def enable_dp_attention(self, ep: int, ep_rank: int) -> None:
         """Data-parallel attention for a MoE model (call before the weights are created): attention, norms and the
@@ -238,6 +248,20 @@ class TransformerLM:
         self._gates.begin()
         return self._gates
 
+    def _attn_gateset(self, inp: StepInput, k_cache: torch.Tensor) -> "ops.GateSet | None":
+        """The forward's attention gates when the suffix decode overlaps the cascade (ATTN_OVERLAP), else None."""
+        m = inp.attn
+        if not (self.attn_overlap and self.device.type == "cuda" and m.num_decode > 0):
+            return None
+        if m.prefix_items is None or m.variant != 3 or m.decode_items is None or m.decode_sk_rows is not None:
+            return None
+        if k_cache.dtype != torch.bfloat16 or torch.cuda.is_current_stream_capturing():
+            return None
+        if self._agates is None:
+            self._agates = ops.GateSet(self.device, len(self.layers) + 8)
+        self._agates.begin()
+        return self._agates
+
     @staticmethod
     def _dense(w: torch.Tensor | None, wt: torch.Tensor | None, glu: bool = False) -> torch.Tensor:
         """The row-major weight for hipBLASLt: the stored one, or (tiled-only mode) a transient untiled copy."""
@@ -265,6 +289,7 @@ class TransformerLM:
         fuse_rope = (self.stream and FUSE_QKV_ROPE and 0 < T <= min(128, self.stream_max_m) and self.layers[0].qkv_t is not None
                      and ops.qkv_rope_fusable(k_caches[0], self.D))
         gs = self._gateset(T, inp, k_caches[0], fuse_rope)
+        ga = self._attn_gateset(inp, k_caches[0]) if gs is None else None
         # gate_up + down gated only with the one-split (fused SwiGLU) plan: a split plan puts silu_mul between them
         glu_gated = gs is not None and self.layers[0].glu and \
             (ops.stream_plan(T, self.layers[0].gate_up_t.shape[0] * 32, cfg.hidden_size) or (0, 0, 0))[2] == 1
@@ -302,7 +327,7 @@ class TransformerLM:
                 ops.rope_kv_write(qkv, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i], inp.slot_mapping,
                                   self.hq, self.hkv, gates=G(wait=g_qkv, sig=g_rope))
             g_attn = paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out,
-                                     gates=(gs, g_rope) if gs is not None else None)
+                                     gates=(gs, g_rope) if gs is not None else ((ga, -1) if ga is not None else None))
             if gs is not None:  # the O projection streams its first weight chunk beside the decode's tail
                 g_o = new()
                 o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t, kind="o", gates=G(wait=g_attn, sig=g_o))
@@ -329,7 +354,7 @@ class TransformerLM:
                 delta = self._linear(a, lw.down, lw.down_t, kind="down", gates=G(wait=g_gu, sig=g_down))
                 pending = False
             else:
-                if self.stream and lw.glu and 0 < T <= self.stream_max_m:
+                if self.stream and lw.glu and 0 < T <= max(self.stream_max_m, STREAM_GU_MAX_M):
                     a = ops.linear_glu(x, lw.gate_up_t)  # SwiGLU in the GEMM epilogue (or on its slabs)
                 else:
                     a = ops.silu_mul(F.linear(x, self._dense(lw.gate_up, lw.gate_up_t, bool(lw.glu))))

@@ -341,6 +341,29 @@ struct DecodeSmem {
   int s_last;
 };
 
+// prefix-partial loads of the merges: plain, or agent-coherent (sc1) when the cascade overlaps this kernel (GATED)
+template <bool WT>
+__device__ __forceinline__ bf16x4 ld_pre8(const bf16* p) {
+  if constexpr (WT)
+    return __builtin_bit_cast(bf16x4, ld_wt8(p));
+  else
+    return *reinterpret_cast<const bf16x4*>(p);
+}
+template <bool WT>
+__device__ __forceinline__ f32x4 ld_pre16(const float* p) {
+  if constexpr (WT)
+    return ld_wt16(p);
+  else
+    return *reinterpret_cast<const f32x4*>(p);
+}
+// wait for a group of inline-asm loads; the empty asm statements pin every use of v after the wait
+template <typename T, int N>
+__device__ __forceinline__ void wt_landed(T (&v)[N]) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int j = 0; j < N; ++j) asm volatile("" : "+v"(v[j]));
+}
+
 // One decode piece: keys [lo, hi) of row b, kv head kvh, piece `split` of S, partial slots from split_offset. Every
 // thread of the workgroup calls it with the same arguments (it synchronises the workgroup); returns when the
 // piece's partial or final rows are written.
@@ -438,7 +461,8 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     // Phase 1: wave w owns heads w, w + 4: lanes load the prefix lse values in parallel, wave-reduce the max and
     // the weight sum, and publish per-split weights in LDS. Phase 2: thread (g, 4 dims) sums weight x partial over
     // the splits with all loads of a group of 8 in flight.
-    if constexpr (GATED) gate_wait(gt.wait2, gt.mode);  // early-launched beside the cascade: its partials are in
+    // early-launched beside the cascade: its partials are in (write-through hand-off: relaxed wait, sc1 loads)
+    if constexpr (GATED) gate_wait(gt.wait2, gt.mode | 1);
     for (int g = w; g < G; g += 4) {
       float Ms = -INFINITY;
 #pragma unroll
@@ -450,7 +474,14 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
       }
       const float ls = Ls > 0.f ? Ms + log2f(Ls) : -INFINITY;
       const int64_t pbase = ((int64_t)b * Hq + kvh * G + g) * S_total;
-      const float lv = lane < split_offset ? lse_part[pbase + lane] : (lane == split_offset ? ls : -INFINITY);
+      float lp = -INFINITY;
+      if (lane < split_offset) {
+        if constexpr (GATED)
+          lp = __hip_atomic_load(lse_part + pbase + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          lp = lse_part[pbase + lane];
+      }
+      const float lv = lane < split_offset ? lp : (lane == split_offset ? ls : -INFINITY);
       float mx = lv;
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
@@ -487,7 +518,8 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
         for (; s2 + MG <= split_offset; s2 += MG) {
           bf16x4 v[MG];
 #pragma unroll
-          for (int j = 0; j < MG; ++j) v[j] = *reinterpret_cast<const bf16x4*>(pb + (s2 + j) * D);
+          for (int j = 0; j < MG; ++j) v[j] = ld_pre8<GATED>(pb + (s2 + j) * D);
+          if constexpr (GATED) wt_landed(v);
 #pragma unroll
           for (int j = 0; j < MG; ++j) {
             const float wj = sW[g][s2 + j];
@@ -495,19 +527,25 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
           }
         }
         for (; s2 < split_offset; ++s2) {
-          const bf16x4 v = *reinterpret_cast<const bf16x4*>(pb + s2 * D);
-          acc4 += f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]} * sW[g][s2];
+          bf16x4 v[1] = {ld_pre8<GATED>(pb + s2 * D)};
+          if constexpr (GATED) wt_landed(v);
+          acc4 += f32x4{(float)v[0][0], (float)v[0][1], (float)v[0][2], (float)v[0][3]} * sW[g][s2];
         }
       } else {
         const float* pp = out_part + pbase;
         for (; s2 + MG <= split_offset; s2 += MG) {
           f32x4 v[MG];
 #pragma unroll
-          for (int j = 0; j < MG; ++j) v[j] = *reinterpret_cast<const f32x4*>(pp + (s2 + j) * D);
+          for (int j = 0; j < MG; ++j) v[j] = ld_pre16<GATED>(pp + (s2 + j) * D);
+          if constexpr (GATED) wt_landed(v);
 #pragma unroll
           for (int j = 0; j < MG; ++j) acc4 += v[j] * sW[g][s2 + j];
         }
-        for (; s2 < split_offset; ++s2) acc4 += *reinterpret_cast<const f32x4*>(pp + s2 * D) * sW[g][s2];
+        for (; s2 < split_offset; ++s2) {
+          f32x4 v[1] = {ld_pre16<GATED>(pp + s2 * D)};
+          if constexpr (GATED) wt_landed(v);
+          acc4 += v[0] * sW[g][s2];
+        }
       }
       const float inv = sWt[g] > 0.f ? 1.f / sWt[g] : 0.f;
       bf16x4 o4;
@@ -561,7 +599,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   }
   __syncthreads();
   if (!sm.s_last) return;
-  if constexpr (GATED) gate_wait(gt.wait2, gt.mode);
+  if constexpr (GATED) gate_wait(gt.wait2, gt.mode | 1);  // write-through hand-off (see the fused merge)
   auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   // 16-B agent-coherent loads (sc1: not served from this XCD's possibly stale L2); inline asm, so the group below
   // waits for them itself
@@ -590,11 +628,12 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
     const float* pp = out_part + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
     int s0 = 0;
-    if (pre_bf16 != nullptr) {  // the cascade's bf16 prefix partials (written by an earlier kernel: plain loads)
+    if (pre_bf16 != nullptr) {  // the cascade's bf16 prefix partials (an earlier kernel's, or write-through if GATED)
       const bf16* pb = pre_bf16 + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
       for (; s0 < split_offset; ++s0) {
-        const bf16x4 v = *reinterpret_cast<const bf16x4*>(pb + s0 * D);
-        acc4 += f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]} * sW[g][s0];
+        bf16x4 v[1] = {ld_pre8<GATED>(pb + s0 * D)};
+        if constexpr (GATED) wt_landed(v);
+        acc4 += f32x4{(float)v[0][0], (float)v[0][1], (float)v[0][2], (float)v[0][3]} * sW[g][s0];
       }
     }
     // groups of 16 partials with all loads in flight (the tail of the kernel: latency, not bandwidth)

@@ -526,9 +526,14 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
     if (!__any(valid[rb])) continue;  // wave-uniform
     const float ll = fits ? (HALF ? lsum[rb] : ls[rb][0]) : __builtin_nanf("");
     const float inv = ll > 0.f ? 1.f / ll : (fits ? 0.f : ll);
-    if (ABL != 8 && part && valid[rb] && h == 0)
-      lse_part[((int64_t)token[rb] * Hq + head[rb]) * S_total + it.split] =
-          ll > 0.f ? m[rb] + log2f(ll) : (fits ? -INFINITY : ll);
+    if (ABL != 8 && part && valid[rb] && h == 0) {
+      float* lp = lse_part + ((int64_t)token[rb] * Hq + head[rb]) * S_total + it.split;
+      const float lv = ll > 0.f ? m[rb] + log2f(ll) : (fits ? -INFINITY : ll);
+      if constexpr (GATED)  // write-through: the overlapped decode reads it before this kernel ends
+        __hip_atomic_store(lp, lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        *lp = lv;
+    }
     const int R0 = 32 * RB * w + 32 * rb;
     const int nvalid = it.q_count * G - R0;
     char* sl = slab + rb * 4096;
@@ -539,14 +544,19 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
         const f32x4 v = *reinterpret_cast<const f32x4*>(sl + row * 128 + 16 * (cc ^ (row & 7)));
         if (row < nvalid) {
           const int R2 = R0 + row, tok2 = it.q_start + R2 / G, head2 = kvh * G + R2 % G;
+          f32x4* dst;
           if (part && !part_bf16)
-            *reinterpret_cast<f32x4*>(out_part + (((int64_t)tok2 * Hq + head2) * S_total + it.split) * D + 32 * rd +
-                                      4 * cc) = v;
+            dst = reinterpret_cast<f32x4*>(out_part + (((int64_t)tok2 * Hq + head2) * S_total + it.split) * D +
+                                           32 * rd + 4 * cc);
           else if (part)  // bf16 partial (O / l in [-max|v|, max|v|]: half the bytes of the cascade round trip)
-            *reinterpret_cast<f32x4*>(reinterpret_cast<bf16*>(out_part) +
-                                      (((int64_t)tok2 * Hq + head2) * S_total + it.split) * D + 64 * rd + 8 * cc) = v;
+            dst = reinterpret_cast<f32x4*>(reinterpret_cast<bf16*>(out_part) +
+                                           (((int64_t)tok2 * Hq + head2) * S_total + it.split) * D + 64 * rd + 8 * cc);
           else
-            *reinterpret_cast<f32x4*>(out + (int64_t)tok2 * out_stride + (int64_t)head2 * D + 64 * rd + 8 * cc) = v;
+            dst = reinterpret_cast<f32x4*>(out + (int64_t)tok2 * out_stride + (int64_t)head2 * D + 64 * rd + 8 * cc);
+          if constexpr (GATED)
+            st_wt16(dst, v);
+          else
+            *dst = v;
         }
       }
     };
@@ -578,9 +588,8 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
       }
     }
   }
-  if constexpr (GATED) {  // one arrival per workgroup
-    __syncthreads();
-    if (tid == 0) gate_arrive(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y), gt.mode);
+  if constexpr (GATED) {  // one relaxed arrival per workgroup after its write-through stores completed
+    if (gt.sig != nullptr) gate_arrive_wt(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y));
   }
   if constexpr (ABL == 8) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -195,6 +195,30 @@ __device__ __forceinline__ void gate_wait(int* g, int mode = 0) {
   if (!(mode & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
+// Write-through hand-off (the cascade -> suffix-decode overlap): the producer writes its outputs with agent-coherent
+// stores (sc1: through to memory, not parked dirty in its XCD's L2), waits for them (vmcnt), and arrives RELAXED; the
+// consumer waits RELAXED and reads them with agent-coherent loads (sc1: not served from its XCD's possibly stale L2)
+// — neither side needs the L2-wide write-back / invalidate of a release / acquire fence.
+__device__ __forceinline__ void st_wt16(void* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ f32x4 ld_wt16(const void* p) {  // the caller waits (s_waitcnt vmcnt) before using it
+  f32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+__device__ __forceinline__ f32x2 ld_wt8(const void* p) {
+  f32x2 r;
+  asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+// after every write-through store of the workgroup: all of them complete, then ONE relaxed arrival
+__device__ __forceinline__ void gate_arrive_wt(int* g, int unit, int total) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) gate_arrive(g, unit, total, 1);
+}
+
 // Launch `kernel`; `early`: without the AQL barrier bit (the kernel waits on a gate before reading its inputs)
 template <typename F, typename... Args>
 inline void launch_maybe_early(F kernel, dim3 grid, dim3 block, hipStream_t st, bool early, Args... args) {
