@@ -339,6 +339,7 @@ struct DecodeSmem {
   float sW[8][65];
   float sWt[8];
   int s_last;
+  int pf[4][64];  // OCC3 == 2: landing zone of each wave's L2-prefetch DMA (never read)
 };
 
 // prefix-partial loads of the merges: plain, or agent-coherent (sc1) when the cascade overlaps this kernel (GATED)
@@ -367,7 +368,7 @@ __device__ __forceinline__ void wt_landed(T (&v)[N]) {
 // One decode piece: keys [lo, hi) of row b, kv head kvh, piece `split` of S, partial slots from split_offset. Every
 // thread of the workgroup calls it with the same arguments (it synchronises the workgroup); returns when the
 // piece's partial or final rows are written.
-template <int D, bool FP8, int MG, bool OCC3 = false, bool GATED = false>
+template <int D, bool FP8, int MG, int OCC3 = 0, bool GATED = false>
 __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __restrict__ q, int64_t q_stride,
                                              const void* __restrict__ k_cache, const void* __restrict__ v_cache,
                                              int Hkv, int G, const int* __restrict__ block_tables, int bt_stride,
@@ -403,7 +404,55 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   __syncthreads();
   WaveAcc<D> acc;
   init_acc<D>(acc);
-  if constexpr (OCC3) {
+  if constexpr (OCC3 == 2) {
+    // OCC3 + L2 prefetch: with this block's K / V loads each wave also touches one dword of every 128-B line of its
+    // NEXT block (2 LDS-DMA dword loads per lane into a never-read LDS landing zone: no VGPR destination), so that
+    // block streams from HBM into L2 under this block's compute. Page ids from LDS only (a global page-id load
+    // would make the compiler wait for every outstanding load at the join). A register double buffer spills at
+    // the 168-VGPR budget of three waves per SIMD.
+    if (w < nb && !FP8) {
+      const bool qrow = r < G;
+      const bf16* kc = static_cast<const bf16*>(k_cache);
+      const bf16* vc = static_cast<const bf16*>(v_cache);
+      const LdsPages lp{sm.pages, pg0};
+      const uint32_t lds_pf = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)&sm.pf[w][0]);
+      for (int bk = w; bk < nb; bk += 4) {
+        const int key0 = a0 + 32 * bk;
+        KVFrag<D> f;
+        f32x16 sacc = {};
+        if (lds_pt) {  // workgroup-uniform
+          int p0, p1;
+          block_pages(lp, key0, hi, p0, p1);
+          load_kv<D>(f, kc, vc, Hkv, kvh, p0, p1, lane);
+          if (bk + 4 < nb) {  // wave-uniform
+            int n0, n1;
+            block_pages(lp, key0 + 128, hi, n0, n1);
+            const int64_t pg = (int64_t)((lane >> 5) ? n1 : n0) * Hkv + kvh;
+            const int off = (lane & 31) * 128;
+            const char* ka = reinterpret_cast<const char*>(kc + pg * (PAGE * D)) + off;
+            const char* va = reinterpret_cast<const char*>(vc + pg * (PAGE * D)) + off;
+            // inline asm: the compiler's wait insertion does not see these two loads, so it adds no LDS-alias
+            // waits; its own vmcnt waits only grow more conservative (in-order completion)
+            asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, off\n\tglobal_load_lds_dword %1, off"
+                         :: "v"(ka), "v"(va), "s"(lds_pf) : "memory", "m0");
+          }
+        } else {
+          int p0, p1;
+          block_pages(bt, key0, hi, p0, p1);
+          load_kv<D>(f, kc, vc, Hkv, kvh, p0, p1, lane);
+        }
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) {
+          bf16x8 qv = *reinterpret_cast<const bf16x8*>(&sm.qs[qrow ? r : 0][16 * kk + 8 * h]);
+          if (!qrow) qv = bf16x8{};
+          sacc = mfma32(f.k[kk], qv, sacc);
+        }
+        const bool masked = (key0 < lo) | (key0 + 32 > hi);
+        softmax_pv<D>(sacc, masked, key0, lo, hi, 0x7fffffff, scale_log2, f.v, acc, lane);
+      }
+    }
+  } else if constexpr (OCC3) {
     // Three waves per SIMD (VGPR budget 168): no Q fragments and no second K/V block in registers — each wave
     // has its one block in flight at a time, and 12 waves per CU (3 workgroups) keep the memory system fed;
     // more resident workgroups also cover each other's piece start / end.
@@ -658,7 +707,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   }
 }
 
-template <int D, bool HEADS_FAST, bool FP8, int MG = 16, bool OCC3 = false, bool GATED = false>
+template <int D, bool HEADS_FAST, bool FP8, int MG = 16, int OCC3 = 0, bool GATED = false>
 __global__ __launch_bounds__(256, OCC3 ? 3 : 2) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
                                                            const void* __restrict__ k_cache,
                                                            const void* __restrict__ v_cache, int Hkv, int G,
@@ -1238,14 +1287,15 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
   }();
   // three workgroups per CU (Q in LDS, one K/V block per wave in flight; bench +0.9 %, profiles/r03/decode_occ3/);
   // KAFKA_DECODE_OCC3=0: two per CU with a one-block register prefetch
-  static const bool occ3 = [] {
+  // KAFKA_DECODE_OCC3=2: three per CU with the software-pipelined block loop (next K under softmax + PV)
+  static const int occ3 = [] {
     const char* e = getenv("KAFKA_DECODE_OCC3");
-    return e == nullptr || e[0] != '0';
+    return e == nullptr ? 1 : (e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1));
   }();
   const dim3 hf(Hkv, n_items), sf(n_items, Hkv);
   if (gt.wait != nullptr || gt.wait2 != nullptr || gt.sig != nullptr) {  // gated: its own instantiation
     if (fp8 || !heads_fast || mg != 32 || !occ3) return hipErrorInvalidValue;
-    go(attn_decode_kernel<128, true, false, 32, true, true>, hf);
+    go(attn_decode_kernel<128, true, false, 32, 1, true>, hf);
     return hipGetLastError();
   }
   if (fp8)
@@ -1254,8 +1304,10 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
     go(attn_decode_kernel<128, false, false>, sf);
   else if (mg == 8)
     go(attn_decode_kernel<128, true, false, 8>, hf);
+  else if (mg == 32 && occ3 == 2)
+    go(attn_decode_kernel<128, true, false, 32, 2>, hf);
   else if (mg == 32 && occ3)
-    go(attn_decode_kernel<128, true, false, 32, true>, hf);
+    go(attn_decode_kernel<128, true, false, 32, 1>, hf);
   else if (mg == 32)
     go(attn_decode_kernel<128, true, false, 32>, hf);
   else
