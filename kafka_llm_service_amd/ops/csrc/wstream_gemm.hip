@@ -269,9 +269,28 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
       for (int i = 0; i < 16; ++i) red[((ct * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
     __syncthreads();
     const int head = cb, d = 32 * ct + r, j = d & 63;
-    const bool is_q = head < ra.Hq, is_k = !is_q && head < ra.Hq + ra.Hkv;
+    const bool is_q = head < ra.Hq, is_k = !is_q && head < ra.Hq + ra.Hkv;  // workgroup-uniform
+    const bool kv = !is_q && ra.slots != nullptr;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MT; ++mt) {
+      // this row block's positions / slots, then its cos / sin, each as ONE batch of independent loads (per element
+      // and behind the previous element's stores, the dependent pairs cost ~17 us of serialised latency per launch)
+      int64_t pos[16], slot[16];
+      float c[16], sn[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = min(mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h, M - 1);
+        pos[i] = (is_q || is_k) ? ra.positions[m] : 0;
+        slot[i] = kv ? ra.slots[m] : -1;
+      }
+      if (is_q || is_k) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float* cs = ra.cos_sin + pos[i] * 128;
+          c[i] = cs[j];
+          sn[i] = cs[64 + j];
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -279,17 +298,14 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
         float y = acc[mt][i];
         if (is_q || is_k) {
           const float xp = red[(((ct ^ 2) * MT + mt) * 16 + i) * 64 + lane];
-          const float* cs = ra.cos_sin + ra.positions[m] * 128;
-          const float c = cs[j], sn = cs[64 + j];
-          y = ct < 2 ? y * c - xp * sn : y * c + xp * sn;
+          y = ct < 2 ? y * c[i] - xp * sn[i] : y * c[i] + xp * sn[i];
         }
         if (is_q) {
           ra.q_out[(int64_t)m * ra.q_stride + head * 128 + d] = (bf16)y;
-        } else if (ra.slots != nullptr) {
-          const int64_t slot = ra.slots[m];
-          if (slot >= 0) {
-            const int64_t blk = slot >> 4;
-            const int off = (int)(slot & 15);
+        } else if (kv) {
+          if (slot[i] >= 0) {
+            const int64_t blk = slot[i] >> 4;
+            const int off = (int)(slot[i] & 15);
             if (is_k)
               ra.k_cache[(blk * ra.Hkv + (head - ra.Hq)) * 2048 + ((d >> 3) * 16 + off) * 8 + (d & 7)] = (bf16)y;
             else
@@ -297,6 +313,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
           }
         }
       }
+    }
     if constexpr (EARLY) {  // one arrival per head tile (the last split's)
       if (gt.sig != nullptr) {
         __syncthreads();
