@@ -376,6 +376,7 @@ _WSTREAM_TARGET = int(os.environ.get("KAFKA_WSTREAM_TARGET", "0"))  # A/B overri
 _WSTREAM_MT3 = os.environ.get("KAFKA_WSTREAM_MT3", "1") != "0"  # 65..96 rows on three row tiles (csrc mt3_off)
 _WSTREAM_MT4_KC256 = os.environ.get("KAFKA_WSTREAM_MT4_KC", "") == "256"  # A/B (csrc mt4_kc256)
 _WSTREAM_ROWSPLIT = os.environ.get("KAFKA_WSTREAM_ROWSPLIT", "0") == "1"  # 64-row tiles sharing L2 (csrc rowsplit_on)
+_WSTREAM_RT1 = os.environ.get("KAFKA_WSTREAM_RT1", "0") == "1"  # 33..64 rows as two 32-row tiles (csrc rt1_on)
 
 
 def stream_plan(M: int, N: int, K: int, max_splits: int = 8, one_tile: bool = False) -> tuple[int, int, int] | None:
@@ -385,7 +386,8 @@ def stream_plan(M: int, N: int, K: int, max_splits: int = 8, one_tile: bool = Fa
     if M < 1 or M > STREAM_KERNEL_MAX_M or N % 32 or N <= 0:
         return None
     mt = 2 if _WSTREAM_ROWSPLIT and not one_tile and M > 64 else \
-        (1 if M <= 32 else (2 if M <= 64 else (3 if M <= 96 and _WSTREAM_MT3 else 4)))
+        (1 if M <= 32 or (_WSTREAM_RT1 and not one_tile and M <= 64) else
+         (2 if M <= 64 else (3 if M <= 96 and _WSTREAM_MT3 else 4)))
     kc = 128 if mt == 4 and not _WSTREAM_MT4_KC256 else 256
     if K % kc or K <= 0:
         return None

@@ -554,6 +554,14 @@ static bool rowsplit_on() {  // mirrored by ops.stream_plan
   return on;
 }
 
+static bool rt1_on() {  // KAFKA_WSTREAM_RT1=1: 33..64 rows as two 32-row tiles sharing each weight slice in L2 (A/B)
+  static const bool on = [] {
+    const char* e = getenv("KAFKA_WSTREAM_RT1");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 static bool mt4_kc256() {  // KAFKA_WSTREAM_MT4_KC=256: four row tiles on 256-deep chunks (128 KB X stage; A/B)
   static const bool on = [] {
     const char* e = getenv("KAFKA_WSTREAM_MT4_KC");
@@ -569,7 +577,8 @@ extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int one_t
   // 65..96 rows (a decode batch plus a short new-turn chunk): three 32-row tiles on 256-deep chunks (96 KB X stage)
   // instead of four on 128-deep ones
   // KAFKA_WSTREAM_ROWSPLIT=1: beyond 64 rows, 64-row tiles whose workgroups share each weight slice in one XCD's L2
-  const int MT = rowsplit_on() && !one_tile && M > 64 ? 2 : (M <= 32 ? 1 : (M <= 64 ? 2 : (M <= 96 && !mt3_off() ? 3 : 4)));
+  const int MT = rowsplit_on() && !one_tile && M > 64 ? 2 : (M <= 32 || (rt1_on() && !one_tile && M <= 64) ? 1 :
+                 (M <= 64 ? 2 : (M <= 96 && !mt3_off() ? 3 : 4)));
   const int KC = MT == 4 && !mt4_kc256() ? 128 : 256;
   if (K % KC != 0 || K <= 0) return 2;
   const int nx = (N + 127) / 128 * ((M + 32 * MT - 1) / (32 * MT));  // workgroups per split (x row tiles)
