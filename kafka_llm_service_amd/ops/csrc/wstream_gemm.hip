@@ -609,6 +609,13 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   const int rt = (M + 32 * mt - 1) / (32 * mt);  // row tiles of 32 * mt rows
   const int nblk = (N + 127) / 128;
   const dim3 grid((rt > 1 ? (nblk + 7) / 8 * 8 : nblk) * rt, splits);  // (row tiles: column blocks padded to 8)
+  // KAFKA_WSTREAM_TILE_NT=0: with several row tiles, cached (not non-temporal) weight loads, so the other tiles of a
+  // slice can hit the copy the first one brought into L2 (A/B)
+  static const bool tile_nt = [] {
+    const char* e = getenv("KAFKA_WSTREAM_TILE_NT");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (rt > 1 && !tile_nt) nt = 0;
   const int ks = K / splits;
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   float* p = splits > 1 ? P : nullptr;
