@@ -251,6 +251,24 @@ def test_stream_decode_gemm_matches_oracle():
     _check_against_oracle(m, prompts, outs)
 
 
+def test_stream_plan_rules(monkeypatch):
+    """The decode GEMM plan (ops.stream_plan, mirrored from csrc kafka_wstream_plan): row tiles by step size (1 / 2 /
+    3 / 4 x 32 rows), 128-deep chunks for four tiles, split-K grown toward the grid target; the A/B switches that
+    split rows into XCD-shared tiles never apply to the fused QKV + RoPE kernel (one row tile: its per-head tickets
+    count the splits of ONE tile)."""
+    from kafka_llm_service_amd import ops
+
+    assert [ops.stream_plan(M, 28672, 4096)[0] for M in (1, 32, 33, 64, 65, 96, 97, 128)] == [1, 1, 2, 2, 3, 3, 4, 4]
+    assert ops.stream_plan(128, 4096, 4096)[1] == 128 and ops.stream_plan(64, 4096, 4096)[1] == 256
+    assert ops.stream_plan(64, 28672, 4096)[2] == 1 and ops.stream_plan(64, 6144, 4096)[2] == 4
+    assert ops.stream_plan(300, 4096, 4096) is None and ops.stream_plan(64, 4100, 4096) is None
+    monkeypatch.setattr(ops, "_WSTREAM_ROWSPLIT", True)
+    monkeypatch.setattr(ops, "_WSTREAM_RT1", True)
+    assert ops.stream_plan(90, 6144, 4096)[0] == 2 and ops.stream_plan(64, 6144, 4096)[0] == 1
+    assert ops.stream_plan(90, 6144, 4096, one_tile=True)[0] == 3
+    assert ops.stream_plan(64, 6144, 4096, one_tile=True)[0] == 2
+
+
 def test_tiled_only_weights_match_stream():
     """Tiled-only mode (the row-major dense weights dropped after tiling, prefill untiles per projection — what a
     model whose second weight copy does not fit gets) generates exactly what the two-copy stream mode does."""
