@@ -54,7 +54,7 @@ TP_OVERLAP = os.environ.get("KAFKA_TP_OVERLAP", "0") == "1"
 PIPE_CHUNKS = max(1, int(os.environ.get("KAFKA_TP_PIPE_CHUNKS", "4")))
 PIPE_ROWS = 256
 SKINNY = frozenset(p for p in os.environ.get("KAFKA_SKINNY", "qkv,o,down").replace("+", ",").split(",")
-                   if p in ("qkv", "o", "down"))
+                   if p in ("qkv", "o", "down", "gate_up"))  # gate_up: fused SwiGLU epilogue (A/B, not default)
 # Early-launched decode layers (env KAFKA_EARLY; ops.GateSet, csrc/common.h Gates). On a decode-only step of the
 # weight-streaming path every kernel of a layer after its input RMSNorm — QKV projection, RoPE/KV write, cascade,
 # suffix decode, O projection, gate_up, down — is launched without the AQL barrier bit: it is dispatched while its
@@ -356,6 +356,11 @@ class TransformerLM:
             else:
                 if self.stream and lw.glu and 0 < T <= max(self.stream_max_m, STREAM_GU_MAX_M):
                     a = ops.linear_glu(x, lw.gate_up_t)  # SwiGLU in the GEMM epilogue (or on its slabs)
+                elif (self.stream and lw.glu and "gate_up" in SKINNY and lw.gate_up_t is not None
+                      and ops.skinny_plan(T, lw.gate_up_t.shape[0] * 32, x.shape[1])):
+                    a = ops.linear_skinny(x, lw.gate_up_t, glu=True)  # fused SwiGLU (one split) or gate | up slabs
+                    if ops.is_slab(a):
+                        a = ops.silu_mul(a)
                 else:
                     a = ops.silu_mul(F.linear(x, self._dense(lw.gate_up, lw.gate_up_t, bool(lw.glu))))
                 if tp and self._can_overlap(T, lw.down_t) and i + 1 < len(self.layers):
