@@ -543,7 +543,16 @@ static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> 
                 "wstream_gemm: slab shape must be [splits, M, N]");
     pp = p->data_ptr<float>();
   }
-  CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, nt ? 1 : 0, 1, glu ? 1 : 0,
+  // two K halves per chunk (8 waves) for 64-row tiles with >= 6 chunks per split: the long streams (gate_up unsplit
+  // with its fused SwiGLU, down) ran 1.6-2.8 % faster in the config sweep, the short ones (qkv, o) slower; headline
+  // +0.24 % (3 / 3 interleaved pairs, profiles/r04/bench_ab_wstream_kw2.jsonl). KAFKA_WSTREAM_KW2=0: one wave per
+  // column tile everywhere
+  static const bool kw2 = [] {
+    const char* e = getenv("KAFKA_WSTREAM_KW2");
+    return e == nullptr || e[0] != '0';
+  }();
+  const int kw = kw2 && mt == 2 && kc == 256 && K / s / kc >= 6 && gt.wait == nullptr && gt.sig == nullptr ? 2 : 1;
+  CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, nt ? 1 : 0, kw, glu ? 1 : 0,
                                       yp, ldy, pp, gt, cur_stream()));
 }
 

@@ -603,7 +603,7 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
                                                int mt, int kc, int splits, int nt, int kw, int glu, bf16* Y,
                                                int64_t ldy, float* P, Gates gt, hipStream_t st) {
   if (M < 1) return hipSuccess;
-  if (glu && (N % 64 != 0 || kw != 1)) return hipErrorInvalidValue;
+  if (glu && (N % 64 != 0 || kw > 2)) return hipErrorInvalidValue;  // (the SwiGLU epilogue runs after the KW fold)
   if (K % (kc * splits) != 0 || (splits > 1 && P == nullptr) || (splits == 1 && P == nullptr && Y == nullptr))
     return hipErrorInvalidValue;
   const int rt = (M + 32 * mt - 1) / (32 * mt);  // row tiles of 32 * mt rows
