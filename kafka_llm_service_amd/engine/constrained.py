@@ -130,6 +130,10 @@ class ToolCallConstraint:
         self._n = 0
         self.done = False
         self._guards: list[tuple[int, frozenset]] = []  # (slot, E): speculated "output_ids[slot] not in E"
+        # slot n -> guarded slot n - 1 when the spec LAUNCHED for slot n (the last __call__ for it: the runner asks at
+        # launch) was speculated past the pending token n - 1; guard slots whose landed token broke the guess
+        self._spec_from: dict[int, int] = {}
+        self._violated: set[int] = set()
 
     def _mode(self, tc):
         if isinstance(tc, dict):
@@ -148,12 +152,15 @@ class ToolCallConstraint:
     # ---- runner protocol ----------------------------------------------------------------------------------------
     # ``output_ids`` may end with ONE placeholder (< 0): the token being sampled by the step in flight (the engine
     # plans step n+1 before step n's token lands). When the spec that token was drawn under makes the NEXT state
-    # depend only on whether the token falls in a small set E — a Mask (free string: E = the closing quote; digits,
-    # "none": E = its extra ids / nothing) or the first free token of "auto" (E = the tool-call start) — the
-    # program consumes a representative token outside E now and records the guard (slot, E). When the real token
-    # lands inside E the guess was wrong: the program is rebuilt from the landed tokens and the token sampled under
-    # the mis-predicted mask (slot + 1) is rolled back by the engine (``rollback_at``). Choice states (tool names,
-    # enums, booleans: the next state depends on WHICH token) cannot be predicted: ``plan_state`` -> "wait".
+    # depend only on whether the token falls in a small set E — a Mask (free string: E = the closing quote; digits
+    # and "none": E is empty, every token ends the value / the state) or the first free token of "auto" (E = the
+    # tool-call start) — the program consumes a representative token outside E now and records the guard (slot, E).
+    # When the real token lands inside E the guess was wrong: the program is rebuilt from the landed tokens, the guard
+    # slot is remembered as violated (``plan_state`` keeps the row out of plans until then), and the token sampled
+    # under the mis-predicted mask (slot + 1) is rolled back by the engine at its landing (``rollback_at``) — only if
+    # the spec LAUNCHED for slot + 1 was the speculated one (a plan dropped and redone after the landing used the
+    # real token). Choice states (tool names, enums, booleans: the next state depends on WHICH token) cannot be
+    # predicted: ``plan_state`` -> "wait".
     def _advance(self, t: int) -> None:
         self._n += 1
         if self._spec is _FREE_FOREVER:
@@ -184,7 +191,8 @@ class ToolCallConstraint:
         if spec is None:  # "auto" before the first token: only the tool-call start token changes the state
             return (0 if self.start != 0 else 1), frozenset([self.start])
         if isinstance(spec, Mask):
-            extra = frozenset(int(e) for e in spec.extra)
+            # digit masks end the value whichever token lands (a lone "0" included): nothing to guard
+            extra = frozenset() if spec.key.startswith("digits") else frozenset(int(e) for e in spec.extra)
             k = (id(spec.base), spec.key, extra)
             rep = _REPS.get(k)
             if rep is None:
@@ -207,6 +215,7 @@ class ToolCallConstraint:
         self._guards = keep
         if bad is None:
             return None
+        self._violated.add(bad)
         self._gen, self._spec, self._n, self.done, self._guards = None, None, 0, False, []
         self._start()
         for t in output_ids[:bad + 1]:
@@ -216,6 +225,8 @@ class ToolCallConstraint:
     def __call__(self, output_ids: list[int]):
         self._start()
         self._validate(output_ids)
+        n = len(output_ids)
+        spec_past = None
         while self._n < len(output_ids):
             t = output_ids[self._n]
             if t < 0:  # the in-flight token: speculate past it (plan_state said the spec allows it)
@@ -227,8 +238,13 @@ class ToolCallConstraint:
                 rep, extra = cls
                 if extra:
                     self._guards.append((self._n, extra))
+                    spec_past = self._n
                 t = rep
             self._advance(t)
+        if spec_past is not None:
+            self._spec_from[n] = spec_past
+        else:
+            self._spec_from.pop(n, None)
         return None if self._spec is _FREE_FOREVER else self._spec
 
     def plan_state(self, output_ids: list[int]) -> str:
@@ -237,6 +253,9 @@ class ToolCallConstraint:
         self._start()
         if self._validate(output_ids) is not None:
             return "rollback"
+        n = len(output_ids)
+        if n and output_ids[-1] < 0 and self._spec_from.get(n - 1) in self._violated:
+            return "rollback"  # the pending token was drawn under a wrong guess: wait for its landing (rollback_at)
         if not output_ids or output_ids[-1] >= 0:
             return "ok"
         if self._n < len(output_ids) - 1:  # consume the landed tokens first (no speculation involved)
@@ -246,8 +265,11 @@ class ToolCallConstraint:
     def rollback_at(self, output_ids: list[int], slot: int) -> bool:
         """At the landing of ``output_ids[slot]``: True if it was drawn under a mis-predicted mask (the token before
         it broke its guard) and must be discarded; the program is rebuilt from the landed tokens then."""
-        bad = self._validate(output_ids[:slot])
-        return bad is not None and bad == slot - 1
+        self._validate(output_ids[:slot])
+        g = self._spec_from.pop(slot, None)
+        hit = g is not None and g in self._violated
+        self._violated = {v for v in self._violated if v >= slot}
+        return hit
 
     # ---- grammar -------------------------------------------------------------------------------------------------
     def _program(self):

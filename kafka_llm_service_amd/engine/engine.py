@@ -415,6 +415,8 @@ class LLMEngine:
                 # the real one, gathered on the device)
                 del s.output_ids[idx:]
                 s.num_computed = s.total_len - 1
+                if s.params.presence_penalty or s.params.frequency_penalty:
+                    self.runner.lp.uncount(s, t)  # the sampler counted it on the device
                 self.stats["grammar_rollbacks"] = self.stats.get("grammar_rollbacks", 0) + 1
                 continue
             s.output_ids[idx] = t

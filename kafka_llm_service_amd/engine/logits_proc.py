@@ -17,7 +17,7 @@ addresses (hipGraph-capturable):
     after that the same state is a row index;
   * ``counts`` int32 [slots, V]: a slot per penalised live sequence, zeroed on (re)assignment; the sampler bumps
     ``counts[slot][token]`` with every token it draws, so the next step (stream-ordered) sees it without the host.
-Table writes (new mask rows, slot zeroing) are ``ProcUpdates`` applied on the stream before the step's sampler — on
+Table writes (new mask rows, slot zeroing, count decrements of rolled-back tokens) are ``ProcUpdates`` applied on the stream before the step's sampler — on
 every TP rank, from the same plan, so every rank samples the same token.
 """
 from __future__ import annotations
@@ -37,10 +37,12 @@ class ProcUpdates:
     mask_rows: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))     # [k] rows of mask_tab
     mask_words: np.ndarray = field(default_factory=lambda: np.zeros((0, 0), np.int32))  # [k, W] their bits
     zero_slots: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))    # [z] count rows to clear
+    # [d, 2] (slot, token): counts[slot][token] -= 1 — a token the sampler counted and the engine rolled back
+    dec: np.ndarray = field(default_factory=lambda: np.zeros((0, 2), np.int32))
 
     @property
     def empty(self) -> bool:
-        return not (self.mask_rows.size or self.zero_slots.size)
+        return not (self.mask_rows.size or self.zero_slots.size or self.dec.size)
 
 
 def pack_bits(keep: np.ndarray, words: int) -> np.ndarray:
@@ -70,6 +72,7 @@ class LogitsProcessor:
         self._rows: OrderedDict = OrderedDict()  # key -> mask row (LRU order)
         self._slots: dict[int, tuple[int, object]] = {}  # seq_id -> (slot, seq)
         self._free: list[int] = list(range(max_slots - 1, -1, -1))
+        self._dec: list[tuple[int, int]] = []  # (slot, token) decrements queued by uncount()
         self.stats = {"mask_uploads": 0, "proc_steps": 0, "forced_rows": 0, "mask_rows_used": 0, "penalty_rows": 0}
 
     # ---- tables (allocated together on first use: a captured graph sees both addresses) -------------------------
@@ -115,6 +118,15 @@ class LogitsProcessor:
         self._slots[seq.seq_id] = (slot, seq)
         zero.append(slot)
         return slot
+
+    def uncount(self, seq, token: int) -> None:
+        """A drawn token the engine discarded (grammar rollback, engine.py ``_finish_step``): the sampler already
+        bumped ``counts[slot][token]``, so the next table update takes it back — otherwise the row keeps penalising a
+        token that is not in its output. Queued on the host; applied by the next step that samples a processed row
+        (every later sample of a penalised sequence is such a row), before its sampler."""
+        e = self._slots.get(seq.seq_id)
+        if e is not None and 0 <= int(token) < self.V:
+            self._dec.append((e[0], int(token)))
 
     def build(self, rows: list[tuple[int, object, object]], n: int) -> tuple[np.ndarray, ProcUpdates]:
         """``rows``: (row, seq, constraint spec) for every sampled row that needs processing (spec None, a list of
@@ -169,6 +181,9 @@ class LogitsProcessor:
             upd.mask_words = np.stack(upd_words).astype(np.int32, copy=False)
         if zero:
             upd.zero_slots = np.asarray(zero, dtype=np.int32)
+        if self._dec:
+            upd.dec = np.asarray(self._dec, dtype=np.int32).reshape(-1, 2)
+            self._dec = []
         return proc, upd
 
     # ---- device side ----------------------------------------------------------------------------------------------
@@ -182,6 +197,12 @@ class LogitsProcessor:
                 raise ValueError("logits processor: mask update does not fit the table")
             rows = upload(upd.mask_rows.astype(np.int64))
             mask_tab.index_copy_(0, rows, upload(upd.mask_words))
+        if upd.dec.size:  # before the zeroing: a recycled slot starts from zero whatever was queued for it
+            if int(upd.dec[:, 0].max()) >= counts.shape[0] or int(upd.dec[:, 1].max()) >= counts.shape[1]:
+                raise ValueError("logits processor: count decrement outside the count table")
+            flat = upd.dec[:, 0].astype(np.int64) * counts.shape[1] + upd.dec[:, 1]
+            idx = upload(flat)
+            counts.view(-1).index_add_(0, idx, torch.full(idx.shape, -1, dtype=counts.dtype, device=counts.device))
         if upd.zero_slots.size:
             if int(upd.zero_slots.max()) >= counts.shape[0]:
                 raise ValueError("logits processor: penalty slot outside the count table")

@@ -97,22 +97,23 @@ def pack_plan(h: HostStep, sp: SampleParams) -> tuple[np.ndarray, np.ndarray]:
              sp.temp.astype(np.float32, copy=False), sp.topp.astype(np.float32, copy=False),
              sp.topk.astype(np.int32, copy=False), sp.seeds.astype(np.int64, copy=False),
              proc.astype(np.int32, copy=False), upd.mask_rows.astype(np.int32, copy=False),
-             upd.mask_words.astype(np.int32, copy=False), upd.zero_slots.astype(np.int32, copy=False)]
+             upd.mask_words.astype(np.int32, copy=False), upd.zero_slots.astype(np.int32, copy=False),
+             upd.dec.astype(np.int32, copy=False)]
     payload = np.concatenate([np.ascontiguousarray(a).reshape(-1).view(np.uint8) for a in parts])
     hdr = np.zeros(PLAN_HDR, dtype=np.int64)
     hdr[0] = 1
     k = len(_PLAN_SCALARS)
     hdr[1:1 + k] = [getattr(h, f) for f in _PLAN_SCALARS]
     W = upd.mask_words.shape[1] if upd.mask_rows.size else 0
-    hdr[1 + k:1 + k + 9] = [h.i64.size, i32.size, n, int(sp.greedy), payload.size, proc.shape[0],
-                            upd.mask_rows.size, W, upd.zero_slots.size]
+    hdr[1 + k:1 + k + 10] = [h.i64.size, i32.size, n, int(sp.greedy), payload.size, proc.shape[0],
+                             upd.mask_rows.size, W, upd.zero_slots.size, upd.dec.shape[0]]
     return hdr, payload
 
 
 def unpack_plan(hdr: np.ndarray, payload: np.ndarray) -> tuple[HostStep, SampleParams]:
     k = len(_PLAN_SCALARS)
     h = HostStep(**{f: int(v) for f, v in zip(_PLAN_SCALARS, hdr[1:1 + k])})
-    n64, n32, n, greedy, _, n_proc, n_mask, W, n_zero = (int(v) for v in hdr[1 + k:1 + k + 9])
+    n64, n32, n, greedy, _, n_proc, n_mask, W, n_zero, n_dec = (int(v) for v in hdr[1 + k:1 + k + 10])
     o = 0
 
     def take(dt, cnt):
@@ -133,7 +134,7 @@ def unpack_plan(hdr: np.ndarray, payload: np.ndarray) -> tuple[HostStep, SampleP
                       bool(greedy))
     proc = take(np.int32, n_proc * 8).reshape(n_proc, 8)
     upd = ProcUpdates(take(np.int32, n_mask), take(np.int32, n_mask * W).reshape(n_mask, W),
-                      take(np.int32, n_zero))
+                      take(np.int32, n_zero), take(np.int32, 2 * n_dec).reshape(n_dec, 2))
     sp.proc = proc if n_proc else None
     sp.upd = None if upd.empty else upd
     return h, sp

@@ -211,3 +211,56 @@ def test_bench_tool_call_loop_async_equals_sync():
             calls = parse_tool_calls(tok.decode(o[start + 1:c]))
             assert calls and calls[0]["function"]["name"] in {t["function"]["name"] for t in tools}
             start = c + 1
+
+
+class _NarrowStrings(ToolCallConstraint):
+    """Free strings over three string-safe tokens: with the closing quote in the same mask it is drawn often, so the
+    plan-ahead guess "the pending token does not close the string" breaks and rows roll back."""
+
+    def __init__(self, tok, tools, choice):
+        import types
+
+        super().__init__(tok, tools, choice)
+        base = self.cls
+        narrow = np.zeros_like(base.str_safe)
+        narrow[np.flatnonzero(base.str_safe)[200:203]] = True
+        self.cls = types.SimpleNamespace(str_safe=narrow, digits=base.digits, digits_nz=base.digits_nz,
+                                         digit_range=base.digit_range)
+
+
+def test_async_rollbacks_equal_sync_and_parse():
+    """ADVICE r04 (high + medium): a landed token that breaks a speculated guard must roll back the token drawn
+    after it (even when the row was planned in between), and a rolled-back token must leave the device penalty
+    counts. Constrained rows whose strings close often (a guard violation every few tokens), some with penalties:
+    async tokens == sync tokens, rollbacks happened, every tool call parses."""
+    from kafka_llm_service_amd.engine.chat_template import parse_tool_calls
+    from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
+
+    tok = get_tokenizer("llama3")
+    g = torch.Generator().manual_seed(3)
+    prompts = [torch.randint(0, 5000, (n,), generator=g).tolist() for n in (11, 26, 19, 33)]
+    model = _engine().model
+    for temp in (0.9, 0.0):
+        outs, stats = [], []
+        for async_on in (False, True):
+            eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", num_kv_blocks=512, max_model_len=2048,
+                                         async_scheduling=async_on), model=model)
+            seqs = []
+            for i, p in enumerate(prompts):
+                kw = dict(temperature=temp, max_tokens=70, ignore_eos=True, seed=40 + i,
+                          allowed_tokens_fn=_NarrowStrings(tok, TOOLS, "required") if i < 3 else None)
+                if i in (1, 2):
+                    kw.update(frequency_penalty=0.9, presence_penalty=0.4)
+                seqs.append(eng.add_request(f"r{i}", p, SamplingParams(**kw)))
+            while any(not s.finished for s in seqs):
+                eng.step()
+            outs.append([list(s.output_ids) for s in seqs])
+            stats.append(dict(eng.stats))
+        assert outs[0] == outs[1], temp
+        if temp > 0:
+            assert stats[1].get("grammar_rollbacks", 0) > 0, stats[1]
+        eom, start = tok.special_id("<|eom_id|>"), tok.special_id("<|python_tag|>")
+        for o in outs[1][:3]:
+            assert o[0] == start and eom in o
+            calls = parse_tool_calls(tok.decode(o[1:o.index(eom)]))
+            assert calls and calls[0]["function"]["name"] in {t["function"]["name"] for t in TOOLS}, tok.decode(o)
