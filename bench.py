@@ -433,6 +433,25 @@ def _barrier(group) -> None:
         dist.barrier(group=group)
 
 
+def _rank_record(args, rank, dev, timing, elapsed, eng) -> dict:
+    """This rank's line of the bench record: its device (index, PCI location, uuid), role and own rate."""
+    import torch
+
+    rec = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": dev,
+           "role": "tp_follower" if args.tp > 1 and rank % args.tp else "replica",
+           "out_tokens": int(timing["out_tokens"]),
+           "tok_s": round(timing["out_tokens"] / elapsed, 1) if elapsed > 0 else 0.0,
+           "ms_per_step": round(elapsed / args.steps * 1e3, 3) if elapsed > 0 else None,
+           "steps": int(eng.stats.get("steps", 0)), "pci": dev}
+    if dev.startswith("cuda"):
+        idx = torch.device(dev).index or 0
+        p = torch.cuda.get_device_properties(idx)
+        rec.update(device_index=idx, pci=f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+                   uuid=str(getattr(p, "uuid", "")), visible_devices=os.environ.get("HIP_VISIBLE_DEVICES",
+                                                                                    os.environ.get("CUDA_VISIBLE_DEVICES")))
+    return rec
+
+
 def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
     import torch
 
@@ -440,11 +459,30 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
 
     ttfts = sorted(timing["ttft"])
     extra = timing["extra"]
+    me = _rank_record(args, rank, dev, timing, elapsed, eng)
+    ranks = [me]
+    dist_info = {"initialized": False}
     if world > 1:
         import torch.distributed as dist
 
         # gloo over the host: the result exchange needs no device collective
         g = dist.new_group(list(range(world)), backend="gloo")
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me, group=g)
+        st = pstate.get()
+        dist_info = {"initialized": True, "backend": dist.get_backend(), "world_size": dist.get_world_size()}
+        if st.tp_group is not None:
+            dist_info.update(tp_backend=dist.get_backend(st.tp_group), tp_group_size=dist.get_world_size(st.tp_group))
+        if getattr(st, "ep_group", None) is not None:
+            dist_info.update(ep_backend=dist.get_backend(st.ep_group), ep_group_size=dist.get_world_size(st.ep_group))
+        if dev.startswith("cuda"):
+            seen = {}
+            for r in ranks:
+                key = r["pci"]
+                if key in seen:
+                    raise SystemExit(f"bench.py: ranks {seen[key]} and {r['rank']} resolved to the same GPU {key} "
+                                     "(check LOCAL_RANK / HIP_VISIBLE_DEVICES)")
+                seen[key] = r["rank"]
         stats = torch.tensor([timing["out_tokens"], elapsed, extra], dtype=torch.float64)
         toks = stats[:1].clone()
         dist.all_reduce(toks, group=g)
@@ -492,6 +530,12 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
         "planned_late_frac": round(eng.stats.get("planned_late", 0) / max(1, eng.stats.get("steps", 1)), 4),
         "step_rows_hist": dict(zip(("<=64", "65-96", "97-128", "129-256", ">256"), eng.runner.rows_hist)),
         "grammar_rollbacks": eng.stats.get("grammar_rollbacks", 0),
+        # self-verification of multi-GPU runs: one record per rank (which GPU it ran on, its own rate and step time;
+        # TP followers report 0 tokens: their leader streams the replica's tokens) and the process groups' backends /
+        # sizes as torch.distributed reports them (backend "nccl" is RCCL on ROCm)
+        "ranks": world,
+        "per_rank": ranks,
+        "dist": dist_info,
     }
     if rank == 0:
         line = json.dumps(res)

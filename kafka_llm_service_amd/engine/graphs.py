@@ -63,7 +63,7 @@ class DecodeGraphs:
         # DP attention: the step's all-to-all capacity (agreed by the group, bucketed) is baked into the captured
         # MoE layers, so it is part of the layout
         cap = self.runner.model.ep_t_cap if getattr(self.runner.model, "dp_attention", False) else 0
-        return (h.B, h.n_dec_items, h.dec_sk, h.s_total, h.n_prefix_items, bool(h.cascade_prefix), h.i64.size, h.i32.size,
+        return (h.B, h.n_dec_items, h.s_total, h.n_prefix_items, bool(h.cascade_prefix), h.i64.size, h.i32.size,
                 h.n_late, h.late_off, sp.greedy, sp.proc is not None, cap)
 
     def eligible(self, h, sp) -> bool:

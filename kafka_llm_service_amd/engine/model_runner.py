@@ -42,7 +42,6 @@ class HostStep:
     n_rows: int = 0
     s_total: int = 1        # partial slots per decode row (cascade prefix chunks + suffix pieces)
     n_dec_items: int = 0
-    dec_sk: int = 0         # stream-K decode workgroups (0: work-item decode); i32 holds rows [B + 1, 4] + start [dec_sk, 2]
     n_prefix_items: int = 0
     cascade_prefix: int = 0  # longest cascade prefix of the step (tokens; 0 = no cascade)
     n_items: int = 0
@@ -73,7 +72,7 @@ class SampleParams:
 
 
 _PLAN_SCALARS = ("B", "T", "nbt", "bt_w", "n_rows", "s_total", "n_dec_items", "n_prefix_items", "cascade_prefix",
-                 "n_items", "prefill_splits", "n_merge", "n_late", "late_off", "bt_need", "dec_sk")
+                 "n_items", "prefill_splits", "n_merge", "n_late", "late_off", "bt_need")
 PLAN_HDR = 32  # int64 header of a broadcast step plan
 PLAN_PAYLOAD_IDX = 1 + len(_PLAN_SCALARS) + 4  # header word holding the payload size (pack_plan)
 
@@ -162,14 +161,9 @@ MIN_DECODE_KEYS = 256      # smallest key range of one decode work item
 # +0.2-0.4 % over 1,152, same boxes (profiles/r03/decode_occ3/decode_target_ab_*.jsonl; 768 was best at two per CU,
 # profiles/r02/decode_items_ab.jsonl)
 ROWS_BUCKETS = (64, 96, 128, 256, 1 << 30)  # step-size histogram buckets (decode GEMM row-tile plans, skinny, BLAS)
-DECODE_TARGET_ITEMS = int(os.environ.get("KAFKA_DECODE_TARGET", "1344"))
+DECODE_TARGET_ITEMS = 1344  # (768 / 1536 / 2304 lose to it: profiles/r04/bench_ab_decode_target_blas.jsonl)
 MAX_PARTIALS = 64           # partial slots per row that the decode kernel's fused merge reads (one lane each)
 MAX_PREFIX_CHUNKS = 32
-# Decode attention as stream-K slices (ops.decode_sk_plan: every workgroup the same KV bytes + per-piece overhead)
-# instead of work items that the dispatcher runs in ~2 rounds of uneven length. KAFKA_DECODE_SK=0/1.
-DECODE_SK = os.environ.get("KAFKA_DECODE_SK", "0") == "1"
-# one H2D copy per step for the plan + sampling parameters (KAFKA_BATCH_UPLOAD=0: one copy per array)
-BATCH_UPLOAD = os.environ.get("KAFKA_BATCH_UPLOAD", "1") == "1"
 
 
 def pad_step_rows(T: int) -> int:
@@ -395,12 +389,11 @@ class ModelRunner:
                          and os.environ.get("KAFKA_PAD_ROWS", "1") == "1")
         self.tile = ops.tile_rows(self.variant) // self.G  # tokens per attention work item
         # the v3 cascade hands its prefix partials to the decode kernel as bf16 (normalised O, fp32 lse): ~33 MB
-        # less HBM traffic per Llama-3-8B layer at 64 threads on an 18k prefix (KAFKA_CASCADE_BF16=0: fp32)
-        self.cascade_bf16 = self.variant == 3 and os.environ.get("KAFKA_CASCADE_BF16", "1") != "0"
+        # less HBM traffic per Llama-3-8B layer at 64 threads on an 18k prefix (+1.4 %,
+        # profiles/r03/bench_ab_cascade_bf16_partials.jsonl)
+        self.cascade_bf16 = self.variant == 3
         self.cascade_min_prefix = cascade_min_prefix
-        self.target_wgs = int(os.environ.get("KAFKA_CASCADE_WGS", target_wgs))
-        # workgroups of the cascade's prefix pass alone (KAFKA_PREFIX_WGS; fewer leave CUs to an overlapped decode)
-        self.prefix_wgs = int(os.environ.get("KAFKA_PREFIX_WGS", self.target_wgs))
+        self.target_wgs = target_wgs  # workgroups the prefill / cascade tile launches are balanced for
         self.prefill_kv_chunk = int(os.environ.get("KAFKA_PREFILL_KV_CHUNK", prefill_kv_chunk))
         self.use_cascade = use_cascade
         self.vocab = model.cfg.vocab_size
@@ -508,7 +501,7 @@ class ModelRunner:
             if groups:
                 # key chunks sized so the prefix pass launches ~target_wgs workgroups over all groups together
                 work = sum(-(-n // self.tile) * p * PAGE for n, p in groups)
-                want = max(1, self.prefix_wgs // self.model.hkv)
+                want = max(1, self.target_wgs // self.model.hkv)
                 chunk = min(MAX_ITEM_KEYS, max(256, -(-work // (want * 32)) * 32))
                 r0 = 0
                 for n, p in groups:
@@ -525,13 +518,7 @@ class ModelRunner:
                     npre[r0:r0 + n] = nc
                     h.cascade_prefix = max(h.cascade_prefix, P)
                     r0 += n
-            if DECODE_SK:
-                rows_sk, start_sk, h.s_total = ops.decode_sk_plan(seq_lens, kv_start, npre, self.model.hkv)
-                h.dec_sk = int(start_sk.shape[0])
-                i32_parts.append(rows_sk.reshape(-1))
-                i32_parts.append(start_sk.reshape(-1))
-            else:
-                self._plan_decode_items(h, seq_lens, kv_start, npre, i32_parts)
+            self._plan_decode_items(h, seq_lens, kv_start, npre, i32_parts)
             if pit:
                 h.n_prefix_items = len(pit)
                 i32_parts.append(np.asarray(pit, dtype=np.int32).reshape(-1))
@@ -548,7 +535,7 @@ class ModelRunner:
         h.i64 = np.concatenate([tokens, positions, slots, np.asarray(logit_rows, dtype=np.int64)])
         h.i32 = np.concatenate(i32_parts)
         h.stats = {"B": B, "T": T, "cascade_prefix": h.cascade_prefix, "cascade_groups": len(groups),
-                   "decode_items": h.n_dec_items, "decode_sk": h.dec_sk, "prefix_items": h.n_prefix_items, "s_total": h.s_total,
+                   "decode_items": h.n_dec_items, "prefix_items": h.n_prefix_items, "s_total": h.s_total,
                    "prefill_splits": h.prefill_splits}
         return h, sample_seqs
 
@@ -568,8 +555,6 @@ class ModelRunner:
         """One H2D copy of the packed buffers (and of the step's sampling parameters when ``sp`` samples with
         temperature: left in ``self._sp_dev`` for ``sample_device``), then views into it (identical on every TP
         rank)."""
-        if not BATCH_UPLOAD:
-            return self.views(self._h2d(h.i64), self._h2d(h.i32), h)
         arrays = [h.i64, h.i32]
         if sp is not None and not sp.greedy and sp.temp.shape[0]:
             arrays += [np.concatenate([sp.temp, sp.topp]), sp.topk, sp.seeds]
@@ -596,14 +581,8 @@ class ModelRunner:
         o += T
         Hq, D = self.model.hq, self.model.D
         if B:
-            if h.dec_sk:
-                meta.decode_sk_rows = d32[o:o + (B + 1) * 4].view(B + 1, 4)
-                o += (B + 1) * 4
-                meta.decode_sk_start = d32[o:o + h.dec_sk * 2].view(h.dec_sk, 2)
-                o += h.dec_sk * 2
-            else:
-                meta.decode_items = d32[o:o + h.n_dec_items * 8].view(-1, 8)
-                o += h.n_dec_items * 8
+            meta.decode_items = d32[o:o + h.n_dec_items * 8].view(-1, 8)
+            o += h.n_dec_items * 8
             if h.n_prefix_items:
                 meta.prefix_items = d32[o:o + h.n_prefix_items * 8].view(-1, 8)
                 o += h.n_prefix_items * 8

@@ -18,7 +18,6 @@ the decode path is hipGraph-capturable (fixed shapes per batch bucket).
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field
 
 import torch
@@ -33,8 +32,6 @@ class AttnMeta:
     block_tables: torch.Tensor | None = None   # int32 [rows, W]; rows [0,B) decode seqs, then prefill seqs
     # decode
     decode_items: torch.Tensor | None = None   # int32 [n, 8] (b, lo, hi, split, nsplit, npre, 0, 0)
-    decode_sk_rows: torch.Tensor | None = None  # stream-K decode instead (ops.decode_sk_plan): int32 [B + 1, 4]
-    decode_sk_start: torch.Tensor | None = None  # int32 [nwg, 2]
     prefix_items: torch.Tensor | None = None   # int32 [m, 8] cascade prefix work items (rows = decode tokens)
     s_total: int = 1                           # partial slots per decode row
     part: torch.Tensor | None = None           # f32 [B, Hq, s_total, D]
@@ -54,20 +51,6 @@ class AttnMeta:
     extra: dict = field(default_factory=dict)
 
 
-# Mixed steps: the new-turn prefill tiles (MFMA/LDS-bound) are independent of the decode path (HBM-bound) inside a
-# layer — both read the post-RoPE q and write disjoint rows of out — so with KAFKA_PREFILL_STREAM=1 they run on a
-# side stream concurrently with the cascade + decode kernels (joined before the O projection).
-PREFILL_STREAM = os.environ.get("KAFKA_PREFILL_STREAM", "0") == "1"
-_SIDE: dict = {}
-
-
-def _side_stream(dev: torch.device):
-    s = _SIDE.get(dev)
-    if s is None:
-        s = _SIDE[dev] = (torch.cuda.Stream(device=dev), [torch.cuda.Event() for _ in range(2)])
-    return s
-
-
 def _prefill_part(q, k_cache, v_cache, meta: AttnMeta, out: torch.Tensor) -> None:
     B = meta.num_decode
     if meta.prefill_splits:
@@ -82,50 +65,20 @@ def _prefill_part(q, k_cache, v_cache, meta: AttnMeta, out: torch.Tensor) -> Non
 
 
 def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, meta: AttnMeta,
-                    out: torch.Tensor, gates=None) -> int:
-    """q [T, Hq, D] (post-RoPE) -> out [T, Hq, D] bf16. ``gates`` = (ops.GateSet, gate id the q / KV writer arrives
-    on) on an early-launched decode-only step (models/llama.py EARLY): the cascade streams its prefix K/V before q is
-    ready, the suffix decode runs beside it and waits for its partials only before the merge. Returns the gate the
-    decode arrives on (-1: none). With ``(GateSet, -1)`` (models/llama.py ATTN_OVERLAP) only the decode is launched
-    early: it runs beside the cascade and waits for the cascade's partials before its merge."""
+                    out: torch.Tensor) -> None:
+    """q [T, Hq, D] (post-RoPE) -> out [T, Hq, D] bf16."""
     B = meta.num_decode
-    gs, g_in = gates if gates is not None else (None, -1)
-    has_prefill = meta.prefill_items is not None and meta.num_tokens > B
-    side = None
-    if has_prefill and B > 0 and PREFILL_STREAM and q.is_cuda and not torch.cuda.is_current_stream_capturing():
-        side, (ev_q, ev_done) = _side_stream(q.device)
-        main = torch.cuda.current_stream(q.device)
-        ev_q.record(main)
-        with torch.cuda.stream(side):
-            side.wait_event(ev_q)
-            _prefill_part(q, k_cache, v_cache, meta, out)
-            ev_done.record(side)
-    g_out = -1
     if B > 0:
         qd = q[:B]
-        g_pre = -1
         if meta.prefix_items is not None:
-            if gs is not None:
-                g_pre = gs.new()
             ops.attn_prefill(meta.prefix_items, qd, k_cache, v_cache, meta.block_tables, meta.q_limit,
                              meta.scale, out_part=meta.pre_part if meta.pre_part is not None else meta.part,
-                             lse_part=meta.lse, variant=meta.variant,
-                             gates=gs.args(wait=g_in, sig=g_pre) if gs is not None else None)
+                             lse_part=meta.lse, variant=meta.variant)
         # the decode kernel merges each row's prefix partials and its own pieces and writes the final rows
-        if meta.decode_sk_rows is not None:
-            ops.attn_decode_sk(qd, k_cache, v_cache, meta.block_tables, meta.decode_sk_rows, meta.decode_sk_start,
-                               meta.part, meta.lse, meta.scale, out=out[:B], pre_part=meta.pre_part)
-        else:
-            if gs is not None and g_in >= 0:  # (g_in = -1: only the cascade -> decode overlap is gated)
-                g_out = gs.new()
-            ops.attn_decode_items(qd, k_cache, v_cache, meta.block_tables, meta.decode_items, meta.part, meta.lse,
-                                  meta.scale, out=out[:B], pre_part=meta.pre_part,
-                                  gates=gs.args(wait=g_in, sig=g_out, wait2=g_pre) if gs is not None else None)
-    if side is not None:
-        torch.cuda.current_stream(q.device).wait_event(ev_done)
-    elif has_prefill:
+        ops.attn_decode_items(qd, k_cache, v_cache, meta.block_tables, meta.decode_items, meta.part, meta.lse,
+                              meta.scale, out=out[:B], pre_part=meta.pre_part)
+    if meta.prefill_items is not None and meta.num_tokens > B:
         _prefill_part(q, k_cache, v_cache, meta, out)
-    return g_out
 
 
 def default_scale(head_dim: int) -> float:

@@ -27,13 +27,6 @@ from kafka_llm_service_amd.models.attention import AttnMeta, paged_attention
 from kafka_llm_service_amd.models.config import ModelConfig
 from kafka_llm_service_amd.parallel import state as pstate
 
-# env KAFKA_FUSE_QKV_ROPE=1: decode-sized steps run RoPE + the paged KV write in the streaming QKV GEMM's epilogue
-# (ops.linear_stream_rope) instead of the rope_kv kernel. Correct (tests/test_kernels_gpu.py::test_wstream_qkv_rope)
-# but measured 4 % SLOWER (7,160 vs 7,477 tok/s, profiles/r02/qkv_rope_fused_ab_rejected.jsonl): the split-K ticket
-# adds write-through partial stores, a device-scope atomic and uncached partial loads to the GEMM's tail — more
-# serialized round trips than the 5.7 us rope_kv launch it removes. Off by default.
-FUSE_QKV_ROPE = os.environ.get("KAFKA_FUSE_QKV_ROPE", "0") == "1"
-
 # TP decode seam overlap (KAFKA_TP_OVERLAP=1): the row-parallel O / down projection of a decode-sized step is
 # computed in two column halves; half 0's all-reduce runs on a second HIP stream (into a persistent buffer) while half
 # 1's GEMM streams its weights on the main one, then ONE launch on the main stream all-reduces half 1, joins half 0
@@ -55,23 +48,6 @@ PIPE_CHUNKS = max(1, int(os.environ.get("KAFKA_TP_PIPE_CHUNKS", "4")))
 PIPE_ROWS = 256
 SKINNY = frozenset(p for p in os.environ.get("KAFKA_SKINNY", "qkv,o,down").replace("+", ",").split(",")
                    if p in ("qkv", "o", "down", "gate_up"))  # gate_up: fused SwiGLU epilogue (A/B, not default)
-# Early-launched decode layers (env KAFKA_EARLY; ops.GateSet, csrc/common.h Gates). On a decode-only step of the
-# weight-streaming path every kernel of a layer after its input RMSNorm — QKV projection, RoPE/KV write, cascade,
-# suffix decode, O projection, gate_up, down — is launched without the AQL barrier bit: it is dispatched while its
-# predecessor's last workgroups still run, does the part of its work that does not depend on them (a projection's
-# first weight chunk, the cascade's page table and first prefix K/V tiles) and then waits on a device gate the
-# predecessor's workgroups arrive on. The suffix decode even runs BESIDE the cascade (both read only q / the KV cache)
-# and waits for the cascade's partials only before its merge. The two post-attention / post-MLP RMSNorms stay ordinary
-# launches (full barriers), so each chain is short and every gate waits on the kernel launched right before it.
-EARLY = os.environ.get("KAFKA_EARLY", "0") == "1"
-# Overlapped attention (env KAFKA_ATTN_OVERLAP): only the suffix decode is launched without the barrier bit, so its
-# workgroups take the CUs the cascade's ~256 tile workgroups leave free (and each CU a tile workgroup finishes)
-# instead of waiting for the cascade's last one; it waits for the cascade's partials (a write-through hand-off:
-# no release / acquire fences, csrc/common.h st_wt16) only before its merge.
-ATTN_OVERLAP = os.environ.get("KAFKA_ATTN_OVERLAP", "0") == "1"
-# gate_up of steps up to this many rows on the streaming kernel (two XCD-shared row tiles beyond 128) instead of
-# hipBLASLt + silu_mul (env KAFKA_STREAM_GU_MAX_M; 0 = the model's stream_max_m)
-STREAM_GU_MAX_M = min(256, int(os.environ.get("KAFKA_STREAM_GU_MAX_M", "0")))
 _OVL: dict = {}
 _SEAM_DONE = object()  # forward(): the previous layer's overlapped seam already produced this layer's input
 
@@ -136,10 +112,6 @@ class TransformerLM:
         self.stream = False  # decode GEMMs on the weight-streaming kernel (enable_stream_weights)
         self.tiled_only = False  # row-major dense weights dropped (enable_stream_weights(tiled_only=True))
         self.stream_max_m = ops.STREAM_MAX_M  # rows up to which a step's projections stream
-        self.early = EARLY  # early-launched decode layers (see EARLY)
-        self._gates: ops.GateSet | None = None
-        self.attn_overlap = ATTN_OVERLAP
-        self._agates: ops.GateSet | None = None  # the overlapped attention's gates (one per layer)
 
     def enable_dp_attention(self, ep: int, ep_rank: int) -> None:
         """Data-parallel attention for a MoE model (call before the weights are created): attention, norms and the
@@ -221,46 +193,16 @@ class TransformerLM:
         return added
 
     def _linear(self, x: torch.Tensor, w: torch.Tensor, wt: torch.Tensor | None, max_splits: int = 8,
-                kind: str = "", gates=None):
+                kind: str = ""):
         """x @ w^T: the weight-streaming kernel for decode-sized x (bf16 or a split-K slab out), the skinny MFMA GEMM
-        for 129..256 rows of the projections in SKINNY, else hipBLASLt. ``gates``: streaming path only."""
+        for 129..256 rows of the projections in SKINNY, else hipBLASLt."""
         M = x.shape[0]
         if self.stream and wt is not None:
             if 0 < M <= self.stream_max_m:
-                return ops.linear_stream(x, wt, max_splits, gates=gates)
+                return ops.linear_stream(x, wt, max_splits)
             if kind in SKINNY and ops.skinny_plan(M, wt.shape[0] * 32, x.shape[1], max_splits):
                 return ops.linear_skinny(x, wt, max_splits)
         return F.linear(x, self._dense(w, wt))
-
-    def _gateset(self, T: int, inp: StepInput, k_cache: torch.Tensor, fuse_rope: bool) -> "ops.GateSet | None":
-        """The forward's device gates when this step runs early-launched layers (EARLY), else None."""
-        m = inp.attn
-        if not (self.early and self.stream and self.tp == 1 and self.moe is None and self.device.type == "cuda"):
-            return None
-        if fuse_rope or not (0 < T <= min(128, self.stream_max_m)) or m.num_decode != T or m.prefill_items is not None:
-            return None
-        if k_cache.dtype != torch.bfloat16 or m.decode_sk_rows is not None or m.decode_items is None:
-            return None
-        if (m.prefix_items is not None and m.variant != 3) or torch.cuda.is_current_stream_capturing():
-            return None
-        if self._gates is None:
-            self._gates = ops.GateSet(self.device, 12 * len(self.layers) + 8)
-        self._gates.begin()
-        return self._gates
-
-    def _attn_gateset(self, inp: StepInput, k_cache: torch.Tensor) -> "ops.GateSet | None":
-        """The forward's attention gates when the suffix decode overlaps the cascade (ATTN_OVERLAP), else None."""
-        m = inp.attn
-        if not (self.attn_overlap and self.device.type == "cuda" and m.num_decode > 0):
-            return None
-        if m.prefix_items is None or m.variant != 3 or m.decode_items is None or m.decode_sk_rows is not None:
-            return None
-        if k_cache.dtype != torch.bfloat16 or torch.cuda.is_current_stream_capturing():
-            return None
-        if self._agates is None:
-            self._agates = ops.GateSet(self.device, len(self.layers) + 8)
-        self._agates.begin()
-        return self._agates
 
     @staticmethod
     def _dense(w: torch.Tensor | None, wt: torch.Tensor | None, glu: bool = False) -> torch.Tensor:
@@ -286,24 +228,7 @@ class TransformerLM:
         eps = cfg.rms_norm_eps
         tp = self.tp > 1
         delta, pending = None, False
-        fuse_rope = (self.stream and FUSE_QKV_ROPE and 0 < T <= min(128, self.stream_max_m) and self.layers[0].qkv_t is not None
-                     and ops.qkv_rope_fusable(k_caches[0], self.D))
-        gs = self._gateset(T, inp, k_caches[0], fuse_rope)
-        ga = self._attn_gateset(inp, k_caches[0]) if gs is None else None
-        # gate_up + down gated only with the one-split (fused SwiGLU) plan: a split plan puts silu_mul between them
-        glu_gated = gs is not None and self.layers[0].glu and \
-            (ops.stream_plan(T, self.layers[0].gate_up_t.shape[0] * 32, cfg.hidden_size) or (0, 0, 0))[2] == 1
-
-        def G(wait: int = -1, sig: int = -1, wait2: int = -1):
-            return gs.args(wait=wait, sig=sig, wait2=wait2) if gs is not None else None
-
-        def new() -> int:
-            return gs.new() if gs is not None else -1
-
-        g_down = -1
         for i, lw in enumerate(self.layers):
-            g_in = -1  # gate the input RMSNorm arrives on (-1: the QKV projection is an ordinary launch)
-            g_prev, g_down = (g_down if gs is not None and i > 0 else -1), -1
             if delta is _SEAM_DONE:
                 pass  # the previous layer's overlapped down seam already wrote residual and x
             elif delta is None:
@@ -314,26 +239,12 @@ class TransformerLM:
             elif pending:
                 pstate.tp_all_reduce_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x)
             else:
-                g_in = new()
-                ops.fused_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x, gates=G(wait=g_prev, sig=g_in))
-            g_rope = -1  # gate the RoPE / KV write arrives on (the attention kernels' input)
-            if fuse_rope:  # RoPE + KV write in the streaming QKV GEMM's epilogue (no rope_kv launch)
-                ops.linear_stream_rope(x, lw.qkv_t, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i],
-                                       inp.slot_mapping, self.hq, self.hkv)
-            else:
-                g_qkv = new()
-                qkv = self._linear(x, lw.qkv, lw.qkv_t, kind="qkv", gates=G(wait=g_in, sig=g_qkv))
-                g_rope = new()
-                ops.rope_kv_write(qkv, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i], inp.slot_mapping,
-                                  self.hq, self.hkv, gates=G(wait=g_qkv, sig=g_rope))
-            g_attn = paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out,
-                                     gates=(gs, g_rope) if gs is not None else ((ga, -1) if ga is not None else None))
-            if gs is not None:  # the O projection streams its first weight chunk beside the decode's tail
-                g_o = new()
-                o = self._linear(attn_out.view(T, -1), lw.o, lw.o_t, kind="o", gates=G(wait=g_attn, sig=g_o))
-                g_post = new() if glu_gated else -1
-                ops.fused_add_rmsnorm(o, residual, lw.post_norm, eps, out=x, gates=G(wait=g_o, sig=g_post))
-            elif tp and self._can_overlap(T, lw.o_t):
+                ops.fused_add_rmsnorm(delta, residual, lw.input_norm, eps, out=x)
+            qkv = self._linear(x, lw.qkv, lw.qkv_t, kind="qkv")
+            ops.rope_kv_write(qkv, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i], inp.slot_mapping,
+                              self.hq, self.hkv)
+            paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out)
+            if tp and self._can_overlap(T, lw.o_t):
                 self._overlapped_seam(attn_out.view(T, -1), lw.o_t, residual, lw.post_norm, eps, x)
             elif tp and self._can_pipe(T, lw.o, lw.o_t):
                 o = pstate.tp_linear_all_reduce(attn_out.view(T, -1), self._dense(lw.o, lw.o_t), self._pipe_chunks(T))
@@ -347,32 +258,26 @@ class TransformerLM:
             if lw.router is not None:
                 delta = self.moe(x, lw)
                 pending = tp and not self.moe.reduced
-            elif glu_gated:
-                g_gu = new()
-                a = ops.linear_glu(x, lw.gate_up_t, gates=G(wait=g_post, sig=g_gu))
-                g_down = new() if i + 1 < len(self.layers) else -1  # the next input RMSNorm waits on it
-                delta = self._linear(a, lw.down, lw.down_t, kind="down", gates=G(wait=g_gu, sig=g_down))
-                pending = False
+                continue
+            if self.stream and lw.glu and 0 < T <= self.stream_max_m:
+                a = ops.linear_glu(x, lw.gate_up_t)  # SwiGLU in the GEMM epilogue (or on its slabs)
+            elif (self.stream and lw.glu and "gate_up" in SKINNY and lw.gate_up_t is not None
+                  and ops.skinny_plan(T, lw.gate_up_t.shape[0] * 32, x.shape[1])):
+                a = ops.linear_skinny(x, lw.gate_up_t, glu=True)  # fused SwiGLU (one split) or gate | up slabs
+                if ops.is_slab(a):
+                    a = ops.silu_mul(a)
             else:
-                if self.stream and lw.glu and 0 < T <= max(self.stream_max_m, STREAM_GU_MAX_M):
-                    a = ops.linear_glu(x, lw.gate_up_t)  # SwiGLU in the GEMM epilogue (or on its slabs)
-                elif (self.stream and lw.glu and "gate_up" in SKINNY and lw.gate_up_t is not None
-                      and ops.skinny_plan(T, lw.gate_up_t.shape[0] * 32, x.shape[1])):
-                    a = ops.linear_skinny(x, lw.gate_up_t, glu=True)  # fused SwiGLU (one split) or gate | up slabs
-                    if ops.is_slab(a):
-                        a = ops.silu_mul(a)
-                else:
-                    a = ops.silu_mul(F.linear(x, self._dense(lw.gate_up, lw.gate_up_t, bool(lw.glu))))
-                if tp and self._can_overlap(T, lw.down_t) and i + 1 < len(self.layers):
-                    # the next layer's input RMSNorm is the seam's normalisation: delta is consumed here
-                    self._overlapped_seam(a, lw.down_t, residual, self.layers[i + 1].input_norm, eps, x)
-                    delta, pending = _SEAM_DONE, False
-                elif tp and self._can_pipe(T, lw.down, lw.down_t):
-                    delta = pstate.tp_linear_all_reduce(a, self._dense(lw.down, lw.down_t), self._pipe_chunks(T))
-                    pending = False  # already reduced: the next seam is a plain add + RMSNorm
-                else:
-                    delta = self._linear(a, lw.down, lw.down_t, kind="down")
-                    pending = tp
+                a = ops.silu_mul(F.linear(x, self._dense(lw.gate_up, lw.gate_up_t, bool(lw.glu))))
+            if tp and self._can_overlap(T, lw.down_t) and i + 1 < len(self.layers):
+                # the next layer's input RMSNorm is the seam's normalisation: delta is consumed here
+                self._overlapped_seam(a, lw.down_t, residual, self.layers[i + 1].input_norm, eps, x)
+                delta, pending = _SEAM_DONE, False
+            elif tp and self._can_pipe(T, lw.down, lw.down_t):
+                delta = pstate.tp_linear_all_reduce(a, self._dense(lw.down, lw.down_t), self._pipe_chunks(T))
+                pending = False  # already reduced: the next seam is a plain add + RMSNorm
+            else:
+                delta = self._linear(a, lw.down, lw.down_t, kind="down")
+                pending = tp
         if pending:
             delta = pstate.tp_all_reduce(delta)
         rows = inp.logit_rows

@@ -49,66 +49,16 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | No
     return out
 
 
-class GateSet:
-    """Device gates of one forward (csrc/common.h ``Gates``): a consumer kernel launched without the AQL barrier bit
-    runs its producer-independent prologue (a projection's first weight chunk, the cascade's prefix K/V tiles) while
-    its producer's tail still runs, and waits on the gate the producer's workgroups arrive on before it reads their
-    outputs. ``begin`` zeroes the gates (an ordinary launch: it waits for everything before it) at the start of a
-    forward; ``new`` hands out gate ids in launch order. The caller's rules: a gated consumer waits on the kernel
-    launched immediately before it and writes nothing before its wait (gates chain transitively, so the caching
-    allocator's stream-order reuse stays safe)."""
-
-    INTS = 17 * 16  # GATE_INTS: 8 arrival-counter lines, the top counter (+ error word), 8 per-XCD done flags
-
-    def __init__(self, device: torch.device, n: int):
-        self.n = n
-        self.buf = torch.zeros(n * self.INTS, dtype=torch.int32, device=device)
-        self.used = 0
-        self.forwards = 0  # forwards that ran gated (stats, tests)
-
-    def begin(self) -> None:
-        self.buf.zero_()
-        self.used = 0
-        self.forwards += 1
-
-    def new(self) -> int:
-        if self.used >= self.n:
-            raise RuntimeError("GateSet: out of gates")
-        self.used += 1
-        return self.used - 1
-
-    def args(self, wait: int = -1, expect: int = 0, sig: int = -1, wait2: int = -1, expect2: int = 0):
-        """The (buffer, args) pair the gated ops take."""
-        return self.buf, [int(wait), int(expect), int(sig), int(wait2), int(expect2)]
-
-    def timed_out(self) -> bool:
-        """Whether any wait of the last forward gave up (host sync: tests and diagnostics)."""
-        return bool(self.buf.view(-1, self.INTS)[:, 8 * 16 + 1].any().item())
-
-    def arrivals(self, g: int) -> int:
-        return int(self.buf.view(-1, self.INTS)[g, 0:8 * 16:16].sum().item())
-
-    def released(self, g: int) -> bool:
-        return bool(self.buf.view(-1, self.INTS)[g, 9 * 16:17 * 16:16].all().item())
-
-
-def _gk(gates) -> dict:
-    """Binding kwargs of an optional (GateSet buffer, args) pair."""
-    return {} if gates is None else {"gates": gates[0], "gate_args": gates[1]}
-
-
 def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
-                      out: torch.Tensor | None = None, gates=None) -> torch.Tensor:
+                      out: torch.Tensor | None = None) -> torch.Tensor:
     """residual <- x + residual (in place); returns rmsnorm(residual) * w (into ``out`` or a new tensor).
-    ``x`` may be a split-K slab [S, T, d] (summed in fp32 before the add). ``gates``: GateSet.args (the kernel
-    arrives on ``sig`` once per row)."""
+    ``x`` may be a split-K slab [S, T, d] (summed in fp32 before the add)."""
     slab = is_slab(x)
     if out is None:
         out = torch.empty(residual.shape, dtype=residual.dtype, device=x.device)
     if _gpu(x):
         xa = x if slab else x.reshape(-1, x.shape[-1])
-        ext().fused_add_rmsnorm(out.view(-1, x.shape[-1]), xa, residual.view(-1, x.shape[-1]), w, float(eps),
-                                **_gk(gates))
+        ext().fused_add_rmsnorm(out.view(-1, x.shape[-1]), xa, residual.view(-1, x.shape[-1]), w, float(eps))
     else:
         y, s = ref.fused_add_rmsnorm(x.sum(0) if slab else x, residual, w, eps)
         residual.copy_(s)
@@ -130,13 +80,10 @@ def silu_mul(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     return out
 
 
-def rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq: int, Hkv: int,
-                  gates=None) -> None:
-    """RoPE on q/k + paged KV write; ``qkv`` is bf16 [T, W] or a split-K slab [S, T, W]. ``gates``: bf16 cache
-    only (the kernel waits on ``wait`` and arrives on ``sig`` once per workgroup)."""
+def rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq: int, Hkv: int) -> None:
+    """RoPE on q/k + paged KV write; ``qkv`` is bf16 [T, W] or a split-K slab [S, T, W]."""
     if _gpu(qkv):
-        ext().rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, int(Hq), int(Hkv),
-                            **_gk(gates))
+        ext().rope_kv_write(qkv, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, int(Hq), int(Hkv))
     else:
         ref.rope_kv_write(qkv.sum(0) if is_slab(qkv) else qkv, positions, cos_sin, q_out, k_cache, v_cache,
                           slot_mapping, Hq, Hkv)
@@ -147,8 +94,8 @@ _TICKETS: dict = {}
 
 def _tickets(dev: torch.device, n: int, pool: str = "decode") -> torch.Tensor:
     """Zeroed int32 counters for a kernel's ticket merge (re-armed by the kernel itself, so one buffer per device and
-    pool serves every layer and step; allocated once, large, so graph capture never allocates). Pools: "decode"
-    (decode attention, per row x kv head), "qkv_rope" (fused QKV epilogue, per head tile)."""
+    pool serves every layer and step; allocated once, large, so graph capture never allocates). Pool "decode":
+    decode attention, per row x kv head."""
     t = _TICKETS.get((dev, pool))
     if t is None or t.numel() < n:
         t = _TICKETS[(dev, pool)] = torch.zeros(max(n, 1 << 16), dtype=torch.int32, device=dev)
@@ -159,7 +106,7 @@ DECODE_ITEM = 8  # int32 fields of a decode work item: (b, lo, hi, split, nsplit
 
 
 def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale: float, out=None,
-                      pre_part=None, gates=None) -> None:
+                      pre_part=None) -> None:
     """Paged decode attention over work items (int32 [n, 8]: row b, key range [lo, hi), piece ``split`` of
     ``nsplit``, ``npre`` prefix partials in front). Each item writes its (O, lse2) partial to slot npre + split of
     [B, Hq, S_total, D]; with ``out`` (npre + nsplit <= 64 per row) the rows are instead merged with their prefix
@@ -169,93 +116,9 @@ def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_pa
     if _gpu(q):
         tk = _tickets(q.device, q.shape[0] * k_cache.shape[1]) if out is not None else None
         ext().attn_decode(q, k_cache, v_cache, block_tables, items, out_part, lse_part, float(scale), out, tk,
-                          pre_part, **_gk(gates))
+                          pre_part)
         return
     ref.attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale, out, pre_part)
-
-
-DECODE_SK_WGS = 512      # stream-K decode grid: two 4-wave workgroups per CU (the kernel's occupancy)
-DECODE_SK_F = int(os.environ.get("KAFKA_DECODE_SK_F", "4"))  # fixed cost of a piece, in 32-key blocks
-DECODE_SK_MAX_PARTIALS = 64
-
-
-def decode_sk_plan(seq_lens: np.ndarray, kv_start: np.ndarray, npre: np.ndarray, hkv: int,
-                   nwg: int = DECODE_SK_WGS, F: int = DECODE_SK_F) -> tuple[np.ndarray, np.ndarray, int]:
-    """Host plan of the stream-K decode kernel (csrc/attention.hip attn_decode_sk_kernel). Units (row b, kv head)
-    lie end to end on one cost line, unit (b, h) = F overhead blocks + nb_b 32-key blocks; workgroup w takes the
-    slice [w T, (w + 1) T). Returns (rows int32 [B + 1, 4] = (kv_lo, kv_hi, npre, C_b) + plan row (T, F, total, 0),
-    start int32 [nwg, 2] = first (row, kv head) per slice (row B: empty slice), partial slots per row)."""
-    lens = np.asarray(seq_lens, dtype=np.int64)
-    lo = np.asarray(kv_start, dtype=np.int64)
-    npre = np.asarray(npre, dtype=np.int64)
-    B = lens.shape[0]
-    a0 = lo - lo % 32
-    nb = np.where(lens > lo, (lens - a0 + 31) // 32, 0)
-    ucost = F + nb
-    rcost = hkv * ucost
-    C = np.zeros(B, dtype=np.int64)
-    if B > 1:
-        C[1:] = np.cumsum(rcost)[:-1]
-    total = int(rcost.sum())
-    # fewest blocks per slice that keep every unit within the fused merge's partial slots
-    room = max(1, DECODE_SK_MAX_PARTIALS - int(npre.max(initial=0)) - 1)
-    T = max(1, -(-total // nwg), -(-int(nb.max(initial=0)) // room))
-    s = np.arange(nwg, dtype=np.int64) * T
-    b = np.clip(np.searchsorted(C, s, side="right") - 1, 0, max(B - 1, 0))
-    kvh = np.minimum((s - C[b]) // np.maximum(ucost[b], 1), hkv - 1)
-    empty = s >= total
-    start = np.stack([np.where(empty, B, b), np.where(empty, 0, kvh)], 1).astype(np.int32)
-    rows = np.zeros((B + 1, 4), dtype=np.int32)
-    rows[:B, 0], rows[:B, 1], rows[:B, 2], rows[:B, 3] = lo, lens, npre, C
-    rows[B] = (T, F, total, 0)
-    # pieces per unit: slices its block range [C_u + F, C_u + F + nb) touches (same for every head of a row up to
-    # the offset; take the max over heads)
-    h = np.arange(hkv, dtype=np.int64)
-    bs = C[:, None] + h[None, :] * ucost[:, None] + F
-    pieces = np.where(nb[:, None] > 0, (bs + nb[:, None] - 1) // T - bs // T + 1, 1).max(1) if B else np.zeros(0)
-    s_total = int((npre + pieces).max(initial=1))
-    return rows, start, s_total
-
-
-def decode_sk_items(rows: np.ndarray, start: np.ndarray, hkv: int) -> list[tuple[int, int, int, int, int, int, int]]:
-    """The pieces a stream-K launch runs, as (b, kvh, lo, hi, split, nsplit, npre) — the kernel's walk mirrored on
-    the host (CPU reference path and tests)."""
-    B = rows.shape[0] - 1
-    T, F, total = int(rows[B, 0]), int(rows[B, 1]), int(rows[B, 2])
-    out = []
-    for w in range(start.shape[0]):
-        s0, e0 = w * T, min(w * T + T, total)
-        b, kvh = int(start[w, 0]), int(start[w, 1])
-        while b < B:
-            lo_b, hi_b, npre, c_b = (int(x) for x in rows[b])
-            a0 = lo_b & ~31
-            nb = (hi_b - a0 + 31) >> 5 if hi_b > lo_b else 0
-            cu = c_b + kvh * (F + nb)
-            if cu >= e0:
-                break
-            bs = cu + F
-            j0, j1 = max(s0, bs) - bs, min(e0, bs + nb) - bs
-            if j1 > j0 and nb > 0:
-                first, last = bs // T, (bs + nb - 1) // T
-                lo, hi = max(lo_b, a0 + 32 * j0), min(hi_b, a0 + 32 * j1)
-                out.append((b, kvh, lo, hi, w - first, last - first + 1, npre))
-            kvh += 1
-            if kvh == hkv:
-                kvh, b = 0, b + 1
-    return out
-
-
-def attn_decode_sk(q, k_cache, v_cache, block_tables, rows, start, out_part, lse_part, scale: float, out=None,
-                   pre_part=None) -> None:
-    """Stream-K paged decode (``decode_sk_plan``): every workgroup streams the same number of KV blocks; pieces write
-    partials at slot npre + split, whole units (or the last piece of a split one, by ticket) merge with the prefix
-    partials into ``out`` (see ``attn_decode_items`` for ``out`` / ``pre_part``)."""
-    if _gpu(q):
-        tk = _tickets(q.device, q.shape[0] * k_cache.shape[1]) if out is not None else None
-        ext().attn_decode_sk(q, k_cache, v_cache, block_tables, rows, start, out_part, lse_part, float(scale), out,
-                             tk, pre_part)
-        return
-    ref.attn_decode_sk(q, k_cache, v_cache, block_tables, rows, start, out_part, lse_part, scale, out, pre_part)
 
 
 def uniform_decode_items(seq_lens: torch.Tensor, kv_start: torch.Tensor | None, num_splits: int,
@@ -291,13 +154,12 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part,
 
 
 def attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, scale: float, out=None, out_part=None,
-                 lse_part=None, variant: int = 0, gates=None) -> None:
+                 lse_part=None, variant: int = 0) -> None:
     """Work-item paged attention (chunked prefill / cascade prefix). ``items`` is int32 [n, 8]:
-    (q_start, q_count, bt_row, kv_lo, kv_hi, split, 0, 0). ``gates`` (tile variant 3, cascade only: the key range
-    must not be written by this step) early-launch it: the prefix K/V streams in before q is ready."""
+    (q_start, q_count, bt_row, kv_lo, kv_hi, split, 0, 0)."""
     if _gpu(q):
         ext().attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, out, out_part, lse_part, float(scale),
-                           int(variant), **_gk(gates))
+                           int(variant))
     else:
         ref.attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale, out, out_part, lse_part)
 
@@ -372,27 +234,17 @@ STREAM_MAX_M = max(1, min(256, int(os.environ.get("KAFKA_STREAM_MAX_M", "128")))
 STREAM_KERNEL_MAX_M = 256
 
 
-_WSTREAM_TARGET = int(os.environ.get("KAFKA_WSTREAM_TARGET", "0"))  # A/B override of the split target (both sides)
-_WSTREAM_MT3 = os.environ.get("KAFKA_WSTREAM_MT3", "1") != "0"  # 65..96 rows on three row tiles (csrc mt3_off)
-_WSTREAM_MT4_KC256 = os.environ.get("KAFKA_WSTREAM_MT4_KC", "") == "256"  # A/B (csrc mt4_kc256)
-_WSTREAM_ROWSPLIT = os.environ.get("KAFKA_WSTREAM_ROWSPLIT", "0") == "1"  # 64-row tiles sharing L2 (csrc rowsplit_on)
-_WSTREAM_RT1 = os.environ.get("KAFKA_WSTREAM_RT1", "0") == "1"  # 33..64 rows as two 32-row tiles (csrc rt1_on)
-
-
-def stream_plan(M: int, N: int, K: int, max_splits: int = 8, one_tile: bool = False) -> tuple[int, int, int] | None:
+def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, int] | None:
     """(row tiles, K chunk, splits) of the decode GEMM for a shape, None if unsupported (same rule as
-    kafka_wstream_plan in csrc/wstream_gemm.hip, mirrored so CPU runs take the same split decisions). ``one_tile``:
-    all rows in one row tile (the fused QKV + RoPE kernel), so the row-split plan does not apply."""
+    kafka_wstream_plan in csrc/wstream_gemm.hip, mirrored so CPU runs take the same split decisions)."""
     if M < 1 or M > STREAM_KERNEL_MAX_M or N % 32 or N <= 0:
         return None
-    mt = 2 if _WSTREAM_ROWSPLIT and not one_tile and M > 64 else \
-        (1 if M <= 32 or (_WSTREAM_RT1 and not one_tile and M <= 64) else
-         (2 if M <= 64 else (3 if M <= 96 and _WSTREAM_MT3 else 4)))
-    kc = 128 if mt == 4 and not _WSTREAM_MT4_KC256 else 256
+    mt = 1 if M <= 32 else (2 if M <= 64 else (3 if M <= 96 else 4))
+    kc = 128 if mt == 4 else 256
     if K % kc or K <= 0:
         return None
     nx, chunks, s = (N + 127) // 128 * ((M + 32 * mt - 1) // (32 * mt)), K // kc, 1
-    target = _WSTREAM_TARGET or (256 if mt == 4 else 192)
+    target = 256 if mt == 4 else 192
     while s * 2 <= max_splits and s * 2 <= 8 and chunks % (s * 2) == 0 and nx * s < target:
         s *= 2
     return mt, kc, s
@@ -437,7 +289,7 @@ def linear_skinny(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, glu: b
 
 
 def linear_stream(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, nt: bool = True,
-                  glu: bool = False, gates=None) -> torch.Tensor:
+                  glu: bool = False) -> torch.Tensor:
     """y = x @ W^T for decode-sized M (<= 128) from the wave-tiled weight ``wt``: the weight-streaming MFMA kernel.
     Returns bf16 [M, N] when the plan has one split, else the fp32 split-K slabs [S, M, N] (a slab; the consumer
     kernels sum it while loading). ``glu`` (wt tiled with glu=True): a one-split plan returns the ACTIVATED
@@ -451,10 +303,10 @@ def linear_stream(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, nt: bo
     if _gpu(x):
         if S == 1:
             y = torch.empty(M, N // 2 if glu else N, dtype=x.dtype, device=x.device)
-            ext().wstream_gemm(x, wt, y, None, int(max_splits), bool(nt), bool(glu), **_gk(gates))
+            ext().wstream_gemm(x, wt, y, None, int(max_splits), bool(nt), bool(glu))
             return y
         p = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
-        ext().wstream_gemm(x, wt, None, p, int(max_splits), bool(nt), bool(glu), **_gk(gates))
+        ext().wstream_gemm(x, wt, None, p, int(max_splits), bool(nt), bool(glu))
         return p
     w = untile_weight(wt, glu).float()
     xf = x.float()
@@ -467,40 +319,12 @@ def linear_stream(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, nt: bo
     return torch.stack([xf[:, s * ks:(s + 1) * ks] @ w[:, s * ks:(s + 1) * ks].t() for s in range(S)])
 
 
-def qkv_rope_fusable(k_cache: torch.Tensor, D: int) -> bool:
-    """Whether linear_stream_rope covers this cache (bf16 pages, head dim 128; fp8 keeps rope_kv_write)."""
-    return D == 128 and k_cache.dtype == torch.bfloat16
-
-
-def linear_stream_rope(x, wt, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq: int, Hkv: int,
-                       max_splits: int = 8, gates=None) -> None:
-    """QKV projection of a decode-sized step (wave-tiled weight ``wt``, N = (Hq + 2 Hkv) * 128) with RoPE and the
-    paged KV write fused into the streaming GEMM's epilogue: the same results as ``linear_stream`` followed by
-    ``rope_kv_write``, without the rope_kv launch (the last split-K workgroup of each head tile finishes it)."""
-    M, K = x.shape
-    N = wt.shape[0] * 32
-    plan = stream_plan(M, N, K, max_splits, one_tile=True)
-    if plan is None or N != (Hq + 2 * Hkv) * 128:
-        raise ValueError(f"linear_stream_rope: unsupported shape M={M} N={N} K={K}")
-    if _gpu(x):
-        S = plan[2]
-        p = torch.empty(S, M, N, dtype=torch.float32, device=x.device) if S > 1 else None
-        ext().wstream_qkv_rope(x, wt, p, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, int(Hq),
-                               int(Hkv), _tickets(x.device, N // 128, pool="qkv_rope"), int(max_splits),
-                               **_gk(gates))
-        return
-    rope_kv_write(linear_stream(x, wt, max_splits), positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq,
-                  Hkv)
-
-
-def linear_glu(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8, gates=None) -> torch.Tensor:
+def linear_glu(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8) -> torch.Tensor:
     """silu(x @ Wg^T) * (x @ Wu^T) from GLU-tiled gate_up weights: fused into the GEMM epilogue when the plan has one
-    split, else the GEMM's slabs go through silu_mul (``gates`` only with one split: ``glu_fused``)."""
+    split, else the GEMM's slabs go through silu_mul."""
     N = wt.shape[0] * 32
     plan = stream_plan(x.shape[0], N, x.shape[1], max_splits)
-    if gates is not None and not (plan is not None and plan[2] == 1):
-        raise ValueError("linear_glu: gates need the one-split (fused SwiGLU) plan")
-    y = linear_stream(x, wt, max_splits, glu=True, gates=gates)
+    y = linear_stream(x, wt, max_splits, glu=True)
     return y if plan is not None and plan[2] == 1 else silu_mul(y)
 
 

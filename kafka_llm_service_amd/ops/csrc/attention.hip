@@ -332,51 +332,28 @@ constexpr int DEC_MAXPG = 2048;  // page ids of one decode piece staged in LDS (
 template <int D>
 struct DecodeSmem {
   int pages[DEC_MAXPG];
-  bf16 qs[8][D];  // OCC3: the unit's G <= 8 query heads (B operand rows), read per block instead of held in VGPRs
+  bf16 qs[8][D];  // bf16: the unit's G <= 8 query heads (B operand rows), read per block instead of held in VGPRs
   float sO[4][8][D];
   float sM[4][8];
   float sL[4][8];
   float sW[8][65];
   float sWt[8];
   int s_last;
-  int pf[4][64];  // OCC3 == 2: landing zone of each wave's L2-prefetch DMA (never read)
 };
-
-// prefix-partial loads of the merges: plain, or agent-coherent (sc1) when the cascade overlaps this kernel (GATED)
-template <bool WT>
-__device__ __forceinline__ bf16x4 ld_pre8(const bf16* p) {
-  if constexpr (WT)
-    return __builtin_bit_cast(bf16x4, ld_wt8(p));
-  else
-    return *reinterpret_cast<const bf16x4*>(p);
-}
-template <bool WT>
-__device__ __forceinline__ f32x4 ld_pre16(const float* p) {
-  if constexpr (WT)
-    return ld_wt16(p);
-  else
-    return *reinterpret_cast<const f32x4*>(p);
-}
-// wait for a group of inline-asm loads; the empty asm statements pin every use of v after the wait
-template <typename T, int N>
-__device__ __forceinline__ void wt_landed(T (&v)[N]) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int j = 0; j < N; ++j) asm volatile("" : "+v"(v[j]));
-}
 
 // One decode piece: keys [lo, hi) of row b, kv head kvh, piece `split` of S, partial slots from split_offset. Every
 // thread of the workgroup calls it with the same arguments (it synchronises the workgroup); returns when the
 // piece's partial or final rows are written.
-template <int D, bool FP8, int MG, int OCC3 = 0, bool GATED = false>
+template <int D, bool FP8>
 __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __restrict__ q, int64_t q_stride,
                                              const void* __restrict__ k_cache, const void* __restrict__ v_cache,
                                              int Hkv, int G, const int* __restrict__ block_tables, int bt_stride,
                                              int b, int kvh, int lo, int hi, int split, int S, int split_offset,
                                              float* __restrict__ out_part, float* __restrict__ lse_part, int S_total,
                                              float scale_log2, bf16* __restrict__ out, int64_t out_stride,
-                                             int* __restrict__ tickets, const bf16* __restrict__ pre_bf16,
-                                             const Gates& gt = Gates{}, int gt_total = 0) {
+                                             int* __restrict__ tickets, const bf16* __restrict__ pre_bf16) {
+  constexpr bool OCC3 = !FP8;  // bf16: three workgroups per CU, Q in LDS, one K/V block per wave in flight
+  constexpr int MG = 32;       // prefix partials per load round trip of the fused merge
   auto& sO = sm.sO;
   auto& sM = sm.sM;
   auto& sL = sm.sL;
@@ -404,55 +381,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   __syncthreads();
   WaveAcc<D> acc;
   init_acc<D>(acc);
-  if constexpr (OCC3 == 2) {
-    // OCC3 + L2 prefetch: with this block's K / V loads each wave also touches one dword of every 128-B line of its
-    // NEXT block (2 LDS-DMA dword loads per lane into a never-read LDS landing zone: no VGPR destination), so that
-    // block streams from HBM into L2 under this block's compute. Page ids from LDS only (a global page-id load
-    // would make the compiler wait for every outstanding load at the join). A register double buffer spills at
-    // the 168-VGPR budget of three waves per SIMD.
-    if (w < nb && !FP8) {
-      const bool qrow = r < G;
-      const bf16* kc = static_cast<const bf16*>(k_cache);
-      const bf16* vc = static_cast<const bf16*>(v_cache);
-      const LdsPages lp{sm.pages, pg0};
-      const uint32_t lds_pf = __builtin_amdgcn_readfirstlane(
-          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)&sm.pf[w][0]);
-      for (int bk = w; bk < nb; bk += 4) {
-        const int key0 = a0 + 32 * bk;
-        KVFrag<D> f;
-        f32x16 sacc = {};
-        if (lds_pt) {  // workgroup-uniform
-          int p0, p1;
-          block_pages(lp, key0, hi, p0, p1);
-          load_kv<D>(f, kc, vc, Hkv, kvh, p0, p1, lane);
-          if (bk + 4 < nb) {  // wave-uniform
-            int n0, n1;
-            block_pages(lp, key0 + 128, hi, n0, n1);
-            const int64_t pg = (int64_t)((lane >> 5) ? n1 : n0) * Hkv + kvh;
-            const int off = (lane & 31) * 128;
-            const char* ka = reinterpret_cast<const char*>(kc + pg * (PAGE * D)) + off;
-            const char* va = reinterpret_cast<const char*>(vc + pg * (PAGE * D)) + off;
-            // inline asm: the compiler's wait insertion does not see these two loads, so it adds no LDS-alias
-            // waits; its own vmcnt waits only grow more conservative (in-order completion)
-            asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, off\n\tglobal_load_lds_dword %1, off"
-                         :: "v"(ka), "v"(va), "s"(lds_pf) : "memory", "m0");
-          }
-        } else {
-          int p0, p1;
-          block_pages(bt, key0, hi, p0, p1);
-          load_kv<D>(f, kc, vc, Hkv, kvh, p0, p1, lane);
-        }
-#pragma unroll
-        for (int kk = 0; kk < D / 16; ++kk) {
-          bf16x8 qv = *reinterpret_cast<const bf16x8*>(&sm.qs[qrow ? r : 0][16 * kk + 8 * h]);
-          if (!qrow) qv = bf16x8{};
-          sacc = mfma32(f.k[kk], qv, sacc);
-        }
-        const bool masked = (key0 < lo) | (key0 + 32 > hi);
-        softmax_pv<D>(sacc, masked, key0, lo, hi, 0x7fffffff, scale_log2, f.v, acc, lane);
-      }
-    }
-  } else if constexpr (OCC3) {
+  if constexpr (OCC3) {
     // Three waves per SIMD (VGPR budget 168): no Q fragments and no second K/V block in registers — each wave
     // has its one block in flight at a time, and 12 waves per CU (3 workgroups) keep the memory system fed;
     // more resident workgroups also cover each other's piece start / end.
@@ -510,8 +439,6 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     // Phase 1: wave w owns heads w, w + 4: lanes load the prefix lse values in parallel, wave-reduce the max and
     // the weight sum, and publish per-split weights in LDS. Phase 2: thread (g, 4 dims) sums weight x partial over
     // the splits with all loads of a group of 8 in flight.
-    // early-launched beside the cascade: its partials are in (write-through hand-off: relaxed wait, sc1 loads)
-    if constexpr (GATED) gate_wait(gt.wait2, gt.mode | 1);
     for (int g = w; g < G; g += 4) {
       float Ms = -INFINITY;
 #pragma unroll
@@ -524,12 +451,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
       const float ls = Ls > 0.f ? Ms + log2f(Ls) : -INFINITY;
       const int64_t pbase = ((int64_t)b * Hq + kvh * G + g) * S_total;
       float lp = -INFINITY;
-      if (lane < split_offset) {
-        if constexpr (GATED)
-          lp = __hip_atomic_load(lse_part + pbase + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          lp = lse_part[pbase + lane];
-      }
+      if (lane < split_offset) lp = lse_part[pbase + lane];
       const float lv = lane < split_offset ? lp : (lane == split_offset ? ls : -INFINITY);
       float mx = lv;
 #pragma unroll
@@ -567,8 +489,7 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
         for (; s2 + MG <= split_offset; s2 += MG) {
           bf16x4 v[MG];
 #pragma unroll
-          for (int j = 0; j < MG; ++j) v[j] = ld_pre8<GATED>(pb + (s2 + j) * D);
-          if constexpr (GATED) wt_landed(v);
+          for (int j = 0; j < MG; ++j) v[j] = *reinterpret_cast<const bf16x4*>(pb + (s2 + j) * D);
 #pragma unroll
           for (int j = 0; j < MG; ++j) {
             const float wj = sW[g][s2 + j];
@@ -576,24 +497,20 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
           }
         }
         for (; s2 < split_offset; ++s2) {
-          bf16x4 v[1] = {ld_pre8<GATED>(pb + s2 * D)};
-          if constexpr (GATED) wt_landed(v);
-          acc4 += f32x4{(float)v[0][0], (float)v[0][1], (float)v[0][2], (float)v[0][3]} * sW[g][s2];
+          const bf16x4 v = *reinterpret_cast<const bf16x4*>(pb + s2 * D);
+          acc4 += f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]} * sW[g][s2];
         }
       } else {
         const float* pp = out_part + pbase;
         for (; s2 + MG <= split_offset; s2 += MG) {
           f32x4 v[MG];
 #pragma unroll
-          for (int j = 0; j < MG; ++j) v[j] = ld_pre16<GATED>(pp + (s2 + j) * D);
-          if constexpr (GATED) wt_landed(v);
+          for (int j = 0; j < MG; ++j) v[j] = *reinterpret_cast<const f32x4*>(pp + (s2 + j) * D);
 #pragma unroll
           for (int j = 0; j < MG; ++j) acc4 += v[j] * sW[g][s2 + j];
         }
         for (; s2 < split_offset; ++s2) {
-          f32x4 v[1] = {ld_pre16<GATED>(pp + s2 * D)};
-          if constexpr (GATED) wt_landed(v);
-          acc4 += v[0] * sW[g][s2];
+          acc4 += *reinterpret_cast<const f32x4*>(pp + s2 * D) * sW[g][s2];
         }
       }
       const float inv = sWt[g] > 0.f ? 1.f / sWt[g] : 0.f;
@@ -601,10 +518,6 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
 #pragma unroll
       for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc4[j] * inv);
       *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
-    }
-    if constexpr (GATED) {  // one arrival per merged (row, kv head)
-      __syncthreads();
-      if (threadIdx.x == 0) gate_arrive(gt.sig, b * Hkv + kvh, gt_total, gt.mode);
     }
     return;
   }
@@ -648,7 +561,6 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   }
   __syncthreads();
   if (!sm.s_last) return;
-  if constexpr (GATED) gate_wait(gt.wait2, gt.mode | 1);  // write-through hand-off (see the fused merge)
   auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   // 16-B agent-coherent loads (sc1: not served from this XCD's possibly stale L2); inline asm, so the group below
   // waits for them itself
@@ -677,12 +589,11 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
     const float* pp = out_part + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
     int s0 = 0;
-    if (pre_bf16 != nullptr) {  // the cascade's bf16 prefix partials (an earlier kernel's, or write-through if GATED)
+    if (pre_bf16 != nullptr) {  // the cascade's bf16 prefix partials
       const bf16* pb = pre_bf16 + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
       for (; s0 < split_offset; ++s0) {
-        bf16x4 v[1] = {ld_pre8<GATED>(pb + s0 * D)};
-        if constexpr (GATED) wt_landed(v);
-        acc4 += f32x4{(float)v[0][0], (float)v[0][1], (float)v[0][2], (float)v[0][3]} * sW[g][s0];
+        const bf16x4 v = *reinterpret_cast<const bf16x4*>(pb + s0 * D);
+        acc4 += f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]} * sW[g][s0];
       }
     }
     // groups of 16 partials with all loads in flight (the tail of the kernel: latency, not bandwidth)
@@ -701,98 +612,33 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc4[j] * inv);
     *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
   }
-  if constexpr (GATED) {  // one arrival per merged (row, kv head)
-    __syncthreads();
-    if (threadIdx.x == 0) gate_arrive(gt.sig, b * Hkv + kvh, gt_total, gt.mode);
-  }
 }
 
-template <int D, bool HEADS_FAST, bool FP8, int MG = 16, int OCC3 = 0, bool GATED = false>
-__global__ __launch_bounds__(256, OCC3 ? 3 : 2) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
-                                                           const void* __restrict__ k_cache,
-                                                           const void* __restrict__ v_cache, int Hkv, int G,
-                                                           const int* __restrict__ block_tables, int bt_stride,
-                                                           const DecodeItem* __restrict__ items, int B,
-                                                           float* __restrict__ out_part, float* __restrict__ lse_part,
-                                                           int S_total, float scale_log2,
-                                                           bf16* __restrict__ out, int64_t out_stride,
-                                                           int* __restrict__ tickets,
-                                                           const bf16* __restrict__ pre_bf16, Gates gt) {
+// grid (Hkv, items): the Hkv heads of an item are consecutive workgroups, dealt to different XCDs, reading one page
+// row together (heads-fast: +7 % over items-fast, three workgroups per CU +5 % over two,
+// profiles/r04/bench_ab_decode_placement_occ.jsonl)
+template <int D, bool FP8>
+__global__ __launch_bounds__(256, FP8 ? 2 : 3) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
+                                                                      const void* __restrict__ k_cache,
+                                                                      const void* __restrict__ v_cache, int Hkv, int G,
+                                                                      const int* __restrict__ block_tables,
+                                                                      int bt_stride,
+                                                                      const DecodeItem* __restrict__ items, int B,
+                                                                      float* __restrict__ out_part,
+                                                                      float* __restrict__ lse_part, int S_total,
+                                                                      float scale_log2, bf16* __restrict__ out,
+                                                                      int64_t out_stride, int* __restrict__ tickets,
+                                                                      const bf16* __restrict__ pre_bf16) {
   __shared__ DecodeSmem<D> sm;
-  // HEADS_FAST: consecutive workgroups are the Hkv heads of one item (grid (Hkv, items)), else the items of one
-  // head (grid (items, Hkv)) — a placement choice only (which XCD's L2 sees which pages)
-  const DecodeItem it = items[HEADS_FAST ? blockIdx.y : blockIdx.x];
-  const int b = it.b, kvh = HEADS_FAST ? blockIdx.x : blockIdx.y, split = it.split, S = it.nsplit, split_offset = it.npre;
+  const DecodeItem it = items[blockIdx.y];
+  const int b = it.b, kvh = blockIdx.x, split = it.split, S = it.nsplit, split_offset = it.npre;
   // a malformed item (host bug) is dropped instead of indexing out of bounds (workgroup-uniform)
   if (b < 0 || b >= B || split < 0 || split >= S || split_offset < 0 || split_offset + S > S_total ||
       (out != nullptr && split_offset + S > 64))
     return;
-  if constexpr (GATED) gate_wait(gt.wait, gt.mode);  // early-launched: q and this step's K/V rows are written
-  decode_piece<D, FP8, MG, OCC3, GATED>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, it.lo, it.hi,
-                           split, S, split_offset, out_part, lse_part, S_total, scale_log2, out, out_stride, tickets,
-                           pre_bf16, gt, B * Hkv);
-}
-
-// ------------------------------------------------------------------------------------------------------------------
-// Stream-K decode: the (row, kv head) units of a step laid end to end in one cost line — unit (b, kvh) occupies
-// [C_b + kvh (F + nb_b), + F + nb_b): F overhead blocks (its fixed cost: item / page-table / first-block latency,
-// combine, merge) then nb_b 32-key blocks — and workgroup w takes the equal slice [w T, (w + 1) T) of it. A unit
-// whose blocks cross slice boundaries is split into pieces (partials + ticket merge, as a split item); a unit inside
-// one slice merges directly. Every workgroup does the same cost: no second round of long pieces after the first
-// (the item plan's 2-round tail), and short histories are packed several to a workgroup.
-//   rows:  int32 [B + 1, 4]  (kv_lo, kv_hi, npre, C_b) per row, then the plan (T, F, total, 0) — device data, so a
-//          captured graph replays any step of the same batch size
-//   start: int32 [nwg, 2] (first row b, first kv head) of each slice (host: searchsorted over C_b; b = B: empty)
-
-template <int D, bool FP8, int MG = 32>
-__global__ __launch_bounds__(256, 2) void attn_decode_sk_kernel(const bf16* __restrict__ q, int64_t q_stride,
-                                                              const void* __restrict__ k_cache,
-                                                              const void* __restrict__ v_cache, int Hkv, int G,
-                                                              const int* __restrict__ block_tables, int bt_stride,
-                                                              const int4* __restrict__ rows,
-                                                              const int2* __restrict__ start, int B,
-                                                              float* __restrict__ out_part,
-                                                              float* __restrict__ lse_part, int S_total,
-                                                              float scale_log2, bf16* __restrict__ out,
-                                                              int64_t out_stride, int* __restrict__ tickets,
-                                                              const bf16* __restrict__ pre_bf16) {
-  __shared__ DecodeSmem<D> sm;
-  const int w = blockIdx.x;
-  const int4 pl = rows[B];
-  const int T = __builtin_amdgcn_readfirstlane(pl.x), F = __builtin_amdgcn_readfirstlane(pl.y);
-  const int total = __builtin_amdgcn_readfirstlane(pl.z);
-  if (T < 1 || F < 0) return;
-  const int s0 = w * T, e0 = min(s0 + T, total);
-  const int2 st = start[w];
-  int b = __builtin_amdgcn_readfirstlane(st.x), kvh = __builtin_amdgcn_readfirstlane(st.y);
-  if (b < 0 || b >= B || kvh < 0 || kvh >= Hkv) return;
-  // pieces of this slice (all values workgroup-uniform; every thread walks the same units)
-  for (int guard = 0; guard < 4096 && b < B; ++guard) {
-    const int4 rw = rows[b];
-    const int lo_b = __builtin_amdgcn_readfirstlane(rw.x), hi_b = __builtin_amdgcn_readfirstlane(rw.y);
-    const int npre = __builtin_amdgcn_readfirstlane(rw.z), c_b = __builtin_amdgcn_readfirstlane(rw.w);
-    const int a0 = lo_b & ~31;
-    const int nb = hi_b > lo_b ? (hi_b - a0 + 31) >> 5 : 0;
-    const int cu = c_b + kvh * (F + nb);  // cost start of unit (b, kvh)
-    if (cu >= e0) break;
-    const int bs = cu + F;  // first block's cost coordinate
-    const int j0 = max(s0, bs) - bs, j1 = min(e0, bs + nb) - bs;
-    if (j1 > j0 && nb > 0) {
-      const int first = bs / T, last = (bs + nb - 1) / T;
-      const int split = w - first, S = last - first + 1;
-      if (split >= 0 && split < S && npre >= 0 && npre + S <= S_total && !(out != nullptr && npre + S > 64)) {
-        const int lo = max(lo_b, a0 + 32 * j0), hi = min(hi_b, a0 + 32 * j1);
-        decode_piece<D, FP8, MG>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, lo, hi,
-                                 split, S, npre, out_part, lse_part, S_total, scale_log2, out, out_stride, tickets,
-                                 pre_bf16);
-        __syncthreads();  // the next piece reuses the LDS
-      }
-    }
-    if (++kvh == Hkv) {
-      kvh = 0;
-      ++b;
-    }
-  }
+  decode_piece<D, FP8>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, it.lo, it.hi,
+                       split, S, split_offset, out_part, lse_part, S_total, scale_log2, out, out_stride, tickets,
+                       pre_bf16);
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -1262,80 +1108,21 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
                                               const void* v_cache, int fp8, int n_items, int B, int Hkv, int G, int D,
                                               const int* block_tables, int bt_stride, const int* items,
                                               float* out_part, float* lse_part, int S_total, float scale, bf16* out,
-                                              int64_t out_stride, int* tickets, const bf16* pre_bf16,
-                                              Gates gt, hipStream_t st) {
+                                              int64_t out_stride, int* tickets, const bf16* pre_bf16, hipStream_t st) {
   if (n_items == 0) return hipSuccess;
-  if (D != 128 || G > 8 || G < 1) return hipErrorInvalidValue;
+  if (D != 128 || G > 8 || G < 1 || n_items > 65535) return hipErrorInvalidValue;
   if (out != nullptr && tickets == nullptr) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
-  static const bool heads_fast = [] {
-    const char* e = getenv("KAFKA_DECODE_HEADS_FAST");
-    return e == nullptr || e[0] != '0';
-  }();
   const auto* di = reinterpret_cast<const DecodeItem*>(items);
-  auto go = [&](auto kern, dim3 grid) {
-    launch_maybe_early(kern, grid, dim3(256), st, gt.wait != nullptr || gt.wait2 != nullptr, q, q_stride, k_cache, v_cache, Hkv, G,
-                       block_tables, bt_stride, di, B, out_part, lse_part, S_total, scale_log2, out, out_stride,
-                       tickets, pre_bf16, gt);
-  };
-  // prefix partials per load round trip in the fused merge (env KAFKA_DECODE_MERGE_GROUP = 8 / 16 / 32; bench A/B
-  // profiles/r02/decode_merge_group_ab.jsonl: 7,491 / 7,489 / 7,505 tok/s — the epilogue is not on the critical path)
-  static const int mg = [] {
-    const char* e = getenv("KAFKA_DECODE_MERGE_GROUP");
-    const int v = e ? atoi(e) : 32;
-    return v == 8 || v == 16 ? v : 32;
-  }();
-  // three workgroups per CU (Q in LDS, one K/V block per wave in flight; bench +0.9 %, profiles/r03/decode_occ3/);
-  // KAFKA_DECODE_OCC3=0: two per CU with a one-block register prefetch
-  // KAFKA_DECODE_OCC3=2: three per CU with the software-pipelined block loop (next K under softmax + PV)
-  static const int occ3 = [] {
-    const char* e = getenv("KAFKA_DECODE_OCC3");
-    return e == nullptr ? 1 : (e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1));
-  }();
-  const dim3 hf(Hkv, n_items), sf(n_items, Hkv);
-  if (gt.wait != nullptr || gt.wait2 != nullptr || gt.sig != nullptr) {  // gated: its own instantiation
-    if (fp8 || !heads_fast || mg != 32 || !occ3) return hipErrorInvalidValue;
-    go(attn_decode_kernel<128, true, false, 32, 1, true>, hf);
-    return hipGetLastError();
-  }
+  const dim3 grid(Hkv, n_items);
   if (fp8)
-    heads_fast ? go(attn_decode_kernel<128, true, true>, hf) : go(attn_decode_kernel<128, false, true>, sf);
-  else if (!heads_fast)
-    go(attn_decode_kernel<128, false, false>, sf);
-  else if (mg == 8)
-    go(attn_decode_kernel<128, true, false, 8>, hf);
-  else if (mg == 32 && occ3 == 2)
-    go(attn_decode_kernel<128, true, false, 32, 2>, hf);
-  else if (mg == 32 && occ3)
-    go(attn_decode_kernel<128, true, false, 32, 1>, hf);
-  else if (mg == 32)
-    go(attn_decode_kernel<128, true, false, 32>, hf);
+    attn_decode_kernel<128, true><<<grid, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride,
+                                                         di, B, out_part, lse_part, S_total, scale_log2, out,
+                                                         out_stride, tickets, pre_bf16);
   else
-    go(attn_decode_kernel<128, true, false, 16>, hf);
-  return hipGetLastError();
-}
-
-// Stream-K decode (attn_decode_sk_kernel): rows int32 [B + 1, 4] (the last row = plan), start int32 [nwg, 2].
-extern "C" hipError_t kafka_launch_attn_decode_sk(const bf16* q, int64_t q_stride, const void* k_cache,
-                                                 const void* v_cache, int fp8, int B, int Hkv, int G, int D,
-                                                 const int* block_tables, int bt_stride, const int* rows,
-                                                 const int* start, int nwg, float* out_part, float* lse_part,
-                                                 int S_total, float scale, bf16* out, int64_t out_stride,
-                                                 int* tickets, const bf16* pre_bf16, hipStream_t st) {
-  if (nwg == 0 || B == 0) return hipSuccess;
-  if (D != 128 || G > 8 || G < 1) return hipErrorInvalidValue;
-  if (out != nullptr && tickets == nullptr) return hipErrorInvalidValue;
-  const float scale_log2 = scale * 1.4426950408889634f;
-  const auto* rw = reinterpret_cast<const int4*>(rows);
-  const auto* sp = reinterpret_cast<const int2*>(start);
-  if (fp8)
-    attn_decode_sk_kernel<128, true><<<nwg, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables,
-                                                          bt_stride, rw, sp, B, out_part, lse_part, S_total,
-                                                          scale_log2, out, out_stride, tickets, pre_bf16);
-  else
-    attn_decode_sk_kernel<128, false><<<nwg, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables,
-                                                           bt_stride, rw, sp, B, out_part, lse_part, S_total,
-                                                           scale_log2, out, out_stride, tickets, pre_bf16);
+    attn_decode_kernel<128, false><<<grid, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables,
+                                                          bt_stride, di, B, out_part, lse_part, S_total, scale_log2,
+                                                          out, out_stride, tickets, pre_bf16);
   return hipGetLastError();
 }
 
@@ -1362,21 +1149,21 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
                                             const void* k_cache, const void* v_cache, int Hkv, int G, int D,
                                             const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
                                             int64_t out_stride, float* out_part, float* lse_part, int S_total,
-                                            float scale, int part_bf16, Gates gt, hipStream_t st);
+                                            float scale, int part_bf16, hipStream_t st);
 
 extern "C" hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride,
                                                const void* k_cache, const void* v_cache, int fp8, int Hkv, int G,
                                                int D, const int* block_tables, int bt_stride, const int* q_limit,
                                                bf16* out, int64_t out_stride, float* out_part, float* lse_part,
-                                               int S_total, float scale, int variant, int part_bf16, Gates gt,
+                                               int S_total, float scale, int variant, int part_bf16,
                                                hipStream_t st) {
   if (n_items == 0) return hipSuccess;
   if (variant == 3) {  // LDS-DMA ring, one wave per SIMD, 256 rows (attn_tile.hip); bf16 pages only
     if (fp8) return hipErrorInvalidValue;
     return kafka_launch_attn_tile(items, n_items, q, q_stride, k_cache, v_cache, Hkv, G, D, block_tables, bt_stride,
-                                  q_limit, out, out_stride, out_part, lse_part, S_total, scale, part_bf16, gt, st);
+                                  q_limit, out, out_stride, out_part, lse_part, S_total, scale, part_bf16, st);
   }
-  if (part_bf16 || gt.wait != nullptr || gt.sig != nullptr) return hipErrorInvalidValue;  // tile v3 only
+  if (part_bf16) return hipErrorInvalidValue;  // tile v3 only
   if (D != 128 || G < 1 || G > 32 || (128 % G) != 0 || n_items > 65535) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
   const auto* it = reinterpret_cast<const AttnWorkItem*>(items);

@@ -3,10 +3,10 @@
 // (`prefill_flash_attention`). Same work items, page layouts and outputs as attn_prefill_kernel (attention.hip);
 // selected as tile variant 3 (ops.tile_rows(3) = 256 rows).
 //
-// Structure (one workgroup = 4 waves = ONE wave per SIMD, 256 query rows of one KV head):
-//   * each wave owns 64 query rows as two 32-row MFMA blocks (rb = 0, 1): every K / V fragment read from LDS feeds
-//     two MFMAs (v2's 8-wave layout read each fragment for one 32-row block: twice the LDS traffic per FLOP), and a
-//     wave has the whole 512-entry register file (O 128 + S 64 + Q 64 + K/V fragments);
+// Structure (one workgroup = 8 waves = two waves per SIMD, 256 query rows of one KV head):
+//   * each wave owns 32 query rows (one 32-row MFMA block); the partner wave's MFMAs run beside this wave's softmax
+//     VALU (a 4-wave / 64-row layout with one wave per SIMD halves the LDS reads but hides no latency: -3.8 % on the
+//     headline, profiles/r04/bench_ab_tile_prologue.jsonl);
 //   * K/V arrive by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction) in 64-key tiles (4 pages: 16 KB
 //     K + 16 KB V) into a 3-slot ring: tile j+2 is issued right after the barrier that retires tile j, so two
 //     tiles (64 KB per CU) stay in flight across every barrier. No register round trip, no ds_write pass, and one
@@ -19,8 +19,7 @@
 //     permutation on the read);
 //   * softmax in the S^T layout (lane = query column: row max / sum are lane-local plus one permlane32 swap) with a
 //     deferred rescale (T13): O and l are rescaled only when some row's max grew by more than 2^THR, so the 64-wide
-//     O rescale almost never runs; the two row blocks give the scheduler independent MFMA (PV of rb 0) and VALU
-//     (exp of rb 1) streams in one basic block.
+//     O rescale almost never runs; the row sums run on the matrix pipe (an MFMA against a ones operand).
 #include "common.h"
 
 #include <cstdlib>
@@ -67,15 +66,6 @@ __device__ __forceinline__ void t3_wait_vmcnt() {
 // would emit one), and no LDS access is moved across it
 __device__ __forceinline__ void t3_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-// diagnostic-build stamp (ABL == 9): shader clock, ordered against the surrounding code
-__device__ __forceinline__ uint64_t t3_stamp() {
-  uint64_t t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-
 // diagnostic-build stamp (ABL == 8): the 100 MHz constant clock, comparable across CUs and XCDs
 __device__ __forceinline__ uint64_t t3_rt() {
   uint64_t t;
@@ -96,16 +86,11 @@ __device__ __forceinline__ void t3_wait_tiles(int n) {
     t3_wait_vmcnt<0>();
 }
 
-// ABL (timing-only ablations, wrong outputs; KAFKA_TILE_ABL): 1 = no DMA inside the tile loop, 2 = no exp2,
-// 3 = no wait / barrier in the loop, 8 = workgroup phase stamps (100 MHz clock; the full kernel runs, lse_part is
-// overwritten with u64 [entry, prologue done, first tile landed, loop done, epilogue done, 0, 0, 0] per workgroup
-// blockIdx.y * Hkv + blockIdx.x), 9 = per-phase shader-clock stamps of the interior loop written over out_part
-// (wave (blockIdx.y * Hkv + blockIdx.x) * 4 + w: u64 [wait + barrier, DMA issue, QK^T + max, rescale + exp + PV,
-// tiles, 0, 0, 0])
-// RB = 32-row MFMA blocks per wave: 2 -> 4 waves (one per SIMD, 512 registers each); 1 -> 8 waves (two per SIMD,
-// 256 registers each: the partner wave's MFMAs run beside this wave's softmax VALU). Rows per workgroup: 256.
-template <int RB, int NSLOT, int ABL = 0, bool GATED = false>
-__global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(const TileItem* __restrict__ items,
+// ABL = 8 (diagnostic build, KAFKA_TILE_ABL=8, benchmarks/attn_tile_stamps.py): workgroup phase stamps on the 100 MHz
+// clock; the full kernel runs and lse_part is overwritten with u64 [entry, prologue done, first tile landed, loop
+// done, epilogue done, 0, 0, 0] per workgroup blockIdx.y * Hkv + blockIdx.x.
+template <int ABL = 0>
+__global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __restrict__ items,
                                                            const bf16* __restrict__ q, int64_t q_stride,
                                                            const bf16* __restrict__ k_cache,
                                                            const bf16* __restrict__ v_cache, int Hkv, int G,
@@ -113,11 +98,11 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
                                                            const int* __restrict__ q_limit, bf16* __restrict__ out,
                                                            int64_t out_stride, float* __restrict__ out_part,
                                                            float* __restrict__ lse_part, int S_total,
-                                                           float scale_log2, int part_bf16, Gates gt) {
+                                                           float scale_log2, int part_bf16) {
   using namespace tile3;
-  static_assert(NSLOT == 3 || NSLOT == 4, "ring depth");
-  static_assert(RB == 1 || RB == 2, "row blocks per wave");
-  constexpr int NW = 8 / RB;              // waves
+  constexpr int RB = 1;                   // 32-row MFMA blocks per wave
+  constexpr int NSLOT = 3;                // ring slots (4 measured no faster)
+  constexpr int NW = 8;                   // waves
   constexpr int DPT = 32 / NW;            // LDS-DMA instructions per wave per tile (16 K + 16 V pieces per tile)
   __shared__ __attribute__((aligned(16))) char smem[lds_bytes<NSLOT>()];
   int* s_pages = reinterpret_cast<int*>(smem + NSLOT * SLOT);
@@ -178,8 +163,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
     }
   };
   // (Q fragments are loaded after the first K/V tiles' DMAs are issued: those are the critical path — Q loads issued
-  // ahead of them delayed the first tile, -0.6 % on the headline, profiles/r04/bench_ab_tile_prologue.jsonl; the
-  // early-launched cascade (common.h Gates) additionally waits for q's producer first)
+  // ahead of them delayed the first tile, -0.6 % on the headline, profiles/r04/bench_ab_tile_prologue.jsonl)
   // per-block wave-uniform bounds: keys past hi_b are masked for every row of the block, keys <= wmin_b for none
   int hi_b[2], wmin_b[2];  // (RB == 1: block 1 mirrors block 0)
 #pragma unroll
@@ -243,140 +227,33 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
 #pragma unroll
   for (int j = 0; j < NSLOT - 1; ++j)
     if (j < ntiles) issue(j);
-  if constexpr (GATED) gate_wait(gt.wait, gt.mode);
   load_q();
 
   // Running state per row block: O^T accumulators; row sums `ls` as an MFMA accumulator (every register of a lane
   // holds its column's sum ones . P: 8 MFMAs per tile instead of 64 adds); the running max m (exp2 domain).
   // (Folding -m into the QK^T accumulator init would save the per-score FMA too, but needs Q prescaled by
   // scale * log2(e) in bf16: +0.4 % relative score error, 0.037 abs on a peaked row vs 0.02 tolerance — rejected.)
-  // HALF (RB == 2, one wave per SIMD with 64 rows): the 512-register budget has no room for both 32-key halves'
-  // scores and an MFMA row-sum accumulator per block (the straight port spilled 122 VGPRs), so each half runs its own
-  // online-softmax step and the row sums are VALU adds (one float per row block).
-  constexpr bool HALF = RB == 2;
   f32x16 o[RB][D / 32], ls[RB];
-  float m[RB], lsum[RB];
+  float m[RB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
     for (int t = 0; t < D / 32; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) o[rb][t][i] = 0.f;
-    if constexpr (!HALF) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) ls[rb][i] = 0.f;
-    }
+    for (int i = 0; i < 16; ++i) ls[rb][i] = 0.f;
     m[rb] = -INFINITY;
-    lsum[rb] = 0.f;
   }
   bf16x8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
-
-  // diagnostic stamps (ABL == 9): phase k accumulates the clock since the previous mark
-  uint64_t st_sum[4] = {0, 0, 0, 0}, st_last = 0;
-  int st_tiles = 0;
-  auto stamp_mark = [&](int k) {
-    const uint64_t t = t3_stamp();
-    if (k == 0) {
-      st_last = t;
-      ++st_tiles;
-      return;
-    }
-    st_sum[k - 1] += t - st_last;
-    st_last = t;
-  };
-
-  // ---- HALF: one 32-key half (kb) of a tile as its own online-softmax step
-  // (always inlined: a call would put the closure's register arrays — o, q, m — in scratch memory)
-  auto half_body = [&](auto masked_c, const char* Ks, const char* Vs, int kb, int key0) __attribute__((always_inline)) {
-    constexpr bool MASKED = decltype(masked_c)::value;
-    f32x16 s[RB];
-    {
-      bf16x8 kf[D / 16];
-#pragma unroll
-      for (int kk = 0; kk < D / 16; ++kk)
-        kf[kk] = *reinterpret_cast<const bf16x8*>(Ks + (2 * kb + (r >> 4)) * 4096 + ((2 * kk + h) * 16 + (r & 15)) * 16);
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
-        f32x16 acc = {};
-#pragma unroll
-        for (int kk = 0; kk < D / 16; ++kk) acc = mfma32(kf[kk], qf[rb][kk], acc);
-        s[rb] = acc;
-      }
-    }
-    if constexpr (MASKED) {
-      const int k0 = key0 + 32 * kb;
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
-        if ((k0 < lo) | (k0 + 32 > hi_b[rb]) | (k0 + 31 > wmin_b[rb])) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = k0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (!((key >= lo) & (key < hi_b[rb]) & (key <= limit[rb]))) s[rb][i] = -INFINITY;
-          }
-        }
-    }
-    float smax[RB];
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-      float mx = s[rb][0];
-#pragma unroll
-      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[rb][i]);
-      smax[rb] = t3_xor32_max(mx) * scale_log2;
-    }
-    bool need = false;
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) need = need | !(smax[rb] <= m[rb] + THR);
-    if (__any(need)) {
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
-        const float mn = fmaxf(m[rb], smax[rb]);
-        const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m[rb] - mn);
-#pragma unroll
-        for (int t = 0; t < D / 32; ++t) o[rb][t] *= alpha;
-        lsum[rb] *= alpha;
-        m[rb] = mn;
-      }
-    }
-    bf16x8 vf[2][D / 32];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int t = 0; t < D / 32; ++t) {
-        const int d = 32 * t + r;
-        vf[s2][t] = *reinterpret_cast<const bf16x8*>(Vs + (2 * kb + s2) * 4096 + d * 32 + 16 * (h ^ ((d >> 3) & 1)));
-      }
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-      const float mu = (m[rb] == -INFINITY) ? 0.f : m[rb];
-      bf16x8 pf[2];
-      float psum = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float x = fmaf(s[rb][i], scale_log2, -mu);
-        const bf16 p = (bf16)(ABL == 2 ? x : exp2f(x));
-        pf[i >> 3][i & 7] = p;
-        psum += (float)p;  // the rounded value the PV product uses
-      }
-      lsum[rb] += t3_xor32_sum(psum);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int t = 0; t < D / 32; ++t) o[rb][t] = mfma32(vf[s2][t], pf[s2], o[rb][t]);
-    }
-  };
 
   // ---- one 64-key tile (processing index j) from ring slot j % NSLOT
   auto tile_body = [&](auto masked_c, int j, int key0) {
     constexpr bool MASKED = decltype(masked_c)::value;
     const char* Ks = smem + (j % NSLOT) * SLOT;  // [page 4][plane 16][key 16][16 B]
     const char* Vs = Ks + KBYTES;                // [page 4][d 128][2 x 16 B] (halves swapped on rows 8..15 of 16)
-    if constexpr (HALF) {
-      half_body(masked_c, Ks, Vs, 0, key0);
-      half_body(masked_c, Ks, Vs, 1, key0);
-      return;
-    }
     // S^T = K . Q^T for both 32-key halves (kb) and both row blocks
     f32x16 s[RB][2];
 #pragma unroll
@@ -417,8 +294,6 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
       for (int i = 1; i < 16; ++i) mx = fmaxf(mx, fmaxf(s[rb][0][i], s[rb][1][i]));
       smax[rb] = t3_xor32_max(mx) * scale_log2;
     }
-    if constexpr (ABL == 9)
-      if (!MASKED) stamp_mark(3);
     bool need = false;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) need = need | !(smax[rb] <= m[rb] + THR);
@@ -452,7 +327,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float x = fmaf(s[rb][kb][i], scale_log2, -mu);
-          pf[i >> 3][i & 7] = (bf16)(ABL == 2 ? x : exp2f(x));
+          pf[i >> 3][i & 7] = (bf16)exp2f(x);
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
@@ -477,44 +352,21 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
   auto step = [&](int i) {
     // tile i landed (this wave's pieces; the NSLOT - 2 younger tiles stay in flight), then every wave's: the
     // barrier also retires every read of slot (i + NSLOT - 1) % NSLOT (index i - 1's)
-    if constexpr (ABL != 3) {
-      t3_wait_tiles<DPT>(min(NSLOT - 2, ntiles - 1 - i));
-      t3_barrier();
-    }
-    if constexpr (ABL == 9) stamp_mark(1);
-    if (ABL != 1 && i + NSLOT - 1 < ntiles) issue(i + NSLOT - 1);
-    if constexpr (ABL == 9) stamp_mark(2);
+    t3_wait_tiles<DPT>(min(NSLOT - 2, ntiles - 1 - i));
+    t3_barrier();
+    if (i + NSLOT - 1 < ntiles) issue(i + NSLOT - 1);
   };
   for (int i = 0; i < n_int; ++i) {
-    if constexpr (ABL == 9) stamp_mark(0);
     step(i);
     if constexpr (ABL == 8)
       if (i == 0) ph[2] = t3_rt();
     tile_body(std::false_type{}, i, base + TK * tile_of(i));
-    if constexpr (ABL == 9) stamp_mark(4);
   }
   for (int i = n_int; i < ntiles; ++i) {
     step(i);
     tile_body(std::true_type{}, i, base + TK * tile_of(i));
   }
 
-  if constexpr (ABL == 9) {
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {  // keep the loop's results live (no output is written in this build)
-#pragma unroll
-      for (int t = 0; t < D / 32; ++t) asm volatile("" ::"a"(o[rb][t]));
-      asm volatile("" ::"a"(ls[rb]), "v"(m[rb]));
-    }
-    if (lane == 0 && out_part != nullptr) {
-      uint64_t* dst = reinterpret_cast<uint64_t*>(out_part) + (((int64_t)blockIdx.y * Hkv + blockIdx.x) * NW + w) * 8;
-      dst[0] = st_sum[0];
-      dst[1] = st_sum[1];
-      dst[2] = st_sum[2];
-      dst[3] = st_sum[3];
-      dst[4] = (uint64_t)st_tiles;
-    }
-    return;
-  }
   if constexpr (ABL == 8) ph[3] = t3_rt();
   // ---- epilogue: through a per-wave LDS transpose (slot ntiles % NSLOT is idle: its last tile was read before the
   // barrier every wave passed NSLOT - 1 tiles ago), so every store instruction writes whole 128-B lines
@@ -524,15 +376,11 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     if (!__any(valid[rb])) continue;  // wave-uniform
-    const float ll = fits ? (HALF ? lsum[rb] : ls[rb][0]) : __builtin_nanf("");
+    const float ll = fits ? ls[rb][0] : __builtin_nanf("");
     const float inv = ll > 0.f ? 1.f / ll : (fits ? 0.f : ll);
     if (ABL != 8 && part && valid[rb] && h == 0) {
       float* lp = lse_part + ((int64_t)token[rb] * Hq + head[rb]) * S_total + it.split;
-      const float lv = ll > 0.f ? m[rb] + log2f(ll) : (fits ? -INFINITY : ll);
-      if constexpr (GATED)  // write-through: the overlapped decode reads it before this kernel ends
-        __hip_atomic_store(lp, lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        *lp = lv;
+      *lp = ll > 0.f ? m[rb] + log2f(ll) : (fits ? -INFINITY : ll);
     }
     const int R0 = 32 * RB * w + 32 * rb;
     const int nvalid = it.q_count * G - R0;
@@ -553,10 +401,7 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
                                            (((int64_t)tok2 * Hq + head2) * S_total + it.split) * D + 64 * rd + 8 * cc);
           else
             dst = reinterpret_cast<f32x4*>(out + (int64_t)tok2 * out_stride + (int64_t)head2 * D + 64 * rd + 8 * cc);
-          if constexpr (GATED)
-            st_wt16(dst, v);
-          else
-            *dst = v;
+          *dst = v;
         }
       }
     };
@@ -588,9 +433,6 @@ __global__ __launch_bounds__(512 / RB, RB == 1 ? 2 : 1) void attn_tile_kernel(co
       }
     }
   }
-  if constexpr (GATED) {  // one relaxed arrival per workgroup after its write-through stores completed
-    if (gt.sig != nullptr) gate_arrive_wt(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y));
-  }
   if constexpr (ABL == 8) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -608,36 +450,19 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
                                             const void* k_cache, const void* v_cache, int Hkv, int G, int D,
                                             const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
                                             int64_t out_stride, float* out_part, float* lse_part, int S_total,
-                                            float scale, int part_bf16, Gates gt, hipStream_t st) {
+                                            float scale, int part_bf16, hipStream_t st) {
   if (n_items == 0) return hipSuccess;
   if (D != 128 || G < 1 || G > 32 || (256 % G) != 0 || n_items > 65535) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
-  static const int slots = [] {
-    const char* e = getenv("KAFKA_TILE_SLOTS");
-    return e && e[0] == '4' ? 4 : 3;
-  }();
-  static const int abl = [] {
+  static const bool stamps = [] {  // diagnostic build (benchmarks/attn_tile_stamps.py)
     const char* e = getenv("KAFKA_TILE_ABL");
-    return e ? atoi(e) : 0;
+    return e && atoi(e) == 8;
   }();
-  static const int rb = [] {  // KAFKA_TILE_WAVES = 8 (two waves per SIMD, 32 rows each) or 4 (one, 64 rows)
-    const char* e = getenv("KAFKA_TILE_WAVES");
-    return e && e[0] == '4' ? 2 : 1;
-  }();
-  auto kern = rb == 2 ? (slots == 4 ? attn_tile_kernel<2, 4> : attn_tile_kernel<2, 3>)
-                      : (slots == 4 ? attn_tile_kernel<1, 4> : attn_tile_kernel<1, 3>);
-  if (abl == 1) kern = rb == 2 ? attn_tile_kernel<2, 3, 1> : attn_tile_kernel<1, 3, 1>;
-  if (abl == 2) kern = rb == 2 ? attn_tile_kernel<2, 3, 2> : attn_tile_kernel<1, 3, 2>;
-  if (abl == 8) kern = rb == 2 ? attn_tile_kernel<2, 3, 8> : attn_tile_kernel<1, 3, 8>;
-  if (abl == 9) kern = rb == 2 ? attn_tile_kernel<2, 3, 9> : attn_tile_kernel<1, 3, 9>;
-  if (gt.wait != nullptr || gt.sig != nullptr) {  // early-launched cascade: its own instantiation (default shape)
-    if (rb != 1 || slots != 3 || abl != 0) return hipErrorInvalidValue;
-    kern = attn_tile_kernel<1, 3, 0, true>;
-  }
-  launch_maybe_early(kern, dim3(Hkv, n_items), dim3(512 / rb), st, gt.wait != nullptr,
-                     reinterpret_cast<const TileItem*>(items), q, q_stride, static_cast<const bf16*>(k_cache),
-                     static_cast<const bf16*>(v_cache), Hkv, G, block_tables, bt_stride, q_limit, out, out_stride,
-                     out_part, lse_part, S_total, scale_log2, part_bf16, gt);
+  auto kern = stamps ? attn_tile_kernel<8> : attn_tile_kernel<0>;
+  kern<<<dim3(Hkv, n_items), 512, 0, st>>>(reinterpret_cast<const TileItem*>(items), q, q_stride,
+                                           static_cast<const bf16*>(k_cache), static_cast<const bf16*>(v_cache), Hkv,
+                                           G, block_tables, bt_stride, q_limit, out, out_stride, out_part, lse_part,
+                                           S_total, scale_log2, part_bf16);
   return hipGetLastError();
 }
 

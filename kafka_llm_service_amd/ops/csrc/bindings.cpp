@@ -7,31 +7,19 @@
 
 typedef unsigned short bf16;  // raw bf16 storage on the host side
 
-// device gates of early-launched consumers (layout of `Gates` in csrc/common.h)
-struct Gates {
-  int* wait = nullptr;
-  int expect = 0;
-  int* sig = nullptr;
-  int* wait2 = nullptr;
-  int expect2 = 0;
-  int mode = 0;
-};
-constexpr int GATE_INTS = 17 * 16;  // csrc/common.h
-
 extern "C" {
 hipError_t kafka_launch_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs, const bf16* w, int T, int d, float eps,
                           hipStream_t st);
 hipError_t kafka_launch_fused_add_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs, bf16* resid, int64_t rs,
-                                    const bf16* w, int T, int d, float eps, Gates gt, hipStream_t st);
+                                    const bf16* w, int T, int d, float eps, hipStream_t st);
 hipError_t kafka_launch_fused_add_rmsnorm_slab(bf16* out, int64_t os, const float* xp, int S, int64_t ps, bf16* resid,
-                                               int64_t rs, const bf16* w, int T, int d, float eps, Gates gt,
-                                               hipStream_t st);
+                                               int64_t rs, const bf16* w, int T, int d, float eps, hipStream_t st);
 hipError_t kafka_launch_silu_mul(bf16* out, const bf16* x, int64_t xs, int T, int F, hipStream_t st);
 hipError_t kafka_launch_silu_mul_slab(bf16* out, const float* xp, int S, int64_t ps, int T, int F, hipStream_t st);
 hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int S, int64_t ps, int64_t qkv_stride,
                                 const int64_t* positions, const float* cos_sin, bf16* q_out, int64_t q_stride,
                                 bf16* k_cache, bf16* v_cache, const int64_t* slot_mapping, int T, int Hq, int Hkv,
-                                int D, int block_size, Gates gt, hipStream_t st);
+                                int D, int block_size, hipStream_t st);
 hipError_t kafka_launch_rope_kv_fp8(const bf16* qkv, const float* qp, int S, int64_t ps, int64_t qkv_stride,
                                     const int64_t* positions, const float* cos_sin, bf16* q_out, int64_t q_stride,
                                     uint8_t* k_cache, uint8_t* v_cache, const int64_t* slot_mapping, int T, int Hq,
@@ -40,33 +28,23 @@ hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const void*
                                     int n_items, int B, int Hkv, int G, int D, const int* block_tables, int bt_stride,
                                     const int* items, float* out_part, float* lse_part, int S_total, float scale,
                                     bf16* out, int64_t out_stride, int* tickets, const bf16* pre_bf16,
-                                    Gates gt, hipStream_t st);
-hipError_t kafka_launch_attn_decode_sk(const bf16* q, int64_t q_stride, const void* k_cache, const void* v_cache,
-                                       int fp8, int B, int Hkv, int G, int D, const int* block_tables, int bt_stride,
-                                       const int* rows, const int* start, int nwg, float* out_part,
-                                       float* lse_part, int S_total, float scale, bf16* out, int64_t out_stride,
-                                       int* tickets, const bf16* pre_bf16, hipStream_t st);
+                                    hipStream_t st);
 hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride,
                                      const void* k_cache, const void* v_cache, int fp8, int Hkv, int G, int D,
                                      const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
                                      int64_t out_stride, float* out_part, float* lse_part, int S_total, float scale,
-                                     int variant, int part_bf16, Gates gt, hipStream_t st);
+                                     int variant, int part_bf16, hipStream_t st);
 hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows, int Hq, int S, int D, bf16* out,
                              int64_t out_stride, float* lse_out, hipStream_t st);
 hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
                          const float* top_p, const int* top_k, const int64_t* seeds, const int64_t* step,
                          int64_t* out_tokens, int* ws, int nsplit, const int* proc, const uint32_t* mask_tab,
                          int64_t mask_ld, int* counts, int64_t cnt_ld, hipStream_t st);
-int kafka_wstream_plan(int M, int N, int K, int max_splits, int one_tile, int* mt, int* kc, int* splits);
+int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits);
 hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt, int kc,
                                      int splits, int nt, int kw, int glu, bf16* Y, int64_t ldy, float* P,
-                                     Gates gt, hipStream_t st);
+                                     hipStream_t st);
 hipError_t kafka_launch_slab_reduce(const float* P, int S, int M, int N, bf16* Y, int64_t ldy, hipStream_t st);
-hipError_t kafka_launch_wstream_qkv_rope(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt,
-                                         int kc, int splits, float* P, const int64_t* positions, const float* cos_sin,
-                                         bf16* q_out, int64_t q_stride, bf16* k_cache, bf16* v_cache,
-                                         const int64_t* slots, int Hq, int Hkv, int* tickets, Gates gt,
-                                         hipStream_t st);
 hipError_t kafka_launch_wstream_grouped(const bf16* X, int64_t ldx, const bf16* Wt, int e_local, int N, int K,
                                         const int* perm_tok, const float* perm_w, const int* expert_off, int e_lo,
                                         int max_rows, int gather, bf16* Y, int64_t ldy, float* out, int64_t ldo,
@@ -128,33 +106,6 @@ static void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
                                   cur_stream()));
 }
 
-// gates: int32 buffer of GATE_INTS words per gate (ops.GateSet); args: [wait, expect, sig, wait2, expect2] with gate
-// ids (-1: none). Missing buffer or args: no gates (an ordinary launch).
-static Gates make_gates(const c10::optional<at::Tensor>& buf, const std::vector<int64_t>& a) {
-  Gates g;
-  if (!buf.has_value() || a.empty()) return g;
-  TORCH_CHECK(buf->scalar_type() == at::kInt && buf->is_contiguous() && buf->is_cuda(), "gates: int32 device buffer");
-  const int64_t n = buf->numel() / GATE_INTS;
-  int* base = buf->data_ptr<int>();
-  auto at_ = [&](size_t i) -> int* {
-    if (i >= a.size() || a[i] < 0) return nullptr;
-    TORCH_CHECK(a[i] < n, "gates: gate id out of range");
-    return base + a[i] * GATE_INTS;
-  };
-  g.wait = at_(0);
-  g.expect = a.size() > 1 ? (int)a[1] : 0;
-  g.sig = at_(2);
-  g.wait2 = at_(3);
-  g.expect2 = a.size() > 4 ? (int)a[4] : 0;
-  static const int mode = [] {  // diagnostics only (csrc/common.h Gates::mode)
-    const char* e = getenv("KAFKA_GATE_MODE");
-    const char* sl = getenv("KAFKA_GATE_SLEEP");
-    return (e && (e[0] == '1' || e[0] == '3') ? 1 : 0) | ((sl ? atoi(sl) : 0) << 4);
-  }();
-  g.mode = mode;
-  return g;  // expect <= 0: the producer's published arrival count
-}
-
 // A split-K slab is an fp32 contiguous [S, T, n] tensor (wstream_gemm output); kernels that accept one sum it on load.
 static bool is_slab(const at::Tensor& x) { return x.scalar_type() == at::kFloat && x.dim() == 3; }
 static void check_slab(const at::Tensor& x) {
@@ -162,9 +113,7 @@ static void check_slab(const at::Tensor& x) {
 }
 
 // x: bf16 [T, d] or slab [S, T, d]
-static void fused_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor residual, at::Tensor w, double eps,
-                              c10::optional<at::Tensor> gates, std::vector<int64_t> gate_args) {
-  const Gates gt = make_gates(gates, gate_args);
+static void fused_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor residual, at::Tensor w, double eps) {
   CHECK_CUDA(x); CHECK_DT(residual, at::kBFloat16); CHECK_DT(w, at::kBFloat16);
   CHECK_DT(out, at::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out); CHECK_LASTDIM(residual);
@@ -180,10 +129,10 @@ static void fused_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor residual,
   if (slab)
     CHECK_HIP(kafka_launch_fused_add_rmsnorm_slab(bptr(out), out.stride(0), x.data_ptr<float>(), x.size(0),
                                                   T * d, bptr(residual), residual.stride(0), bptr(w), T, d, eps,
-                                                  gt, cur_stream()));
+                                                  cur_stream()));
   else
     CHECK_HIP(kafka_launch_fused_add_rmsnorm(bptr(out), out.stride(0), bptr(x), x.stride(0), bptr(residual),
-                                              residual.stride(0), bptr(w), T, d, eps, gt, cur_stream()));
+                                              residual.stride(0), bptr(w), T, d, eps, cur_stream()));
 }
 
 // x: bf16 [T, 2F] or slab [S, T, 2F]
@@ -226,8 +175,7 @@ static void check_cache_pair(const at::Tensor& k_cache, const at::Tensor& v_cach
 
 static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin, at::Tensor q_out,
                           at::Tensor k_cache, at::Tensor v_cache, c10::optional<at::Tensor> slot_mapping, int64_t Hq,
-                          int64_t Hkv, c10::optional<at::Tensor> gates, std::vector<int64_t> gate_args) {
-  const Gates gt = make_gates(gates, gate_args);
+                          int64_t Hkv) {
   CHECK_CUDA(qkv); CHECK_DT(q_out, at::kBFloat16);
   const bool slab = is_slab(qkv);
   if (slab) check_slab(qkv); else CHECK_DT(qkv, at::kBFloat16);
@@ -235,7 +183,6 @@ static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_s
   TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && cos_sin.is_contiguous() &&
                   positions.is_contiguous(), "rope_kv_write: caches/positions/cos_sin must be contiguous");
   const bool fp8 = is_fp8_cache(k_cache);
-  TORCH_CHECK(!fp8 || (gt.wait == nullptr && gt.sig == nullptr), "rope_kv_write: gates need a bf16 cache");
   int D, bs = 16;
   if (fp8) {
     check_cache_pair(k_cache, v_cache);
@@ -273,7 +220,7 @@ static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_s
     CHECK_HIP(kafka_launch_rope_kv(slab ? nullptr : bptr(qkv), slab ? qkv.data_ptr<float>() : nullptr,
                                     slab ? qkv.size(0) : 0, slab ? (int64_t)T * W : 0, slab ? W : qkv.stride(0),
                                     positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), bptr(q_out),
-                                    q_out.stride(0), bptr(k_cache), bptr(v_cache), sm, T, Hq, Hkv, D, bs, gt,
+                                    q_out.stride(0), bptr(k_cache), bptr(v_cache), sm, T, Hq, Hkv, D, bs,
                                     cur_stream()));
 }
 
@@ -282,9 +229,7 @@ static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_s
 static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
                         at::Tensor items, at::Tensor out_part, at::Tensor lse_part, double scale,
                         c10::optional<at::Tensor> out, c10::optional<at::Tensor> tickets,
-                        c10::optional<at::Tensor> pre_part, c10::optional<at::Tensor> gates,
-                        std::vector<int64_t> gate_args) {
-  const Gates gt = make_gates(gates, gate_args);
+                        c10::optional<at::Tensor> pre_part) {
   CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
   CHECK_DT(block_tables, at::kInt); CHECK_DT(items, at::kInt); CHECK_DT(out_part, at::kFloat);
   CHECK_DT(lse_part, at::kFloat);
@@ -324,66 +269,13 @@ static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at
                                       is_fp8_cache(k_cache) ? 1 : 0, items.size(0), B, Hkv,
                                       Hq / Hkv, 128, block_tables.data_ptr<int>(), block_tables.stride(0),
                                       items.data_ptr<int>(), out_part.data_ptr<float>(), lse_part.data_ptr<float>(),
-                                      S_total, scale, op, ostride, tp, pre, gt, cur_stream()));
-}
-
-// Stream-K decode: rows int32 [B + 1, 4] (kv_lo, kv_hi, npre, cost start; last row = plan (T, F, total, 0)), start
-// int32 [nwg, 2] (first row, kv head of each workgroup's slice) — see attention.hip attn_decode_sk_kernel. Row /
-// slot values are device data; the kernel drops a piece whose row or slots fall outside the checked shapes.
-static void attn_decode_sk(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
-                           at::Tensor rows, at::Tensor start, at::Tensor out_part, at::Tensor lse_part, double scale, c10::optional<at::Tensor> out,
-                           c10::optional<at::Tensor> tickets, c10::optional<at::Tensor> pre_part) {
-  CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
-  CHECK_DT(block_tables, at::kInt); CHECK_DT(rows, at::kInt); CHECK_DT(start, at::kInt);
-  CHECK_DT(out_part, at::kFloat); CHECK_DT(lse_part, at::kFloat);
-  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == 128 && q.size(2) == 128, "q must be [B, Hq, 128]");
-  const int B = q.size(0), Hq = q.size(1), Hkv = k_cache.size(1);
-  TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 8, "decode kernel needs Hq/Hkv <= 8");
-  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.stride(1) == 1, "block_tables");
-  TORCH_CHECK(rows.is_cuda() && rows.is_contiguous() && rows.dim() == 2 && rows.size(0) == B + 1 &&
-                  rows.size(1) == 4, "rows must be a device int32 [B + 1, 4]");
-  TORCH_CHECK(start.is_cuda() && start.is_contiguous() && start.dim() == 2 && start.size(1) == 2 &&
-                  start.size(0) <= 65535, "start must be a device int32 [nwg, 2]");
-  const int nwg = start.size(0);
-  TORCH_CHECK(out_part.is_contiguous() && out_part.dim() == 4 && out_part.size(0) >= B && out_part.size(1) == Hq &&
-                  out_part.size(3) == 128, "out_part must be [B, Hq, S_total, 128]");
-  const int S_total = out_part.size(2);
-  TORCH_CHECK(lse_part.is_contiguous() && lse_part.numel() >= (int64_t)B * Hq * S_total, "lse_part");
-  bf16* op = nullptr;
-  int64_t ostride = 0;
-  int* tp = nullptr;
-  if (out.has_value()) {
-    CHECK_DT(out.value(), at::kBFloat16);
-    TORCH_CHECK(out->dim() == 3 && out->size(0) >= B && out->size(1) == Hq && out->size(2) == 128 &&
-                    out->stride(2) == 1 && out->stride(1) == 128,
-                "attn_decode_sk: fused-merge out must be [B, Hq, 128]");
-    op = bptr(out.value());
-    ostride = out->stride(0);
-    TORCH_CHECK(tickets.has_value() && tickets->is_cuda() && tickets->scalar_type() == at::kInt &&
-                    tickets->numel() >= (int64_t)B * Hkv,
-                "attn_decode_sk: the fused merge needs an int32 ticket buffer of >= B * Hkv zeros");
-    tp = tickets->data_ptr<int>();
-  }
-  const bf16* pre = nullptr;
-  if (pre_part.has_value()) {
-    CHECK_DT(pre_part.value(), at::kBFloat16);
-    TORCH_CHECK(pre_part->is_contiguous() && pre_part->sizes() == out_part.sizes(),
-                "attn_decode_sk: pre_part must match out_part's shape");
-    pre = bptr(pre_part.value());
-  }
-  CHECK_HIP(kafka_launch_attn_decode_sk(bptr(q), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
-                                         is_fp8_cache(k_cache) ? 1 : 0, B, Hkv, Hq / Hkv, 128,
-                                         block_tables.data_ptr<int>(), block_tables.stride(0), rows.data_ptr<int>(),
-                                         start.data_ptr<int>(), nwg, out_part.data_ptr<float>(), lse_part.data_ptr<float>(), S_total, scale, op,
-                                         ostride, tp, pre, cur_stream()));
+                                      S_total, scale, op, ostride, tp, pre, cur_stream()));
 }
 
 static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                          at::Tensor block_tables, at::Tensor q_limit, c10::optional<at::Tensor> out,
                          c10::optional<at::Tensor> out_part, c10::optional<at::Tensor> lse_part, double scale,
-                         int64_t variant, c10::optional<at::Tensor> gates, std::vector<int64_t> gate_args) {
-  const Gates gt = make_gates(gates, gate_args);
-  TORCH_CHECK((gt.wait == nullptr && gt.sig == nullptr) || variant == 3, "attn_prefill: gates need tile variant 3");
+                         int64_t variant) {
   CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
   CHECK_DT(items, at::kInt); CHECK_DT(block_tables, at::kInt); CHECK_DT(q_limit, at::kInt);
   TORCH_CHECK(items.is_contiguous() && items.dim() == 2 && items.size(1) == 8, "items must be [n, 8] int32");
@@ -424,7 +316,7 @@ static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at:
   CHECK_HIP(kafka_launch_attn_prefill(items.data_ptr<int>(), items.size(0), bptr(q), q.stride(0), k_cache.data_ptr(),
                                        v_cache.data_ptr(), is_fp8_cache(k_cache) ? 1 : 0, Hkv, G, 128, block_tables.data_ptr<int>(),
                                        block_tables.stride(0), q_limit.data_ptr<int>(), op, os, pp, lp, S_total,
-                                       scale, (int)variant, part_bf16, gt, cur_stream()));
+                                       scale, (int)variant, part_bf16, cur_stream()));
 }
 
 static void attn_merge(at::Tensor part, at::Tensor lse, at::Tensor out, c10::optional<at::Tensor> lse_out) {
@@ -507,16 +399,14 @@ static void sample(at::Tensor logits, c10::optional<at::Tensor> temperature, c10
 // (mt, kc, splits) of the weight-streaming decode GEMM for a shape, or (0, 0, 0) if unsupported
 static std::vector<int64_t> wstream_plan(int64_t M, int64_t N, int64_t K, int64_t max_splits) {
   int mt = 0, kc = 0, s = 0;
-  if (kafka_wstream_plan((int)M, (int)N, (int)K, (int)max_splits, 0, &mt, &kc, &s) != 0) return {0, 0, 0};
+  if (kafka_wstream_plan((int)M, (int)N, (int)K, (int)max_splits, &mt, &kc, &s) != 0) return {0, 0, 0};
   return {mt, kc, s};
 }
 
 // x [M, K] bf16 . W^T with W given wave-tiled as wt [N/32, K/16, 64, 8] (ops.tile_weight). Writes bf16 y [M, N]
 // (splits == 1) or fp32 slabs p [splits, M, N].
 static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y, c10::optional<at::Tensor> p,
-                         int64_t max_splits, bool nt, bool glu, c10::optional<at::Tensor> gates,
-                         std::vector<int64_t> gate_args) {
-  const Gates gt = make_gates(gates, gate_args);
+                         int64_t max_splits, bool nt, bool glu) {
   CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0, "wstream_gemm: x must be [M, K] with 16-B rows");
   TORCH_CHECK(wt.dim() == 4 && wt.is_contiguous() && wt.size(2) == 64 && wt.size(3) == 8,
@@ -525,7 +415,7 @@ static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> 
   TORCH_CHECK(wt.size(1) * 16 == K, "wstream_gemm: K mismatch");
   TORCH_CHECK(!glu || N % 64 == 0, "wstream_gemm: GLU weights need N % 64 == 0");
   int mt = 0, kc = 0, s = 0;
-  TORCH_CHECK(kafka_wstream_plan(M, N, K, (int)max_splits, 0, &mt, &kc, &s) == 0, "wstream_gemm: unsupported shape");
+  TORCH_CHECK(kafka_wstream_plan(M, N, K, (int)max_splits, &mt, &kc, &s) == 0, "wstream_gemm: unsupported shape");
   bf16* yp = nullptr;
   int64_t ldy = 0;
   float* pp = nullptr;
@@ -545,15 +435,10 @@ static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> 
   }
   // two K halves per chunk (8 waves) for 64-row tiles with >= 6 chunks per split: the long streams (gate_up unsplit
   // with its fused SwiGLU, down) ran 1.6-2.8 % faster in the config sweep, the short ones (qkv, o) slower; headline
-  // +0.24 % (3 / 3 interleaved pairs, profiles/r04/bench_ab_wstream_kw2.jsonl). KAFKA_WSTREAM_KW2=0: one wave per
-  // column tile everywhere
-  static const bool kw2 = [] {
-    const char* e = getenv("KAFKA_WSTREAM_KW2");
-    return e == nullptr || e[0] != '0';
-  }();
-  const int kw = kw2 && mt == 2 && kc == 256 && K / s / kc >= 6 && gt.wait == nullptr && gt.sig == nullptr ? 2 : 1;
+  // +0.24 % (3 / 3 interleaved pairs, profiles/r04/bench_ab_wstream_kw2.jsonl)
+  const int kw = mt == 2 && kc == 256 && K / s / kc >= 6 ? 2 : 1;
   CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, nt ? 1 : 0, kw, glu ? 1 : 0,
-                                      yp, ldy, pp, gt, cur_stream()));
+                                      yp, ldy, pp, cur_stream()));
 }
 
 // Skinny MFMA GEMM (csrc/skinny_gemm.hip) for 129..256 rows on the wave-tiled weights: y bf16 for one split
@@ -592,50 +477,6 @@ static void skinny_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y
                                      cur_stream()));
 }
 
-// QKV projection on the streaming kernel with RoPE + the paged KV write in its epilogue (bf16 cache, head dim 128):
-// replaces wstream_gemm + rope_kv_write on decode-sized steps. p: fp32 scratch [splits, M, N] when the plan splits K.
-static void wstream_qkv_rope(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> p, at::Tensor positions,
-                             at::Tensor cos_sin, at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache,
-                             c10::optional<at::Tensor> slot_mapping, int64_t Hq, int64_t Hkv, at::Tensor tickets,
-                             int64_t max_splits, c10::optional<at::Tensor> gates, std::vector<int64_t> gate_args) {
-  const Gates gt = make_gates(gates, gate_args);
-  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
-  CHECK_DT(positions, at::kLong); CHECK_DT(cos_sin, at::kFloat); CHECK_DT(q_out, at::kBFloat16);
-  CHECK_DT(k_cache, at::kBFloat16); CHECK_DT(v_cache, at::kBFloat16); CHECK_DT(tickets, at::kInt);
-  TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0, "wstream_qkv_rope: x must be [M, K] with 16-B rows");
-  TORCH_CHECK(wt.dim() == 4 && wt.is_contiguous() && wt.size(2) == 64 && wt.size(3) == 8, "wstream_qkv_rope: wt");
-  const int M = x.size(0), K = x.size(1), N = wt.size(0) * 32;
-  TORCH_CHECK(wt.size(1) * 16 == K && N == (Hq + 2 * Hkv) * 128, "wstream_qkv_rope: K / N mismatch");
-  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && k_cache.dim() == 4 && v_cache.dim() == 4 &&
-                  k_cache.size(1) == Hkv && k_cache.size(2) == 16 && k_cache.size(3) == 128 &&
-                  v_cache.size(1) == Hkv && v_cache.size(2) == 128 && v_cache.size(3) == 16 &&
-                  v_cache.size(0) == k_cache.size(0), "wstream_qkv_rope: cache shape");
-  TORCH_CHECK(positions.is_contiguous() && positions.numel() == M && cos_sin.is_contiguous() && cos_sin.dim() == 2 &&
-                  cos_sin.size(1) == 128, "wstream_qkv_rope: positions / cos_sin");
-  TORCH_CHECK(q_out.dim() == 3 && q_out.size(0) == M && q_out.size(1) == Hq && q_out.size(2) == 128 &&
-                  q_out.stride(2) == 1 && q_out.stride(1) == 128, "wstream_qkv_rope: q_out shape");
-  TORCH_CHECK(tickets.is_contiguous() && tickets.numel() >= N / 128, "wstream_qkv_rope: tickets");
-  const int64_t* sm = nullptr;
-  if (slot_mapping.has_value()) {
-    CHECK_DT(slot_mapping.value(), at::kLong);
-    TORCH_CHECK(slot_mapping->is_contiguous() && slot_mapping->numel() == M, "wstream_qkv_rope: slot_mapping");
-    sm = slot_mapping->data_ptr<int64_t>();
-  }
-  int mt = 0, kc = 0, s = 0;
-  TORCH_CHECK(kafka_wstream_plan(M, N, K, (int)max_splits, 1, &mt, &kc, &s) == 0, "wstream_qkv_rope: unsupported shape");
-  float* pp = nullptr;
-  if (s > 1) {
-    TORCH_CHECK(p.has_value(), "wstream_qkv_rope: scratch required for a split plan");
-    CHECK_DT(p.value(), at::kFloat);
-    TORCH_CHECK(p->is_contiguous() && p->numel() >= (int64_t)s * M * N, "wstream_qkv_rope: scratch too small");
-    pp = p->data_ptr<float>();
-  }
-  CHECK_HIP(kafka_launch_wstream_qkv_rope(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, pp,
-                                          positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), bptr(q_out),
-                                          q_out.stride(0), bptr(k_cache), bptr(v_cache), sm, (int)Hq, (int)Hkv,
-                                          tickets.data_ptr<int>(), gt, cur_stream()));
-}
-
 // explicit-configuration variant (microbenchmark sweeps): (mt, kc, splits) as given, no planning
 static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y, c10::optional<at::Tensor> p,
                              int64_t mt, int64_t kc, int64_t s, bool nt, int64_t kw) {
@@ -653,7 +494,7 @@ static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tens
   CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, (int)mt, (int)kc, (int)s, nt ? 1 : 0,
                                       (int)kw, 0,
                                       s == 1 ? bptr(y.value()) : nullptr, s == 1 ? y->stride(0) : 0,
-                                      s == 1 ? nullptr : p->data_ptr<float>(), Gates{}, cur_stream()));
+                                      s == 1 ? nullptr : p->data_ptr<float>(), cur_stream()));
 }
 
 // Expert MLP halves on wave-tiled expert weights wt [E_local, N/32, K/16, 64, 8] (ops.tile_experts). glu: gate_up
@@ -949,37 +790,24 @@ static void ep_combine(at::Tensor back, at::Tensor slot_map, at::Tensor topk_w, 
 PYBIND11_MODULE(_kafka_ops, m) {
   m.doc() = "kafka_llm_service_amd CDNA4 (gfx950) HIP kernels";
   m.def("rmsnorm", &rmsnorm);
-  m.def("fused_add_rmsnorm", &fused_add_rmsnorm, py::arg("out"), py::arg("x"), py::arg("residual"), py::arg("w"),
-        py::arg("eps"), py::arg("gates") = py::none(), py::arg("gate_args") = std::vector<int64_t>{});
+  m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
   m.def("silu_mul", &silu_mul);
-  m.def("rope_kv_write", &rope_kv_write, py::arg("qkv"), py::arg("positions"), py::arg("cos_sin"), py::arg("q_out"),
-        py::arg("k_cache"), py::arg("v_cache"), py::arg("slot_mapping"), py::arg("Hq"), py::arg("Hkv"),
-        py::arg("gates") = py::none(), py::arg("gate_args") = std::vector<int64_t>{});
+  m.def("rope_kv_write", &rope_kv_write);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("items"), py::arg("out_part"), py::arg("lse_part"), py::arg("scale"), py::arg("out"),
-        py::arg("tickets"), py::arg("pre_part") = py::none(), py::arg("gates") = py::none(),
-        py::arg("gate_args") = std::vector<int64_t>{});
+        py::arg("tickets"), py::arg("pre_part") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("items"), py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("block_tables"), py::arg("q_limit"), py::arg("out"), py::arg("out_part"), py::arg("lse_part"),
-        py::arg("scale"), py::arg("variant") = 0, py::arg("gates") = py::none(),
-        py::arg("gate_args") = std::vector<int64_t>{});
+        py::arg("scale"), py::arg("variant") = 0);
   m.def("attn_merge", &attn_merge);
-  m.def("attn_decode_sk", &attn_decode_sk, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
-        py::arg("block_tables"), py::arg("rows"), py::arg("start"), py::arg("out_part"), py::arg("lse_part"), py::arg("scale"), py::arg("out") = py::none(),
-        py::arg("tickets") = py::none(), py::arg("pre_part") = py::none());
   m.def("sample", &sample, py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"),
         py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none(), py::arg("nsplit") = 1,
         py::arg("proc") = py::none(), py::arg("mask_tab") = py::none(), py::arg("counts") = py::none());
   m.def("wstream_plan", &wstream_plan);
   m.def("wstream_gemm", &wstream_gemm, py::arg("x"), py::arg("wt"), py::arg("y"), py::arg("p"),
-        py::arg("max_splits"), py::arg("nt"), py::arg("glu"), py::arg("gates") = py::none(),
-        py::arg("gate_args") = std::vector<int64_t>{});
+        py::arg("max_splits"), py::arg("nt"), py::arg("glu"));
   m.def("skinny_plan", &skinny_plan);
   m.def("skinny_gemm", &skinny_gemm);
-  m.def("wstream_qkv_rope", &wstream_qkv_rope, py::arg("x"), py::arg("wt"), py::arg("p"), py::arg("positions"),
-        py::arg("cos_sin"), py::arg("q_out"), py::arg("k_cache"), py::arg("v_cache"), py::arg("slot_mapping"),
-        py::arg("Hq"), py::arg("Hkv"), py::arg("tickets"), py::arg("max_splits"), py::arg("gates") = py::none(),
-        py::arg("gate_args") = std::vector<int64_t>{});
   m.def("wstream_gemm_cfg", &wstream_gemm_cfg);
   m.def("slab_reduce", &slab_reduce);
   m.def("wstream_grouped", &wstream_grouped);

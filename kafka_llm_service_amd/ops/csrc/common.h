@@ -9,7 +9,6 @@
 //       B: lane l holds B[k = 8*(l>>5) + j][col l&31]
 //       C/D: lane l, reg i -> row (i&3) + 8*(i>>2) + 4*(l>>5), col l&31
 #pragma once
-#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -116,120 +115,6 @@ __device__ __forceinline__ void load_in8(float (&v)[8], const bf16* __restrict__
 
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// ---- device gates: early-launched consumers ---------------------------------------------------------------------
-// A consumer kernel launched WITHOUT the AQL barrier bit (hipExtAnyOrderLaunch) is dispatched as soon as its
-// predecessor's last workgroup has been dispatched, so it runs its producer-independent prologue (the weight stream
-// of a projection, page tables, first K/V tiles) while the producer's tail still runs, then waits on a gate. Dispatch
-// order within a queue guarantees every producer workgroup is resident before any consumer workgroup, so a waiting
-// consumer can never starve its producer.
-// A gate is 17 cache lines (no line is hot): lines 0..7 are arrival counters (a producer unit u arrives on line
-// u & 7), line 8 the top counter (+ error word), lines 9..16 per-XCD "done" flags. The last arrival of a line bumps
-// the top counter; the last of those raises all 8 flags. A consumer workgroup polls ONE flag (line 9 + its id & 7),
-// so each line sees a handful of same-address accesses instead of every workgroup of both kernels.
-// The producer's arrivals are agent-scope acq_rel RMWs after a workgroup barrier (release cumulativity carries the
-// whole workgroup's writes), the flags release stores, the consumer's wait ends with an agent-scope acquire.
-// Rule for callers (ops.GateSet / models): a gated consumer writes nothing to global memory before its wait, and it
-// waits on the kernel launched immediately before it (gates then chain transitively, and the caching allocator's
-// stream-order reuse stays safe).
-constexpr int GATE_LINE = 16;                // int32 per 64-B line
-constexpr int GATE_INTS = 17 * GATE_LINE;
-struct Gates {
-  int* wait = nullptr;   // wait until this gate's producer has fully arrived (nullptr: no wait)
-  int expect = 0;        // (unused: the producer counts its own arrivals)
-  int* sig = nullptr;    // arrive on this gate when the unit's outputs are written (nullptr: none)
-  int* wait2 = nullptr;  // a second gate (decode attention: the cascade partials, before the merge)
-  int expect2 = 0;
-  int mode = 0;          // diagnostics: bit 0 (KAFKA_GATE_MODE=1/3) = no release / acquire (timing only: unordered
-                         // reads); bits 4.. (KAFKA_GATE_SLEEP) = poll back-off level
-};
-
-__device__ __forceinline__ int gate_block_id() {
-  return (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
-}
-
-// ONE thread, after a __syncthreads() that follows every global write of arrival unit `unit` (0 <= unit < total; a
-// launch arrives `total` times, each unit once)
-__device__ __forceinline__ void gate_arrive(int* g, int unit, int total, int mode = 0) {
-  if (g == nullptr) return;
-  const int s = unit & 7;
-  const int n_s = total / 8 + (s < total % 8 ? 1 : 0);
-  const int lines = total < 8 ? total : 8;
-  const bool rlx = mode & 1;
-  const int old = rlx ? __hip_atomic_fetch_add(g + s * GATE_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : __hip_atomic_fetch_add(g + s * GATE_LINE, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-  if (old != n_s - 1) return;
-  const int top = rlx ? __hip_atomic_fetch_add(g + 8 * GATE_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : __hip_atomic_fetch_add(g + 8 * GATE_LINE, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-  if (top != lines - 1) return;
-#pragma unroll
-  for (int x = 0; x < 8; ++x) {
-    if (rlx)
-      __hip_atomic_store(g + (9 + x) * GATE_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      __hip_atomic_store(g + (9 + x) * GATE_LINE, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// every thread of the workgroup (workgroup-uniform arguments); bounded: after 2 s the error word is raised and the
-// wait gives up (the host fails the step instead of hanging the GPU)
-__device__ __forceinline__ void gate_wait(int* g, int mode = 0) {
-  if (g == nullptr) return;
-  if (threadIdx.x == 0) {
-    const int* flag = g + (9 + (gate_block_id() & 7)) * GATE_LINE;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
-        __hip_atomic_store(g + 8 * GATE_LINE + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      switch (mode >> 4) {  // uniform
-        case 0: __builtin_amdgcn_s_sleep(1); break;
-        case 1: __builtin_amdgcn_s_sleep(8); break;
-        default: __builtin_amdgcn_s_sleep(32); break;
-      }
-    }
-  }
-  __syncthreads();
-  if (!(mode & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-
-// Write-through hand-off (the cascade -> suffix-decode overlap): the producer writes its outputs with agent-coherent
-// stores (sc1: through to memory, not parked dirty in its XCD's L2), waits for them (vmcnt), and arrives RELAXED; the
-// consumer waits RELAXED and reads them with agent-coherent loads (sc1: not served from its XCD's possibly stale L2)
-// — neither side needs the L2-wide write-back / invalidate of a release / acquire fence.
-__device__ __forceinline__ void st_wt16(void* p, f32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ f32x4 ld_wt16(const void* p) {  // the caller waits (s_waitcnt vmcnt) before using it
-  f32x4 r;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
-  return r;
-}
-__device__ __forceinline__ f32x2 ld_wt8(const void* p) {
-  f32x2 r;
-  asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
-  return r;
-}
-// after every write-through store of the workgroup: all of them complete, then ONE relaxed arrival
-__device__ __forceinline__ void gate_arrive_wt(int* g, int unit, int total) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) gate_arrive(g, unit, total, 1);
-}
-
-// Launch `kernel`; `early`: without the AQL barrier bit (the kernel waits on a gate before reading its inputs)
-template <typename F, typename... Args>
-inline void launch_maybe_early(F kernel, dim3 grid, dim3 block, hipStream_t st, bool early, Args... args) {
-  static const bool ordered = [] {  // diagnostics: KAFKA_GATE_MODE=2 keeps the barrier bit (gates without overlap)
-    const char* e = getenv("KAFKA_GATE_MODE");
-    return e && (e[0] == '2' || e[0] == '3');
-  }();
-  if (early && !ordered)
-    hipExtLaunchKernelGGL(kernel, grid, block, 0, st, nullptr, nullptr, hipExtAnyOrderLaunch, args...);
-  else
-    hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
 }
 
 // Counter-based RNG (splitmix64 finaliser): deterministic given (seed, stream, index).

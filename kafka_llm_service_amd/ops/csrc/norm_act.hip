@@ -14,12 +14,12 @@ namespace kafka {
 
 // y = x * rsqrt(mean(x^2) + eps) * w     (x: [T, d] with row stride, out: [T, d] contiguous)
 // If RESID: r = x + r (rounded to bf16, written back to r), y = norm(r) * w.
-template <int NV, bool RESID, int NT = 256, bool GATED = false>
+template <int NV, bool RESID, int NT = 256>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int64_t out_stride,
                                                        const bf16* __restrict__ x, const float* __restrict__ xp,
                                                        int S, int64_t ps, int64_t x_stride,
                                                        bf16* __restrict__ resid, int64_t r_stride,
-                                                       const bf16* __restrict__ w, int d, float eps, Gates gt) {
+                                                       const bf16* __restrict__ w, int d, float eps) {
   __shared__ float red[NT / 64];
   const int64_t row = blockIdx.x;
   const int nvec = d >> 3;
@@ -31,10 +31,6 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int
   for (int i = 0; i < NV; ++i) {
     const int vi = threadIdx.x + i * NT;
     if (vi < nvec) wv[i] = load_bf16x8(w + vi * 8);
-  }
-  if constexpr (GATED) {  // early-launched (common.h Gates): the producer of x has finished
-    asm volatile("" ::: "memory");
-    gate_wait(gt.wait, gt.mode);
   }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -67,10 +63,6 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int
       store_bf16x8(out + row * out_stride + vi * 8, o);
     }
   }
-  if constexpr (GATED) {  // one arrival per row (common.h Gates)
-    __syncthreads();
-    if (threadIdx.x == 0) gate_arrive(gt.sig, (int)blockIdx.x, (int)gridDim.x, gt.mode);
-  }
 }
 
 // out[t, :] = silu(x[t, :F]) * x[t, F:]   (x: [T, 2F] row stride xs (bf16 or slabs), out: [T, F] contiguous)
@@ -93,35 +85,21 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(bf16* __restrict__ out, c
 template <bool RESID>
 static hipError_t launch_rmsnorm_t(bf16* out, int64_t os, const bf16* x, const float* xp, int S, int64_t ps,
                                    int64_t xs, bf16* r, int64_t rs, const bf16* w, int T, int d, float eps,
-                                   hipStream_t st, Gates gt = Gates{}) {
+                                   hipStream_t st) {
   const int nvec = d / 8;
   const int nv = (nvec + 255) / 256;
   dim3 grid(T), block(256);
   if (T == 0) return hipSuccess;
-  const bool gated = gt.wait != nullptr || gt.sig != nullptr;  // (the gated code is its own instantiation)
   if (nvec <= 512 && nvec > 256) {  // e.g. d = 4096: one 16-B vector per thread, twice the loads in flight per row
-    if (gated)
-      launch_maybe_early(rmsnorm_kernel<1, RESID, 512, true>, grid, dim3(512), st, gt.wait != nullptr, out, os, x, xp,
-                         S, ps, xs, r, rs, w, d, eps, gt);
-    else
-      rmsnorm_kernel<1, RESID, 512><<<grid, 512, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt);
+    rmsnorm_kernel<1, RESID, 512><<<grid, 512, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps);
     return hipGetLastError();
   }
   switch (nv) {
-#define KAFKA_RMS(NV_)                                                                                          \
-  do {                                                                                                         \
-    if (gated)                                                                                                 \
-      launch_maybe_early(rmsnorm_kernel<NV_, RESID, 256, true>, grid, block, st, gt.wait != nullptr, out, os, x, xp, \
-                         S, ps, xs, r, rs, w, d, eps, gt);                                                    \
-    else                                                                                                       \
-      rmsnorm_kernel<NV_, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps, gt);       \
-  } while (0)
-    case 1: KAFKA_RMS(1); break;
-    case 2: KAFKA_RMS(2); break;
+    case 1: rmsnorm_kernel<1, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
+    case 2: rmsnorm_kernel<2, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
     case 3:
-    case 4: KAFKA_RMS(4); break;
-    default: KAFKA_RMS(8); break;
-#undef KAFKA_RMS
+    case 4: rmsnorm_kernel<4, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
+    default: rmsnorm_kernel<8, RESID><<<grid, block, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps); break;
   }
   return hipGetLastError();
 }
@@ -132,15 +110,15 @@ extern "C" hipError_t kafka_launch_rmsnorm(bf16* out, int64_t os, const bf16* x,
 }
 
 extern "C" hipError_t kafka_launch_fused_add_rmsnorm(bf16* out, int64_t os, const bf16* x, int64_t xs, bf16* resid, int64_t rs,
-                                    const bf16* w, int T, int d, float eps, Gates gt, hipStream_t st) {
-  return launch_rmsnorm_t<true>(out, os, x, nullptr, 0, 0, xs, resid, rs, w, T, d, eps, st, gt);
+                                    const bf16* w, int T, int d, float eps, hipStream_t st) {
+  return launch_rmsnorm_t<true>(out, os, x, nullptr, 0, 0, xs, resid, rs, w, T, d, eps, st);
 }
 
 // fused add + RMSNorm whose x input is S fp32 split-K slabs [S][T][d] (row stride d, slab stride ps)
 extern "C" hipError_t kafka_launch_fused_add_rmsnorm_slab(bf16* out, int64_t os, const float* xp, int S, int64_t ps,
                                                          bf16* resid, int64_t rs, const bf16* w, int T, int d,
-                                                         float eps, Gates gt, hipStream_t st) {
-  return launch_rmsnorm_t<true>(out, os, nullptr, xp, S, ps, d, resid, rs, w, T, d, eps, st, gt);
+                                                         float eps, hipStream_t st) {
+  return launch_rmsnorm_t<true>(out, os, nullptr, xp, S, ps, d, resid, rs, w, T, d, eps, st);
 }
 
 extern "C" hipError_t kafka_launch_silu_mul(bf16* out, const bf16* x, int64_t xs, int T, int F, hipStream_t st) {

@@ -1,7 +1,4 @@
 // Rotary embedding on Q/K fused with the paged KV-cache write (gfx950).
-// (Decode-sized steps with a bf16 cache run the same math in the streaming QKV GEMM's epilogue instead —
-// wstream_gemm.hip, RopeKV; this kernel serves prefill, the fp8 cache and the hipBLASLt path.)
-//
 // Input is the fused QKV projection output [T, (Hq + 2*Hkv) * D] — bf16, or S fp32 split-K slabs of the decode
 // GEMM (wstream_gemm.hip) summed while loading. One workgroup per token, one thread per 8-element unit:
 //   * Q heads: rotate-half RoPE -> q_out[T, Hq, D]
@@ -35,7 +32,7 @@ namespace kafka {
 
 __device__ __forceinline__ int vt_pos(int o) { return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1); }
 
-template <int D, bool GATED = false>
+template <int D>
 __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ qkv, const float* __restrict__ qp,
                                                        int S, int64_t ps, int64_t qkv_stride,
                                                        const int64_t* __restrict__ positions,
@@ -43,11 +40,10 @@ __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ 
                                                        bf16* __restrict__ q_out, int64_t q_stride,
                                                        bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
                                                        const int64_t* __restrict__ slot_mapping, int Hq, int Hkv,
-                                                       int block_size, Gates gt) {
+                                                       int block_size) {
   constexpr int HALF = D / 2;
   constexpr int RU = HALF / 8;  // rope units (8 rotation pairs each) per head
   constexpr int VU = D / 8;     // v copy units (8 elements) per head
-  if constexpr (GATED) gate_wait(gt.wait, gt.mode);  // early-launched (common.h Gates): the QKV slabs are complete
   const int64_t t = blockIdx.x;
   const int64_t pos = positions[t];
   const int64_t slot = slot_mapping ? slot_mapping[t] : -1;
@@ -97,10 +93,6 @@ __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) dst[(int64_t)(c + j) * block_size] = (bf16)x[j];
     }
-  }
-  if constexpr (GATED) {  // one arrival per workgroup
-    __syncthreads();
-    if (threadIdx.x == 0) gate_arrive(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y), gt.mode);
   }
 }
 
@@ -246,42 +238,23 @@ extern "C" hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int
                                           const int64_t* positions, const float* cos_sin, bf16* q_out,
                                           int64_t q_stride, bf16* k_cache, bf16* v_cache,
                                           const int64_t* slot_mapping, int T, int Hq, int Hkv, int D,
-                                          int block_size, Gates gt, hipStream_t st) {
+                                          int block_size, hipStream_t st) {
   if (T == 0) return hipSuccess;
   if (D != 128 && D != 64) return hipErrorInvalidValue;
   // one thread per work unit (8 rotation pairs of a Q/K head, or 8 V elements), so a token's whole row is one
-  // round of loads instead of a strided loop paying the HBM latency twice (448 units for Llama-3-8B)
-  // A token's units are spread over gridDim.y workgroups of 64 threads (env KAFKA_ROPE_WG overrides; 0 = one
-  // workgroup per token): at decode T is the batch (64), and one workgroup per token leaves 3/4 of the CUs idle
-  // while each busy CU pulls the token's S slabs (~100 KB) through its own L2 port. Bench A/B
-  // (profiles/r02/rope_wg_ab.jsonl): 64 -> +0.5 % tok/s over one workgroup per token (128 / 256 in between).
-  static const int wg_env = [] {
-    const char* e = getenv("KAFKA_ROPE_WG");
-    return e ? atoi(e) : 64;
-  }();
+  // round of loads instead of a strided loop paying the HBM latency twice (448 units for Llama-3-8B), spread over
+  // workgroups of 64 threads: at decode T is the batch (64), and one workgroup per token leaves 3/4 of the CUs idle
+  // while each busy CU pulls the token's S slabs (~100 KB) through its own L2 port (+0.5 % tok/s over one workgroup
+  // per token, profiles/r02/rope_wg_ab.jsonl)
   const int units = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
-  int nt = units <= 256 ? 256 : (units <= 512 ? 512 : 1024);
-  int ny = 1;
-  if (wg_env >= 64 && wg_env <= 1024 && wg_env % 64 == 0 && wg_env < units) {
-    nt = wg_env;
-    ny = (units + nt - 1) / nt;
-  }
+  const int nt = 64, ny = (units + nt - 1) / nt;
   const dim3 grid(T, ny);
-  const bool early = gt.wait != nullptr;
-  if (gt.wait != nullptr || gt.sig != nullptr) {  // (the gated code is its own instantiation)
-    if (D == 128)
-      launch_maybe_early(rope_kv_kernel<128, true>, grid, dim3(nt), st, early, qkv, qp, S, ps, qkv_stride, positions,
-                         cos_sin, q_out, q_stride, k_cache, v_cache, slot_mapping, Hq, Hkv, block_size, gt);
-    else
-      launch_maybe_early(rope_kv_kernel<64, true>, grid, dim3(nt), st, early, qkv, qp, S, ps, qkv_stride, positions,
-                         cos_sin, q_out, q_stride, k_cache, v_cache, slot_mapping, Hq, Hkv, block_size, gt);
-  } else if (D == 128) {
+  if (D == 128)
     rope_kv_kernel<128><<<grid, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
-                                          v_cache, slot_mapping, Hq, Hkv, block_size, gt);
-  } else {
+                                          v_cache, slot_mapping, Hq, Hkv, block_size);
+  else
     rope_kv_kernel<64><<<grid, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
-                                         v_cache, slot_mapping, Hq, Hkv, block_size, gt);
-  }
+                                         v_cache, slot_mapping, Hq, Hkv, block_size);
   return hipGetLastError();
 }
 

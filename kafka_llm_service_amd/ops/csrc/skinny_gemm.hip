@@ -184,27 +184,18 @@ extern "C" int kafka_skinny_plan(int M, int N, int K, int max_splits, int* split
   return 0;
 }
 
-// cfg (KAFKA_SKINNY_CFG, benchmarks): 0 = BK 64 x 3 stages (144 KB, one workgroup per CU), 1 = BK 32 x 6 stages
-// (144 KB), 2 = BK 32 x 3 stages (72 KB, two workgroups per CU)
+// BK 64 x 3 stages (144 KB of LDS, one workgroup per CU; BK 32 x 6 stages and BK 32 x 3 stages at two workgroups
+// per CU measured slower, profiles/r03/skinny_gemm/)
 extern "C" hipError_t kafka_launch_skinny_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K,
                                               int splits, int glu, bf16* Y, int64_t ldy, float* P, hipStream_t st) {
   using namespace skg;
   if (M <= 0 || M > BM || N % BN != 0 || splits < 1 || K % (64 * splits) != 0 || ldx % 8 != 0) return hipErrorInvalidValue;
   if ((splits > 1) != (P != nullptr) || (splits == 1 && Y == nullptr) || (glu && N % 64 != 0))
     return hipErrorInvalidValue;
-  static const int cfg = [] {
-    const char* e = getenv("KAFKA_SKINNY_CFG");
-    return e ? atoi(e) : 0;
-  }();
   const dim3 grid(N / BN, splits);
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   const int ks = K / splits;
-  if (cfg == 1)
-    skinny_gemm_kernel<32, 6, 1><<<grid, NW * 64, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, P, glu);
-  else if (cfg == 2)
-    skinny_gemm_kernel<32, 3, 2><<<grid, NW * 64, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, P, glu);
-  else
-    skinny_gemm_kernel<64, 3, 1><<<grid, NW * 64, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, P, glu);
+  skinny_gemm_kernel<64, 3, 1><<<grid, NW * 64, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, P, glu);
   return hipGetLastError();
 }
 

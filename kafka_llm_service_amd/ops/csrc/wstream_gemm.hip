@@ -27,32 +27,11 @@
 
 namespace kafka {
 
-// QKV-projection epilogue (ROPE instantiations): rotate-half RoPE on the q / k heads, q to q_out, k / v straight
-// into their paged-cache layouts (bf16 cache, head dim 128, 16-token pages: the layouts of rope_kv.hip) — the
-// rope_kv kernel and its launch gap leave the decode step. A 128-column workgroup tile is exactly one head. With
-// split-K (S > 1) every split publishes its fp32 partial with agent-coherent write-through stores and takes a
-// ticket; the LAST split of a column tile sums the others (agent-coherent loads; no fence that would write back the
-// whole L2, see attention.hip's ticket merge), applies the epilogue and re-arms the counter.
-struct RopeKV {
-  const int64_t* positions;  // [M]
-  const float* cos_sin;      // [max_pos, 128]: cos in [0, 64), sin in [64, 128)
-  bf16* q_out;               // [M, Hq, 128] (row stride q_stride)
-  int64_t q_stride;
-  bf16* k_cache;             // [blocks, Hkv, 16, 128] as 16 chunk planes [16 keys][8]
-  bf16* v_cache;             // [blocks, Hkv, 128, 16] V^T, key o at rope_vt_pos(o)
-  const int64_t* slots;      // [M] cache slot per row (-1: no KV write), or nullptr
-  int Hq, Hkv;
-  int* tickets;              // [N / 128] zeroed once, re-armed by the last split
-};
-
-__device__ __forceinline__ int rope_vt_pos(int o) { return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1); }
-
-template <int MT, int KC, bool NT, int KW, bool ROPE = false, bool EARLY = false>
+template <int MT, int KC, bool NT, int KW>
 __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                                  const bf16x8* __restrict__ Wt, int M, int N, int K,
                                                                  int ks, bf16* __restrict__ Y, int64_t ldy,
-                                                                 float* __restrict__ P, int glu, RopeKV ra,
-                                                                 int row_tiles, Gates gt) {
+                                                                 float* __restrict__ P, int glu, int row_tiles) {
   constexpr int NTH = 256 * KW;
   constexpr int ROWS = 32 * MT;
   constexpr int CPR = KC / 8;             // 16-B chunks per X row of one K chunk
@@ -74,12 +53,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
     const int grp = blockIdx.x / (8 * row_tiles), rem = blockIdx.x % (8 * row_tiles);
     cb = grp * 8 + rem % 8;
     rti = rem / 8;
-    if (cb >= (N + 127) / 128) {  // padding workgroup (workgroup-uniform): no work, but a gated launch counts it
-      if constexpr (EARLY) {
-        if (gt.sig != nullptr && threadIdx.x == 0) gate_arrive(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y), gt.mode);
-      }
-      return;
-    }
+    if (cb >= (N + 127) / 128) return;  // padding workgroup (workgroup-uniform)
   }
   const int row0 = rti * ROWS;
   const int Mtot = M;
@@ -140,37 +114,12 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
   };
 
   bf16x8 wa[KSW], wb[KSW];
+  // X first: its LDS image is written while the first weight chunk is still in flight (loads return in order)
+  load_x(0);
+  load_w(wa, 0);
+  store_x(0);
+  __syncthreads();
   int ch = 0;
-  if (!EARLY || gt.wait == nullptr) {  // (EARLY: the gated instantiation, common.h Gates)
-    // X first: its LDS image is written while the first weight chunk is still in flight (loads return in order)
-    load_x(0);
-    load_w(wa, 0);
-    store_x(0);
-    __syncthreads();
-  } else {
-    load_w(wa, 0);
-    // early-launched (common.h Gates): the first two K chunks of this workgroup's weight slice are in flight while
-    // the producer of X finishes; X is read only after the gate. The first trip is peeled (chunk 1 is loaded).
-    const bool two = nchunks > 2;  // workgroup-uniform
-    if (two) load_w(wb, 1);
-    asm volatile("" ::: "memory");
-    gate_wait(gt.wait, gt.mode);
-    load_x(0);
-    store_x(0);
-    __syncthreads();
-    if (two) {
-      load_x(1);
-      compute(0, wa);
-      store_x(1);
-      __syncthreads();
-      load_x(2);
-      load_w(wa, 2);
-      compute(1, wb);
-      store_x(0);
-      __syncthreads();
-      ch = 2;
-    }
-  }
   // steady state: two chunks per trip, both prefetches in range (no conditional loads inside the trip); chunk ch is
   // in buffer 0 / wa
   for (; ch + 2 < nchunks; ch += 2) {
@@ -218,110 +167,6 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
           for (int i = 0; i < 16; ++i) acc[mt][i] += red[((((j - 1) * 4 + ct) * MT + mt) * 16 + i) * 64 + lane];
     }
   }
-  if constexpr (ROPE) {
-    static_assert(KW == 1, "rope epilogue: one K part per chunk");
-    __shared__ int s_last;
-    const int S = gridDim.y;
-    const int n = nb * 32 + r;  // N % 128 == 0 (host-checked): every wave is active
-    if (S > 1) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (m < M)
-            __hip_atomic_store(P + ((int64_t)blockIdx.y * Mtot + m) * N + n, acc[mt][i], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        int* tk = ra.tickets + cb;
-        const int t = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = t == S - 1;
-        if (t == S - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-      if (!s_last) return;
-      for (int s2 = 0; s2 < S; ++s2) {
-        if (s2 == (int)blockIdx.y) continue;
-        float v[MT][16];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int m = min(mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h, M - 1);
-            v[mt][i] = __hip_atomic_load(P + ((int64_t)s2 * Mtot + m) * N + n, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-          }
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) acc[mt][i] += v[mt][i];
-      }
-    }
-    // rotate-half partner d +- 64 lives in wave ct ^ 2 (same lane): exchange through LDS (the X stage is dead)
-    float* red = reinterpret_cast<float*>(&xs[0][0]);
-    __syncthreads();
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) red[((ct * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
-    __syncthreads();
-    const int head = cb, d = 32 * ct + r, j = d & 63;
-    const bool is_q = head < ra.Hq, is_k = !is_q && head < ra.Hq + ra.Hkv;  // workgroup-uniform
-    const bool kv = !is_q && ra.slots != nullptr;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      // this row block's positions / slots, then its cos / sin, each as ONE batch of independent loads (per element
-      // and behind the previous element's stores, the dependent pairs cost ~17 us of serialised latency per launch)
-      int64_t pos[16], slot[16];
-      float c[16], sn[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int m = min(mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h, M - 1);
-        pos[i] = (is_q || is_k) ? ra.positions[m] : 0;
-        slot[i] = kv ? ra.slots[m] : -1;
-      }
-      if (is_q || is_k) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float* cs = ra.cos_sin + pos[i] * 128;
-          c[i] = cs[j];
-          sn[i] = cs[64 + j];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (m >= M) continue;
-        float y = acc[mt][i];
-        if (is_q || is_k) {
-          const float xp = red[(((ct ^ 2) * MT + mt) * 16 + i) * 64 + lane];
-          y = ct < 2 ? y * c[i] - xp * sn[i] : y * c[i] + xp * sn[i];
-        }
-        if (is_q) {
-          ra.q_out[(int64_t)m * ra.q_stride + head * 128 + d] = (bf16)y;
-        } else if (kv) {
-          if (slot[i] >= 0) {
-            const int64_t blk = slot[i] >> 4;
-            const int off = (int)(slot[i] & 15);
-            if (is_k)
-              ra.k_cache[(blk * ra.Hkv + (head - ra.Hq)) * 2048 + ((d >> 3) * 16 + off) * 8 + (d & 7)] = (bf16)y;
-            else
-              ra.v_cache[(blk * ra.Hkv + (head - ra.Hq - ra.Hkv)) * 2048 + d * 16 + rope_vt_pos(off)] = (bf16)y;
-          }
-        }
-      }
-    }
-    if constexpr (EARLY) {  // one arrival per head tile (the last split's)
-      if (gt.sig != nullptr) {
-        __syncthreads();
-        if (tid == 0) gate_arrive(gt.sig, (int)blockIdx.x, (int)gridDim.x, gt.mode);
-      }
-    }
-    return;
-  }
   if (glu && P == nullptr) {
     // fused SwiGLU epilogue (weight tiles GLU-interleaved: tile 2j = gate rows [32j, 32j+32), tile 2j+1 = the
     // matching up rows): odd waves hand their up tile to the even wave of the pair through LDS, which writes
@@ -363,12 +208,6 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
             Y[(int64_t)m * ldy + n] = (bf16)acc[mt][i];
         }
       }
-  }
-  if constexpr (EARLY) {  // one arrival per workgroup
-    if (gt.sig != nullptr) {
-      __syncthreads();
-      if (tid == 0) gate_arrive(gt.sig, gate_block_id(), (int)(gridDim.x * gridDim.y), gt.mode);
-    }
   }
 }
 
@@ -536,61 +375,26 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   store_bf16x8(Y + (int64_t)m * ldy + n, o);
 }
 
-// Host plan: row tiles MT, K chunk KC and split count S for a shape; returns 0 if supported.
-//   max_splits caps S (1 forces a direct bf16 output).
-static bool mt3_off() {  // KAFKA_WSTREAM_MT3=0: 65..96 rows on the four-tile kernel (A/B; mirrored by ops.stream_plan)
-  static const bool off = [] {
-    const char* e = getenv("KAFKA_WSTREAM_MT3");
-    return e != nullptr && e[0] == '0';
-  }();
-  return off;
-}
-
-static bool rowsplit_on() {  // mirrored by ops.stream_plan
-  static const bool on = [] {
-    const char* e = getenv("KAFKA_WSTREAM_ROWSPLIT");
-    return e != nullptr && e[0] == '1';
-  }();
-  return on;
-}
-
-static bool rt1_on() {  // KAFKA_WSTREAM_RT1=1: 33..64 rows as two 32-row tiles sharing each weight slice in L2 (A/B)
-  static const bool on = [] {
-    const char* e = getenv("KAFKA_WSTREAM_RT1");
-    return e != nullptr && e[0] == '1';
-  }();
-  return on;
-}
-
-static bool mt4_kc256() {  // KAFKA_WSTREAM_MT4_KC=256: four row tiles on 256-deep chunks (128 KB X stage; A/B)
-  static const bool on = [] {
-    const char* e = getenv("KAFKA_WSTREAM_MT4_KC");
-    return e != nullptr && atoi(e) == 256;
-  }();
-  return on;
-}
-
-// one_tile: the plan must cover all M rows with one row tile (the fused QKV + RoPE kernel: its epilogue's per-head
-// tickets count split-K workgroups of ONE row tile), so KAFKA_WSTREAM_ROWSPLIT does not apply
-extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int one_tile, int* mt, int* kc, int* splits) {
+// Host plan: row tiles MT, K chunk KC and split count S for a shape; returns 0 if supported (mirrored by
+// ops.stream_plan). max_splits caps S (1 forces a direct bf16 output).
+//   MT: 1 tile up to 32 rows, 2 up to 64, 3 up to 96 (a decode batch plus a short new-turn chunk: three 32-row tiles
+//   on 256-deep chunks, 96 KB X stage; +0.24 % over four on 128-deep ones, profiles/r04/bench_ab_wstream_mt3.jsonl),
+//   else 4 (128-deep chunks: 256-deep ones lose 1.9 %, profiles/r04/bench_ab_wstream_mt4_kc256.jsonl). Beyond 128
+//   rows (tiled-only models) the rows are split over row tiles of 128.
+//   Measured and rejected (profiles/r04/): 64-row tiles sharing a weight slice in one XCD's L2 beyond 64 rows (-0.6 %)
+//   and 33..64 rows as two 32-row tiles (-4.8 %).
+extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits) {
   if (M < 1 || M > 256 || N % 32 != 0 || N <= 0) return 1;
-  // 65..96 rows (a decode batch plus a short new-turn chunk): three 32-row tiles on 256-deep chunks (96 KB X stage)
-  // instead of four on 128-deep ones
-  // KAFKA_WSTREAM_ROWSPLIT=1: beyond 64 rows, 64-row tiles whose workgroups share each weight slice in one XCD's L2
-  const int MT = rowsplit_on() && !one_tile && M > 64 ? 2 : (M <= 32 || (rt1_on() && !one_tile && M <= 64) ? 1 :
-                 (M <= 64 ? 2 : (M <= 96 && !mt3_off() ? 3 : 4)));
-  const int KC = MT == 4 && !mt4_kc256() ? 128 : 256;
+  const int MT = M <= 32 ? 1 : (M <= 64 ? 2 : (M <= 96 ? 3 : 4));
+  const int KC = MT == 4 ? 128 : 256;
   if (K % KC != 0 || K <= 0) return 2;
   const int nx = (N + 127) / 128 * ((M + 32 * MT - 1) / (32 * MT));  // workgroups per split (x row tiles)
   const int chunks = K / KC;
-  // split until the grid reaches ~192 (MT <= 2) / 256 (MT = 4) workgroups: measured on MI355X
-  // (benchmarks/wstream_sweep.py, profiles/wstream_sweep_r01.log) — every extra split adds 2 x M x N x 4 B of slab
-  // traffic, so e.g. gate_up (N = 28672) at M = 64 runs fastest unsplit and qkv (N = 6144) with S = 4
-  static const int target_env = [] {  // KAFKA_WSTREAM_TARGET (A/B only; mirrored by ops.stream_plan)
-    const char* e = getenv("KAFKA_WSTREAM_TARGET");
-    return e ? atoi(e) : 0;
-  }();
-  const int target = target_env > 0 ? target_env : (MT == 4 ? 256 : 192);
+  // split until the grid reaches ~192 (MT <= 3) / 256 (MT = 4) workgroups: measured on MI355X
+  // (benchmarks/wstream_sweep.py, profiles/wstream_sweep_r01.log; split targets 96..384 re-checked in
+  // profiles/r04/bench_ab_split_target_*.jsonl) — every extra split adds 2 x M x N x 4 B of slab traffic, so e.g.
+  // gate_up (N = 28672) at M = 64 runs fastest unsplit and qkv (N = 6144) with S = 4
+  const int target = MT == 4 ? 256 : 192;
   int s = 1;
   while (s * 2 <= max_splits && s * 2 <= 8 && chunks % (s * 2) == 0 && nx * s < target) s *= 2;
   *mt = MT;
@@ -601,7 +405,7 @@ extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int one_t
 
 extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K,
                                                int mt, int kc, int splits, int nt, int kw, int glu, bf16* Y,
-                                               int64_t ldy, float* P, Gates gt, hipStream_t st) {
+                                               int64_t ldy, float* P, hipStream_t st) {
   if (M < 1) return hipSuccess;
   if (glu && (N % 64 != 0 || kw > 2)) return hipErrorInvalidValue;  // (the SwiGLU epilogue runs after the KW fold)
   if (K % (kc * splits) != 0 || (splits > 1 && P == nullptr) || (splits == 1 && P == nullptr && Y == nullptr))
@@ -609,76 +413,25 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   const int rt = (M + 32 * mt - 1) / (32 * mt);  // row tiles of 32 * mt rows
   const int nblk = (N + 127) / 128;
   const dim3 grid((rt > 1 ? (nblk + 7) / 8 * 8 : nblk) * rt, splits);  // (row tiles: column blocks padded to 8)
-  // KAFKA_WSTREAM_TILE_NT=0: with several row tiles, cached (not non-temporal) weight loads, so the other tiles of a
-  // slice can hit the copy the first one brought into L2 (A/B)
-  static const bool tile_nt = [] {
-    const char* e = getenv("KAFKA_WSTREAM_TILE_NT");
-    return e == nullptr || e[0] != '0';
-  }();
-  if (rt > 1 && !tile_nt) nt = 0;
   const int ks = K / splits;
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   float* p = splits > 1 ? P : nullptr;
-  const bool early = gt.wait != nullptr, gated = early || gt.sig != nullptr;
-  // (gated launches use their own instantiation, EARLY: the ordinary kernel is exactly the ungated code)
-#define KAFKA_WS(MT_, KC_, KW_)                                                                                \
-  do {                                                                                                        \
-    if (gated && nt && KW_ == 1)                                                                              \
-      launch_maybe_early(wstream_gemm_kernel<MT_, KC_, true, KW_, false, true>, grid, dim3(256 * KW_), st, early, \
-                         X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, RopeKV{}, rt, gt);                          \
-    else if (gated)                                                                                           \
-      return hipErrorInvalidValue;                                                                            \
-    else if (nt)                                                                                              \
-      wstream_gemm_kernel<MT_, KC_, true, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, \
-                                                                           RopeKV{}, rt, gt);                \
-    else                                                                                                      \
-      wstream_gemm_kernel<MT_, KC_, false, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p,   \
-                                                                            glu, RopeKV{}, rt, gt);           \
+#define KAFKA_WS(MT_, KC_, KW_)                                                                                  \
+  do {                                                                                                          \
+    if (nt)                                                                                                     \
+      wstream_gemm_kernel<MT_, KC_, true, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, rt); \
+    else                                                                                                        \
+      wstream_gemm_kernel<MT_, KC_, false, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, rt); \
   } while (0)
   if (mt == 1 && kc == 256 && kw == 1) KAFKA_WS(1, 256, 1);
   else if (mt == 1 && kc == 256 && kw == 2) KAFKA_WS(1, 256, 2);
-  else if (mt == 1 && kc == 512 && kw == 1) KAFKA_WS(1, 512, 1);
-  else if (mt == 2 && kc == 128 && kw == 1) KAFKA_WS(2, 128, 1);
-  else if (mt == 2 && kc == 128 && kw == 2) KAFKA_WS(2, 128, 2);
   else if (mt == 2 && kc == 256 && kw == 1) KAFKA_WS(2, 256, 1);
   else if (mt == 2 && kc == 256 && kw == 2) KAFKA_WS(2, 256, 2);
   else if (mt == 3 && kc == 256 && kw == 1) KAFKA_WS(3, 256, 1);
-  else if (mt == 4 && kc == 256 && kw == 1) KAFKA_WS(4, 256, 1);
   else if (mt == 4 && kc == 128 && kw == 1) KAFKA_WS(4, 128, 1);
   else if (mt == 4 && kc == 128 && kw == 2) KAFKA_WS(4, 128, 2);
   else return hipErrorInvalidValue;
 #undef KAFKA_WS
-  return hipGetLastError();
-}
-
-// QKV projection + RoPE + paged KV write (see RopeKV): the plan's (mt, kc, splits); P = fp32 scratch
-// [splits, M, N] when splits > 1; N = (Hq + 2 Hkv) * 128.
-extern "C" hipError_t kafka_launch_wstream_qkv_rope(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K,
-                                                   int mt, int kc, int splits, float* P, const int64_t* positions,
-                                                   const float* cos_sin, bf16* q_out, int64_t q_stride,
-                                                   bf16* k_cache, bf16* v_cache, const int64_t* slots, int Hq,
-                                                   int Hkv, int* tickets, Gates gt, hipStream_t st) {
-  if (M < 1) return hipSuccess;
-  if (M > 128 || M > 32 * mt || N != (Hq + 2 * Hkv) * 128 || K % (kc * splits) != 0 ||
-      (splits > 1 && (P == nullptr || tickets == nullptr)))
-    return hipErrorInvalidValue;
-  const dim3 grid(N / 128, splits);
-  const int ks = K / splits;
-  const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
-  const RopeKV ra{positions, cos_sin, q_out, q_stride, k_cache, v_cache, slots, Hq, Hkv, tickets};
-  if (gt.wait != nullptr || gt.sig != nullptr) return hipErrorInvalidValue;  // the fused QKV + RoPE kernel: never gated
-  if (mt == 1 && kc == 256)
-    wstream_gemm_kernel<1, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1, gt);
-  else if (mt == 2 && kc == 256)
-    wstream_gemm_kernel<2, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1, gt);
-  else if (mt == 3 && kc == 256)
-    wstream_gemm_kernel<3, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1, gt);
-  else if (mt == 4 && kc == 256)
-    wstream_gemm_kernel<4, 256, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1, gt);
-  else if (mt == 4 && kc == 128)
-    wstream_gemm_kernel<4, 128, true, 1, true><<<grid, 256, 0, st>>>(X, ldx, wt, M, N, K, ks, nullptr, 0, P, 0, ra, 1, gt);
-  else
-    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -251,38 +251,6 @@ def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_pa
             attn_merge(parts.contiguous(), lp[b:b + 1, :, :n].contiguous(), out[b:b + 1])
 
 
-def attn_decode_sk(q, k_cache, v_cache, block_tables, rows, start, out_part, lse_part, scale, out=None,
-                   pre_part=None):
-    """Reference for the stream-K decode kernel (ops/csrc/attention.hip attn_decode_sk_kernel): the pieces of
-    ``ops.decode_sk_items`` (one kv head each), then the same merge as the work-item kernel."""
-    from kafka_llm_service_amd.ops import decode_sk_items
-
-    B, Hq, D = q.shape
-    Hkv = k_cache.shape[1]
-    G = Hq // Hkv
-    S_total = out_part.shape[2]
-    lp = lse_part.view(out_part.shape[0], Hq, S_total)
-    nparts, npres = {}, {}
-    for b, h, lo, hi, split, nsplit, npre in decode_sk_items(rows.cpu().numpy(), start.cpu().numpy(), Hkv):
-        if not (0 <= b < B and 0 <= split < nsplit and npre + nsplit <= S_total):
-            continue
-        nparts[(b, h)] = npre + nsplit  # per unit: the heads of one row may be split differently
-        npres[(b, h)] = npre
-        k, v = gather_kv(k_cache, v_cache, block_tables[b], hi)
-        mask = torch.zeros(1, hi, dtype=torch.bool, device=q.device)
-        mask[:, lo:hi] = True
-        oh, lh = _attend(q[b, h * G:(h + 1) * G].float()[None], k[:, h], v[:, h], mask, scale)
-        out_part[b, h * G:(h + 1) * G, npre + split] = oh[0]
-        lp[b, h * G:(h + 1) * G, npre + split] = lh[0]
-    if out is not None:
-        for (b, h), n in nparts.items():
-            hs = slice(h * G, (h + 1) * G)
-            parts = out_part[b:b + 1, hs, :n].clone()
-            if pre_part is not None:
-                parts[:, :, :npres[(b, h)]] = pre_part[b:b + 1, hs, :npres[(b, h)]].float()
-            attn_merge(parts.contiguous(), lp[b:b + 1, hs, :n].contiguous(), out[b:b + 1, hs])
-
-
 def attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale, out=None, out_part=None,
                        lse_part=None):
     """Reference for the work-item prefill / cascade kernel (see ops/csrc/attention.hip)."""

@@ -17,12 +17,12 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
-def _run(extra):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4",
+def _run(extra, n=2):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "4",
            "--warmup", "2", "--model", "tiny-llama", "--prefix-tokens", "200", "--threads", "4", "--min-out", "4",
            "--max-out", "8", "--user-tokens", "8", "--ttft-samples", "4", *extra]
-    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env = dict(os.environ, OMP_NUM_THREADS="1" if n > 2 else "2")
     p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=500)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -47,6 +47,39 @@ def test_bench_tp2_json_line():
     d = _run(["--tp", "2"])
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["config"]["parallelism"] == "dp1-tp2" and d["config"]["global_batch"] == 4
+
+
+def _check_ranks(d, n, tp):
+    """The self-verifying part of a multi-rank line: one record per rank, every rank counted once, the replicas'
+    token counts add up to the whole-job value's tokens, and the process groups are the ones asked for."""
+    assert d["ranks"] == n and len(d["per_rank"]) == n
+    assert sorted(r["rank"] for r in d["per_rank"]) == list(range(n))
+    replicas = [r for r in d["per_rank"] if r["role"] == "replica"]
+    assert len(replicas) == n // tp and all(r["tok_s"] > 0 and r["ms_per_step"] > 0 for r in replicas)
+    assert all(r["out_tokens"] == 0 for r in d["per_rank"] if r["role"] == "tp_follower")
+    assert abs(sum(r["out_tokens"] for r in replicas) / (d["ms_per_step"] * d["steps"] / 1e3) - d["value"]) \
+        <= 0.02 * d["value"] + 1
+    assert d["dist"]["initialized"] and d["dist"]["world_size"] == n and d["dist"]["backend"] == "gloo"
+    if tp > 1:
+        assert d["dist"]["tp_group_size"] == tp
+    else:
+        assert "tp_group_size" not in d["dist"]
+
+
+@pytest.mark.timeout(900)
+def test_bench_dp4_per_rank_records():
+    """DP = 4 (the driver's N = 4 launch shape): four replica records, gloo world of 4."""
+    d = _run([], n=4)
+    assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp4"
+    _check_ranks(d, 4, 1)
+
+
+@pytest.mark.timeout(900)
+def test_bench_tp2x2_per_rank_records():
+    """TP = 2 x 2 replicas over 4 ranks: two replica leaders, two followers, TP groups of 2."""
+    d = _run(["--tp", "2"], n=4)
+    assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp2-tp2" and d["config"]["global_batch"] == 8
+    _check_ranks(d, 4, 2)
 
 
 @pytest.mark.timeout(600)

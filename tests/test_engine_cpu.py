@@ -253,20 +253,13 @@ def test_stream_decode_gemm_matches_oracle():
 
 def test_stream_plan_rules(monkeypatch):
     """The decode GEMM plan (ops.stream_plan, mirrored from csrc kafka_wstream_plan): row tiles by step size (1 / 2 /
-    3 / 4 x 32 rows), 128-deep chunks for four tiles, split-K grown toward the grid target; the A/B switches that
-    split rows into XCD-shared tiles never apply to the fused QKV + RoPE kernel (one row tile: its per-head tickets
-    count the splits of ONE tile)."""
+    3 / 4 x 32 rows), 128-deep chunks for four tiles, split-K grown toward the grid target."""
     from kafka_llm_service_amd import ops
 
     assert [ops.stream_plan(M, 28672, 4096)[0] for M in (1, 32, 33, 64, 65, 96, 97, 128)] == [1, 1, 2, 2, 3, 3, 4, 4]
     assert ops.stream_plan(128, 4096, 4096)[1] == 128 and ops.stream_plan(64, 4096, 4096)[1] == 256
     assert ops.stream_plan(64, 28672, 4096)[2] == 1 and ops.stream_plan(64, 6144, 4096)[2] == 4
     assert ops.stream_plan(300, 4096, 4096) is None and ops.stream_plan(64, 4100, 4096) is None
-    monkeypatch.setattr(ops, "_WSTREAM_ROWSPLIT", True)
-    monkeypatch.setattr(ops, "_WSTREAM_RT1", True)
-    assert ops.stream_plan(90, 6144, 4096)[0] == 2 and ops.stream_plan(64, 6144, 4096)[0] == 1
-    assert ops.stream_plan(90, 6144, 4096, one_tile=True)[0] == 3
-    assert ops.stream_plan(64, 6144, 4096, one_tile=True)[0] == 2
 
 
 def test_tiled_only_weights_match_stream():
@@ -299,12 +292,12 @@ def test_multi_group_cascade_equals_plain(base_engine, monkeypatch):
     custom prompt) plus a stateless row with no shared prefix: every group gets its own cascade pass and the
     result equals plain per-row attention (fp32 prefix partials: token-exact; the bf16 default is checked to
     logit tolerance by test_bf16_cascade_partials_close_to_fp32)."""
-    monkeypatch.setenv("KAFKA_CASCADE_BF16", "0")
     groups = [_prompts(seed=10 + i, shared=96, tails=(3, 9, 30)) for i in range(3)]
     loner = _prompts(seed=20, shared=0, tails=(50,))
     prompts = [p for g in groups for p in g] + loner
     e1 = _engine(model=base_engine.model, use_cascade=False)
     e2 = _engine(model=base_engine.model, use_cascade=True, cascade_min_prefix=16)
+    e2.runner.cascade_bf16 = False
     for g in groups:
         e2.generate([g[0][:96] + [7]], GREEDY)
     plain = e1.generate(prompts, GREEDY)
@@ -446,8 +439,8 @@ def test_bf16_cascade_partials_close_to_fp32(base_engine, monkeypatch):
     prompts = _prompts(seed=31, shared=96, tails=(3, 9, 30))
     logits = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("KAFKA_CASCADE_BF16", mode)
         e = _engine(model=base_engine.model, use_cascade=True, cascade_min_prefix=16)
+        e.runner.cascade_bf16 = mode == "1"
         e.generate([prompts[0][:96] + [7]], GREEDY)
         seen = []
         orig = e.runner.sample_device

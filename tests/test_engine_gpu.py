@@ -117,75 +117,3 @@ def _run_logits(e, prompts, sps):
     finally:
         e.runner.sample_device = orig
     return outs, seen
-
-
-def test_early_launched_layers_match_ordinary(eng):
-    """Early-launched decode layers (models/llama.py EARLY: kernels launched without the AQL barrier bit behind
-    device gates, the suffix decode beside the cascade) compute exactly what ordinary launches do: bitwise-equal
-    logits on every step (cascade + split rows, greedy and seeded sampling), every gate released by its producer.
-    Two fresh engines over the same weights, so both runs schedule identical steps."""
-    prompts = _prompts(9, 1200, (3, 40, 77, 500))
-    sps = [SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True),
-           SamplingParams(temperature=0.8, max_tokens=12, ignore_eos=True, seed=3),
-           SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True),
-           SamplingParams(temperature=0.7, top_p=0.9, max_tokens=12, ignore_eos=True, seed=4)]
-    m = eng.model
-
-    def run(early: bool):
-        e = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", num_kv_blocks=4096, max_model_len=8192,
-                                   cascade_min_prefix=64, prefill_kv_chunk=256), model=m)
-        m.early = early
-        try:
-            e.generate([prompts[0][:1200] + [1]], GREEDY)  # cache the shared prefix: decode steps run the cascade
-            n0 = m._gates.forwards if m._gates is not None else 0
-            outs, logits = _run_logits(e, prompts, sps)
-            gated = (m._gates.forwards - n0) if m._gates is not None else 0
-            timed_out = m._gates.timed_out() if m._gates is not None else False
-        finally:
-            m.early = False
-        return outs, logits, gated, timed_out
-
-    ref_outs, ref_logits, _, _ = run(False)
-    outs, logits, gated, timed_out = run(True)
-    assert gated >= 8, f"only {gated} forwards ran early-launched layers"
-    assert not timed_out, "a gate wait timed out"
-    assert outs == ref_outs
-    assert len(logits) == len(ref_logits)
-    for a, b in zip(logits, ref_logits):
-        assert torch.equal(a, b)
-
-
-def test_attn_overlap_matches_ordinary(eng):
-    """The suffix decode launched beside the cascade (models/llama.py ATTN_OVERLAP: any-order launch, write-through
-    hand-off of the cascade's partials before the merge) computes exactly what ordinary launches do: bitwise-equal
-    logits on every step (cascade + split rows incl. mixed steps), every wait satisfied. Two fresh engines over the
-    same weights, so both runs schedule identical steps."""
-    prompts = _prompts(11, 1200, (3, 40, 77, 500))
-    sps = [SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True),
-           SamplingParams(temperature=0.8, max_tokens=12, ignore_eos=True, seed=5),
-           SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True),
-           SamplingParams(temperature=0.7, top_p=0.9, max_tokens=12, ignore_eos=True, seed=6)]
-    m = eng.model
-
-    def run(ovl: bool):
-        e = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", num_kv_blocks=4096, max_model_len=8192,
-                                   cascade_min_prefix=64, prefill_kv_chunk=256), model=m)
-        m.attn_overlap = ovl
-        try:
-            e.generate([prompts[0][:1200] + [1]], GREEDY)  # cache the shared prefix: decode steps run the cascade
-            n0 = m._agates.forwards if m._agates is not None else 0
-            outs, logits = _run_logits(e, prompts, sps)
-            gated = (m._agates.forwards - n0) if m._agates is not None else 0
-            timed_out = m._agates.timed_out() if m._agates is not None else False
-        finally:
-            m.attn_overlap = False
-        return outs, logits, gated, timed_out
-
-    ref_outs, ref_logits, _, _ = run(False)
-    outs, logits, gated, timed_out = run(True)
-    assert gated >= 8, f"only {gated} forwards ran the overlapped attention"
-    assert not timed_out, "a gate wait timed out"
-    assert outs == ref_outs
-    assert len(logits) == len(ref_logits)
-    for a, b in zip(logits, ref_logits):
-        assert torch.equal(a, b)

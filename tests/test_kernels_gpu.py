@@ -568,41 +568,6 @@ def test_attn_merge_ignores_unwritten_slots(cuda):
     _close(out, ref_out, atol=0.02, msg="merge with unwritten slots")
 
 
-@pytest.mark.parametrize("M,Hq,Hkv,K", [(1, 32, 8, 4096), (17, 32, 8, 4096), (64, 32, 8, 4096), (90, 32, 8, 4096),
-                                        (100, 32, 8, 4096),
-                                        (128, 32, 8, 4096), (48, 8, 1, 1024)])
-def test_wstream_qkv_rope(cuda, M, Hq, Hkv, K):
-    """QKV streaming GEMM with RoPE + the paged KV write in its epilogue (split-K tickets) vs the fp32 reference of
-    x W^T -> rope_kv_write, and vs the unfused GPU path; called twice so the re-armed tickets are exercised."""
-    torch.manual_seed(11)
-    D, nb = 128, 16
-    N = (Hq + 2 * Hkv) * D
-    w = (torch.randn(N, K, device=cuda) * 0.02).to(torch.bfloat16)
-    wt = ops.tile_weight(w)
-    cs = ref.rope_cos_sin(8192, D, 500000.0, None, device=cuda)
-    for rep in range(2):
-        x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
-        pos = torch.randint(0, 8000, (M,), device=cuda, dtype=torch.long)
-        slots = torch.randperm(nb * 16, device=cuda)[:M].long()
-        slots[M // 2] = -1
-        q = torch.empty(M, Hq, D, device=cuda, dtype=torch.bfloat16)
-        k, v = _make_cache(nb, Hkv, D, cuda)
-        ops.linear_stream_rope(x, wt, pos, cs, q, k, v, slots, Hq, Hkv)
-        q2 = torch.empty(M, Hq, D, dtype=torch.bfloat16)
-        k2, v2 = _make_cache(nb, Hkv, D)
-        y = x.float().cpu() @ w.float().cpu().t()
-        ref.rope_kv_write(y, pos.cpu(), cs.cpu(), q2, k2, v2, slots.cpu(), Hq, Hkv)
-        _close(q, q2, atol=0.03, rtol=0.01, msg=f"q rep {rep}")
-        _close(k, k2, atol=0.03, rtol=0.01, msg=f"k rep {rep}")
-        _close(v, v2, atol=0.03, rtol=0.01, msg=f"v rep {rep}")
-        q3 = torch.empty_like(q)
-        k3, v3 = _make_cache(nb, Hkv, D, cuda)
-        ops.rope_kv_write(ops.linear_stream(x, wt), pos, cs, q3, k3, v3, slots, Hq, Hkv)
-        _close(q, q3, atol=0.016, rtol=0.008, msg="q vs unfused")
-        _close(k, k3, atol=0.016, rtol=0.008, msg="k vs unfused")
-        _close(v, v3, atol=0.016, rtol=0.008, msg="v vs unfused")
-
-
 @pytest.mark.parametrize("T,ep,E,k", [(37, 2, 8, 2), (64, 4, 8, 2), (5, 8, 8, 2)])
 def test_ep_dispatch_route_combine_match_reference(cuda, T, ep, E, k):
     """csrc/moe.hip ep_dispatch / ep_recv_route / ep_combine == the fp32/host references of the same image layout
