@@ -47,6 +47,7 @@ class HostStep:
     n_items: int = 0
     prefill_splits: int = 0
     n_merge: int = 0        # prefill row ranges whose tiles were split: i32[-2 n_merge:] = (lo, hi) pairs
+    prefix_joined: int = 0  # prefill tiles that ride in the cascade prefix pass (alt partials into prefill_part)
     i64: np.ndarray | None = None
     i32: np.ndarray | None = None
     # (row, seq, position): decode inputs whose token was still being sampled at planning time, filled at launch
@@ -72,7 +73,7 @@ class SampleParams:
 
 
 _PLAN_SCALARS = ("B", "T", "nbt", "bt_w", "n_rows", "s_total", "n_dec_items", "n_prefix_items", "cascade_prefix",
-                 "n_items", "prefill_splits", "n_merge", "n_late", "late_off", "bt_need")
+                 "n_items", "prefill_splits", "n_merge", "n_late", "late_off", "bt_need", "prefix_joined")
 PLAN_HDR = 32  # int64 header of a broadcast step plan
 PLAN_PAYLOAD_IDX = 1 + len(_PLAN_SCALARS) + 4  # header word holding the payload size (pack_plan)
 
@@ -178,10 +179,12 @@ def pad_step_rows(T: int) -> int:
     return t if t <= 256 else T
 
 
-def plan_prefill_items(tiles: list[tuple[int, int, int, int, int]], hkv: int, target_wgs: int, min_chunk: int,
+def plan_prefill_items(tiles: list[tuple], hkv: int, target_wgs: int, min_chunk: int,
                        max_keys: int = MAX_ITEM_KEYS) -> tuple[list[tuple], int, list[tuple[int, int]]]:
-    """Work items of the prefill tile kernel from query tiles (q0, count, bt_row, extent, hi): ``extent`` = keys the
-    tile attends (its last token's position + 1), ``hi`` = key bound of the chunk.
+    """Work items of the prefill tile kernel from query tiles (q0, count, bt_row, extent, hi[, lo, s0]): ``extent`` =
+    keys the tile attends (its last token's position + 1), ``hi`` = key bound of the chunk. A tile with ``lo`` > 0
+    attends only keys [lo, extent) — its keys below lo (a shared system prefix) were attended by the step's cascade
+    prefix pass, whose partials sit in slots [0, s0) of the row — so it always writes partials, at slots s0, s0 + 1, ...
 
     The tile kernel's time per workgroup is ~a + b x (32-key blocks), so a launch is as long as its longest item. A
     causal prompt's tiles grow linearly (a 2k prompt: 2 .. 64 blocks) and a new turn's few tiles each span a ~20k-token
@@ -191,30 +194,32 @@ def plan_prefill_items(tiles: list[tuple[int, int, int, int, int]], hkv: int, ta
     (the dispatcher then packs the tail). Returns (items, partial slots per row, merged row ranges)."""
     if not tiles:
         return [], 0, []
-    total = sum(t[3] for t in tiles) * hkv
-    longest = max(t[3] for t in tiles)
+    tiles = [tuple(t) + (0, 0) if len(t) == 5 else tuple(t) for t in tiles]
+    total = sum(t[3] - t[5] for t in tiles) * hkv
+    longest = max(t[3] - t[5] for t in tiles)
     if len(tiles) * hkv >= 2 * target_wgs:
         ck = max_keys  # many tiles: split only what exceeds the LDS page-staging bound
     else:
         ck = min(max(min_chunk, -(-total // (target_wgs * 32)) * 32), max_keys)
         if longest < 3 * ck // 2 and longest <= max_keys:
             ck = max_keys  # nothing long enough for a split to shorten the launch by much
-        elif all(t[3] > ck for t in tiles):
+        elif all(t[3] - t[5] > ck for t in tiles):
             # every tile is split (new turns against a long cached context): keep the launch to ONE round of
             # workgroups — per-tile rounding up can overshoot target_wgs by a few, and a second round of a handful
             # of workgroups doubles the launch (r03 trace: 272 workgroups for a new turn, 125 us vs ~60)
-            while ck < max_keys and sum(-(-t[3] // ck) for t in tiles) * hkv > target_wgs:
+            while ck < max_keys and sum(-(-(t[3] - t[5]) // ck) for t in tiles) * hkv > target_wgs:
                 ck += 32
     items, splits, ranges = [], 0, []
-    for q0, cnt, btr, ext, hi in tiles:
-        if ext <= ck:
+    for q0, cnt, btr, ext, hi, lo, s0 in tiles:
+        span = ext - lo
+        if span <= ck and lo == 0:
             items.append((q0, cnt, btr, 0, hi, -1, 0, 0))
             continue
-        nsp = -(-ext // ck)
-        ps = -(-ext // (nsp * 32)) * 32
-        nsp = -(-ext // ps)
-        items += [(q0, cnt, btr, c * ps, min(hi, (c + 1) * ps), c, 0, 0) for c in range(nsp)]
-        splits = max(splits, nsp)
+        nsp = max(1, -(-span // ck))
+        ps = -(-span // (nsp * 32)) * 32
+        nsp = -(-span // ps)
+        items += [(q0, cnt, btr, lo + c * ps, min(hi, lo + (c + 1) * ps), s0 + c, 0, 0) for c in range(nsp)]
+        splits = max(splits, s0 + nsp)
         if ranges and ranges[-1][1] == q0:
             ranges[-1] = (ranges[-1][0], q0 + cnt)
         else:
@@ -494,26 +499,36 @@ class ModelRunner:
         # ---- decode metadata (+ cascade over each group's shared prefix)
         h = HostStep(B=B, T=T, nbt=nbt, bt_w=bt_w, bt_need=min(need, bt_w), n_rows=len(logit_rows), patch=patch)
         i32_parts = [bt.reshape(-1), q_limit]
+        # new-turn prefill chunks whose block table starts with a cascade group's prefix pages (the ~18k shared
+        # system prompt every new turn of a thread re-attends): their tokens join the group's prefix pass — one read
+        # of the prefix pages per step for all rows — and their own tiles attend only the keys behind the prefix
+        joins = self._prefix_joins(bt, B, pre, groups, tiles) if groups and self.variant == 3 else {}
         if B:
             kv_start = np.zeros(B, dtype=np.int64)
             npre = np.zeros(B, dtype=np.int64)
             pit = []
             if groups:
                 # key chunks sized so the prefix pass launches ~target_wgs workgroups over all groups together
-                work = sum(-(-n // self.tile) * p * PAGE for n, p in groups)
+                work = sum(-(-n // self.tile) * p * PAGE for n, p in groups) + \
+                    sum(len(js) * groups[gi][1] * PAGE for gi, js in joins.items())
                 want = max(1, self.target_wgs // self.model.hkv)
                 chunk = min(MAX_ITEM_KEYS, max(256, -(-work // (want * 32)) * 32))
                 r0 = 0
-                for n, p in groups:
+                for gi, (n, p) in enumerate(groups):
                     P = p * PAGE
                     nc = -(-P // chunk)
                     ck = chunk
                     if nc > MAX_PREFIX_CHUNKS:
                         ck = -(-P // (MAX_PREFIX_CHUNKS * 32)) * 32
                         nc = -(-P // ck)
-                    for g0 in range(r0, r0 + n, self.tile):
-                        for c in range(nc):
+                    for c in range(nc):  # chunk-major: the row tiles of one chunk run together (L2 sharing)
+                        for g0 in range(r0, r0 + n, self.tile):
                             pit.append((g0, min(self.tile, r0 + n - g0), r0, c * ck, min(P, (c + 1) * ck), c, 0, 0))
+                        for ti in joins.get(gi, ()):  # prefill tiles: q rows B + q0, fp32 alt partials
+                            q0, cnt = tiles[ti][0], tiles[ti][1]
+                            pit.append((B + q0, cnt, r0, c * ck, min(P, (c + 1) * ck), c, 1, 0))
+                    for ti in joins.get(gi, ()):
+                        tiles[ti] = tiles[ti][:5] + (P, nc)
                     kv_start[r0:r0 + n] = P
                     npre[r0:r0 + n] = nc
                     h.cascade_prefix = max(h.cascade_prefix, P)
@@ -534,10 +549,35 @@ class ModelRunner:
                 i32_parts.append(np.asarray(ranges, dtype=np.int32).reshape(-1))
         h.i64 = np.concatenate([tokens, positions, slots, np.asarray(logit_rows, dtype=np.int64)])
         h.i32 = np.concatenate(i32_parts)
+        h.prefix_joined = sum(len(v) for v in joins.values())
         h.stats = {"B": B, "T": T, "cascade_prefix": h.cascade_prefix, "cascade_groups": len(groups),
+                   "prefix_joined_tiles": h.prefix_joined,
                    "decode_items": h.n_dec_items, "prefix_items": h.n_prefix_items, "s_total": h.s_total,
                    "prefill_splits": h.prefill_splits}
         return h, sample_seqs
+
+    @staticmethod
+    def _prefix_joins(bt: np.ndarray, B: int, pre: list, groups: list[tuple[int, int]],
+                      tiles: list[tuple]) -> dict[int, list[int]]:
+        """{group index: prefill tile indices} of the prefill chunks that start at or behind a cascade group's
+        shared prefix and whose block table holds the same prefix pages (the groups' rows are contiguous from row
+        0 in group order; a tile names its chunk through its block-table row B + j)."""
+        starts, r0 = [], 0
+        for n, p in groups:
+            starts.append((r0, p))
+            r0 += n
+        chunk_group: dict[int, int] = {}
+        for j, (s, a, b) in enumerate(pre):
+            for gi, (g_row, p) in enumerate(starts):
+                if a >= p * PAGE and np.array_equal(bt[B + j, :p], bt[g_row, :p]):
+                    chunk_group[B + j] = gi
+                    break
+        joins: dict[int, list[int]] = {}
+        for ti, t in enumerate(tiles):
+            gi = chunk_group.get(t[2])
+            if gi is not None:
+                joins.setdefault(gi, []).append(ti)
+        return joins
 
     def _plan_decode_items(self, h: HostStep, seq_lens: np.ndarray, kv_start: np.ndarray, npre: np.ndarray,
                            i32_parts: list) -> None:
@@ -604,6 +644,7 @@ class ModelRunner:
                                                 device=self.device)
                 meta.prefill_lse = torch.full((Tp, Hq, h.prefill_splits), float("-inf"), dtype=torch.float32,
                                               device=self.device)
+                meta.prefix_joined = h.prefix_joined > 0
         if h.n_late:
             L, n = h.late_off, h.n_late
             t_tokens.index_copy_(0, d64[L:L + n], self.tok_buf.index_select(0, d64[L + n:L + 2 * n]))

@@ -46,6 +46,7 @@ class AttnMeta:
     prefill_part: torch.Tensor | None = None
     prefill_lse: torch.Tensor | None = None
     prefill_merge: list = field(default_factory=list)  # (lo, hi) prefill row ranges of split tiles
+    prefix_joined: bool = False                # prefill rows take part in the cascade prefix pass (alt partials)
     scale: float = 1.0
     variant: int = 0                           # tile-kernel variant (ops.tile_rows): 0 = 8 waves / 256 rows
     extra: dict = field(default_factory=dict)
@@ -71,9 +72,14 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     if B > 0:
         qd = q[:B]
         if meta.prefix_items is not None:
-            ops.attn_prefill(meta.prefix_items, qd, k_cache, v_cache, meta.block_tables, meta.q_limit,
-                             meta.scale, out_part=meta.pre_part if meta.pre_part is not None else meta.part,
-                             lse_part=meta.lse, variant=meta.variant)
+            # new-turn prefill rows that share the prefix ride along (items flagged alt: fp32 partials in their own
+            # merge buffer, model_runner.build_host); the kernel reads only the q rows its items name
+            joined = meta.prefix_joined and meta.prefill_part is not None
+            ops.attn_prefill(meta.prefix_items, q if joined else qd, k_cache, v_cache, meta.block_tables,
+                             meta.q_limit, meta.scale,
+                             out_part=meta.pre_part if meta.pre_part is not None else meta.part, lse_part=meta.lse,
+                             variant=meta.variant, alt_part=meta.prefill_part if joined else None,
+                             alt_lse=meta.prefill_lse if joined else None, alt_tok_off=B)
         # the decode kernel merges each row's prefix partials and its own pieces and writes the final rows
         ops.attn_decode_items(qd, k_cache, v_cache, meta.block_tables, meta.decode_items, meta.part, meta.lse,
                               meta.scale, out=out[:B], pre_part=meta.pre_part)

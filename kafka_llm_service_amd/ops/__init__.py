@@ -154,14 +154,17 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, kv_start, out_part,
 
 
 def attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, scale: float, out=None, out_part=None,
-                 lse_part=None, variant: int = 0) -> None:
+                 lse_part=None, variant: int = 0, alt_part=None, alt_lse=None, alt_tok_off: int = 0) -> None:
     """Work-item paged attention (chunked prefill / cascade prefix). ``items`` is int32 [n, 8]:
-    (q_start, q_count, bt_row, kv_lo, kv_hi, split, 0, 0)."""
+    (q_start, q_count, bt_row, kv_lo, kv_hi, split, alt, 0). Items with ``alt`` set (tile variant 3) write their
+    partial into ``alt_part`` / ``alt_lse`` (fp32 [rows, Hq, S2, D], row = token - ``alt_tok_off``) instead of
+    ``out_part``: the cascade's prefix pass over a step's new-turn prefill rows."""
     if _gpu(q):
         ext().attn_prefill(items, q, k_cache, v_cache, block_tables, q_limit, out, out_part, lse_part, float(scale),
-                           int(variant))
+                           int(variant), alt_part, alt_lse, int(alt_tok_off))
     else:
-        ref.attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale, out, out_part, lse_part)
+        ref.attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale, out, out_part, lse_part,
+                               alt_part, alt_lse, alt_tok_off)
 
 
 def tile_rows(variant: int = 0) -> int:

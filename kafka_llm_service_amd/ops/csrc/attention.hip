@@ -1149,21 +1149,23 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
                                             const void* k_cache, const void* v_cache, int Hkv, int G, int D,
                                             const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
                                             int64_t out_stride, float* out_part, float* lse_part, int S_total,
-                                            float scale, int part_bf16, hipStream_t st);
+                                            float scale, int part_bf16, float* alt_part, float* alt_lse, int alt_S,
+                                            int alt_tok_off, hipStream_t st);
 
 extern "C" hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride,
                                                const void* k_cache, const void* v_cache, int fp8, int Hkv, int G,
                                                int D, const int* block_tables, int bt_stride, const int* q_limit,
                                                bf16* out, int64_t out_stride, float* out_part, float* lse_part,
-                                               int S_total, float scale, int variant, int part_bf16,
-                                               hipStream_t st) {
+                                               int S_total, float scale, int variant, int part_bf16, float* alt_part,
+                                               float* alt_lse, int alt_S, int alt_tok_off, hipStream_t st) {
   if (n_items == 0) return hipSuccess;
-  if (variant == 3) {  // LDS-DMA ring, one wave per SIMD, 256 rows (attn_tile.hip); bf16 pages only
+  if (variant == 3) {  // LDS-DMA ring, 8 waves, 256 rows (attn_tile.hip); bf16 pages only
     if (fp8) return hipErrorInvalidValue;
     return kafka_launch_attn_tile(items, n_items, q, q_stride, k_cache, v_cache, Hkv, G, D, block_tables, bt_stride,
-                                  q_limit, out, out_stride, out_part, lse_part, S_total, scale, part_bf16, st);
+                                  q_limit, out, out_stride, out_part, lse_part, S_total, scale, part_bf16, alt_part,
+                                  alt_lse, alt_S, alt_tok_off, st);
   }
-  if (part_bf16) return hipErrorInvalidValue;  // tile v3 only
+  if (part_bf16 || alt_part != nullptr) return hipErrorInvalidValue;  // tile v3 only
   if (D != 128 || G < 1 || G > 32 || (128 % G) != 0 || n_items > 65535) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
   const auto* it = reinterpret_cast<const AttnWorkItem*>(items);

@@ -40,7 +40,17 @@ constexpr float THR = 24.f;             // deferred-rescale threshold (log2 doma
 }  // namespace tile3
 
 struct TileItem {
-  int q_start, q_count, bt_row, kv_lo, kv_hi, split, pad0, pad1;
+  int q_start, q_count, bt_row, kv_lo, kv_hi, split, alt, pad1;
+};
+
+// Second partial buffer of a launch (fp32 [rows, Hq, S, D] + lse [rows, Hq, S]) for the items flagged `alt`: the
+// cascade's prefix pass also serves the new-turn prefill rows of the step, whose prefix partials join their own
+// suffix tiles' partials (merged by attn_merge) instead of the decode rows' bf16 slots. Row = token - tok_off.
+struct AltPart {
+  float* part = nullptr;
+  float* lse = nullptr;
+  int S = 0;
+  int tok_off = 0;
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -98,7 +108,7 @@ __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __res
                                                            const int* __restrict__ q_limit, bf16* __restrict__ out,
                                                            int64_t out_stride, float* __restrict__ out_part,
                                                            float* __restrict__ lse_part, int S_total,
-                                                           float scale_log2, int part_bf16) {
+                                                           float scale_log2, int part_bf16, AltPart ap) {
   using namespace tile3;
   constexpr int RB = 1;                   // 32-row MFMA blocks per wave
   constexpr int NSLOT = 3;                // ring slots (4 measured no faster)
@@ -371,6 +381,11 @@ __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __res
   // ---- epilogue: through a per-wave LDS transpose (slot ntiles % NSLOT is idle: its last tile was read before the
   // barrier every wave passed NSLOT - 1 tiles ago), so every store instruction writes whole 128-B lines
   const bool part = it.split >= 0;
+  const bool alt = part && it.alt != 0 && ap.part != nullptr;  // (workgroup-uniform)
+  float* const opart = alt ? ap.part : out_part;
+  float* const lpart = alt ? ap.lse : lse_part;
+  const int Sx = alt ? ap.S : S_total, toff = alt ? ap.tok_off : 0;
+  const bool pbf = part_bf16 && !alt;
   char* slab = smem + (ntiles % NSLOT) * SLOT + w * (4096 * RB);
   const int cc = lane & 7;
 #pragma unroll
@@ -379,7 +394,7 @@ __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __res
     const float ll = fits ? ls[rb][0] : __builtin_nanf("");
     const float inv = ll > 0.f ? 1.f / ll : (fits ? 0.f : ll);
     if (ABL != 8 && part && valid[rb] && h == 0) {
-      float* lp = lse_part + ((int64_t)token[rb] * Hq + head[rb]) * S_total + it.split;
+      float* lp = lpart + ((int64_t)(token[rb] - toff) * Hq + head[rb]) * Sx + it.split;
       *lp = ll > 0.f ? m[rb] + log2f(ll) : (fits ? -INFINITY : ll);
     }
     const int R0 = 32 * RB * w + 32 * rb;
@@ -393,8 +408,8 @@ __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __res
         if (row < nvalid) {
           const int R2 = R0 + row, tok2 = it.q_start + R2 / G, head2 = kvh * G + R2 % G;
           f32x4* dst;
-          if (part && !part_bf16)
-            dst = reinterpret_cast<f32x4*>(out_part + (((int64_t)tok2 * Hq + head2) * S_total + it.split) * D +
+          if (part && !pbf)
+            dst = reinterpret_cast<f32x4*>(opart + (((int64_t)(tok2 - toff) * Hq + head2) * Sx + it.split) * D +
                                            32 * rd + 4 * cc);
           else if (part)  // bf16 partial (O / l in [-max|v|, max|v|]: half the bytes of the cascade round trip)
             dst = reinterpret_cast<f32x4*>(reinterpret_cast<bf16*>(out_part) +
@@ -405,7 +420,7 @@ __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __res
         }
       }
     };
-    if (part && !part_bf16) {
+    if (part && !pbf) {
 #pragma unroll
       for (int rd = 0; rd < 4; ++rd) {
 #pragma unroll
@@ -450,7 +465,8 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
                                             const void* k_cache, const void* v_cache, int Hkv, int G, int D,
                                             const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
                                             int64_t out_stride, float* out_part, float* lse_part, int S_total,
-                                            float scale, int part_bf16, hipStream_t st) {
+                                            float scale, int part_bf16, float* alt_part, float* alt_lse, int alt_S,
+                                            int alt_tok_off, hipStream_t st) {
   if (n_items == 0) return hipSuccess;
   if (D != 128 || G < 1 || G > 32 || (256 % G) != 0 || n_items > 65535) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
@@ -462,7 +478,7 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
   kern<<<dim3(Hkv, n_items), 512, 0, st>>>(reinterpret_cast<const TileItem*>(items), q, q_stride,
                                            static_cast<const bf16*>(k_cache), static_cast<const bf16*>(v_cache), Hkv,
                                            G, block_tables, bt_stride, q_limit, out, out_stride, out_part, lse_part,
-                                           S_total, scale_log2, part_bf16);
+                                           S_total, scale_log2, part_bf16, AltPart{alt_part, alt_lse, alt_S, alt_tok_off});
   return hipGetLastError();
 }
 

@@ -33,7 +33,8 @@ hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16*
                                      const void* k_cache, const void* v_cache, int fp8, int Hkv, int G, int D,
                                      const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
                                      int64_t out_stride, float* out_part, float* lse_part, int S_total, float scale,
-                                     int variant, int part_bf16, hipStream_t st);
+                                     int variant, int part_bf16, float* alt_part, float* alt_lse, int alt_S,
+                                     int alt_tok_off, hipStream_t st);
 hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows, int Hq, int S, int D, bf16* out,
                              int64_t out_stride, float* lse_out, hipStream_t st);
 hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
@@ -275,7 +276,8 @@ static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at
 static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                          at::Tensor block_tables, at::Tensor q_limit, c10::optional<at::Tensor> out,
                          c10::optional<at::Tensor> out_part, c10::optional<at::Tensor> lse_part, double scale,
-                         int64_t variant) {
+                         int64_t variant, c10::optional<at::Tensor> alt_part, c10::optional<at::Tensor> alt_lse,
+                         int64_t alt_tok_off) {
   CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
   CHECK_DT(items, at::kInt); CHECK_DT(block_tables, at::kInt); CHECK_DT(q_limit, at::kInt);
   TORCH_CHECK(items.is_contiguous() && items.dim() == 2 && items.size(1) == 8, "items must be [n, 8] int32");
@@ -305,18 +307,36 @@ static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at:
     TORCH_CHECK(!part_bf16 || variant == 3, "attn_prefill: bf16 out_part needs tile variant 3");
     if (!part_bf16) CHECK_DT(out_part.value(), at::kFloat);
     CHECK_DT(lse_part.value(), at::kFloat);
-    TORCH_CHECK(out_part->is_contiguous() && out_part->dim() == 4 && out_part->size(0) >= T &&
+    // (with alt partials the main buffer covers the rows below alt_tok_off: the decode rows of a cascade pass whose
+    // prefill rows write the alt buffer)
+    const int64_t rows_main = alt_part.has_value() ? std::min<int64_t>(T, alt_tok_off) : T;
+    TORCH_CHECK(out_part->is_contiguous() && out_part->dim() == 4 && out_part->size(0) >= rows_main &&
                     out_part->size(1) == Hq && out_part->size(3) == 128, "out_part must be [T, Hq, S, 128]");
     S_total = out_part->size(2);
-    TORCH_CHECK(lse_part->is_contiguous() && lse_part->numel() >= (int64_t)T * Hq * S_total, "lse_part");
+    TORCH_CHECK(lse_part->is_contiguous() && lse_part->numel() >= rows_main * Hq * S_total, "lse_part");
     pp = reinterpret_cast<float*>(out_part->data_ptr());
     lp = lse_part->data_ptr<float>();
   }
   TORCH_CHECK(op != nullptr || pp != nullptr, "attn_prefill needs out or out_part");
+  // alt partials (items with field 6 set, tile variant 3): fp32 [rows, Hq, S2, 128] + lse, row = token - alt_tok_off
+  float* ap = nullptr;
+  float* al = nullptr;
+  int S2 = 0;
+  if (alt_part.has_value()) {
+    TORCH_CHECK(variant == 3 && alt_lse.has_value(), "attn_prefill: alt partials need tile variant 3 and alt_lse");
+    CHECK_DT(alt_part.value(), at::kFloat); CHECK_DT(alt_lse.value(), at::kFloat);
+    TORCH_CHECK(alt_part->is_contiguous() && alt_part->dim() == 4 && alt_part->size(1) == Hq &&
+                    alt_part->size(3) == 128 && alt_tok_off >= 0 && alt_part->size(0) + alt_tok_off >= T,
+                "attn_prefill: alt_part must be [>= T - alt_tok_off, Hq, S, 128]");
+    S2 = alt_part->size(2);
+    TORCH_CHECK(alt_lse->is_contiguous() && alt_lse->numel() >= alt_part->size(0) * Hq * S2, "attn_prefill: alt_lse");
+    ap = alt_part->data_ptr<float>();
+    al = alt_lse->data_ptr<float>();
+  }
   CHECK_HIP(kafka_launch_attn_prefill(items.data_ptr<int>(), items.size(0), bptr(q), q.stride(0), k_cache.data_ptr(),
                                        v_cache.data_ptr(), is_fp8_cache(k_cache) ? 1 : 0, Hkv, G, 128, block_tables.data_ptr<int>(),
                                        block_tables.stride(0), q_limit.data_ptr<int>(), op, os, pp, lp, S_total,
-                                       scale, (int)variant, part_bf16, cur_stream()));
+                                       scale, (int)variant, part_bf16, ap, al, S2, (int)alt_tok_off, cur_stream()));
 }
 
 static void attn_merge(at::Tensor part, at::Tensor lse, at::Tensor out, c10::optional<at::Tensor> lse_out) {
@@ -798,7 +818,8 @@ PYBIND11_MODULE(_kafka_ops, m) {
         py::arg("tickets"), py::arg("pre_part") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("items"), py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("block_tables"), py::arg("q_limit"), py::arg("out"), py::arg("out_part"), py::arg("lse_part"),
-        py::arg("scale"), py::arg("variant") = 0);
+        py::arg("scale"), py::arg("variant") = 0, py::arg("alt_part") = py::none(), py::arg("alt_lse") = py::none(),
+        py::arg("alt_tok_off") = 0);
   m.def("attn_merge", &attn_merge);
   m.def("sample", &sample, py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"),
         py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none(), py::arg("nsplit") = 1,

@@ -252,8 +252,9 @@ def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_pa
 
 
 def attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale, out=None, out_part=None,
-                       lse_part=None):
-    """Reference for the work-item prefill / cascade kernel (see ops/csrc/attention.hip)."""
+                       lse_part=None, alt_part=None, alt_lse=None, alt_tok_off=0):
+    """Reference for the work-item prefill / cascade kernel (see ops/csrc/attention.hip, attn_tile.hip); items with
+    field 6 set write their partial to alt_part / alt_lse at row token - alt_tok_off."""
     T, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     G = Hq // Hkv
@@ -279,6 +280,10 @@ def attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale,
                 l2[:, h * G:(h + 1) * G] = lh
         if split < 0:
             out[toks] = o.to(out.dtype)
+        elif it[6] and alt_part is not None:
+            rows = toks - alt_tok_off
+            alt_part[rows, :, split] = o.to(alt_part.dtype)
+            alt_lse.view(alt_part.shape[0], Hq, alt_part.shape[2])[rows, :, split] = l2
         else:
             out_part[toks, :, split] = o.to(out_part.dtype)
             lse_part.view(out_part.shape[0], Hq, out_part.shape[2])[toks, :, split] = l2

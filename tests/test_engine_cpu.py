@@ -455,3 +455,43 @@ def test_bf16_cascade_partials_close_to_fp32(base_engine, monkeypatch):
     a, b = logits["0"][1], logits["1"][1]  # first decode step (the cascade pass ran)
     assert a.shape == b.shape
     assert (a - b).abs().max().item() < 0.05 * a.abs().max().item() + 0.05
+
+
+def test_new_turn_rows_join_the_prefix_pass(base_engine):
+    """New-turn prefill chunks that start behind a cascade group's cached prefix take part in the group's prefix
+    pass (model_runner._prefix_joins: one read of the shared pages per step for decode AND prefill rows, fp32
+    partials merged with the chunk's own tiles over the keys behind the prefix): the tokens equal plain per-row
+    attention, and the joined path actually ran (steps with joined tiles)."""
+    prompts = _prompts(seed=41, shared=160, tails=(5, 23, 40))
+    late = _prompts(seed=42, shared=0, tails=(37, 90))  # new turns arriving while the group decodes
+    late = [prompts[0][:160] + t for t in late]
+    sp = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
+    outs = []
+    for cascade in (False, True):
+        e = _engine(model=base_engine.model, use_cascade=cascade, cascade_min_prefix=16, prefill_kv_chunk=64)
+        e.runner.cascade_bf16 = False  # fp32 prefix partials: token-exact against the plain path
+        e.generate([prompts[0][:160] + [7]], GREEDY)  # the shared prefix is cached
+        seqs = [e.add_request(f"r{i}", p, sp) for i, p in enumerate(prompts)]
+        for _ in range(3):
+            e.step()
+        seqs += [e.add_request(f"l{i}", p, sp) for i, p in enumerate(late)]
+        while any(not s.finished for s in seqs):
+            e.step()
+        outs.append([list(s.output_ids) for s in seqs])
+        if cascade:
+            joined = [st.get("prefix_joined_tiles", 0) for st in e.runner.recent_stats]
+            assert max(joined) >= 2, joined
+    assert outs[0] == outs[1]
+
+
+def test_plan_prefill_items_with_prefix_offset():
+    """A tile behind a cascade prefix (lo > 0) attends only [lo, extent) and writes partials from slot s0 on."""
+    from kafka_llm_service_amd.engine.model_runner import plan_prefill_items
+
+    tiles = [(0, 64, 3, 20000, 20100, 18000, 28), (64, 36, 3, 20100, 20100, 18000, 28), (100, 50, 4, 900, 950)]
+    items, splits, ranges = plan_prefill_items(tiles, 8, 256, 256)
+    mine = [it for it in items if it[0] in (0, 64)]
+    assert mine and all(it[3] >= 18000 and it[5] >= 28 for it in mine)
+    assert min(it[3] for it in mine if it[0] == 0) == 18000 and max(it[4] for it in mine if it[0] == 0) >= 20000
+    assert splits == max(it[5] for it in items) + 1
+    assert any(lo <= 0 and hi >= 100 for lo, hi in ranges)

@@ -690,3 +690,72 @@ def test_sample_proc_matches_reference(cuda):
                     assert int(tok[i]) == int(forced[i])
                 else:
                     assert bool(allowed[i, int(tok[i])]), (i, int(tok[i]))
+
+
+def test_cascade_pass_with_new_turn_rows(cuda):
+    """The cascade prefix pass over decode rows AND a new turn's prefill rows in ONE launch (tile v3, items flagged
+    alt write fp32 partials into the prefill merge buffer at row token - B), then the new turn's own tiles over the
+    keys behind the prefix (slots from nc on) and the merge: the new turn's rows equal fp32 causal attention over
+    their whole context, and the decode rows' bf16 prefix partials are bitwise those of a pass without the new
+    turn."""
+    torch.manual_seed(14)
+    Hq, Hkv, D = 32, 8, 128
+    G = Hq // Hkv
+    P, hist, Tn = 1024, 200, 70  # shared prefix, the new turn's own history, new-turn tokens
+    B = 5
+    g = torch.Generator().manual_seed(15)
+    n_pref = P // 16
+    ctx = P + hist + Tn
+    nb_total = n_pref + B * 4 + (ctx - P) // 16 + 4
+    k = torch.randn(nb_total, Hkv, 16, D, generator=g).to(torch.bfloat16).to(cuda)
+    v = torch.randn(nb_total, Hkv, D, 16, generator=g).to(torch.bfloat16).to(cuda)
+    bt = torch.zeros(B + 1, 128, dtype=torch.int32)
+    for b in range(B):
+        bt[b, :n_pref] = torch.arange(n_pref)
+        bt[b, n_pref:n_pref + 4] = torch.arange(n_pref + 4 * b, n_pref + 4 * b + 4)
+    nn = -(-(ctx - P) // 16)
+    bt[B, :n_pref] = torch.arange(n_pref)
+    bt[B, n_pref:n_pref + nn] = torch.arange(n_pref + 4 * B, n_pref + 4 * B + nn)
+    bt = bt.to(cuda)
+    T = B + Tn
+    q = torch.randn(T, Hq, D, device=cuda, dtype=torch.bfloat16)
+    a = P + hist  # first new-turn position
+    q_limit = torch.cat([torch.full((B,), P + 40, dtype=torch.int32), torch.arange(a, a + Tn, dtype=torch.int32)])
+    q_limit = q_limit.to(cuda)
+    scale = 1 / math.sqrt(D)
+    nc, ck = 4, P // 4
+    tile = 256 // G
+    pre_items = [(0, B, 0, c * ck, (c + 1) * ck, c, 0, 0) for c in range(nc)]
+    alt_items = [(B + t0, min(tile, Tn - t0), 0, c * ck, (c + 1) * ck, c, 1, 0)
+                 for c in range(nc) for t0 in range(0, Tn, tile)]
+    S_dec, S_new = nc + 1, nc + 3
+    pre_a = torch.zeros(B, Hq, S_dec, D, device=cuda, dtype=torch.bfloat16)
+    lse_a = torch.zeros(B, Hq, S_dec, device=cuda)
+    pre_b, lse_b = pre_a.clone(), lse_a.clone()
+    part_new = torch.zeros(Tn, Hq, S_new, D, device=cuda)
+    lse_new = torch.full((Tn, Hq, S_new), float("-inf"), device=cuda)
+    it_all = torch.tensor(pre_items + alt_items, dtype=torch.int32, device=cuda)
+    ops.attn_prefill(it_all, q, k, v, bt, q_limit, scale, out_part=pre_a, lse_part=lse_a, variant=3,
+                     alt_part=part_new, alt_lse=lse_new, alt_tok_off=B)
+    ops.attn_prefill(torch.tensor(pre_items, dtype=torch.int32, device=cuda), q[:B], k, v, bt, q_limit, scale,
+                     out_part=pre_b, lse_part=lse_b, variant=3)
+    torch.cuda.synchronize()
+    assert torch.equal(pre_a, pre_b) and torch.equal(lse_a, lse_b)
+    # the new turn's own keys [P, ctx) in 3 pieces, slots nc.., rows relative to B
+    own = [(t0, min(tile, Tn - t0), B, P + c * 160, min(ctx, P + (c + 1) * 160), nc + c, 0, 0)
+           for t0 in range(0, Tn, tile) for c in range(3)]
+    ops.attn_prefill(torch.tensor(own, dtype=torch.int32, device=cuda), q[B:], k, v, bt, q_limit[B:], scale,
+                     out_part=part_new, lse_part=lse_new, variant=3)
+    out = torch.empty(Tn, Hq, D, device=cuda, dtype=torch.bfloat16)
+    ops.attn_merge(part_new, lse_new, out)
+    # fp32 reference: causal attention of each new-turn token over its whole context through block-table row B
+    kk, vv = ref.gather_kv(k.cpu(), v.cpu(), bt[B].cpu(), ctx)
+    o_ref = torch.empty(Tn, Hq, D)
+    for t in range(Tn):
+        pos = a + t
+        for h in range(Hkv):
+            qs = q[B + t, h * G:(h + 1) * G].float().cpu()
+            s_ = (qs @ kk[:pos + 1, h].float().t()) * scale
+            p_ = torch.softmax(s_, -1)
+            o_ref[t, h * G:(h + 1) * G] = p_ @ vv[:pos + 1, h].float()
+    _close(out, o_ref, atol=0.02, msg="new-turn rows through the cascade pass")
