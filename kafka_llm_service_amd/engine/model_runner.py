@@ -301,6 +301,51 @@ def decode_items(seq_lens: np.ndarray, kv_start: np.ndarray, npre: np.ndarray, h
     return it
 
 
+def decode_items_fixed(seq_lens: np.ndarray, kv_start: np.ndarray, npre: np.ndarray, hkv: int,
+                       target: int = DECODE_TARGET_ITEMS) -> np.ndarray:
+    """``decode_items`` with EXACTLY n = max(B, target // hkv) items (a captured decode graph's launch shape then
+    depends on B alone, no padded grid): the n pieces are dealt to the rows in proportion to their 32-key blocks
+    (largest remainder, at least one per row, at most MAX_PARTIALS - npre and one per block), each row's blocks split
+    evenly; rows too short to take their share leave null items (split -1: the kernel drops them)."""
+    B = seq_lens.shape[0]
+    n = max(B, target // hkv)
+    a0 = kv_start - kv_start % 32
+    nb = np.maximum((seq_lens - a0 + 31) // 32, 1).astype(np.int64)
+    cap = np.maximum(1, np.minimum(nb, MAX_PARTIALS - npre))
+    ns = np.minimum(cap, np.maximum(1, (n * nb) // max(1, int(nb.sum()))))
+    while int(ns.sum()) > n:  # the at-least-one floor overshot: take pieces back from the lightest split rows
+        more = ns > 1
+        if not more.any():
+            break
+        load = np.where(more, nb / ns, np.inf)
+        ns[int(np.argmin(load))] -= 1
+    left = n - int(ns.sum())
+    while left > 0:  # largest blocks-per-piece first
+        room = ns < cap
+        if not room.any():
+            break
+        load = np.where(room, nb / ns, -1.0)
+        k = min(left, int(room.sum()))
+        for b in np.argsort(-load, kind="stable")[:k]:
+            ns[b] += 1
+        left = n - int(ns.sum())
+    rows = np.repeat(np.arange(B), ns)
+    first = np.cumsum(ns) - ns
+    split = np.arange(rows.shape[0]) - np.repeat(first, ns)
+    b_lo = (split * nb[rows]) // ns[rows]
+    b_hi = ((split + 1) * nb[rows]) // ns[rows]
+    lo = np.maximum(kv_start[rows], a0[rows] + b_lo * 32)
+    hi = np.minimum(seq_lens[rows], a0[rows] + b_hi * 32)
+    z = np.zeros_like(rows)
+    it = np.stack([rows, lo, hi, split, ns[rows], npre[rows], z, z], 1).astype(np.int32)
+    it = it[np.argsort(it[:, 1] - it[:, 2], kind="stable")]
+    if it.shape[0] < n:
+        pad = np.zeros((n - it.shape[0], 8), dtype=np.int32)
+        pad[:, 3] = -1
+        it = np.concatenate([it, pad])
+    return it
+
+
 _NP2TORCH = {np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32, np.dtype(np.float32): torch.float32}
 
 
@@ -415,6 +460,7 @@ class ModelRunner:
         # rows whose token was still being sampled at launch gather their input ids from it on the stream
         self.tok_buf = torch.zeros(max_num_seqs * 2 + 64, dtype=torch.int64, device=self.device)
         self.graphs = None  # engine/graphs.py DecodeGraphs when hipGraph decode is enabled
+        self.fixed_decode_items = False  # decode_items_fixed without graphs too (equivalence tests)
         # grammar masks / forced tokens / penalties inside the sampler kernel (tables allocated on first use)
         self.lp = LogitsProcessor(self.device, self.vocab, max_slots=max(256, max_num_seqs))
 
@@ -581,14 +627,15 @@ class ModelRunner:
 
     def _plan_decode_items(self, h: HostStep, seq_lens: np.ndarray, kv_start: np.ndarray, npre: np.ndarray,
                            i32_parts: list) -> None:
-        ditems = decode_items(seq_lens, kv_start, npre, self.model.hkv)
-        if self.graphs is not None:  # fixed-size item list per bucket (graph replay); pads are dropped
-            cap = max(64, 1 << (int(ditems.shape[0]) - 1).bit_length())
-            pad = np.zeros((cap - ditems.shape[0], 8), dtype=np.int32)
-            pad[:, 3] = -1
-            ditems = np.concatenate([ditems, pad])
+        if self.graphs is not None or self.fixed_decode_items:  # graph replay: the decode grid depends on B alone
+            ditems = decode_items_fixed(seq_lens, kv_start, npre, self.model.hkv)
+        else:
+            ditems = decode_items(seq_lens, kv_start, npre, self.model.hkv)
         h.n_dec_items = int(ditems.shape[0])
-        h.s_total = int((npre[ditems[:, 0]] + ditems[:, 4]).max()) if h.B else 1
+        real = ditems[:, 3] >= 0
+        h.s_total = int((npre[ditems[real, 0]] + ditems[real, 4]).max()) if h.B else 1
+        if self.graphs is not None:
+            h.s_total = MAX_PARTIALS  # (a graph layout key; the partial buffer's unused slots are never touched)
         i32_parts.append(ditems.reshape(-1))
 
     def to_device(self, h: HostStep, sp: "SampleParams | None" = None) -> StepInput:

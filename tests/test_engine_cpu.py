@@ -333,6 +333,24 @@ def test_prefix_groups_and_decode_items():
         assert (rows[:, 3] == np.arange(len(rows))).all() and (rows[:, 4] == len(rows)).all()
         assert (rows[:, 5] == npre[b]).all() and len(rows) + npre[b] <= MAX_PARTIALS
     assert (it[:, 0] == 3).sum() > (it[:, 0] == 1).sum() == 1  # the long row is split, the short one is not
+    # fixed-count items (graph replay): exactly max(B, target // hkv) items, the same coverage rules, null pads
+    from kafka_llm_service_amd.engine.model_runner import decode_items_fixed
+
+    rng = np.random.default_rng(3)
+    for B, target in ((4, 64), (4, 1344), (64, 1344), (3, 8)):
+        lens = rng.integers(300, 30000, B)
+        ks = np.minimum(lens - 1, rng.integers(0, 20000, B) // 16 * 16)
+        npre = rng.integers(0, 33, B)
+        it = decode_items_fixed(lens, ks, npre, hkv=8, target=target)
+        assert it.shape[0] == max(B, target // 8)
+        real = it[it[:, 3] >= 0]
+        for b in range(B):
+            rows = real[real[:, 0] == b]
+            rows = rows[np.argsort(rows[:, 3])]
+            assert rows[0, 1] == ks[b] and rows[-1, 2] == lens[b]
+            assert (rows[1:, 1] == rows[:-1, 2]).all() and (rows[1:, 1] % 32 == 0).all() and (rows[:, 2] > rows[:, 1]).all()
+            assert (rows[:, 3] == np.arange(len(rows))).all() and (rows[:, 4] == len(rows)).all()
+            assert len(rows) + npre[b] <= MAX_PARTIALS
 
 
 def test_tiled_only_mixtral_and_export(tmp_path):

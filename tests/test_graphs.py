@@ -7,6 +7,7 @@ from kafka_llm_service_amd.engine.sequence import SamplingParams
 def _run(use_graphs, model=None):
     eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", num_kv_blocks=256, max_model_len=2048,
                                  use_graphs=use_graphs, cascade_min_prefix=32), model=model)
+    eng.runner.fixed_decode_items = True  # the graphed runner's decode plan (decode_items_fixed) for both runs
     shared = list(range(500, 548))
     prompts = [shared + list(range(900 + 10 * i, 905 + 13 * i)) for i in range(5)]
     params = [SamplingParams(temperature=0.0, max_tokens=9, ignore_eos=True)] * 2 + \
