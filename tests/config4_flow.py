@@ -30,9 +30,11 @@ def _frames(text: str) -> list:
     return [json.loads(b[6:]) for b in text.split("\n\n") if b.strip().startswith("data: {")]
 
 
-def run(tmp_path, model: str, engine_kwargs: dict, **cfg_kw) -> tuple[str, list, list]:
+def run(tmp_path, model: str, engine_kwargs: dict, sections: list[str] | None = ("intro",), on_done=None,
+        **cfg_kw) -> tuple[str, list, list]:
     """Start a sandbox service + the API server, run one /v1/threads/{id}/agent/run turn; returns (SSE text,
-    frames, persisted messages)."""
+    frames, persisted messages). ``sections=None``: the served default system prompt (the reference's 13 sections
+    + the tool schemas, ~18k tokens)."""
     import httpx
     from fastapi.testclient import TestClient
 
@@ -58,7 +60,8 @@ def run(tmp_path, model: str, engine_kwargs: dict, **cfg_kw) -> tuple[str, list,
                 time.sleep(0.1)
         cfg = ServerConfig(backend="engine", model=model, sandbox="shared", sandbox_url=f"http://127.0.0.1:{port}",
                            tool_choice=SCRIPT, tool_overrides=OVERRIDES, agent_max_iterations=3,
-                           prompt_sections=["intro"], engine_kwargs=engine_kwargs, **cfg_kw)
+                           prompt_sections=list(sections) if sections else None, engine_kwargs=engine_kwargs,
+                           **cfg_kw)
         st = ServerState(cfg, db=MemoryDBClient())
         with TestClient(create_app(state=st)) as c:
             assert c.get("/health").json()["kafka_initialized"]
@@ -68,6 +71,8 @@ def run(tmp_path, model: str, engine_kwargs: dict, **cfg_kw) -> tuple[str, list,
                                                                           "check the weather in London."}],
                                 "temperature": 0.7, "max_tokens": 96}).text
             msgs = c.get(f"/v1/threads/{tid}/messages").json()["messages"]
+            if on_done is not None:
+                on_done(c)
     finally:
         sbx.terminate()
         sbx.wait(timeout=30)
