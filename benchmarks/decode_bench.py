@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from kafka_llm_service_amd import ops
-from kafka_llm_service_amd.engine.model_runner import decode_items
+from kafka_llm_service_amd.engine.model_runner import decode_items, decode_items_fixed
 
 
 def timeit(fn, iters=20, rounds=5):
@@ -44,7 +44,9 @@ def main():
     ap.add_argument("--layers", type=int, default=4)
     ap.add_argument("--pool-blocks", type=int, default=40000)
     ap.add_argument("--npre", type=int, default=32)
-    ap.add_argument("--check", action="store_true", help="compare every kernel with the fp32 reference once")
+    ap.add_argument("--targets", default="1344", help="decode workgroup targets to sweep (items x Hkv)")
+    ap.add_argument("--layouts", default="contiguous,scattered")
+    ap.add_argument("--plans", default="adaptive,fixed")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     Hq, Hkv, D = 32, 8, 128
@@ -64,14 +66,21 @@ def main():
     scale = D ** -0.5
     npre = np.full(B, args.npre)
     kv_start = np.full(B, P)
-    items = torch.from_numpy(decode_items(lens.astype(np.int64), kv_start.astype(np.int64), npre, Hkv)).to(dev)
-    S = int((npre[items[:, 0].cpu().numpy()] + items[:, 4].cpu().numpy()).max())
+    plans = {}
+    for t in (int(x) for x in args.targets.split(",")):
+        if "adaptive" in args.plans:
+            plans[f"adaptive{t}"] = decode_items(lens.astype(np.int64), kv_start.astype(np.int64), npre, Hkv,
+                                                 target=t)
+        if "fixed" in args.plans:
+            plans[f"fixed{t}"] = decode_items_fixed(lens.astype(np.int64), kv_start.astype(np.int64), npre, Hkv,
+                                                    target=t)
+    S = 64
     part = torch.empty(B, Hq, S, D, device=dev)
     lse = torch.randn(B, Hq, S, device=dev) - 40.0  # prefix partials count, suffix dominates
     pre = torch.randn(B, Hq, S, D, device=dev).to(torch.bfloat16)
     out = torch.empty(B, Hq, D, device=dev, dtype=torch.bfloat16)
     suffix_bytes = int(suffix.sum()) * Hkv * D * 2 * 2
-    for layout in ("contiguous", "scattered"):
+    for layout in args.layouts.split(","):
         bt = np.zeros((B, maxb), dtype=np.int32)
         free = np.arange(n_pref, nb)
         if layout == "scattered":
@@ -83,11 +92,12 @@ def main():
             bt[b, n_pref:n_pref + k] = free[c:c + k]
             c += k
         btd = torch.from_numpy(bt).to(dev)
-        kern = {"decode": lambda i: ops.attn_decode_items(q, *caches[i % args.layers], btd, items, part, lse, scale,
-                                                          out=out, pre_part=pre)}
-        for name, fn in kern.items():
+        for pname, plan in plans.items():
+            items = torch.from_numpy(plan).to(dev)
+            fn = lambda i, items=items: ops.attn_decode_items(q, *caches[i % args.layers], btd, items, part, lse,  # noqa: E731
+                                                                scale, out=out, pre_part=pre)
             us = timeit(fn)
-            print(json.dumps({"kernel": name, "layout": layout, "items": int(items.shape[0]), "S": S,
+            print(json.dumps({"kernel": "decode", "plan": pname, "layout": layout, "items": int(items.shape[0]),
                               "us": round(us, 1), "TB/s": round(suffix_bytes / us / 1e6, 3)}), flush=True)
 
 
