@@ -530,6 +530,7 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
         "planned_late_frac": round(eng.stats.get("planned_late", 0) / max(1, eng.stats.get("steps", 1)), 4),
         "step_rows_hist": dict(zip(("<=64", "65-96", "97-128", "129-256", ">256"), eng.runner.rows_hist)),
         "grammar_rollbacks": eng.stats.get("grammar_rollbacks", 0),
+        "graph_stats": dict(eng.runner.graphs.stats) if eng.runner.graphs is not None else None,
         # self-verification of multi-GPU runs: one record per rank (which GPU it ran on, its own rate and step time;
         # TP followers report 0 tokens: their leader streams the replica's tokens) and the process groups' backends /
         # sizes as torch.distributed reports them (backend "nccl" is RCCL on ROCm)

@@ -48,6 +48,9 @@ class EngineConfig:
     step_rows_fit: int | None = None    # row fit (engine/scheduler.py); None = env KAFKA_STEP_ROWS_FIT, default 0
     max_model_len: int = 131072
     enable_prefix_cache: bool = True
+    # pages a decoding sequence takes at a time as ONE run of consecutive block ids (the spare ones reserved for it):
+    # a thread's history then lies in long runs of the pool (runtime/csrc/kv_manager.cpp)
+    kv_run_pages: int = 1
     use_cascade: bool = True
     cascade_min_prefix: int = 512
     target_wgs: int = 256               # tile-kernel workgroups per pass (8-wave WGs, one per CU)
@@ -169,7 +172,7 @@ class LLMEngine:
         kshape, vshape, kv_dt = ops.kv_cache_shapes(nb, hkv, D, cfg.kv_dtype)
         self.k_cache = torch.zeros(L, *kshape, dtype=kv_dt, device=self.device)
         self.v_cache = torch.zeros(L, *vshape, dtype=kv_dt, device=self.device)
-        self.kvm = KVManager(nb, 16, cfg.enable_prefix_cache)
+        self.kvm = KVManager(nb, 16, cfg.enable_prefix_cache, cfg.kv_run_pages)
         max_blocks = (cfg.max_model_len + 15) // 16
         self.sched = Scheduler(SchedulerConfig(max_num_seqs=cfg.max_num_seqs,
                                                max_num_batched_tokens=cfg.max_num_batched_tokens,

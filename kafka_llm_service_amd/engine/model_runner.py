@@ -559,6 +559,12 @@ class ModelRunner:
                     sum(len(js) * groups[gi][1] * PAGE for gi, js in joins.items())
                 want = max(1, self.target_wgs // self.model.hkv)
                 chunk = min(MAX_ITEM_KEYS, max(256, -(-work // (want * 32)) * 32))
+                # one round of workgroups: per-group rounding up can overshoot the target by a few items, and a
+                # second round of a handful of workgroups doubles the launch
+                tiles_per_group = [-(-n // self.tile) + len(joins.get(gi, ())) for gi, (n, _) in enumerate(groups)]
+                while chunk < MAX_ITEM_KEYS and sum(t * -(-(p * PAGE) // chunk) for t, (_, p) in
+                                                    zip(tiles_per_group, groups)) > want:
+                    chunk += 32
                 r0 = 0
                 for gi, (n, p) in enumerate(groups):
                     P = p * PAGE

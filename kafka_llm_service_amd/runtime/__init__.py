@@ -22,5 +22,5 @@ def native():
     return _MOD
 
 
-def KVManager(num_blocks: int, page: int = 16, prefix_cache: bool = True):
-    return native().KVManager(num_blocks, page, prefix_cache)
+def KVManager(num_blocks: int, page: int = 16, prefix_cache: bool = True, run: int = 1):
+    return native().KVManager(num_blocks, page, prefix_cache, run)

@@ -8,7 +8,12 @@
 //     the uncached tail is prefilled. Pages are registered as soon as a sequence has written them completely (during
 //     chunked prefill and during decode), which is what turns agent iteration k+1 and turn t+1 of a thread into
 //     prefix hits,
-//   * LRU eviction of unreferenced leaf pages when the free list runs dry.
+//   * LRU eviction of unreferenced leaf pages when the free list runs dry,
+//   * contiguous page runs: free pages are an ordered set handed out next-fit, a sequence takes its pages in runs of
+//     consecutive block ids (a prefill chunk at once, decode growth `run` pages at a time, the spare ones reserved
+//     for it), so a thread's history is a few long runs of the pool instead of one page every 64 blocks — its K/V
+//     pages for a layer are read as long sweeps (DRAM pages, TLB reach). Reserved pages are reclaimed whenever the
+//     pool runs short.
 //
 // Reference counting: node->ref = number of live sequences whose block table contains the node's page. A block is
 // on the free list iff it is neither owned by a live sequence (exclusively) nor held by a tree node. A node with
@@ -49,6 +54,7 @@ struct Node {
 struct Seq {
   std::vector<int32_t> tokens;  // all tokens known for the sequence (prompt + generated)
   std::vector<int> blocks;      // block table
+  std::vector<int> reserve;     // pages taken for this sequence's growth, not in its table yet (ascending)
   std::vector<Node*> nodes;     // nodes[i] != nullptr iff blocks[i] is a tree page referenced by this seq
   int64_t n_cached = 0;         // tokens whose KV came from the prefix cache at admission
   int64_t n_registered_pages = 0;
@@ -65,11 +71,10 @@ static inline uint64_t hash_page(const int32_t* t, int n) {
 
 class KVManager {
  public:
-  KVManager(int num_blocks, int page, bool prefix_cache)
-      : num_blocks_(num_blocks), page_(page), prefix_cache_(prefix_cache) {
+  KVManager(int num_blocks, int page, bool prefix_cache, int run = 1)
+      : num_blocks_(num_blocks), page_(page), prefix_cache_(prefix_cache), run_(std::max(1, run)) {
     if (num_blocks <= 0 || page <= 0) throw std::invalid_argument("num_blocks and page must be positive");
-    free_.reserve(num_blocks);
-    for (int b = num_blocks - 1; b >= 0; --b) free_.push_back(b);
+    for (int b = 0; b < num_blocks; ++b) free_.insert(free_.end(), b);
     root_ = std::make_unique<Node>();
     root_->id = 0;
   }
@@ -78,11 +83,13 @@ class KVManager {
   int page() const { return page_; }
   int num_blocks() const { return num_blocks_; }
   int num_free() const { return (int)free_.size(); }
+  int num_reserved() const { return (int)n_reserved_; }
+  int run() const { return run_; }
   // unreferenced cached pages (whole ref==0 subtrees: a sequence holding a page holds its whole chain)
   int num_evictable() const { return (int)n_unref_; }
   int num_cached_pages() const { return (int)n_nodes_; }
-  // blocks that can be obtained right now (free + evictable)
-  int available() const { return (int)free_.size() + (int)n_unref_; }
+  // blocks that can be obtained right now (free + evictable + other sequences' reserves)
+  int available() const { return (int)free_.size() + (int)n_unref_ + (int)n_reserved_; }
 
   bool has_seq(int64_t sid) const { return seqs_.count(sid) != 0; }
 
@@ -130,11 +137,27 @@ class KVManager {
     const int need = blocks_needed(sid, total_len);
     if (need == 0) return true;
     if (need > available()) return false;
-    for (int i = 0; i < need; ++i) {
-      int b = pop_block();
-      s.blocks.push_back(b);
-      s.nodes.push_back(nullptr);
+    int left = need;
+    // own reserve first
+    while (left > 0 && !s.reserve.empty()) {
+      take_table(s, s.reserve.front());
+      s.reserve.erase(s.reserve.begin());
+      --n_reserved_;
+      --left;
     }
+    if (left == 0) return true;
+    if ((int64_t)free_.size() + n_unref_ < left) reclaim_reserves();
+    // one run of consecutive pages: the whole need (a prefill chunk), or `run` pages for decode growth with the
+    // spare ones reserved for this sequence
+    const int want = std::max(left, run_);
+    std::vector<int> got;
+    if (want > 1 && (int64_t)free_.size() >= want && pop_run(want, got)) {
+      for (int i = 0; i < left; ++i) take_table(s, got[i]);
+      for (size_t i = left; i < got.size(); ++i) s.reserve.push_back(got[i]);
+      n_reserved_ += (int64_t)got.size() - left;
+      return true;
+    }
+    for (int i = 0; i < left; ++i) take_table(s, pop_block());
     return true;
   }
 
@@ -182,6 +205,8 @@ class KVManager {
       if (s.nodes[i]) release(s.nodes[i]);
       else push_block(s.blocks[i]);
     }
+    for (int b : s.reserve) push_block(b);
+    n_reserved_ -= (int64_t)s.reserve.size();
     seqs_.erase(it);
   }
 
@@ -239,6 +264,7 @@ class KVManager {
     py::dict d;
     d["num_blocks"] = num_blocks_;
     d["free"] = (int)free_.size();
+    d["reserved"] = n_reserved_;
     d["evictable"] = n_unref_;
     d["cached_pages"] = n_nodes_;
     d["sequences"] = (int64_t)seqs_.size();
@@ -271,8 +297,11 @@ class KVManager {
       for (auto& kv : n->children)
         for (Node* c : kv.second) stack.push_back(c);
     }
+    int64_t reserved = 0;
     for (auto& kv : seqs_) {
       const Seq& s = *kv.second;
+      for (int b : s.reserve) owner[b]++;
+      reserved += (int64_t)s.reserve.size();
       for (size_t i = 0; i < s.blocks.size(); ++i) {
         if (s.nodes[i]) {
           refs[s.nodes[i]]++;
@@ -284,6 +313,7 @@ class KVManager {
     }
     for (int b = 0; b < num_blocks_; ++b)
       if (owner[b] != 1) return false;
+    if (reserved != n_reserved_) return false;
     int64_t unref = 0;
     // node refs must equal the number of sequences referencing them
     stack.push_back(root_.get());
@@ -374,7 +404,7 @@ class KVManager {
     auto& bucket = p->children[hash_page(n->tokens.data(), page_)];
     bucket.erase(std::find(bucket.begin(), bucket.end(), n));
     if (bucket.empty()) p->children.erase(hash_page(n->tokens.data(), page_));
-    free_.push_back(n->block);
+    free_.insert(n->block);
     delete n;
     --n_nodes_;
     --n_unref_;
@@ -382,16 +412,62 @@ class KVManager {
     if (--p->n_children == 0 && p != root_.get() && p->ref == 0) lru_insert(p);
   }
 
+  void take_table(Seq& s, int b) {
+    s.blocks.push_back(b);
+    s.nodes.push_back(nullptr);
+  }
+
+  // next-fit: the first free page at or after the cursor (wrapping)
   int pop_block() {
     if (free_.empty()) {
-      if (lru_.empty()) throw std::runtime_error("KV pool exhausted");
-      evict_one();
+      if (lru_.empty()) reclaim_reserves();
+      if (free_.empty()) {
+        if (lru_.empty()) throw std::runtime_error("KV pool exhausted");
+        evict_one();
+      }
     }
-    int b = free_.back();
-    free_.pop_back();
+    auto it = free_.lower_bound(cursor_);
+    if (it == free_.end()) it = free_.begin();
+    const int b = *it;
+    free_.erase(it);
+    cursor_ = b + 1;
     return b;
   }
-  void push_block(int b) { free_.push_back(b); }
+
+  // n consecutive free pages at or after the cursor (a bounded search over candidate starts, wrapping once);
+  // false (nothing taken) if no such run was found
+  bool pop_run(int n, std::vector<int>& out) {
+    out.clear();
+    auto it = free_.lower_bound(cursor_);
+    for (int pass = 0, tries = 0; pass < 2 && tries < 512; ++pass) {
+      if (pass == 1) it = free_.begin();
+      while (it != free_.end() && tries < 512) {
+        ++tries;
+        const int b0 = *it;
+        auto jt = it;
+        int k = 1;
+        for (++jt; k < n && jt != free_.end() && *jt == b0 + k; ++jt) ++k;
+        if (k == n) {
+          for (int i = 0; i < n; ++i) out.push_back(b0 + i);
+          free_.erase(it, jt);
+          cursor_ = b0 + n;
+          return true;
+        }
+        it = jt;  // the next candidate start: past the short run
+      }
+    }
+    return false;
+  }
+  void push_block(int b) { free_.insert(b); }
+
+  // every sequence's spare pages back to the pool (the pool ran short)
+  void reclaim_reserves() {
+    for (auto& kv : seqs_) {
+      for (int b : kv.second->reserve) free_.insert(b);
+      kv.second->reserve.clear();
+    }
+    n_reserved_ = 0;
+  }
 
   void clear_tree(Node* n) {
     for (auto& kv : n->children)
@@ -405,7 +481,10 @@ class KVManager {
   int num_blocks_;
   int page_;
   bool prefix_cache_;
-  std::vector<int> free_;
+  int run_;
+  std::set<int> free_;
+  int cursor_ = 0;
+  int64_t n_reserved_ = 0;
   std::unique_ptr<Node> root_;
   std::set<LruKey> lru_;
   std::unordered_map<int64_t, std::unique_ptr<Seq>> seqs_;
@@ -430,7 +509,10 @@ PYBIND11_MODULE(_kafka_runtime, m) {
   kafka::register_plan_channel(m);
   kafka::register_group_board(m);
   py::class_<kafka::KVManager>(m, "KVManager")
-      .def(py::init<int, int, bool>(), py::arg("num_blocks"), py::arg("page") = 16, py::arg("prefix_cache") = true)
+      .def(py::init<int, int, bool, int>(), py::arg("num_blocks"), py::arg("page") = 16,
+           py::arg("prefix_cache") = true, py::arg("run") = 1)
+      .def_property_readonly("run", &kafka::KVManager::run)
+      .def("num_reserved", &kafka::KVManager::num_reserved)
       .def_property_readonly("page", &kafka::KVManager::page)
       .def_property_readonly("num_blocks", &kafka::KVManager::num_blocks)
       .def("num_free", &kafka::KVManager::num_free)

@@ -225,3 +225,48 @@ def test_plan_channel_idle_follower_waits_until_leader_exits():
             lead.kill()
     with pytest.raises(RuntimeError):
         rt.PlanChannel(name, 0)  # nothing left to attach to
+
+
+def test_page_runs_contiguous_and_invariants():
+    """run = 16: a sequence's decode growth comes in runs of consecutive block ids (the spare pages reserved for it),
+    a prefill chunk is one run, reserves are reclaimed when the pool runs short, and every page stays in exactly
+    one place (free set, a table, a reserve or the tree) under random admit / grow / commit / free traffic."""
+    import random
+
+    import numpy as np
+
+    kv = KVManager(600, 16, True, 16)
+    assert kv.run == 16
+    kv.add_sequence(1, np.arange(1, 200, dtype=np.int32))
+    assert kv.ensure_capacity(1, 199)
+    bt = kv.block_table(1)
+    assert bt == list(range(bt[0], bt[0] + len(bt)))  # one run for the prefill
+    for n in range(200, 200 + 16 * 20):  # decode growth: consecutive within each run of 16
+        assert kv.ensure_capacity(1, n)
+    bt = kv.block_table(1)
+    jumps = sum(1 for a, b in zip(bt, bt[1:]) if b != a + 1)
+    assert jumps <= 21 and kv.num_reserved() <= 15 and kv.check_invariants()
+    rng = random.Random(7)
+    live = {1: 200 + 16 * 20}
+    for step in range(400):
+        op = rng.random()
+        if op < 0.2 and len(live) < 12:
+            sid = 100 + step
+            toks = np.array([rng.randrange(1, 50) for _ in range(rng.randrange(2, 120))], dtype=np.int32)
+            kv.add_sequence(sid, toks)
+            if kv.ensure_capacity(sid, len(toks)):
+                live[sid] = len(toks)
+            else:
+                kv.free_sequence(sid)
+        elif op < 0.75 and live:
+            sid = rng.choice(list(live))
+            if kv.ensure_capacity(sid, live[sid] + 1):
+                kv.append_token(sid, rng.randrange(1, 50))
+                live[sid] += 1
+                kv.commit(sid, live[sid] - 1)
+        elif live:
+            sid = rng.choice(list(live))
+            kv.free_sequence(sid)
+            del live[sid]
+        assert kv.check_invariants(), step
+    assert kv.available() >= kv.num_free()
