@@ -383,6 +383,7 @@ def main(argv=None):
     if dev.startswith("cuda"):
         torch.cuda.synchronize()
     _barrier(leaders)
+    host0 = dict(eng.host_s)
     prof = None
     if os.environ.get("KAFKA_CPROFILE"):  # host-side profile of the timed steps only (scripts/gpu_cpu_prof.sh)
         import cProfile
@@ -396,6 +397,7 @@ def main(argv=None):
     if dev.startswith("cuda"):
         torch.cuda.synchronize()
     t1 = time.perf_counter()
+    timing["host_ms"] = {k: round((eng.host_s[k] - host0[k]) * 1e3 / max(1, args.steps), 3) for k in host0}
     if prof is not None:
         import pstats
 
@@ -531,6 +533,7 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
         "step_rows_hist": dict(zip(("<=64", "65-96", "97-128", "129-256", ">256"), eng.runner.rows_hist)),
         "grammar_rollbacks": eng.stats.get("grammar_rollbacks", 0),
         "graph_stats": dict(eng.runner.graphs.stats) if eng.runner.graphs is not None else None,
+        "host_ms_per_step": timing.get("host_ms"),  # rank 0's engine host time per timed step, by activity
         # self-verification of multi-GPU runs: one record per rank (which GPU it ran on, its own rate and step time;
         # TP followers report 0 tokens: their leader streams the replica's tokens) and the process groups' backends /
         # sizes as torch.distributed reports them (backend "nccl" is RCCL on ROCm)

@@ -15,7 +15,7 @@ from kafka_llm_service_amd.ops import _ext
 
 from wstream_bench import SHAPES, timeit  # noqa: E402
 
-VARIANTS = [(1, 256, 1), (1, 256, 2), (2, 128, 1), (2, 128, 2), (2, 256, 1), (2, 256, 2), (4, 128, 1), (4, 128, 2)]
+VARIANTS = [(1, 256, 1), (1, 256, 2), (2, 256, 1), (2, 256, 2), (3, 256, 1), (4, 128, 1), (4, 128, 2)]
 
 
 def main():

@@ -200,6 +200,9 @@ class LLMEngine:
         self.requests: dict[str, Sequence] = {}
         self.stats = {"steps": 0, "prompt_tokens": 0, "cached_tokens": 0, "output_tokens": 0, "step_time": 0.0,
                       "replans": 0, "planned_ahead": 0, "planned_late": 0}
+        # host seconds per activity (plan: schedule + build_host, launch: enqueue a step, wait: blocked on a step's
+        # tokens, finish: bookkeeping of landed tokens) — the bench reports them per step
+        self.host_s = {"plan": 0.0, "launch": 0.0, "wait": 0.0, "finish": 0.0}
         self._inflight: _InFlight | None = None  # the step on the GPU that has not been collected yet
         self.step_ms: deque = deque(maxlen=512)  # intervals between consecutive step completions (busy periods)
         self._t_done = 0.0
@@ -296,19 +299,23 @@ class LLMEngine:
             self.fi.on_step()
         cut: list[StepOutput] = []
         if self._inflight is None:
+            t_p = time.perf_counter()
             with trace.span("schedule"):
                 batch = self.sched.schedule()
                 cut = self._cut_outputs(batch)
                 if batch.empty:
                     return cut
                 host, sampled = self.runner.build_host(batch)
+            self.host_s["plan"] += time.perf_counter() - t_p
             self._inflight = self._launch(batch, host, sampled, None)
         cur = self._inflight
         self._inflight = None
         plan = None
         if self.cfg.async_scheduling:
+            t_p = time.perf_counter()
             with trace.span("plan_ahead"):
                 plan = self._speculate()
+            self.host_s["plan"] += time.perf_counter() - t_p
         if plan is not None and not self._needs_landed(plan.sampled):
             self.stats["planned_ahead"] += 1
             self._inflight = self._launch(plan.batch, plan.host, plan.sampled, cur)
@@ -381,6 +388,7 @@ class LLMEngine:
         t0 = time.perf_counter()
         with trace.span("launch", B=host.B, T=host.T):
             launched = self.runner.launch(host, sampled, prev.launched if prev is not None else None)
+        self.host_s["launch"] += time.perf_counter() - t0
         # advance computed counts + register completed pages in the prefix tree (the step's KV writes are ordered
         # before any later reader on the stream); the sampled tokens are pending until the step lands
         for s in batch.decode:
@@ -399,9 +407,11 @@ class LLMEngine:
         return _InFlight(sampled, slots, launched, t0)
 
     def _finish_step(self, cur: "_InFlight") -> list[StepOutput]:
+        t_w = time.perf_counter()
         with trace.span("collect"):
             toks = self.runner.collect(cur.launched)
         now = time.perf_counter()
+        self.host_s["wait"] += now - t_w
         if now - self._t_done < 1.0:  # back-to-back steps: the interval is this GPU's step time
             self.step_ms.append((now - self._t_done) * 1e3)
         self._t_done = now
@@ -439,6 +449,7 @@ class LLMEngine:
                 trace.request_span(s, now)
             outs.append(StepOutput(s.request_id, [t], reason is not None, reason, len(s.prompt_ids), n_out,
                                    s.num_cached))
+        self.host_s["finish"] += time.perf_counter() - now
         return outs
 
     def _cut_outputs(self, batch) -> list[StepOutput]:
