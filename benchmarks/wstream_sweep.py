@@ -15,13 +15,16 @@ from kafka_llm_service_amd.ops import _ext
 
 from wstream_bench import SHAPES, timeit  # noqa: E402
 
-VARIANTS = [(1, 256, 1), (1, 256, 2), (2, 256, 1), (2, 256, 2), (3, 256, 1), (4, 128, 1), (4, 128, 2)]
+# (MT, KC, KW, PIN): PIN = weight prefetch pinned ahead of the MFMAs (wstream_gemm_kernel)
+VARIANTS = [(mt, kc, kw, pin) for mt, kc, kw in ((1, 256, 1), (1, 256, 2), (2, 256, 1), (2, 256, 2), (3, 256, 1),
+                                               (4, 128, 1), (4, 128, 2)) for pin in (0, 1)]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", default="16,64,128")
     ap.add_argument("--shapes", default="8b.qkv,8b.o,8b.gate_up,8b.down,8b.lm_head")
+    ap.add_argument("--variants", default="", help="MT:KC:KW:PIN,... (default: all)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     ext = _ext.load()
@@ -33,7 +36,9 @@ def main():
         for M in [int(m) for m in args.M.split(",")]:
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             ref = x.float() @ ops.untile_weight(wts[0]).float().t()
-            for mt, kc, kw in VARIANTS:
+            variants = ([tuple(int(v) for v in x.split(":")) for x in args.variants.split(",")] if args.variants
+                        else VARIANTS)
+            for mt, kc, kw, pin in variants:
                 if M > 32 * mt:
                     continue
                 for s in (1, 2, 4, 8):
@@ -42,8 +47,8 @@ def main():
                     y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
                     p = torch.empty(s, M, N, device=dev) if s > 1 else None
 
-                    def run(wt, y=y, p=p, mt=mt, kc=kc, s=s, kw=kw):
-                        ext.wstream_gemm_cfg(x, wt, y if s == 1 else None, p, mt, kc, s, True, kw)
+                    def run(wt, y=y, p=p, mt=mt, kc=kc, s=s, kw=kw, pin=pin):
+                        ext.wstream_gemm_cfg(x, wt, y if s == 1 else None, p, mt, kc, s, True, kw, pin)
 
                     t = timeit([lambda wt=wt: run(wt) for wt in wts])
                     t_red = timeit([lambda: ext.slab_reduce(p, y)]) if s > 1 else 0.0
@@ -51,7 +56,8 @@ def main():
                     if s > 1:
                         ext.slab_reduce(p, y)
                     err = (y.float() - ref).abs().max().item()
-                    print(json.dumps({"shape": name, "M": M, "mt": mt, "kc": kc, "kw": kw, "S": s, "us": round(t, 1),
+                    print(json.dumps({"shape": name, "M": M, "mt": mt, "kc": kc, "kw": kw, "pin": pin, "S": s,
+                                      "us": round(t, 1),
                                       "TB/s": round(nbytes / t / 1e6, 2), "reduce_us": round(t_red, 1), "err": round(err, 4),
                                       "grid": ((N + 127) // 128) * s}), flush=True)
         del wts

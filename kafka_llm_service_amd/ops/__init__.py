@@ -247,7 +247,7 @@ def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, 
     if K % kc or K <= 0:
         return None
     nx, chunks, s = (N + 127) // 128 * ((M + 32 * mt - 1) // (32 * mt)), K // kc, 1
-    target = 256 if mt == 4 else 192
+    target = 192
     while s * 2 <= max_splits and s * 2 <= 8 and chunks % (s * 2) == 0 and nx * s < target:
         s *= 2
     return mt, kc, s

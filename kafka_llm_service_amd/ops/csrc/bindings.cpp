@@ -43,7 +43,7 @@ hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride,
                          int64_t mask_ld, int* counts, int64_t cnt_ld, hipStream_t st);
 int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits);
 hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt, int kc,
-                                     int splits, int nt, int kw, int glu, bf16* Y, int64_t ldy, float* P,
+                                     int splits, int nt, int kw, int pin, int glu, bf16* Y, int64_t ldy, float* P,
                                      hipStream_t st);
 hipError_t kafka_launch_slab_reduce(const float* P, int S, int M, int N, bf16* Y, int64_t ldy, hipStream_t st);
 hipError_t kafka_launch_wstream_grouped(const bf16* X, int64_t ldx, const bf16* Wt, int e_local, int N, int K,
@@ -457,7 +457,13 @@ static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> 
   // with its fused SwiGLU, down) ran 1.6-2.8 % faster in the config sweep, the short ones (qkv, o) slower; headline
   // +0.24 % (3 / 3 interleaved pairs, profiles/r04/bench_ab_wstream_kw2.jsonl)
   const int kw = mt == 2 && kc == 256 && K / s / kc >= 6 ? 2 : 1;
-  CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, nt ? 1 : 0, kw, glu ? 1 : 0,
+  // weight prefetch pinned ahead of the MFMAs (wstream_gemm_kernel PIN) when a split streams >= 3 chunks: -1..-4 us
+  // per projection at 64 rows, -4..-7 us at 97..128 rows; not for 96-row tiles (their 348 registers leave one wave
+  // per SIMD and the longer live ranges lose) nor 2-chunk splits (o at 64 rows: +0.9 us)
+  // (profiles/r05/wstream_sweep_pin.jsonl)
+  const int pin = mt != 3 && K / s / kc >= 3 ? 1 : 0;
+  CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, nt ? 1 : 0, kw, pin,
+                                      glu ? 1 : 0,
                                       yp, ldy, pp, cur_stream()));
 }
 
@@ -499,7 +505,7 @@ static void skinny_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y
 
 // explicit-configuration variant (microbenchmark sweeps): (mt, kc, splits) as given, no planning
 static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y, c10::optional<at::Tensor> p,
-                             int64_t mt, int64_t kc, int64_t s, bool nt, int64_t kw) {
+                             int64_t mt, int64_t kc, int64_t s, bool nt, int64_t kw, int64_t pin) {
   CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0 && wt.dim() == 4 && wt.is_contiguous(), "wstream_gemm_cfg: x/wt");
   const int M = x.size(0), K = x.size(1), N = wt.size(0) * 32;
@@ -512,7 +518,7 @@ static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tens
     CHECK_DT(p.value(), at::kFloat);
   }
   CHECK_HIP(kafka_launch_wstream_gemm(bptr(x), x.stride(0), bptr(wt), M, N, K, (int)mt, (int)kc, (int)s, nt ? 1 : 0,
-                                      (int)kw, 0,
+                                      (int)kw, (int)pin, 0,
                                       s == 1 ? bptr(y.value()) : nullptr, s == 1 ? y->stride(0) : 0,
                                       s == 1 ? nullptr : p->data_ptr<float>(), cur_stream()));
 }

@@ -27,7 +27,7 @@
 
 namespace kafka {
 
-template <int MT, int KC, bool NT, int KW>
+template <int MT, int KC, bool NT, int KW, bool PIN>
 __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                                  const bf16x8* __restrict__ Wt, int M, int N, int K,
                                                                  int ks, bf16* __restrict__ Y, int64_t ldy,
@@ -95,6 +95,10 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
       const bf16x8* p = wp + (int64_t)(ch * KSTEP + t) * 64;
       wv[t] = NT ? __builtin_nontemporal_load(p) : *p;
     }
+    // PIN keeps the prefetch where it is issued: left alone, the machine scheduler sinks these loads (and the X
+    // loads before them) below the MFMAs of the current chunk (shorter register live ranges), which leaves the next
+    // chunk a prefetch distance of ~0, so every chunk waits out the full HBM latency
+    if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
   };
   f32x16 acc[MT];
 #pragma unroll
@@ -390,11 +394,13 @@ extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, 
   if (K % KC != 0 || K <= 0) return 2;
   const int nx = (N + 127) / 128 * ((M + 32 * MT - 1) / (32 * MT));  // workgroups per split (x row tiles)
   const int chunks = K / KC;
-  // split until the grid reaches ~192 (MT <= 3) / 256 (MT = 4) workgroups: measured on MI355X
-  // (benchmarks/wstream_sweep.py, profiles/wstream_sweep_r01.log; split targets 96..384 re-checked in
-  // profiles/r04/bench_ab_split_target_*.jsonl) — every extra split adds 2 x M x N x 4 B of slab traffic, so e.g.
-  // gate_up (N = 28672) at M = 64 runs fastest unsplit and qkv (N = 6144) with S = 4
-  const int target = MT == 4 ? 256 : 192;
+  // split until the grid reaches ~192 workgroups: measured on MI355X (benchmarks/wstream_sweep.py,
+  // profiles/wstream_sweep_r01.log; split targets 96..384 re-checked in profiles/r04/bench_ab_split_target_*.jsonl)
+  // — every extra split adds 2 x M x N x 4 B of slab traffic, so e.g. gate_up (N = 28672) at M = 64 runs fastest
+  // unsplit and qkv (N = 6144) with S = 4. With the pinned prefetch, gate_up at 97..128 rows also runs fastest
+  // unsplit (53.3 us at 114 rows with its fused SwiGLU vs 60.4 + a SwiGLU pass split in two;
+  // profiles/r05/wstream_sweep_pin.jsonl), so MT = 4 shares the target (it was 256).
+  const int target = 192;
   int s = 1;
   while (s * 2 <= max_splits && s * 2 <= 8 && chunks % (s * 2) == 0 && nx * s < target) s *= 2;
   *mt = MT;
@@ -404,7 +410,7 @@ extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, 
 }
 
 extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K,
-                                               int mt, int kc, int splits, int nt, int kw, int glu, bf16* Y,
+                                               int mt, int kc, int splits, int nt, int kw, int pin, int glu, bf16* Y,
                                                int64_t ldy, float* P, hipStream_t st) {
   if (M < 1) return hipSuccess;
   if (glu && (N % 64 != 0 || kw > 2)) return hipErrorInvalidValue;  // (the SwiGLU epilogue runs after the KW fold)
@@ -416,21 +422,31 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   const int ks = K / splits;
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   float* p = splits > 1 ? P : nullptr;
-#define KAFKA_WS(MT_, KC_, KW_)                                                                                  \
+#define KAFKA_WS(MT_, KC_, KW_, PIN_)                                                                            \
   do {                                                                                                          \
     if (nt)                                                                                                     \
-      wstream_gemm_kernel<MT_, KC_, true, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, rt); \
+      wstream_gemm_kernel<MT_, KC_, true, KW_, PIN_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, \
+                                                                              glu, rt);                         \
     else                                                                                                        \
-      wstream_gemm_kernel<MT_, KC_, false, KW_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, glu, rt); \
+      wstream_gemm_kernel<MT_, KC_, false, KW_, PIN_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, \
+                                                                               glu, rt);                        \
   } while (0)
-  if (mt == 1 && kc == 256 && kw == 1) KAFKA_WS(1, 256, 1);
-  else if (mt == 1 && kc == 256 && kw == 2) KAFKA_WS(1, 256, 2);
-  else if (mt == 2 && kc == 256 && kw == 1) KAFKA_WS(2, 256, 1);
-  else if (mt == 2 && kc == 256 && kw == 2) KAFKA_WS(2, 256, 2);
-  else if (mt == 3 && kc == 256 && kw == 1) KAFKA_WS(3, 256, 1);
-  else if (mt == 4 && kc == 128 && kw == 1) KAFKA_WS(4, 128, 1);
-  else if (mt == 4 && kc == 128 && kw == 2) KAFKA_WS(4, 128, 2);
+#define KAFKA_WS_IF(MT_, KC_, KW_)                                      \
+  if (mt == MT_ && kc == KC_ && kw == KW_) {                           \
+    if (pin)                                                           \
+      KAFKA_WS(MT_, KC_, KW_, true);                                   \
+    else                                                               \
+      KAFKA_WS(MT_, KC_, KW_, false);                                  \
+  }
+  KAFKA_WS_IF(1, 256, 1)
+  else KAFKA_WS_IF(1, 256, 2)
+  else KAFKA_WS_IF(2, 256, 1)
+  else KAFKA_WS_IF(2, 256, 2)
+  else KAFKA_WS_IF(3, 256, 1)
+  else KAFKA_WS_IF(4, 128, 1)
+  else KAFKA_WS_IF(4, 128, 2)
   else return hipErrorInvalidValue;
+#undef KAFKA_WS_IF
 #undef KAFKA_WS
   return hipGetLastError();
 }

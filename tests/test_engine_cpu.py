@@ -259,6 +259,7 @@ def test_stream_plan_rules(monkeypatch):
     assert [ops.stream_plan(M, 28672, 4096)[0] for M in (1, 32, 33, 64, 65, 96, 97, 128)] == [1, 1, 2, 2, 3, 3, 4, 4]
     assert ops.stream_plan(128, 4096, 4096)[1] == 128 and ops.stream_plan(64, 4096, 4096)[1] == 256
     assert ops.stream_plan(64, 28672, 4096)[2] == 1 and ops.stream_plan(64, 6144, 4096)[2] == 4
+    assert ops.stream_plan(114, 28672, 4096)[2] == 1  # gate_up unsplit at 97..128 rows (fused SwiGLU)
     assert ops.stream_plan(300, 4096, 4096) is None and ops.stream_plan(64, 4100, 4096) is None
 
 
