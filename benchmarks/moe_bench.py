@@ -61,6 +61,11 @@ def main():
 
         us = timeit(layer)
         us_s = timeit(layer_stream) if T <= 512 else None
+        us_u = None
+        if us_s:  # the grouped streaming kernel without the pinned prefetch (A/B of ops.GROUPED_PIN)
+            ops.GROUPED_PIN = False
+            us_u = timeit(layer_stream)
+            ops.GROUPED_PIN = True
         r = ops.moe_route(torch.nn.functional.linear(x, router), K)
         used = int((r.expert_off[1:] - r.expert_off[:-1] > 0).sum().item())
         bytes_w = used * (2 * F * d + d * F) * 2
@@ -68,7 +73,8 @@ def main():
                           "weight_TB/s": round(bytes_w / us / 1e6, 2),
                           "TFLOP/s": round(2 * T * K * 3 * F * d / us / 1e6, 1),
                           "stream_us_per_layer": round(us_s, 1) if us_s else None,
-                          "stream_weight_TB/s": round(bytes_w / us_s / 1e6, 2) if us_s else None}), flush=True)
+                          "stream_weight_TB/s": round(bytes_w / us_s / 1e6, 2) if us_s else None,
+                          "stream_unpinned_us_per_layer": round(us_u, 1) if us_u else None}), flush=True)
 
 
 if __name__ == "__main__":

@@ -348,6 +348,11 @@ def stream_moe_supported(N: int, K: int) -> bool:
     return N % 64 == 0 and K % 256 == 0
 
 
+# weight prefetch of the grouped streaming kernel pinned ahead of its MFMAs (as the dense one; toggled by
+# benchmarks/moe_bench.py for its A/B)
+GROUPED_PIN = True
+
+
 def grouped_stream_glu(x: torch.Tensor, wt: torch.Tensor, r: "MoERouting", e_lo: int = 0) -> torch.Tensor:
     """silu(gate) * up for every routed (token, local expert) entry, rows in expert-sorted order [n_ent, F]: the
     weight-streaming grouped kernel on GLU-tiled expert weights (``tile_experts(w13, glu=True)``)."""
@@ -356,7 +361,8 @@ def grouped_stream_glu(x: torch.Tensor, wt: torch.Tensor, r: "MoERouting", e_lo:
     F = wt.shape[1] * 16
     y = torch.empty(n_ent, F, dtype=x.dtype, device=x.device)
     if _gpu(x):
-        ext().wstream_grouped(x, wt, r.perm_tok, r.perm_w, r.expert_off, int(e_lo), int(T), True, y, None)
+        ext().wstream_grouped(x, wt, r.perm_tok, r.perm_w, r.expert_off, int(e_lo), int(T), True, y, None,
+                              GROUPED_PIN)
         return y
     h = ref_grouped(x, untile_experts(wt, glu=True), r, e_lo, gather=True)
     y.copy_(ref.silu_mul(h))
@@ -367,7 +373,8 @@ def grouped_stream_combine(a: torch.Tensor, wt: torch.Tensor, r: "MoERouting", T
                            e_lo: int = 0) -> torch.Tensor:
     """out[token] += w * (a[entry] @ W_e^T) over the local experts' entries (out f32 [T, N], zeroed by the caller)."""
     if _gpu(a):
-        ext().wstream_grouped(a, wt, r.perm_tok, r.perm_w, r.expert_off, int(e_lo), int(T), False, None, out)
+        ext().wstream_grouped(a, wt, r.perm_tok, r.perm_w, r.expert_off, int(e_lo), int(T), False, None, out,
+                              GROUPED_PIN)
         return out
     ref.grouped_gemm(a, untile_experts(wt), r.perm_tok, r.perm_w, r.expert_off, e_lo, False, None, out)
     return out

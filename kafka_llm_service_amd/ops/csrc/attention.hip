@@ -589,8 +589,18 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
     const float* pp = out_part + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
     int s0 = 0;
-    if (pre_bf16 != nullptr) {  // the cascade's bf16 prefix partials
+    if (pre_bf16 != nullptr) {  // the cascade's bf16 prefix partials, MG loads per round trip (as the one-piece path)
       const bf16* pb = pre_bf16 + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
+      for (; s0 + MG <= split_offset; s0 += MG) {
+        bf16x4 v[MG];
+#pragma unroll
+        for (int j = 0; j < MG; ++j) v[j] = *reinterpret_cast<const bf16x4*>(pb + (s0 + j) * D);
+#pragma unroll
+        for (int j = 0; j < MG; ++j) {
+          const float wj = sW[g][s0 + j];
+          acc4 += f32x4{(float)v[j][0], (float)v[j][1], (float)v[j][2], (float)v[j][3]} * wj;
+        }
+      }
       for (; s0 < split_offset; ++s0) {
         const bf16x4 v = *reinterpret_cast<const bf16x4*>(pb + s0 * D);
         acc4 += f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]} * sW[g][s0];

@@ -49,7 +49,7 @@ hipError_t kafka_launch_slab_reduce(const float* P, int S, int M, int N, bf16* Y
 hipError_t kafka_launch_wstream_grouped(const bf16* X, int64_t ldx, const bf16* Wt, int e_local, int N, int K,
                                         const int* perm_tok, const float* perm_w, const int* expert_off, int e_lo,
                                         int max_rows, int gather, bf16* Y, int64_t ldy, float* out, int64_t ldo,
-                                        hipStream_t st);
+                                        int pin, hipStream_t st);
 hipError_t kafka_launch_moe_route(const bf16* logits, int64_t ld, int T, int E, int K, int BM, float* topk_w,
                                   int* topk_e, int* perm_tok, float* perm_w, int* expert_off, int* tile_off,
                                   hipStream_t st);
@@ -528,7 +528,7 @@ static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tens
 // bounds every expert segment (a token picks an expert at most once).
 static void wstream_grouped(at::Tensor x, at::Tensor wt, at::Tensor perm_tok, at::Tensor perm_w, at::Tensor expert_off,
                             int64_t e_lo, int64_t max_rows, bool gather, c10::optional<at::Tensor> y,
-                            c10::optional<at::Tensor> out) {
+                            c10::optional<at::Tensor> out, bool pin) {
   CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
   CHECK_DT(perm_tok, at::kInt); CHECK_DT(perm_w, at::kFloat); CHECK_DT(expert_off, at::kInt);
   TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0, "wstream_grouped: x must be [rows, K] with 16-B rows");
@@ -561,7 +561,8 @@ static void wstream_grouped(at::Tensor x, at::Tensor wt, at::Tensor perm_tok, at
   }
   CHECK_HIP(kafka_launch_wstream_grouped(bptr(x), x.stride(0), bptr(wt), E_local, N, K, perm_tok.data_ptr<int>(),
                                          perm_w.data_ptr<float>(), expert_off.data_ptr<int>(), (int)e_lo,
-                                         (int)max_rows, gather ? 1 : 0, yp, ldy, op, ldo, cur_stream()));
+                                         (int)max_rows, gather ? 1 : 0, yp, ldy, op, ldo, pin ? 1 : 0,
+                                         cur_stream()));
 }
 
 // y [M, N] bf16 = sum over the slabs p [S, M, N]
@@ -837,7 +838,9 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("skinny_gemm", &skinny_gemm);
   m.def("wstream_gemm_cfg", &wstream_gemm_cfg);
   m.def("slab_reduce", &slab_reduce);
-  m.def("wstream_grouped", &wstream_grouped);
+  m.def("wstream_grouped", &wstream_grouped, py::arg("x"), py::arg("wt"), py::arg("perm_tok"), py::arg("perm_w"),
+        py::arg("expert_off"), py::arg("e_lo"), py::arg("max_rows"), py::arg("gather"), py::arg("y"), py::arg("out"),
+        py::arg("pin") = true);
   m.def("moe_route", &moe_route);
   m.def("cu_mask_stream", &cu_mask_stream);
   m.def("stream_cu_mask", &stream_cu_mask);

@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
 //   GATHER: A row = X[perm_tok[entry]] (token activations), else X[entry] (expert-sorted intermediate).
 //   Epilogue GLU (GLU-interleaved tiles): Y[entry, :N/2] = silu(gate) * up, bf16 — the SwiGLU of the expert MLP.
 //   Epilogue COMBINE: out_f32[perm_tok[entry], n] += perm_w[entry] * y (a token gets exactly k contributions).
-template <int MT, int KC, bool GATHER, bool COMBINE>
+template <int MT, int KC, bool GATHER, bool COMBINE, bool PIN>
 __global__ __launch_bounds__(256) void wstream_grouped_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                                const bf16x8* __restrict__ Wt, int N, int K,
                                                                const int* __restrict__ perm_tok,
@@ -275,6 +275,7 @@ __global__ __launch_bounds__(256) void wstream_grouped_kernel(const bf16* __rest
   auto load_w = [&](bf16x8(&wv)[KSTEP], int ch) {
 #pragma unroll
     for (int t = 0; t < KSTEP; ++t) wv[t] = __builtin_nontemporal_load(wp + (int64_t)(ch * KSTEP + t) * 64);
+    if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);  // (prefetch kept ahead of the MFMAs, as wstream_gemm)
   };
   const int mt_used = (rows + 31) >> 5;  // row tiles with live rows (uniform)
   f32x16 acc[MT];
@@ -469,15 +470,22 @@ namespace kafka {
 extern "C" hipError_t kafka_launch_wstream_grouped(const bf16* X, int64_t ldx, const bf16* Wt, int e_local, int N,
                                                   int K, const int* perm_tok, const float* perm_w,
                                                   const int* expert_off, int e_lo, int max_rows, int gather,
-                                                  bf16* Y, int64_t ldy, float* out, int64_t ldo, hipStream_t st) {
+                                                  bf16* Y, int64_t ldy, float* out, int64_t ldo, int pin,
+                                                  hipStream_t st) {
   if (max_rows < 1 || e_local < 1) return hipSuccess;
   if (N % 64 != 0 || K % 256 != 0 || (out == nullptr) == (Y == nullptr)) return hipErrorInvalidValue;
   const int MT = max_rows <= 32 ? 1 : 2;
   const dim3 grid((N + 127) / 128, e_local, (max_rows + 32 * MT - 1) / (32 * MT));
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
-#define KAFKA_WG(MT_, G_, C_)                                                                              \
-  wstream_grouped_kernel<MT_, 256, G_, C_><<<grid, 256, 0, st>>>(X, ldx, wt, N, K, perm_tok, perm_w, expert_off, \
-                                                                 e_lo, Y, ldy, out, ldo)
+#define KAFKA_WG(MT_, G_, C_)                                                                                   \
+  do {                                                                                                         \
+    if (pin)                                                                                                   \
+      wstream_grouped_kernel<MT_, 256, G_, C_, true><<<grid, 256, 0, st>>>(X, ldx, wt, N, K, perm_tok, perm_w,      \
+                                                                           expert_off, e_lo, Y, ldy, out, ldo);  \
+    else                                                                                                       \
+      wstream_grouped_kernel<MT_, 256, G_, C_, false><<<grid, 256, 0, st>>>(X, ldx, wt, N, K, perm_tok, perm_w,     \
+                                                                            expert_off, e_lo, Y, ldy, out, ldo); \
+  } while (0)
   const bool comb = out != nullptr;
   if (MT == 1) {
     if (gather) { if (comb) KAFKA_WG(1, true, true); else KAFKA_WG(1, true, false); }

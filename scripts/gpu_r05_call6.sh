@@ -1,0 +1,8 @@
+#!/bin/bash
+# cascade / decode launches alone and in sequence (after batching the ticket merge's prefix loads), decode tests
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export KAFKA_NO_BUILD=1 TMPDIR=/tmp PYTHONPATH=$GRAFT_REPO_ROOT; mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_kernels_gpu.py -k "decode or cascade" > gpurun_out/call6_tests.log 2>&1 || { tail -30 gpurun_out/call6_tests.log; exit 1; }
+tail -1 gpurun_out/call6_tests.log
+timeout -k 10 300 python benchmarks/cascade_overlap_bench.py > gpurun_out/cascade_overlap2.jsonl 2>&1 || { tail -20 gpurun_out/cascade_overlap2.jsonl; exit 1; }
+grep mode gpurun_out/cascade_overlap2.jsonl
