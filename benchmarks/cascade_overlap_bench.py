@@ -3,7 +3,9 @@
 18k shared prefix, per-row suffixes of ~1.3k-4k keys), run three ways:
 
   seq       the engine's order today: prefix pass (bf16 partials) -> decode kernel (suffix + fused ticket merge)
+  seq_fp32  as seq with fp32 prefix partials (the fused merge reads them as 16-B loads)
   seqsplit  prefix pass (fp32 partials) -> decode kernel (suffix partials only) -> attn_merge
+  seqsplit_bf16  as seqsplit with the prefix partials in bf16 (attn_merge reads slots < npre from them)
   conc      prefix pass on a second stream CONCURRENT with the decode kernel (suffix partials), then attn_merge
   cascade / decode_fused / decode_part / merge   each launch of the above alone (inputs left by a previous run)
 
@@ -71,7 +73,8 @@ def main():
     part = torch.empty(B, Hq, S, D, device=dev)
     lse = torch.full((B, Hq, S), float("-inf"), device=dev)
     pre = torch.empty(B, Hq, S, D, device=dev, dtype=torch.bfloat16)
-    outs = {m: torch.empty(B, Hq, D, device=dev, dtype=torch.bfloat16) for m in ("seq", "seqsplit", "conc")}
+    outs = {m: torch.empty(B, Hq, D, device=dev, dtype=torch.bfloat16) for m in ("seq", "seq_fp32", "seqsplit", "seqsplit_bf16",
+                                                                                   "conc")}
     side = torch.cuda.Stream(dev)
     main_s = torch.cuda.current_stream(dev)
 
@@ -84,10 +87,19 @@ def main():
         if mode == "seq":
             cascade(i, pre)
             ops.attn_decode_items(q, kc, vc, btd, dit, part, lse, scale, out=outs[mode], pre_part=pre)
+        elif mode == "seq_fp32":
+            cascade(i, part)
+            ops.attn_decode_items(q, kc, vc, btd, dit, part, lse, scale, out=outs[mode])
         elif mode == "seqsplit":
             cascade(i, part)
             ops.attn_decode_items(q, kc, vc, btd, dit, part, lse, scale)
             ops.attn_merge(part, lse, outs[mode])
+        elif mode == "seqsplit_bf16":
+            cascade(i, pre)
+            ops.attn_decode_items(q, kc, vc, btd, dit, part, lse, scale)
+            ops.attn_merge(part, lse, outs[mode], pre=pre, npre=npre)
+        elif mode == "merge_bf16":
+            ops.attn_merge(part, lse, outs["seqsplit_bf16"], pre=pre, npre=npre)
         elif mode == "cascade":
             cascade(i, pre)
         elif mode == "decode_fused":
@@ -104,7 +116,8 @@ def main():
             main_s.wait_stream(side)
             ops.attn_merge(part, lse, outs[mode])
 
-    for mode in ("seq", "seqsplit", "conc", "cascade", "decode_fused", "decode_part", "merge"):
+    for mode in ("seq", "seq_fp32", "seqsplit", "seqsplit_bf16", "conc", "cascade", "decode_fused", "decode_part", "merge",
+                 "merge_bf16"):
         res = []
         for _ in range(5):
             run(mode, 0)
@@ -118,7 +131,8 @@ def main():
             res.append(s.elapsed_time(e) * 1e3 / args.iters)
         run(mode, 0)
         torch.cuda.synchronize()
-        err = (outs[mode].float() - outs["seq"].float()).abs().max().item() if mode in ("seqsplit", "conc") else 0.0
+        err = (outs[mode].float() - outs["seq"].float()).abs().max().item() if mode in ("seq_fp32", "seqsplit", "seqsplit_bf16", "conc") \
+            else 0.0
         print(json.dumps({"mode": mode, "us": round(statistics.median(res), 1), "S": S, "prefix_items": npre,
                           "decode_items": int(ditems.shape[0]), "err_vs_seq": round(err, 4)}), flush=True)
 

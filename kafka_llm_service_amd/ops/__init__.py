@@ -172,11 +172,13 @@ def tile_rows(variant: int = 0) -> int:
     return 256 if variant in (0, 3) else 128
 
 
-def attn_merge(part, lse, out, lse_out=None) -> None:
+def attn_merge(part, lse, out, lse_out=None, pre=None, npre: int = 0) -> None:
+    """Log-sum-exp merge of the S partials per (row, head) of part f32 [rows, Hq, S, D] -> out bf16; with ``pre``
+    (bf16, part's shape) slots [0, npre) are read from it (the cascade's prefix partials)."""
     if _gpu(part):
-        ext().attn_merge(part, lse, out, lse_out)
+        ext().attn_merge(part, lse, out, lse_out, pre, int(npre))
     else:
-        ref.attn_merge(part, lse, out, lse_out)
+        ref.attn_merge(part, lse, out, lse_out, pre, npre)
 
 
 _SAMPLE_WS: dict = {}

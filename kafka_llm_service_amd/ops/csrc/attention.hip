@@ -1066,10 +1066,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_prefill_kernel(const Att
 // Merge S partials: grid (rows, ceil(Hq / 8)), 256 threads = 8 heads x 32 lanes x float4 columns. Each lane
 // recomputes its head's max / sum over the S lse values (L1-resident broadcast reads), then accumulates its 4 columns.
 constexpr int MERGE_MAX_S = 256;
+// pre (optional): slots [0, npre) are read from this bf16 buffer of part's layout instead (the cascade's prefix
+// partials, tile v3 part_bf16)
 template <int D>
 __global__ __launch_bounds__(256) void attn_merge_kernel(const float* __restrict__ part, const float* __restrict__ lse,
                                                           int S, bf16* __restrict__ out, int64_t out_stride, int Hq,
-                                                          float* __restrict__ lse_out) {
+                                                          float* __restrict__ lse_out, const bf16* __restrict__ pre,
+                                                          int npre) {
   static_assert(D == 128, "merge maps 32 lanes x float4 onto one head");
   const int64_t row = blockIdx.x;
   const int hh = blockIdx.y * 8 + (threadIdx.x >> 5);
@@ -1086,6 +1089,24 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(const float* __restrict
     // a slot with lse = -inf (a row with fewer pieces than S) has weight 0 and was never written: select it away
     // instead of multiplying (0 x a stale NaN is NaN)
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    if (pre != nullptr) {
+      const bf16* pb = pre + ((row * Hq + hh) * S) * D + c;
+      auto pre_at = [&](int s2, float w) {
+        const bf16x4 v = *reinterpret_cast<const bf16x4*>(pb + s2 * D);
+        return w > 0.f ? f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]} * w : z;
+      };
+      for (; s + 4 <= npre; s += 4) {
+        const float w0 = exp2f(l[s] - M), w1 = exp2f(l[s + 1] - M), w2 = exp2f(l[s + 2] - M),
+                    w3 = exp2f(l[s + 3] - M);
+        acc += pre_at(s, w0) + pre_at(s + 1, w1) + pre_at(s + 2, w2) + pre_at(s + 3, w3);
+        L += (w0 + w1) + (w2 + w3);
+      }
+      for (; s < npre; ++s) {
+        const float w0 = exp2f(l[s] - M);
+        acc += pre_at(s, w0);
+        L += w0;
+      }
+    }
     auto part_at = [&](int s2, float w) {
       const f32x4 a = *reinterpret_cast<const f32x4*>(p + s2 * D);
       return w > 0.f ? a * w : z;
@@ -1189,10 +1210,11 @@ extern "C" hipError_t kafka_launch_attn_prefill(const void* items, int n_items, 
 }
 
 extern "C" hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows, int Hq, int S, int D, bf16* out,
-                             int64_t out_stride, float* lse_out, hipStream_t st) {
+                             int64_t out_stride, float* lse_out, const bf16* pre, int npre, hipStream_t st) {
   if (rows == 0) return hipSuccess;
-  if (D != 128 || S > MERGE_MAX_S) return hipErrorInvalidValue;
-  attn_merge_kernel<128><<<dim3(rows, (Hq + 7) / 8), 256, 0, st>>>(part, lse, S, out, out_stride, Hq, lse_out);
+  if (D != 128 || S > MERGE_MAX_S || npre < 0 || npre > S) return hipErrorInvalidValue;
+  attn_merge_kernel<128><<<dim3(rows, (Hq + 7) / 8), 256, 0, st>>>(part, lse, S, out, out_stride, Hq, lse_out, pre,
+                                                                    pre != nullptr ? npre : 0);
   return hipGetLastError();
 }
 

@@ -36,7 +36,7 @@ hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16*
                                      int variant, int part_bf16, float* alt_part, float* alt_lse, int alt_S,
                                      int alt_tok_off, hipStream_t st);
 hipError_t kafka_launch_attn_merge(const float* part, const float* lse, int rows, int Hq, int S, int D, bf16* out,
-                             int64_t out_stride, float* lse_out, hipStream_t st);
+                                   int64_t out_stride, float* lse_out, const bf16* pre, int npre, hipStream_t st);
 hipError_t kafka_launch_sample(const void* logits, bool is_bf16, int64_t stride, int B, int V, const float* temperature,
                          const float* top_p, const int* top_k, const int64_t* seeds, const int64_t* step,
                          int64_t* out_tokens, int* ws, int nsplit, const int* proc, const uint32_t* mask_tab,
@@ -339,7 +339,8 @@ static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at:
                                        scale, (int)variant, part_bf16, ap, al, S2, (int)alt_tok_off, cur_stream()));
 }
 
-static void attn_merge(at::Tensor part, at::Tensor lse, at::Tensor out, c10::optional<at::Tensor> lse_out) {
+static void attn_merge(at::Tensor part, at::Tensor lse, at::Tensor out, c10::optional<at::Tensor> lse_out,
+                       c10::optional<at::Tensor> pre, int64_t npre) {
   CHECK_CUDA(part); CHECK_DT(part, at::kFloat); CHECK_DT(lse, at::kFloat); CHECK_DT(out, at::kBFloat16);
   TORCH_CHECK(part.is_contiguous() && part.dim() == 4 && part.size(3) == 128, "part must be [rows, Hq, S, 128]");
   const int rows = out.size(0), Hq = part.size(1), S = part.size(2);
@@ -352,8 +353,14 @@ static void attn_merge(at::Tensor part, at::Tensor lse, at::Tensor out, c10::opt
     TORCH_CHECK(lse_out->numel() >= (int64_t)rows * Hq, "lse_out");
     lo = lse_out->data_ptr<float>();
   }
+  const bf16* pp = nullptr;
+  if (pre.has_value()) {  // bf16 prefix partials in slots [0, npre), part's shape
+    CHECK_DT(pre.value(), at::kBFloat16);
+    TORCH_CHECK(pre->is_contiguous() && pre->sizes() == part.sizes() && npre >= 0 && npre <= S, "attn_merge: pre");
+    pp = bptr(pre.value());
+  }
   CHECK_HIP(kafka_launch_attn_merge(part.data_ptr<float>(), lse.data_ptr<float>(), rows, Hq, S, 128, bptr(out),
-                                     out.stride(0), lo, cur_stream()));
+                                     out.stride(0), lo, pp, (int)npre, cur_stream()));
 }
 
 static void sample(at::Tensor logits, c10::optional<at::Tensor> temperature, c10::optional<at::Tensor> top_p,
@@ -827,7 +834,8 @@ PYBIND11_MODULE(_kafka_ops, m) {
         py::arg("block_tables"), py::arg("q_limit"), py::arg("out"), py::arg("out_part"), py::arg("lse_part"),
         py::arg("scale"), py::arg("variant") = 0, py::arg("alt_part") = py::none(), py::arg("alt_lse") = py::none(),
         py::arg("alt_tok_off") = 0);
-  m.def("attn_merge", &attn_merge);
+  m.def("attn_merge", &attn_merge, py::arg("part"), py::arg("lse"), py::arg("out"), py::arg("lse_out") = py::none(),
+        py::arg("pre") = py::none(), py::arg("npre") = 0);
   m.def("sample", &sample, py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"),
         py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none(), py::arg("nsplit") = 1,
         py::arg("proc") = py::none(), py::arg("mask_tab") = py::none(), py::arg("counts") = py::none());

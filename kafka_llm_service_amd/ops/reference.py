@@ -289,9 +289,12 @@ def attn_prefill_items(items, q, k_cache, v_cache, block_tables, q_limit, scale,
             lse_part.view(out_part.shape[0], Hq, out_part.shape[2])[toks, :, split] = l2
 
 
-def attn_merge(part, lse, out, lse_out=None):
+def attn_merge(part, lse, out, lse_out=None, pre=None, npre=0):
     rows = out.shape[0]
-    p = part[:rows]
+    p = part[:rows].float()
+    if pre is not None and npre:  # bf16 prefix partials in slots [0, npre)
+        p = p.clone()
+        p[:, :, :npre] = pre[:rows, :, :npre].float()
     l = lse.view(part.shape[0], part.shape[1], part.shape[2])[:rows]
     M = l.amax(-1, keepdim=True)
     Mu = torch.where(torch.isinf(M), torch.zeros_like(M), M)

@@ -248,12 +248,31 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
         return await completion_json(msgs, req, None)
 
     async def agent_events(gen) -> AsyncGenerator[str, None]:
+        # the agent routes feed the same serving metrics as the chat route: TTFT at the first generated frame
+        # (content or a tool-call delta), end-to-end time, output tokens and TPOT from the run's summed usage
+        t0 = time.perf_counter()
+        t_first = None
+        n_out = 0
         try:
             async for ev in gen:
+                if t_first is None:
+                    ch = ev.get("choices")
+                    delta = (ch[0].get("delta") or {}) if ch else {}
+                    if delta.get("content") or delta.get("tool_calls"):
+                        t_first = time.perf_counter()
+                        M.TTFT.observe(t_first - t0)
+                if ev.get("type") == "agent_done":
+                    n_out = (ev.get("usage") or {}).get("completion_tokens", 0) or 0
                 yield f"data: {json.dumps(ev)}\n\n"  # json.dumps spacing, as the reference
         except Exception as e:
             log.exception("agent stream failed")
             yield f"data: {json.dumps({'error': {'message': str(e), 'type': 'agent_error'}})}\n\n"
+        t_end = time.perf_counter()
+        M.E2E.observe(t_end - t0)
+        if n_out:
+            M.OUTPUT_TOKENS.inc(n_out)
+            if n_out > 1 and t_first is not None:
+                M.TPOT.observe((t_end - t_first) / (n_out - 1))
         yield "data: [DONE]\n\n"
 
     @app.post("/v1/agent/run")

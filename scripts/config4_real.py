@@ -38,8 +38,8 @@ def main():
         metrics["text"] = c.get("/metrics").text
 
     with tempfile.TemporaryDirectory() as td:
-        text, frames, msgs = config4_flow.run(Path(td), args.model, {"max_model_len": args.max_model_len},
-                                              sections=None, on_done=grab)
+        text, frames, msgs = config4_flow.run(Path(td), args.model, {}, sections=None, on_done=grab,
+                                              max_model_len=args.max_model_len)
     (out / "metrics.txt").write_text(metrics.get("text", ""))
     wall = time.perf_counter() - t0
     (out / "agent_run_sse.txt").write_text(text)

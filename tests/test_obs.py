@@ -52,6 +52,34 @@ def test_metrics_histograms_exported():
     assert "kafka_tpot_seconds_bucket" in m and "kafka_output_tokens_total" in m
 
 
+def test_agent_run_feeds_serving_metrics():
+    """/v1/threads/{id}/agent/run observes TTFT / end-to-end time and counts its output tokens, as the chat route."""
+    import re
+
+    from fastapi.testclient import TestClient
+
+    from kafka_llm_service_amd.db.local import MemoryDBClient
+    from kafka_llm_service_amd.llm.stub import ScriptedProvider
+    from kafka_llm_service_amd.server.app import create_app
+    from kafka_llm_service_amd.server.state import ServerConfig, ServerState
+
+    def grab(m, name):
+        x = re.search(rf"^{name} ([0-9.e+]+)$", m, re.M)
+        return float(x.group(1)) if x else 0.0
+
+    llm = ScriptedProvider([{"text": "all done here"}])
+    st = ServerState(ServerConfig(backend="stub", sandbox="none"), llm_provider=llm, db=MemoryDBClient())
+    with TestClient(create_app(state=st)) as c:
+        m0 = c.get("/metrics").text
+        tid = c.post("/v1/threads").json()["thread_id"]
+        body = c.post(f"/v1/threads/{tid}/agent/run", json={"messages": [{"role": "user", "content": "hi"}]}).text
+        m1 = c.get("/metrics").text
+    assert body.rstrip().endswith("data: [DONE]")
+    assert grab(m1, "kafka_ttft_seconds_count") == grab(m0, "kafka_ttft_seconds_count") + 1
+    assert grab(m1, "kafka_request_seconds_count") == grab(m0, "kafka_request_seconds_count") + 1
+    assert grab(m1, "kafka_output_tokens_total") > grab(m0, "kafka_output_tokens_total")
+
+
 def test_json_logging_lines():
     import io
     import logging
