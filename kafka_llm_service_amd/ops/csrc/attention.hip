@@ -197,7 +197,7 @@ __device__ __forceinline__ void softmax_pv(f32x16& s, bool masked, int key0, int
   float psum = 0.f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const float p = exp2f(fmaf(s[i], scale_log2, -m_use));
+    const float p = fast_exp2(fmaf(s[i], scale_log2, -m_use));
     s[i] = p;
     psum += p;
   }

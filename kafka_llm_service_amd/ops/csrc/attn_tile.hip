@@ -111,7 +111,8 @@ __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __res
                                                            float scale_log2, int part_bf16, AltPart ap) {
   using namespace tile3;
   constexpr int RB = 1;                   // 32-row MFMA blocks per wave
-  constexpr int NSLOT = 3;                // ring slots (4 measured no faster)
+  constexpr int NSLOT = 3;                // ring slots (4: 30.9 vs 29.9 us per cascade launch,
+                                          // profiles/r05/cascade/cascade_nslot_*.jsonl)
   constexpr int NW = 8;                   // waves
   constexpr int DPT = 32 / NW;            // LDS-DMA instructions per wave per tile (16 K + 16 V pieces per tile)
   __shared__ __attribute__((aligned(16))) char smem[lds_bytes<NSLOT>()];
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __res
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float x = fmaf(s[rb][kb][i], scale_log2, -mu);
-          pf[i >> 3][i & 7] = (bf16)exp2f(x);
+          pf[i >> 3][i & 7] = (bf16)fast_exp2(x);
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {

@@ -113,6 +113,10 @@ __device__ __forceinline__ void load_in8(float (&v)[8], const bf16* __restrict__
   }
 }
 
+// 2^x as the single v_exp_f32: exp2f() adds a denormal range fix-up (compare, select, add, ldexp: 6 VALU ops per
+// value) that softmax does not need — its arguments are <= a small bound and results below 2^-126 may flush to 0.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
