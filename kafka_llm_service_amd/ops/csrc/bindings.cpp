@@ -516,7 +516,8 @@ static void wstream_gemm_cfg(at::Tensor x, at::Tensor wt, c10::optional<at::Tens
   CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0 && wt.dim() == 4 && wt.is_contiguous(), "wstream_gemm_cfg: x/wt");
   const int M = x.size(0), K = x.size(1), N = wt.size(0) * 32;
-  TORCH_CHECK(wt.size(1) * 16 == K && M >= 1 && M <= 32 * mt && K % (kc * s) == 0, "wstream_gemm_cfg: shape/config");
+  // (M beyond 32 * mt runs as row tiles of 32 * mt rows, as the planned path does above 128 rows)
+  TORCH_CHECK(wt.size(1) * 16 == K && M >= 1 && M <= 256 && K % (kc * s) == 0, "wstream_gemm_cfg: shape/config");
   if (s == 1) {
     TORCH_CHECK(y.has_value() && y->dim() == 2 && y->size(0) == M && y->size(1) == N, "wstream_gemm_cfg: y");
     CHECK_DT(y.value(), at::kBFloat16); CHECK_LASTDIM(y.value());
