@@ -11,12 +11,14 @@ run() {  # name dir
   tail -1 "gpurun_out/ab_$1.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); d['variant']='$1'; print(json.dumps(d))" >> gpurun_out/ab.jsonl
   tail -1 gpurun_out/ab.jsonl | cut -c1-160
 }
-# variants: new (this tree), old (ab_old/), newg (this tree, --graphs), newe (this tree + $AB_ENV env)
+# variants: new (this tree), old (ab_old/), prev (ab_prev/: the last commit, built), newg (this tree, --graphs),
+# newe (this tree + $AB_ENV env)
 for i in $(seq 1 ${AB_PAIRS:-2}); do
   for v in ${AB_SEQ:-new old}; do
     case $v in
       new) run new$i "$R" ;;
       old) run old$i "$R/ab_old" ;;
+      prev) run prev$i "$R/ab_prev" ;;
       newg) ARGS="$ARGS --graphs" run newg$i "$R" ;;
       newe) env $AB_ENV bash -c true && ( export $AB_ENV; run newe$i "$R" ) || exit 1 ;;
     esac
