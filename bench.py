@@ -390,6 +390,7 @@ def main(argv=None):
 
         prof = cProfile.Profile()
         prof.enable()
+    eng.runner.step_events = [] if dev.startswith("cuda") else None
     t0 = time.perf_counter()
     window[0] = t0
     for _ in range(args.steps):
@@ -397,6 +398,15 @@ def main(argv=None):
     if dev.startswith("cuda"):
         torch.cuda.synchronize()
     t1 = time.perf_counter()
+    ev = eng.runner.step_events
+    eng.runner.step_events = None
+    if ev:
+        # GPU time inside the timed steps' spans (plan upload .. token download, kernel gaps included) vs the GPU
+        # time between consecutive spans (idle unless the host had already queued the next step)
+        inside = sum(a.elapsed_time(b) for a, b in ev)
+        between = [ev[i][1].elapsed_time(ev[i + 1][0]) for i in range(len(ev) - 1)]
+        timing["gpu_ms"] = {"in_step": round(inside / len(ev), 3),
+                            "between_steps": round(sum(max(0.0, x) for x in between) / max(1, len(between)), 3)}
     timing["host_ms"] = {k: round((eng.host_s[k] - host0[k]) * 1e3 / max(1, args.steps), 3) for k in host0}
     if prof is not None:
         import pstats
@@ -534,6 +544,7 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
         "grammar_rollbacks": eng.stats.get("grammar_rollbacks", 0),
         "graph_stats": dict(eng.runner.graphs.stats) if eng.runner.graphs is not None else None,
         "host_ms_per_step": timing.get("host_ms"),  # rank 0's engine host time per timed step, by activity
+        "gpu_ms_per_step": timing.get("gpu_ms"),  # rank 0: GPU time inside step spans / idle between them
         # self-verification of multi-GPU runs: one record per rank (which GPU it ran on, its own rate and step time;
         # TP followers report 0 tokens: their leader streams the replica's tokens) and the process groups' backends /
         # sizes as torch.distributed reports them (backend "nccl" is RCCL on ROCm)

@@ -416,6 +416,28 @@ class _Stager:
         dev.view(torch.uint8).copy_(stage, non_blocking=True)
         return dev.view(a.shape)
 
+    def upload_into(self, arrays: list[np.ndarray | None], offs: list[int], dst: torch.Tensor) -> None:
+        """Arrays staged at their byte offsets of ``dst`` (a uint8 device buffer whose layout the caller fixed; None
+        leaves a range untouched) and moved by ONE async copy of the whole range — a hipGraph's static inputs refreshed
+        with one copy launch instead of an upload plus a device copy per array."""
+        n = dst.numel()
+        if self.device.type != "cuda":
+            for a, o in zip(arrays, offs):
+                if a is not None:
+                    dst[o:o + a.nbytes].copy_(torch.from_numpy(np.ascontiguousarray(a).reshape(-1).view(np.uint8)))
+            return
+        base = (self.off + 255) & ~255
+        buf = self.bufs[self.i]
+        if buf is None or base + n > buf.numel():
+            self.bufs[self.i] = buf = torch.empty(max(self.nbytes, 2 * (base + n)), dtype=torch.uint8, pin_memory=True)
+        host = buf.numpy()
+        for a, o in zip(arrays, offs):
+            if a is not None:
+                a = np.ascontiguousarray(a)
+                host[base + o:base + o + a.nbytes] = a.reshape(-1).view(np.uint8)
+        self.off = base + n
+        dst.copy_(buf[base:base + n], non_blocking=True)
+
 
 class ModelRunner:
     def __init__(self, model: TransformerLM, k_caches, v_caches, kvm, max_num_seqs: int, max_blocks_per_seq: int,
@@ -461,6 +483,7 @@ class ModelRunner:
         self.tok_buf = torch.zeros(max_num_seqs * 2 + 64, dtype=torch.int64, device=self.device)
         self.graphs = None  # engine/graphs.py DecodeGraphs when hipGraph decode is enabled
         self.fixed_decode_items = False  # decode_items_fixed without graphs too (equivalence tests)
+        self.step_events: list | None = None  # (start, end) timing events per launched step when a list is set
         # grammar masks / forced tokens / penalties inside the sampler kernel (tables allocated on first use)
         self.lp = LogitsProcessor(self.device, self.vocab, max_slots=max(256, max_num_seqs))
 
@@ -641,7 +664,9 @@ class ModelRunner:
         real = ditems[:, 3] >= 0
         h.s_total = int((npre[ditems[real, 0]] + ditems[real, 4]).max()) if h.B else 1
         if self.graphs is not None:
-            h.s_total = MAX_PARTIALS  # (a graph layout key; the partial buffer's unused slots are never touched)
+            # (a graph layout key: rounded up to a multiple of 8 so a handful of layouts cover every step; the
+            # partial buffers' unused slots are never touched)
+            h.s_total = min(MAX_PARTIALS, -(-h.s_total // 8) * 8)
         i32_parts.append(ditems.reshape(-1))
 
     def to_device(self, h: HostStep, sp: "SampleParams | None" = None) -> StepInput:
@@ -816,6 +841,10 @@ class ModelRunner:
         self.stager.begin()
         if self.broadcast is not None:  # TP leader: followers run the same step on their shards
             self.broadcast(host, sp)
+        ev_s = None
+        if self.step_events is not None and self.device.type == "cuda":
+            ev_s = torch.cuda.Event(enable_timing=True)
+            ev_s.record()
         toks = self._run(host, sp)
         rows = {s.seq_id: i for i, s in enumerate(sample_seqs)}
         if self.device.type != "cuda":
@@ -837,6 +866,10 @@ class ModelRunner:
             car.error_async(self._err_host, err_idx)
         ev = torch.cuda.Event()
         ev.record()
+        if ev_s is not None:  # GPU span of the step (plan upload -> token download), read back after the run
+            ev_e = torch.cuda.Event(enable_timing=True)
+            ev_e.record()
+            self.step_events.append((ev_s, ev_e))
         return Launched(out, ev, toks, rows, err_idx, sp.known)
 
     def _custom_ar(self):
