@@ -88,6 +88,8 @@ def parse(argv=None):
     ap.add_argument("--graphs", action="store_true", default=None,
                     help="hipGraph decode steps (default: on for --tp > 1, off at TP = 1)")
     ap.add_argument("--no-graphs", dest="graphs", action="store_false")
+    ap.add_argument("--kv-run-pages", type=int, default=1,
+                    help="KV pages handed out per growth step in consecutive runs (EngineConfig.kv_run_pages)")
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"],
                     help="paged KV cache precision (fp8 = e4m3 + per-token scales; an opt-in A/B, not the headline)")
     ap.add_argument("--seed", type=int, default=0)
@@ -283,7 +285,8 @@ def main(argv=None):
 
     cfg = EngineConfig(model=args.model, device=dev, seed=args.seed, max_num_seqs=max(256, 2 * args.threads),
                        use_cascade=not args.no_cascade, use_graphs=args.graphs, kv_dtype=args.kv_dtype,
-                       max_model_len=131072 if args.prefix_tokens > 6000 else 8192, tp=tp, tp_rank=st.tp_rank, dp_attention=dpa)
+                       max_model_len=131072 if args.prefix_tokens > 6000 else 8192, tp=tp, tp_rank=st.tp_rank, dp_attention=dpa,
+                       kv_run_pages=args.kv_run_pages)
     eng = LLMEngine(cfg)
     leaders = None
     if tp > 1:
