@@ -588,6 +588,13 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   if (g < G) {
     f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
     const float* pp = out_part + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
+    const int p0 = pre_bf16 != nullptr ? split_offset : 0;  // first fp32 slot (the pieces, or every slot)
+    // one round trip for the common row: the first PQ fp32 slots (agent-coherent loads) and MG bf16 prefix slots
+    // are all in flight before the first wait (was: the prefix batch, then the pieces batch — two tail latencies)
+    constexpr int PQ = 8;
+    f32x4 pv[PQ];
+#pragma unroll
+    for (int j = 0; j < PQ; ++j) pv[j] = ld4(pp + min(p0 + j, n - 1) * D);
     int s0 = 0;
     if (pre_bf16 != nullptr) {  // the cascade's bf16 prefix partials, MG loads per round trip (as the one-piece path)
       const bf16* pb = pre_bf16 + ((int64_t)b * Hq + kvh * G + g) * S_total * D + c;
@@ -606,8 +613,12 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
         acc4 += f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]} * sW[g][s0];
       }
     }
-    // groups of 16 partials with all loads in flight (the tail of the kernel: latency, not bandwidth)
-    for (int s2 = s0; s2 < n; s2 += 16) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the inline-asm loads above are not tracked by hipcc)
+#pragma unroll
+    for (int j = 0; j < PQ; ++j)
+      if (p0 + j < n) acc4 += pv[j] * sW[g][p0 + j];
+    // rows with more pieces: groups of 16 with all loads in flight (the tail of the kernel: latency, not bandwidth)
+    for (int s2 = p0 + PQ; s2 < n; s2 += 16) {
       f32x4 v[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) v[j] = ld4(pp + min(s2 + j, n - 1) * D);
