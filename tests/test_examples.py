@@ -16,7 +16,10 @@ def test_agent_example_forced_tool_call():
     out = subprocess.run([sys.executable, str(ROOT / "examples/agent.py"), "--model", "tiny-llama", "--device", "cpu",
                           "--max-iterations", "2", "--prompt-sections", "intro,core_tools", "--tool-choice",
                           '{"type":"function","function":{"name":"get_weather"}}'],
-                         capture_output=True, text=True, timeout=600, env=dict(os.environ, KAFKA_WEATHER_MODE="offline"))
+                         capture_output=True, text=True, timeout=600,
+                         # two intra-op threads: under pytest -n the runs share the CPUs, and 8-thread OpenMP pools
+                         # oversubscribed 4x spend their time in barriers (15 s alone, > 150 s with 4 at once)
+                         env={"OMP_NUM_THREADS": "2", **os.environ, "KAFKA_WEATHER_MODE": "offline"})
     assert out.returncode == 0, out.stderr[-2000:]
     assert "[tool call] get_weather" in out.stdout and "[tool result] Weather in" in out.stdout
     assert "[done]" in out.stdout
