@@ -55,8 +55,9 @@ struct AltPart {
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
+template <int AUX = 0>
 __device__ __forceinline__ void dma16(const void* g, char* lds) {
-  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds, 16, 0, AUX);
 }
 
 __device__ __forceinline__ float t3_xor32_max(float x) {
@@ -99,7 +100,7 @@ __device__ __forceinline__ void t3_wait_tiles(int n) {
 // ABL = 8 (diagnostic build, KAFKA_TILE_ABL=8, benchmarks/attn_tile_stamps.py): workgroup phase stamps on the 100 MHz
 // clock; the full kernel runs and lse_part is overwritten with u64 [entry, prologue done, first tile landed, loop
 // done, epilogue done, 0, 0, 0] per workgroup blockIdx.y * Hkv + blockIdx.x.
-template <int ABL = 0>
+template <int ABL = 0, int KVAUX = 0>
 __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __restrict__ items,
                                                            const bf16* __restrict__ q, int64_t q_stride,
                                                            const bf16* __restrict__ k_cache,
@@ -231,8 +232,8 @@ __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __res
     for (int cc = 0; cc < DPT / 2; ++cc) {
       const int c = c0 + cc;
       const int L = c * 64 + lane;
-      dma16(kp + L * 8, kd + c * 1024);
-      dma16(vp + (L ^ ((L >> 4) & 1)) * 8, vd + c * 1024);
+      dma16<KVAUX>(kp + L * 8, kd + c * 1024);
+      dma16<KVAUX>(vp + (L ^ ((L >> 4) & 1)) * 8, vd + c * 1024);
     }
   };
 #pragma unroll
@@ -475,7 +476,11 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
     const char* e = getenv("KAFKA_TILE_ABL");
     return e && atoi(e) == 8;
   }();
-  auto kern = stamps ? attn_tile_kernel<8> : attn_tile_kernel<0>;
+  // The cascade prefix pass (bf16 partials) reads each K / V tile of the shared prefix once per KV head and 256 query
+  // rows (one workgroup at the headline's 64 streams): its DMAs go nt (aux = 2), +0.9 % on the headline
+  // (profiles/r05/cascade/bench_ab_kv_nt.jsonl). Prefill launches keep the default policy: their query tiles re-read
+  // the same keys.
+  auto kern = stamps ? attn_tile_kernel<8> : part_bf16 ? attn_tile_kernel<0, 2> : attn_tile_kernel<0>;
   kern<<<dim3(Hkv, n_items), 512, 0, st>>>(reinterpret_cast<const TileItem*>(items), q, q_stride,
                                            static_cast<const bf16*>(k_cache), static_cast<const bf16*>(v_cache), Hkv,
                                            G, block_tables, bt_stride, q_limit, out, out_stride, out_part, lse_part,
