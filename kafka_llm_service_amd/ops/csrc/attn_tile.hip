@@ -100,7 +100,9 @@ __device__ __forceinline__ void t3_wait_tiles(int n) {
 // ABL = 8 (diagnostic build, KAFKA_TILE_ABL=8, benchmarks/attn_tile_stamps.py): workgroup phase stamps on the 100 MHz
 // clock; the full kernel runs and lse_part is overwritten with u64 [entry, prologue done, first tile landed, loop
 // done, epilogue done, 0, 0, 0] per workgroup blockIdx.y * Hkv + blockIdx.x.
-template <int ABL = 0, int KVAUX = 0>
+// PST = 1: the bf16 prefix partials are stored sc1 (16-B stores whose lines leave this XCD's L2: the reader, the
+// suffix decode's merge, runs on any XCD, and the launch ends with fewer dirty lines to write back)
+template <int ABL = 0, int KVAUX = 0, int PST = 0>
 __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __restrict__ items,
                                                            const bf16* __restrict__ q, int64_t q_stride,
                                                            const bf16* __restrict__ k_cache,
@@ -410,6 +412,12 @@ __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __res
         if (row < nvalid) {
           const int R2 = R0 + row, tok2 = it.q_start + R2 / G, head2 = kvh * G + R2 % G;
           f32x4* dst;
+          if (PST && pbf) {
+            float* d = reinterpret_cast<float*>(reinterpret_cast<bf16*>(out_part) +
+                                                (((int64_t)tok2 * Hq + head2) * S_total + it.split) * D + 64 * rd + 8 * cc);
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(d), "v"(v) : "memory");
+            continue;
+          }
           if (part && !pbf)
             dst = reinterpret_cast<f32x4*>(opart + (((int64_t)(tok2 - toff) * Hq + head2) * Sx + it.split) * D +
                                            32 * rd + 4 * cc);
@@ -480,7 +488,8 @@ extern "C" hipError_t kafka_launch_attn_tile(const void* items, int n_items, con
   // rows (one workgroup at the headline's 64 streams): its DMAs go nt (aux = 2), +0.9 % on the headline
   // (profiles/r05/cascade/bench_ab_kv_nt.jsonl). Prefill launches keep the default policy: their query tiles re-read
   // the same keys.
-  auto kern = stamps ? attn_tile_kernel<8> : part_bf16 ? attn_tile_kernel<0, 2> : attn_tile_kernel<0>;
+  // Its bf16 partials are stored sc1 (16-B stores that leave this XCD's L2: +0.2..0.6 %, bench_ab_part_sc1.jsonl).
+  auto kern = stamps ? attn_tile_kernel<8> : part_bf16 ? attn_tile_kernel<0, 2, 1> : attn_tile_kernel<0>;
   kern<<<dim3(Hkv, n_items), 512, 0, st>>>(reinterpret_cast<const TileItem*>(items), q, q_stride,
                                            static_cast<const bf16*>(k_cache), static_cast<const bf16*>(v_cache), Hkv,
                                            G, block_tables, bt_stride, q_limit, out, out_stride, out_part, lse_part,
