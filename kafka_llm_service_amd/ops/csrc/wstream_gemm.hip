@@ -31,7 +31,8 @@ template <int MT, int KC, bool NT, int KW, bool PIN>
 __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                                  const bf16x8* __restrict__ Wt, int M, int N, int K,
                                                                  int ks, bf16* __restrict__ Y, int64_t ldy,
-                                                                 float* __restrict__ P, int glu, int row_tiles) {
+                                                                 float* __restrict__ P, int glu, int row_tiles,
+                                                                 int slab16) {
   constexpr int NTH = 256 * KW;
   constexpr int ROWS = 32 * MT;
   constexpr int CPR = KC / 8;             // 16-B chunks per X row of one K chunk
@@ -196,6 +197,29 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
             Y[(int64_t)m * ldy + n] = (bf16)(g / (1.0f + __expf(-g)) * u);
           }
         }
+    }
+  } else if (P != nullptr && slab16) {
+    // split-K slab through a per-wave LDS transpose (the X stage is dead): each lane then holds 4 consecutive columns
+    // of a row and writes them with one 16-B sc1 store (the line leaves this XCD's L2 — the consumer kernel runs on
+    // every XCD — and the launch ends with fewer dirty lines to write back)
+    float* tp = reinterpret_cast<float*>(&xs[0][0]) + ct * (ROWS * 32);
+    __syncthreads();  // (workgroup-uniform: P and slab16 are kernel arguments)
+    if (active && kh == 0) {
+      const int cbase = glu ? ((nb & 1) ? (N >> 1) : 0) + (nb >> 1) * 32 : nb * 32;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tp[(mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = acc[mt][i];
+      // (one wave's LDS accesses complete in order: the reads below see its writes)
+#pragma unroll
+      for (int j = 0; j < ROWS / 8; ++j) {
+        const int q = j * 64 + lane, row = q >> 3, c4 = q & 7;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(tp + row * 32 + 4 * c4);
+        if (row < M) {
+          float* d = P + ((int64_t)blockIdx.y * Mtot + row) * N + cbase + 4 * c4;
+          asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(d), "v"(v) : "memory");
+        }
+      }
     }
   } else if (active && kh == 0) {
     // GLU-interleaved tiles written un-split: tile 2j -> gate columns [32j, +32), tile 2j+1 -> up columns N/2 + 32j
@@ -423,14 +447,21 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   const int ks = K / splits;
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
   float* p = splits > 1 ? P : nullptr;
+  // split-K slabs leave as 16-B sc1 stores through an LDS transpose (was one 4-B store per accumulator, the lines
+  // kept dirty in the XCD's L2): +2.0 % on the headline, in-step GPU time 7.50 vs 7.65 ms
+  // (profiles/r05/bench_ab_wstream_slab16_sc1.jsonl); KAFKA_WSTREAM_SLAB16=0 restores the old epilogue
+  static const int slab16 = [] {
+    const char* e = getenv("KAFKA_WSTREAM_SLAB16");
+    return e ? atoi(e) : 1;
+  }();
 #define KAFKA_WS(MT_, KC_, KW_, PIN_)                                                                            \
   do {                                                                                                          \
     if (nt)                                                                                                     \
       wstream_gemm_kernel<MT_, KC_, true, KW_, PIN_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, \
-                                                                              glu, rt);                         \
+                                                                              glu, rt, slab16);                 \
     else                                                                                                        \
       wstream_gemm_kernel<MT_, KC_, false, KW_, PIN_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, \
-                                                                               glu, rt);                        \
+                                                                               glu, rt, slab16);                \
   } while (0)
 #define KAFKA_WS_IF(MT_, KC_, KW_)                                      \
   if (mt == MT_ && kc == KC_ && kw == KW_) {                           \
