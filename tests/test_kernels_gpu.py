@@ -447,6 +447,31 @@ def test_wstream_gemm(cuda, M, N, K):
         torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("M", [17, 64, 128])
+def test_wstream_slabs_reused_buffer(cuda, M):
+    """The split-K slabs leave the GEMM as sc1 stores (their lines bypass the writer XCD's L2). Rewrite ONE slab buffer
+    many times after consumers on every XCD have read (and cached) its previous contents, as the engine does layer
+    after layer, and check every round against fp32: no reader may see a stale line."""
+    ext = ops._ext.load()
+    N, K = 6144, 4096
+    w = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+    wt = ops.tile_weight(w)
+    mt, kc, S = ops.stream_plan(M, N, K)
+    assert S > 1
+    p = torch.empty(S, M, N, device=cuda)
+    y = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    g = torch.Generator(device=cuda).manual_seed(5)
+    for it in range(6):
+        x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16, generator=g)
+        ext.wstream_gemm(x, wt, None, p, 8, True, False)
+        ext.slab_reduce(p, y)                      # our kernel, every XCD
+        s2 = p.sum(0)                              # a torch kernel reading the same lines
+        ref_y = x.float() @ w.float().t()
+        _close(y, ref_y, atol=0.02, rtol=0.01, msg=f"slab_reduce round {it}")
+        _close(s2, ref_y, atol=0.02, rtol=0.01, msg=f"torch sum round {it}")
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("M", [1, 40, 64, 80, 100, 168, 256])
 @pytest.mark.parametrize("N,K", [(28672, 4096), (7168, 8192), (2048, 1024)])
 def test_wstream_glu(cuda, M, N, K):
