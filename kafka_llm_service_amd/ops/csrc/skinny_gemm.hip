@@ -152,6 +152,30 @@ __global__ __launch_bounds__(512, OCC) void skinny_gemm_kernel(const bf16* __res
       }
     return;
   }
+  if (P) {
+    // split-K slab through a per-wave LDS transpose (the ring is dead once every wave is past its last stage): each
+    // lane then writes 4 consecutive columns of a row with one 16-B sc1 store, 16 lanes per 256-B row (as the decode
+    // GEMM's slabs)
+    __syncthreads();  // (workgroup-uniform: P is a kernel argument)
+    float* tp = reinterpret_cast<float*>(smem) + w * 64 * 64;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tp[(32 * a + (i & 3) + 8 * (i >> 2) + 4 * h) * 64 + 32 * b + r] = acc[a][b][i];
+    // (one wave's LDS accesses complete in order: the reads below see its writes)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int q = j * 64 + lane, row = q >> 4, c4 = q & 15;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(tp + row * 64 + 4 * c4);
+      const int m = 64 * rg + row;
+      // GLU-interleaved pair: tile nb0 -> gate columns, nb0 + 1 -> up columns N/2 + ...
+      const int n = glu ? ((c4 >> 3) ? (N >> 1) : 0) + (nb0 >> 1) * 32 + 4 * (c4 & 7) : nb0 * 32 + 4 * c4;
+      if (m < M) store16_slab(P + ((int64_t)blockIdx.y * M + m) * N + n, v);
+    }
+    return;
+  }
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
     const int nb = nb0 + b;

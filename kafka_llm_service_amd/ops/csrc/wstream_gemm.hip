@@ -216,8 +216,7 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
         const int q = j * 64 + lane, row = q >> 3, c4 = q & 7;
         const f32x4 v = *reinterpret_cast<const f32x4*>(tp + row * 32 + 4 * c4);
         if (row < M) {
-          float* d = P + ((int64_t)blockIdx.y * Mtot + row) * N + cbase + 4 * c4;
-          asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(d), "v"(v) : "memory");
+          store16_slab(P + ((int64_t)blockIdx.y * Mtot + row) * N + cbase + 4 * c4, v);
         }
       }
     }

@@ -472,6 +472,29 @@ def test_wstream_slabs_reused_buffer(cuda, M):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("M", [130, 200, 256])
+def test_skinny_slabs_reused_buffer(cuda, M):
+    """As test_wstream_slabs_reused_buffer for the skinny GEMM's sc1 slab stores (129..256-row steps)."""
+    ext = ops._ext.load()
+    N, K = 4096, 14336
+    w = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+    wt = ops.tile_weight(w)
+    S = ops.skinny_plan(M, N, K)
+    assert S > 1
+    p = torch.empty(S, M, N, device=cuda)
+    y = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    g = torch.Generator(device=cuda).manual_seed(6)
+    for it in range(6):
+        x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16, generator=g)
+        ext.skinny_gemm(x, wt, None, p, S, False)
+        ext.slab_reduce(p, y)
+        s2 = p.sum(0)
+        ref_y = x.float() @ w.float().t()
+        _close(y, ref_y, atol=0.03, rtol=0.01, msg=f"skinny slab_reduce round {it}")
+        _close(s2, ref_y, atol=0.03, rtol=0.01, msg=f"skinny torch sum round {it}")
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("M", [1, 40, 64, 80, 100, 168, 256])
 @pytest.mark.parametrize("N,K", [(28672, 4096), (7168, 8192), (2048, 1024)])
 def test_wstream_glu(cuda, M, N, K):
