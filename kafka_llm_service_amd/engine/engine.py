@@ -180,7 +180,7 @@ class LLMEngine:
                                                prefill_tokens_while_decoding=cfg.prefill_tokens_while_decoding,
                                                step_rows_fit=self._step_rows_fit(),
                                                prefill_cost_budget=int(os.environ.get("KAFKA_PREFILL_COST_BUDGET",
-                                                                                      "512")),
+                                                                                      "384")),
                                                burst_sqrt_k=float(os.environ.get("KAFKA_BURST_SQRT_K", "0")),
                                                max_model_len=cfg.max_model_len, max_blocks_per_seq=max_blocks),
                                self.kvm)

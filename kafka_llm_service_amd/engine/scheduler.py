@@ -51,7 +51,10 @@ class SchedulerConfig:
     # of the budget (the group size minimizing the mean completion of n equal jobs over steps of floor + group x
     # job). Measured on MI355X it only trades later turns for the synchronized first one (profiles/r03/
     # serve_burst_ab.jsonl: turn-0 p50 ~240 vs ~255 ms, turns 1-3 ~100-180 vs ~50-70 ms), so it is off (0).
-    prefill_cost_budget: int = 512
+    # Budget 384 (was 512): served burst (64 threads x 4 turns) p50 41-43 vs 47-53 ms, p99 196 vs 215-243 ms; 256
+    # doubles the first turn's p50; the headline moves -0.1..-0.3 % (profiles/r05/serve/burst_budget_*.log,
+    # profiles/r05/bench_ab_prefill_budget_384.jsonl); 768-2048 were worse in round 4 (profiles/r04/serve/)
+    prefill_cost_budget: int = 384
     attn_equiv_keys: int = 30000
     burst_sqrt_k: float = 0.0
 
