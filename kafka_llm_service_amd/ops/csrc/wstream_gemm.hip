@@ -185,7 +185,27 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
         for (int i = 0; i < 16; ++i) red[(((ct >> 1) * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
     }
     __syncthreads();
-    if (active && kh == 0 && !(ct & 1)) {
+    if (slab16 & 2) {
+      // the workgroup's 64 output columns (128 B per row) through an LDS tile, then 16-B sc1 stores: 8 lanes per row
+      bf16* ty = reinterpret_cast<bf16*>(red + 2 * MT * 16 * 64);  // [ROWS][64], after the up-tile exchange
+      if (active && kh == 0 && !(ct & 1)) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float g = acc[mt][i], u = red[(((ct >> 1) * MT + mt) * 16 + i) * 64 + lane];
+            ty[(mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h) * 64 + (ct >> 1) * 32 + r] = (bf16)(g / (1.0f + __expf(-g)) * u);
+          }
+      }
+      __syncthreads();
+      const int c0 = cb * 64, W2 = N >> 1;
+      for (int q = tid; q < ROWS * 8; q += NTH) {
+        const int row = q >> 3, c = q & 7;
+        if (row < M && c0 + 8 * c < W2)
+          store16_slab(reinterpret_cast<float*>(Y + (int64_t)row * ldy + c0 + 8 * c),
+                       *reinterpret_cast<const f32x4*>(ty + row * 64 + 8 * c));
+      }
+    } else if (active && kh == 0 && !(ct & 1)) {
       const int n = (nb >> 1) * 32 + r;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -198,7 +218,26 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
           }
         }
     }
-  } else if (P != nullptr && slab16) {
+  } else if (P == nullptr && !glu && (slab16 & 2)) {
+    // un-split bf16 output (the lm_head): the workgroup's 128 columns (256 B per row) through an LDS tile, then
+    // 16-B sc1 stores, 8 lanes per 128-B line
+    bf16* ty = reinterpret_cast<bf16*>(&xs[0][0]);  // [ROWS][128]
+    __syncthreads();  // (workgroup-uniform: P, glu and slab16 are kernel arguments)
+    if (active && kh == 0) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ty[(mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h) * 128 + ct * 32 + r] = (bf16)acc[mt][i];
+    }
+    __syncthreads();
+    const int c0 = cb * 128;
+    for (int q = tid; q < ROWS * 16; q += NTH) {
+      const int row = q >> 4, c = q & 15;
+      if (row < M && c0 + 8 * c < N)
+        store16_slab(reinterpret_cast<float*>(Y + (int64_t)row * ldy + c0 + 8 * c),
+                     *reinterpret_cast<const f32x4*>(ty + row * 128 + 8 * c));
+    }
+  } else if (P != nullptr && (slab16 & 1)) {
     // split-K slab through a per-wave LDS transpose (the X stage is dead): each lane then holds 4 consecutive columns
     // of a row and writes them with one 16-B sc1 store (the line leaves this XCD's L2 — the consumer kernel runs on
     // every XCD — and the launch ends with fewer dirty lines to write back)
@@ -449,18 +488,21 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   // split-K slabs leave as 16-B sc1 stores through an LDS transpose (was one 4-B store per accumulator, the lines
   // kept dirty in the XCD's L2): +2.0 % on the headline, in-step GPU time 7.50 vs 7.65 ms
   // (profiles/r05/bench_ab_wstream_slab16_sc1.jsonl); KAFKA_WSTREAM_SLAB16=0 restores the old epilogue
+  // bit 1: the un-split bf16 outputs (fused SwiGLU, lm_head) the same way through a workgroup LDS tile
   static const int slab16 = [] {
     const char* e = getenv("KAFKA_WSTREAM_SLAB16");
     return e ? atoi(e) : 1;
   }();
+  // (16-B stores of Y need 16-B aligned rows)
+  const int wide = (Y != nullptr && (ldy % 8 != 0 || reinterpret_cast<uintptr_t>(Y) % 16 != 0)) ? (slab16 & 1) : slab16;
 #define KAFKA_WS(MT_, KC_, KW_, PIN_)                                                                            \
   do {                                                                                                          \
     if (nt)                                                                                                     \
       wstream_gemm_kernel<MT_, KC_, true, KW_, PIN_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, \
-                                                                              glu, rt, slab16);                 \
+                                                                              glu, rt, wide);                   \
     else                                                                                                        \
       wstream_gemm_kernel<MT_, KC_, false, KW_, PIN_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, \
-                                                                               glu, rt, slab16);                \
+                                                                               glu, rt, wide);                  \
   } while (0)
 #define KAFKA_WS_IF(MT_, KC_, KW_)                                      \
   if (mt == MT_ && kc == KC_ && kw == KW_) {                           \
