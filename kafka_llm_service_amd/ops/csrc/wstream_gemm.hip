@@ -488,10 +488,12 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   // split-K slabs leave as 16-B sc1 stores through an LDS transpose (was one 4-B store per accumulator, the lines
   // kept dirty in the XCD's L2): +2.0 % on the headline, in-step GPU time 7.50 vs 7.65 ms
   // (profiles/r05/bench_ab_wstream_slab16_sc1.jsonl); KAFKA_WSTREAM_SLAB16=0 restores the old epilogue
-  // bit 1: the un-split bf16 outputs (fused SwiGLU, lm_head) the same way through a workgroup LDS tile
+  // bit 1: the un-split bf16 outputs (fused SwiGLU, lm_head) the same way through a workgroup LDS tile, whole 128-B
+  // lines per store instruction (was one 2-B store per accumulator, half lines): +1.1..2.1 %, in-step GPU time 7.37
+  // vs 7.45-7.49 ms (profiles/r05/bench_ab_wstream_wide_y.jsonl)
   static const int slab16 = [] {
     const char* e = getenv("KAFKA_WSTREAM_SLAB16");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 3;
   }();
   // (16-B stores of Y need 16-B aligned rows)
   const int wide = (Y != nullptr && (ldy % 8 != 0 || reinterpret_cast<uintptr_t>(Y) % 16 != 0)) ? (slab16 & 1) : slab16;
