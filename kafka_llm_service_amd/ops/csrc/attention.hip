@@ -521,6 +521,34 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     }
     return;
   }
+  if (out != nullptr) {
+    // ticket merge: each split's partial row leaves as 16-B write-through (sc1, agent-coherent) stores — 4-B ones
+    // cost several times more per byte — and the last workgroup reads it back with 16-B sc1 loads (ld4 below)
+    for (int idx4 = threadIdx.x; idx4 < G * D / 4; idx4 += 256) {
+      const int g = idx4 / (D / 4), d0 = (idx4 % (D / 4)) * 4;
+      float M = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) M = fmaxf(M, sM[i][g]);
+      float L = 0.f;
+      f32x4 O4 = {0.f, 0.f, 0.f, 0.f};
+      if (M != -INFINITY) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float f = exp2f(sM[i][g] - M);
+          L += f * sL[i][g];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) O4[j] += f * sO[i][g][d0 + j];
+        }
+      }
+      const int64_t pidx = ((int64_t)b * Hq + kvh * G + g) * S_total + split_offset + split;
+      const float inv = L > 0.f ? 1.f / L : 0.f, lv = L > 0.f ? M + log2f(L) : -INFINITY;
+      f32x4 ov4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ov4[j] = L > 0.f ? O4[j] * inv : 0.f;
+      store16_slab(out_part + pidx * D + d0, ov4);
+      if (d0 == 0) __hip_atomic_store(lse_part + pidx, lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else
   for (int idx = threadIdx.x; idx < G * D; idx += 256) {
     const int g = idx / D, d = idx % D;
     float M = -INFINITY;

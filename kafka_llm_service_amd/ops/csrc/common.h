@@ -65,9 +65,10 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 
 __device__ __forceinline__ bf16x8 load_bf16x8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 __device__ __forceinline__ void store_bf16x8(bf16* p, bf16x8 v) { *reinterpret_cast<bf16x8*>(p) = v; }
-// 16-B fp32 store that bypasses this XCD's L2 (sc1). Used only for split-K slabs: write-only in their kernel, 8 or 16
-// lanes filling whole 128-B lines per instruction, read by the next kernel (profiles/r05/bench_ab_wstream_slab16_sc1
-// .jsonl); sc1 outputs elsewhere (RMSNorm, RoPE, tile outputs) left readers stale data (README "Measured and removed")
+// 16-B fp32 store that bypasses this XCD's L2 (sc1). Used for split-K slabs and GEMM outputs (write-only in their
+// kernel, whole 128-B lines per instruction, read by the next kernel: profiles/r05/bench_ab_wstream_slab16_sc1.jsonl)
+// and for the decode ticket merge's partial rows (read back in the same launch with sc1 loads); sc1 outputs in
+// RMSNorm / RoPE / tile kernels left readers stale data (README "Measured and removed")
 __device__ __forceinline__ void store16_slab(float* p, f32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
