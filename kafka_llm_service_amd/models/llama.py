@@ -48,6 +48,9 @@ PIPE_CHUNKS = max(1, int(os.environ.get("KAFKA_TP_PIPE_CHUNKS", "4")))
 PIPE_ROWS = 256
 SKINNY = frozenset(p for p in os.environ.get("KAFKA_SKINNY", "qkv,o,down").replace("+", ",").split(",")
                    if p in ("qkv", "o", "down", "gate_up"))  # gate_up: fused SwiGLU epilogue (A/B, not default)
+# Fused decode layer (forward -> _forward_fused; env KAFKA_FUSED_DECODE=0 turns it off for A/B runs): 6 launches per
+# layer instead of 9 — deferred RMSNorm and RoPE + KV write inside the streaming GEMMs' epilogues.
+FUSED = os.environ.get("KAFKA_FUSED_DECODE", "1") != "0"
 _OVL: dict = {}
 _SEAM_DONE = object()  # forward(): the previous layer's overlapped seam already produced this layer's input
 
@@ -112,6 +115,7 @@ class TransformerLM:
         self.stream = False  # decode GEMMs on the weight-streaming kernel (enable_stream_weights)
         self.tiled_only = False  # row-major dense weights dropped (enable_stream_weights(tiled_only=True))
         self.stream_max_m = ops.STREAM_MAX_M  # rows up to which a step's projections stream
+        self._fused_shapes = None  # whether the fused decode layer applies to this model (decided on first use)
 
     def enable_dp_attention(self, ep: int, ep_rank: int) -> None:
         """Data-parallel attention for a MoE model (call before the weights are created): attention, norms and the
@@ -220,6 +224,8 @@ class TransformerLM:
         (the custom xGMI all-reduce fuses all three when the message fits its buffer, parallel/comm.py)."""
         cfg = self.cfg
         T = inp.tokens.shape[0]
+        if self._fused_ok(T, k_caches):
+            return self._forward_fused(inp, k_caches, v_caches, gather)
         h = self._embed(inp.tokens)
         residual = h
         x = torch.empty_like(h)
@@ -290,6 +296,58 @@ class TransformerLM:
         if tp:
             logits = pstate.tp_all_gather_lastdim(logits)
         return logits[:, :cfg.vocab_size]
+
+    def _fused_ok(self, T: int, k_caches: list[torch.Tensor]) -> bool:
+        """Decode-sized TP = 1 dense steps run the fused layer (FUSED above) when every projection has its wave-tiled
+        copy, the KV cache is bf16 with 128-dim heads and the shapes fit the fused epilogues."""
+        if not (FUSED and self.stream and self.tp == 1 and not self.dp_attention and 0 < T <= self.stream_max_m):
+            return False
+        if self._fused_shapes is None:
+            lw0 = self.layers[0]
+            ok = all(lw.router is None and lw.glu and lw.qkv_t is not None and lw.o_t is not None and
+                     lw.down_t is not None for lw in self.layers)
+            self._fused_shapes = ok and self.D == 128 and not ops.is_fp8_cache(k_caches[0]) and \
+                ops.stream_plan(1, self.cfg.hidden_size, lw0.down_t.shape[1] * 16) is not None
+        if not self._fused_shapes:
+            return False
+        lw0 = self.layers[0]
+        return ops.fin_supported(T, self.cfg.hidden_size, lw0.qkv_t.shape[0] * 32, lw0.gate_up_t.shape[0] * 32, self.D) \
+            and ops.stream_plan(T, self.cfg.hidden_size, lw0.down_t.shape[1] * 16) is not None
+
+    def _forward_fused(self, inp: StepInput, k_caches: list[torch.Tensor], v_caches: list[torch.Tensor],
+                       gather: bool) -> torch.Tensor:
+        """The decode layer as 6 launches (qkv + RoPE/KV write -> cascade -> decode -> o + residual add -> gate_up +
+        SwiGLU -> down + residual add): RMSNorm is deferred into the consuming GEMMs (the residual producer writes
+        bf16(h * w) and per-column-block sums of h^2, the consumer scales rows by rsqrt(mean h^2 + eps)) and RoPE +
+        the paged KV write run in the QKV GEMM's split-K finisher (ops.linear_res / linear_qkv_rope / linear_glu_rs,
+        csrc/wstream_gemm.hip FIN_*). Only layer 0's input norm (from the embedding) and the final norm stay kernels."""
+        cfg = self.cfg
+        T = inp.tokens.shape[0]
+        d, eps = cfg.hidden_size, cfg.rms_norm_eps
+        residual = self._embed(inp.tokens)  # a fresh tensor at TP = 1: the residual stream owns it
+        x = torch.empty_like(residual)
+        q = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
+        attn_out = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
+        ss = torch.empty(2, d // 128, T, dtype=torch.float32, device=self.device)
+        ops.rmsnorm(residual, self.layers[0].input_norm, eps, out=x)
+        ss_in, delta = None, None
+        L = len(self.layers)
+        for i, lw in enumerate(self.layers):
+            ops.linear_qkv_rope(x, lw.qkv_t, ss_in, eps, inp.positions, self.cos_sin, q, k_caches[i], v_caches[i],
+                                inp.slot_mapping, self.hq, self.hkv)
+            paged_attention(q, k_caches[i], v_caches[i], inp.attn, attn_out)
+            ops.linear_res(attn_out.view(T, -1), lw.o_t, residual, lw.post_norm, x, ss[0], pool="fin_o")
+            a = ops.linear_glu_rs(x, lw.gate_up_t, ss[0], eps)
+            if i + 1 < L:
+                ops.linear_res(a, lw.down_t, residual, self.layers[i + 1].input_norm, x, ss[1], pool="fin_down")
+                ss_in = ss[1]
+            else:
+                delta = self._linear(a, lw.down, lw.down_t, kind="down")
+        rows = inp.logit_rows
+        d_sel = delta.index_select(1 if ops.is_slab(delta) else 0, rows)
+        hf = ops.fused_add_rmsnorm(d_sel, residual.index_select(0, rows), self.final_norm, eps)
+        logits = self._linear(hf, self.lm_head, self.lm_head_t, max_splits=1)
+        return logits if not gather else logits[:, :cfg.vocab_size]
 
     def _can_pipe(self, T: int, w: torch.Tensor | None, wt: torch.Tensor | None) -> bool:
         """A prefill-sized seam that goes to the library all-reduce (beyond the custom all-reduce's buffer) and is

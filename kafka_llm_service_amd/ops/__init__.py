@@ -333,6 +333,98 @@ def linear_glu(x: torch.Tensor, wt: torch.Tensor, max_splits: int = 8) -> torch.
     return y if plan is not None and plan[2] == 1 else silu_mul(y)
 
 
+# ---- fused decode layer (csrc/wstream_gemm.hip FIN_*): deferred RMSNorm + split-K finishers ----------------------
+# A decode layer runs as qkv(+RoPE/KV write) -> attention -> o(+residual add, next norm) -> gate_up(+row scale,
+# SwiGLU) -> down(+residual add, next norm): the RMSNorm and RoPE kernels leave the step. The residual producer writes
+# X' = bf16(h * w) and per-128-column partial sums of h^2 (``ss`` fp32 [d/128, T]); the consumer GEMM scales each
+# output row by r = rsqrt(sum(ss) / d + eps) — rmsnorm(h) . W^T = r * ((h * w) . W^T).
+
+def fin_row_scale(ss: torch.Tensor | None, M: int, d: int, eps: float) -> torch.Tensor | None:
+    """r[m] = rsqrt(sum_j ss[j, m] / d + eps) (fp32 [M]) — the deferred RMSNorm scale; None without partials."""
+    if ss is None:
+        return None
+    return torch.rsqrt(ss[:, :M].float().sum(0) / d + eps)
+
+
+def _fin_scratch(x: torch.Tensor, N: int, max_splits: int) -> tuple[int, torch.Tensor | None]:
+    M, K = x.shape
+    plan = stream_plan(M, N, K, max_splits)
+    if plan is None or M > 128 or N % 128:
+        raise ValueError(f"fused decode GEMM: unsupported shape M={M} N={N} K={K}")
+    S = plan[2]
+    return S, (torch.empty(S, M, N, dtype=torch.float32, device=x.device) if S > 1 else None)
+
+
+def linear_res(x: torch.Tensor, wt: torch.Tensor, resid: torch.Tensor, nw: torch.Tensor, xn: torch.Tensor,
+               ss_out: torch.Tensor, max_splits: int = 8, pool: str = "fin") -> None:
+    """resid <- bf16(resid + x @ W^T) in place; xn <- bf16(resid * nw); ss_out[cb, m] = sum of resid[m, 128 cb:+128]^2
+    (the o / down projection with the residual add and the next RMSNorm's producer half, csrc FIN_RES)."""
+    N = wt.shape[0] * 32
+    if _gpu(x):
+        S, p = _fin_scratch(x, N, max_splits)
+        ext().wstream_fin(1, x, wt, None, p, _tickets(x.device, N // 128 + 1, pool), None, 0.0, resid, nw, xn, ss_out,
+                          None, None, None, None, None, None, 0, 0, int(max_splits))
+        return
+    M = x.shape[0]
+    y = x.float() @ untile_weight(wt).float().t()
+    s = (resid.float() + y).to(resid.dtype)
+    resid.copy_(s)
+    xn.copy_((s.float() * nw.float()).to(xn.dtype))
+    ss_out[:, :M] = s.float().pow(2).view(M, N // 128, 128).sum(-1).t()
+
+
+def linear_qkv_rope(x: torch.Tensor, wt: torch.Tensor, ss_in: torch.Tensor | None, eps: float, positions, cos_sin,
+                    q_out, k_cache, v_cache, slot_mapping, Hq: int, Hkv: int, max_splits: int = 8,
+                    pool: str = "fin_qkv") -> None:
+    """RoPE + paged KV write of r * (x @ Wqkv^T) (r: the deferred RMSNorm of x from ``ss_in``, or 1), in the QKV
+    GEMM's split-K finisher (csrc FIN_ROPE); bf16 caches, head dim 128."""
+    N = wt.shape[0] * 32
+    M, K = x.shape
+    if _gpu(x):
+        S, p = _fin_scratch(x, N, max_splits)
+        ext().wstream_fin(2, x, wt, None, p, _tickets(x.device, N // 128 + 1, pool), ss_in, float(eps), None, None,
+                          None, None, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, int(Hq), int(Hkv),
+                          int(max_splits))
+        return
+    y = x.float() @ untile_weight(wt).float().t()
+    r = fin_row_scale(ss_in, M, K, eps)
+    if r is not None:
+        y = y * r[:, None]
+    ref.rope_kv_write(y, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, Hq, Hkv)
+
+
+def linear_glu_rs(x: torch.Tensor, wt: torch.Tensor, ss_in: torch.Tensor | None, eps: float) -> torch.Tensor:
+    """silu(r g) * (r u) with [g | u] = x @ Wgu^T from GLU-tiled weights, one split (csrc FIN_GLU); r as above."""
+    N = wt.shape[0] * 32
+    M, K = x.shape
+    if _gpu(x):
+        y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
+        ext().wstream_fin(3, x, wt, y, None, _tickets(x.device, 1, "fin"), ss_in, float(eps), None, None, None, None,
+                          None, None, None, None, None, None, 0, 0, 1)
+        return y
+    y = x.float() @ untile_weight(wt, glu=True).float().t()
+    r = fin_row_scale(ss_in, M, K, eps)
+    if r is not None:
+        y = y * r[:, None]
+    F = N // 2
+    return (torch.nn.functional.silu(y[:, :F]) * y[:, F:]).to(x.dtype)
+
+
+def fin_supported(M: int, d: int, n_qkv: int, n_gu: int, head_dim: int, kw_gate_up: int = 2) -> bool:
+    """Shapes the fused decode layer takes (else the model runs the unfused kernels): one row tile, 128-column heads,
+    the gate_up row-scale partials fit its threads."""
+    if not (1 <= M <= 128 and head_dim == 128 and d % 128 == 0 and n_qkv % 128 == 0 and n_gu % 128 == 0):
+        return False
+    if stream_plan(M, n_gu, d, 1) is None or stream_plan(M, n_qkv, d) is None or stream_plan(M, d, d) is None:
+        return False
+    mt, kc, _ = stream_plan(M, n_gu, d, 1)
+    nth = 256 * (2 if mt == 2 and kc == 256 and d // kc >= 6 else 1)
+    ssl, nss, tpr = 4096 // nth, d // 128, 1
+    while tpr * ssl < nss:
+        tpr *= 2
+    return tpr <= 64 and M * tpr <= nth
+
+
 def tile_experts(w: torch.Tensor, glu: bool = False) -> torch.Tensor:
     """Expert weights [E, N, K] -> wave-tiled [E, N/32, K/16, 64, 8] (``tile_weight`` per expert)."""
     E, N, K = w.shape

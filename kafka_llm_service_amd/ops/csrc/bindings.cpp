@@ -46,6 +46,32 @@ hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, const bf16* Wt,
                                      int splits, int nt, int kw, int pin, int glu, bf16* Y, int64_t ldy, float* P,
                                      hipStream_t st);
 hipError_t kafka_launch_slab_reduce(const float* P, int S, int M, int N, bf16* Y, int64_t ldy, hipStream_t st);
+// host mirror of wstream_gemm.hip's FinArgs (same field order and types; size cross-checked at first use)
+struct FinArgs {
+  int* tickets;
+  const float* ss_in;
+  int nss, ss_ld;
+  float inv_d, eps;
+  bf16* resid;
+  int64_t ldr;
+  const bf16* nw;
+  bf16* xn;
+  int64_t ldxn;
+  float* ss_out;
+  int ss_out_ld;
+  const int64_t* positions;
+  const float* cos_sin;
+  bf16* q_out;
+  int64_t q_stride;
+  bf16* k_cache;
+  bf16* v_cache;
+  const int64_t* slots;
+  int Hq, Hkv;
+};
+int kafka_fin_args_size();
+hipError_t kafka_launch_wstream_fin(int fin, const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt,
+                                    int kc, int splits, int kw, int pin, bf16* Y, int64_t ldy, float* P,
+                                    const FinArgs* fa, hipStream_t st);
 hipError_t kafka_launch_wstream_grouped(const bf16* X, int64_t ldx, const bf16* Wt, int e_local, int N, int K,
                                         const int* perm_tok, const float* perm_w, const int* expert_off, int e_lo,
                                         int max_rows, int gather, bf16* Y, int64_t ldy, float* out, int64_t ldo,
@@ -474,6 +500,108 @@ static void wstream_gemm(at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> 
                                       yp, ldy, pp, cur_stream()));
 }
 
+// Fused decode-layer GEMMs (wstream_gemm.hip FIN_*): fin 1 = o / down with the split-K finisher doing the residual
+// add, the next RMSNorm's weight and its row partial sums (resid, nw, xn, ss_out); 2 = qkv with RoPE + paged KV
+// write in the finisher (positions, cos_sin, q_out, caches, slots, Hq, Hkv); 3 = gate_up with the SwiGLU epilogue
+// (one split, y [M, N/2]). ss_in (fp32 [K/128, >= M]): partial sums of squares of X's rows — X is then the
+// un-normalised bf16(h * w) and each row is scaled by rsqrt(sum / K + eps) after the GEMM.
+static void wstream_fin(int64_t fin, at::Tensor x, at::Tensor wt, c10::optional<at::Tensor> y,
+                        c10::optional<at::Tensor> p, at::Tensor tickets, c10::optional<at::Tensor> ss_in, double eps,
+                        c10::optional<at::Tensor> resid, c10::optional<at::Tensor> nw, c10::optional<at::Tensor> xn,
+                        c10::optional<at::Tensor> ss_out, c10::optional<at::Tensor> positions,
+                        c10::optional<at::Tensor> cos_sin, c10::optional<at::Tensor> q_out,
+                        c10::optional<at::Tensor> k_cache, c10::optional<at::Tensor> v_cache,
+                        c10::optional<at::Tensor> slots, int64_t Hq, int64_t Hkv, int64_t max_splits) {
+  static const bool abi_ok = kafka_fin_args_size() == (int)sizeof(FinArgs);
+  TORCH_CHECK(abi_ok, "wstream_fin: FinArgs layout differs between the kernel and the bindings");
+  TORCH_CHECK(fin >= 1 && fin <= 3, "wstream_fin: fin must be 1, 2 or 3");
+  CHECK_CUDA(x); CHECK_DT(x, at::kBFloat16); CHECK_DT(wt, at::kBFloat16); CHECK_LASTDIM(x);
+  TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0, "wstream_fin: x must be [M, K] with 16-B rows");
+  TORCH_CHECK(wt.dim() == 4 && wt.is_contiguous() && wt.size(2) == 64 && wt.size(3) == 8,
+              "wstream_fin: wt must be contiguous [N/32, K/16, 64, 8]");
+  const int M = x.size(0), K = x.size(1), N = wt.size(0) * 32;
+  TORCH_CHECK(wt.size(1) * 16 == K && M >= 1 && M <= 128 && N % 128 == 0, "wstream_fin: shape");
+  int mt = 0, kc = 0, s = 0;
+  TORCH_CHECK(kafka_wstream_plan(M, N, K, fin == 3 ? 1 : (int)max_splits, &mt, &kc, &s) == 0,
+              "wstream_fin: unsupported shape");
+  CHECK_DT(tickets, at::kInt);
+  TORCH_CHECK(tickets.is_cuda() && tickets.is_contiguous() && tickets.numel() >= N / 128, "wstream_fin: tickets");
+  FinArgs fa{};
+  fa.tickets = tickets.data_ptr<int>();
+  fa.eps = (float)eps;
+  fa.inv_d = 1.f / (float)K;
+  if (ss_in.has_value()) {
+    CHECK_DT(ss_in.value(), at::kFloat);
+    TORCH_CHECK(ss_in->is_cuda() && ss_in->dim() == 2 && ss_in->stride(1) == 1 && ss_in->size(0) * 128 == K &&
+                    ss_in->size(1) >= M, "wstream_fin: ss_in must be fp32 [K/128, >= M]");
+    fa.ss_in = ss_in->data_ptr<float>();
+    fa.nss = ss_in->size(0);
+    fa.ss_ld = ss_in->stride(0);
+  }
+  const int kw = mt == 2 && kc == 256 && K / s / kc >= 6 ? 2 : 1;  // (the wstream_gemm rules above)
+  const int pin = mt != 3 && K / s / kc >= 3 ? 1 : 0;
+  bf16* yp = nullptr;
+  int64_t ldy = 0;
+  float* pp = nullptr;
+  if (s > 1) {
+    TORCH_CHECK(p.has_value(), "wstream_fin: slab scratch required");
+    CHECK_DT(p.value(), at::kFloat);
+    TORCH_CHECK(p->is_cuda() && p->is_contiguous() && p->dim() == 3 && p->size(0) == s && p->size(1) == M &&
+                    p->size(2) == N, "wstream_fin: slab scratch must be [splits, M, N]");
+    TORCH_CHECK((int64_t)s * M * N * 4 < 0x7fffffffLL, "wstream_fin: slab scratch beyond 2 GiB");
+    pp = p->data_ptr<float>();
+  }
+  if (fin == 1) {
+    TORCH_CHECK(resid.has_value() && nw.has_value() && xn.has_value() && ss_out.has_value(), "wstream_fin: fin 1 args");
+    CHECK_DT(resid.value(), at::kBFloat16); CHECK_DT(nw.value(), at::kBFloat16); CHECK_DT(xn.value(), at::kBFloat16);
+    CHECK_DT(ss_out.value(), at::kFloat);
+    CHECK_LASTDIM(resid.value()); CHECK_LASTDIM(xn.value()); CHECK_LASTDIM(ss_out.value());
+    TORCH_CHECK(resid->dim() == 2 && resid->size(0) == M && resid->size(1) == N && resid->stride(0) % 4 == 0 &&
+                    xn->dim() == 2 && xn->size(0) == M && xn->size(1) == N && xn->stride(0) % 4 == 0 &&
+                    nw->is_contiguous() && nw->numel() == N && ss_out->dim() == 2 && ss_out->size(0) == N / 128 &&
+                    ss_out->size(1) >= M, "wstream_fin: fin 1 shapes");
+    fa.resid = bptr(resid.value());
+    fa.ldr = resid->stride(0);
+    fa.nw = bptr(nw.value());
+    fa.xn = bptr(xn.value());
+    fa.ldxn = xn->stride(0);
+    fa.ss_out = ss_out->data_ptr<float>();
+    fa.ss_out_ld = ss_out->stride(0);
+  } else if (fin == 2) {
+    TORCH_CHECK(positions.has_value() && cos_sin.has_value() && q_out.has_value(), "wstream_fin: fin 2 args");
+    CHECK_DT(positions.value(), at::kLong); CHECK_DT(cos_sin.value(), at::kFloat); CHECK_DT(q_out.value(), at::kBFloat16);
+    TORCH_CHECK(N == (Hq + 2 * Hkv) * 128, "wstream_fin: qkv width must be (Hq + 2 Hkv) * 128");
+    TORCH_CHECK(positions->is_contiguous() && positions->numel() == M && cos_sin->is_contiguous() &&
+                    cos_sin->dim() == 2 && cos_sin->size(1) == 128, "wstream_fin: positions / cos_sin");
+    TORCH_CHECK(q_out->dim() == 3 && q_out->size(0) == M && q_out->size(1) == Hq && q_out->size(2) == 128 &&
+                    q_out->stride(2) == 1 && q_out->stride(1) == 128 && q_out->stride(0) % 4 == 0, "wstream_fin: q_out");
+    fa.positions = positions->data_ptr<int64_t>();
+    fa.cos_sin = cos_sin->data_ptr<float>();
+    fa.q_out = bptr(q_out.value());
+    fa.q_stride = q_out->stride(0);
+    fa.Hq = Hq;
+    fa.Hkv = Hkv;
+    if (slots.has_value()) {
+      TORCH_CHECK(k_cache.has_value() && v_cache.has_value(), "wstream_fin: caches required with slots");
+      check_cache_pair(k_cache.value(), v_cache.value());
+      TORCH_CHECK(!is_fp8_cache(k_cache.value()) && k_cache->size(1) == Hkv, "wstream_fin: bf16 caches of Hkv heads");
+      CHECK_DT(slots.value(), at::kLong);
+      TORCH_CHECK(slots->is_contiguous() && slots->numel() == M, "wstream_fin: slots shape");
+      fa.slots = slots->data_ptr<int64_t>();
+      fa.k_cache = bptr(k_cache.value());
+      fa.v_cache = bptr(v_cache.value());
+    }
+  } else {
+    TORCH_CHECK(s == 1 && y.has_value(), "wstream_fin: fin 3 needs one split and y");
+    CHECK_DT(y.value(), at::kBFloat16); CHECK_LASTDIM(y.value());
+    TORCH_CHECK(y->dim() == 2 && y->size(0) == M && y->size(1) == N / 2, "wstream_fin: y must be [M, N/2]");
+    yp = bptr(y.value());
+    ldy = y->stride(0);
+  }
+  CHECK_HIP(kafka_launch_wstream_fin((int)fin, bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, kw, pin, yp, ldy, pp,
+                                     &fa, cur_stream()));
+}
+
 // Skinny MFMA GEMM (csrc/skinny_gemm.hip) for 129..256 rows on the wave-tiled weights: y bf16 for one split
 // ([M, N/2] activated with glu), else fp32 slabs p [splits, M, N]
 static int64_t skinny_plan(int64_t M, int64_t N, int64_t K, int64_t max_splits) {
@@ -843,6 +971,10 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("wstream_plan", &wstream_plan);
   m.def("wstream_gemm", &wstream_gemm, py::arg("x"), py::arg("wt"), py::arg("y"), py::arg("p"),
         py::arg("max_splits"), py::arg("nt"), py::arg("glu"));
+  m.def("wstream_fin", &wstream_fin, py::arg("fin"), py::arg("x"), py::arg("wt"), py::arg("y"), py::arg("p"),
+        py::arg("tickets"), py::arg("ss_in"), py::arg("eps"), py::arg("resid"), py::arg("nw"), py::arg("xn"),
+        py::arg("ss_out"), py::arg("positions"), py::arg("cos_sin"), py::arg("q_out"), py::arg("k_cache"),
+        py::arg("v_cache"), py::arg("slots"), py::arg("Hq"), py::arg("Hkv"), py::arg("max_splits"));
   m.def("skinny_plan", &skinny_plan);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("wstream_gemm_cfg", &wstream_gemm_cfg);

@@ -27,12 +27,218 @@
 
 namespace kafka {
 
-template <int MT, int KC, bool NT, int KW, bool PIN>
+// ---- Fused decode-layer epilogues (FIN template argument) -------------------------------------------------------
+// A pure decode layer used to be 9 launches: add+RMSNorm -> qkv -> RoPE/KV write -> cascade -> decode -> o ->
+// add+RMSNorm -> gate_up -> down. With FIN the GEMMs absorb the three small kernels (VERDICT r05 "Next" #1):
+//
+//   * deferred RMSNorm: rmsnorm(h) . W^T = r (.) ((h (.) w) . W^T) with r[m] = rsqrt(mean_k h[m,k]^2 + eps). The
+//     producer of h (the residual stream) writes X' = bf16(h (.) w) and, per 128-column block, the partial sums of
+//     h^2 (ss [N/128][M]); the consumer GEMM streams X' as its A operand and applies r in its epilogue.
+//   * split-K finisher: every split writes its fp32 tile as 16-B sc1 (write-through, agent-coherent) stores, waits
+//     for them (vmcnt 0), takes a per-column-block ticket (relaxed agent-scope atomic), and the LAST split of the
+//     column block sums the other S - 1 slabs with sc1 loads (compiler-tracked buffer loads, policy bit sc1) plus its
+//     own tile from LDS, then runs the fused epilogue and re-arms the ticket. No fence: a release fence at agent scope
+//     would write back this XCD's whole L2 from every workgroup (see attention.hip's ticket merge).
+//       FIN_RES  (o, down):  h = resid + sum; resid <- bf16(h); xn <- bf16(h (.) nw); ss_out[cb][m] = sum_cols h^2
+//       FIN_ROPE (qkv):      y = r (.) sum; rotate-half RoPE on q / k heads; q -> q_out, k / v -> the paged caches
+//   * FIN_GLU (gate_up, one split): silu(r g) * (r u) in the SwiGLU epilogue; r from ss_in, whose loads are issued
+//     at kernel start (their latency hides under the weight stream).
+// One 128-column workgroup tile is exactly one head (D = 128), so the RoPE partner d +- 64 is in the same
+// workgroup. Memory-model notes: common.h "Store / load scopes".
+enum { FIN_NONE = 0, FIN_RES = 1, FIN_ROPE = 2, FIN_GLU = 3 };
+
+struct FinArgs {
+  int* tickets;                 // [N / 128] zeroed once, re-armed by each column block's finisher
+  const float* ss_in;           // [nss][ss_ld] partial sums of h^2 of X's rows (nullptr: X is already normalised)
+  int nss, ss_ld;
+  float inv_d, eps;
+  bf16* resid;                  // FIN_RES: residual stream [M, N] (row stride ldr), updated in place
+  int64_t ldr;
+  const bf16* nw;               // FIN_RES: the next RMSNorm's weight [N]
+  bf16* xn;                     // FIN_RES: bf16(h (.) nw) [M, N] (row stride ldxn): the next GEMM's A operand
+  int64_t ldxn;
+  float* ss_out;                // FIN_RES: [N / 128][ss_out_ld]
+  int ss_out_ld;
+  const int64_t* positions;     // FIN_ROPE
+  const float* cos_sin;         // [max_pos, 128]: cos in [0, 64), sin in [64, 128)
+  bf16* q_out;                  // [M, Hq, 128] (row stride q_stride)
+  int64_t q_stride;
+  bf16* k_cache;                // [blocks, Hkv, 16, 128] in D/8 chunk planes (rope_kv.hip)
+  bf16* v_cache;                // [blocks, Hkv, 128, 16] V^T, key o at vt_pos(o)
+  const int64_t* slots;         // [M] (-1: no KV write) or nullptr
+  int Hq, Hkv;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
+  // raw buffer over 2 GiB from p (gfx9 dword3: untyped 32-bit data)
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+// 16-B agent-coherent load (cache policy sc1): not served from this XCD's L2. A compiler builtin, so hipcc's
+// waitcnt pass tracks it (unlike an inline-asm load).
+__device__ __forceinline__ f32x4 load16_sc1(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16));
+}
+
+__device__ __forceinline__ int vt_pos16(int o) { return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1); }
+
+// tp: this split's tile [4 column tiles][ROWS][32] fp32 in LDS; own column c of row m at tp[((c >> 5) * ROWS + m) * 32
+// + (c & 31)]. P: slabs [S][Mtot][N]; the finisher is split `by`.
+template <int S, int ROWS, int NTH>
+__device__ __forceinline__ void fin_res(const float* tp, const float* P, int by, int M, int Mtot, int N, int cb,
+                                        const FinArgs& fa, int tid) {
+  constexpr int O = S - 1;                                  // the other splits' slabs
+  constexpr int UB = O == 0 ? 8 : (28 / O >= 8 ? 8 : (28 / O < 1 ? 1 : 28 / O));  // <= 28 loads in flight
+  const auto rs = buf_rsrc(P);
+  const int c0 = cb * 128, nunits = M * 32;                 // unit = (row, 4 columns); a row = 32 consecutive lanes
+  for (int q0 = tid; q0 < nunits; q0 += NTH * UB) {
+    f32x4 pv[UB][O > 0 ? O : 1];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int q = min(q0 + u * NTH, nunits - 1);
+      const int row = q >> 5, g = q & 31;
+#pragma unroll
+      for (int j = 0; j < O; ++j) {
+        const int s = j < by ? j : j + 1;
+        pv[u][j] = load16_sc1(rs, (int)((((int64_t)s * Mtot + row) * N + c0 + 4 * g) * 4));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int q = q0 + u * NTH;
+      const bool valid = q < nunits;  // whole 32-lane rows are valid or not (nunits = 32 M)
+      const int row = min(q, nunits - 1) >> 5, g = q & 31;
+      f32x4 v = *reinterpret_cast<const f32x4*>(tp + ((g >> 3) * ROWS + row) * 32 + 4 * (g & 7));
+#pragma unroll
+      for (int j = 0; j < O; ++j) v += pv[u][j];
+      const int64_t col = c0 + 4 * g;
+      const bf16x4 rb = *reinterpret_cast<const bf16x4*>(fa.resid + row * fa.ldr + col);
+      const bf16x4 wb = *reinterpret_cast<const bf16x4*>(fa.nw + col);
+      bf16x4 hs, xo;
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        hs[j] = (bf16)(v[j] + (float)rb[j]);  // the residual stream is bf16 (as fused_add_rmsnorm)
+        const float hf = (float)hs[j];
+        ss += hf * hf;
+        xo[j] = (bf16)(hf * (float)wb[j]);
+      }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+      if (valid) {
+        *reinterpret_cast<bf16x4*>(fa.resid + row * fa.ldr + col) = hs;
+        *reinterpret_cast<bf16x4*>(fa.xn + row * fa.ldxn + col) = xo;
+        if (g == 0) fa.ss_out[(int64_t)cb * fa.ss_out_ld + row] = ss;
+      }
+    }
+  }
+}
+
+template <int S, int ROWS, int NTH>
+__device__ __forceinline__ void fin_rope(const float* tp, const float* P, int by, int M, int Mtot, int N, int cb,
+                                         const FinArgs& fa, int tid, const float* s_r, const int* s_pos,
+                                         const int64_t* s_slot) {
+  constexpr int O = S - 1;
+  const auto rs = buf_rsrc(P);
+  const int head = cb, c0 = cb * 128;
+  const bool is_q = head < fa.Hq, is_k = !is_q && head < fa.Hq + fa.Hkv;  // workgroup-uniform
+  if (is_q || is_k) {
+    // unit = (row, g < 16): columns 4g..4g+3 and their rotate-half partners 64 + 4g..
+    constexpr int UB = O == 0 ? 4 : (14 / O >= 4 ? 4 : (14 / O < 1 ? 1 : 14 / O));
+    const int nunits = M * 16;
+    for (int q0 = tid; q0 < nunits; q0 += NTH * UB) {
+      f32x4 pa[UB][O > 0 ? O : 1], pb[UB][O > 0 ? O : 1];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int q = min(q0 + u * NTH, nunits - 1);
+        const int row = q >> 4, g = q & 15;
+#pragma unroll
+        for (int j = 0; j < O; ++j) {
+          const int s = j < by ? j : j + 1;
+          const int64_t base = ((int64_t)s * Mtot + row) * N + c0 + 4 * g;
+          pa[u][j] = load16_sc1(rs, (int)(base * 4));
+          pb[u][j] = load16_sc1(rs, (int)((base + 64) * 4));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int q = q0 + u * NTH;
+        if (q >= nunits) continue;
+        const int row = q >> 4, g = q & 15;
+        f32x4 x1 = *reinterpret_cast<const f32x4*>(tp + ((g >> 3) * ROWS + row) * 32 + 4 * (g & 7));
+        f32x4 x2 = *reinterpret_cast<const f32x4*>(tp + ((2 + (g >> 3)) * ROWS + row) * 32 + 4 * (g & 7));
+#pragma unroll
+        for (int j = 0; j < O; ++j) {
+          x1 += pa[u][j];
+          x2 += pb[u][j];
+        }
+        const float rr = s_r[row];
+        const float* cs = fa.cos_sin + (int64_t)s_pos[row] * 128;
+        const f32x4 cv = *reinterpret_cast<const f32x4*>(cs + 4 * g);
+        const f32x4 sv = *reinterpret_cast<const f32x4*>(cs + 64 + 4 * g);
+        bf16x4 o1, o2;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float a = x1[j] * rr, b = x2[j] * rr;
+          o1[j] = (bf16)(a * cv[j] - b * sv[j]);
+          o2[j] = (bf16)(b * cv[j] + a * sv[j]);
+        }
+        if (is_q) {
+          bf16* dst = fa.q_out + row * fa.q_stride + head * 128 + 4 * g;
+          *reinterpret_cast<bf16x4*>(dst) = o1;
+          *reinterpret_cast<bf16x4*>(dst + 64) = o2;
+        } else {
+          const int64_t slot = s_slot[row];
+          if (slot >= 0) {
+            // element (key o, d) of a page at ((d >> 3) * 16 + o) * 8 + (d & 7): d = 4g..4g+3 is one 8-B run
+            bf16* dst = fa.k_cache + ((slot >> 4) * fa.Hkv + (head - fa.Hq)) * 2048 + (slot & 15) * 8 +
+                        (g >> 1) * 128 + 4 * (g & 1);
+            *reinterpret_cast<bf16x4*>(dst) = o1;
+            *reinterpret_cast<bf16x4*>(dst + 8 * 128) = o2;  // d + 64: 8 chunk planes further
+          }
+        }
+      }
+    }
+  } else {
+    // V head: unit = (row, g < 32), columns 4g..4g+3, scaled and transposed into the V^T page
+    constexpr int UB = O == 0 ? 8 : (28 / O >= 8 ? 8 : (28 / O < 1 ? 1 : 28 / O));
+    const int nunits = M * 32, vh = head - fa.Hq - fa.Hkv;
+    for (int q0 = tid; q0 < nunits; q0 += NTH * UB) {
+      f32x4 pv[UB][O > 0 ? O : 1];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int q = min(q0 + u * NTH, nunits - 1);
+        const int row = q >> 5, g = q & 31;
+#pragma unroll
+        for (int j = 0; j < O; ++j) {
+          const int s = j < by ? j : j + 1;
+          pv[u][j] = load16_sc1(rs, (int)((((int64_t)s * Mtot + row) * N + c0 + 4 * g) * 4));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int q = q0 + u * NTH;
+        if (q >= nunits) continue;
+        const int row = q >> 5, g = q & 31;
+        const int64_t slot = s_slot[row];
+        if (slot < 0) continue;
+        f32x4 v = *reinterpret_cast<const f32x4*>(tp + ((g >> 3) * ROWS + row) * 32 + 4 * (g & 7));
+#pragma unroll
+        for (int j = 0; j < O; ++j) v += pv[u][j];
+        const float rr = s_r[row];
+        bf16* dst = fa.v_cache + ((slot >> 4) * fa.Hkv + vh) * 2048 + vt_pos16((int)(slot & 15)) + (4 * g) * 16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dst[j * 16] = (bf16)(v[j] * rr);
+      }
+    }
+  }
+}
+
+template <int MT, int KC, bool NT, int KW, bool PIN, int FIN = FIN_NONE>
 __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                                  const bf16x8* __restrict__ Wt, int M, int N, int K,
                                                                  int ks, bf16* __restrict__ Y, int64_t ldy,
                                                                  float* __restrict__ P, int glu, int row_tiles,
-                                                                 int slab16) {
+                                                                 int slab16, FinArgs fa) {
   constexpr int NTH = 256 * KW;
   constexpr int ROWS = 32 * MT;
   constexpr int CPR = KC / 8;             // 16-B chunks per X row of one K chunk
@@ -71,6 +277,19 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
   const int nchunks = ks / KC;
   const bf16x8* wp =
       Wt + ((int64_t)(active ? nb : (N >> 5) - 1) * (K >> 4) + (k0 >> 4) + kh * KSW) * 64 + lane;
+
+  // FIN_GLU: this thread's share of the row-scale partials ss_in[j][row], issued before the stream (host-checked:
+  // tpr = a power of two >= nss / SSL threads per row, M * tpr <= NTH)
+  constexpr int SSL = FIN == FIN_GLU ? 4096 / NTH : 1;
+  float ssv[SSL];
+  int tpr = 1;
+  if constexpr (FIN == FIN_GLU) {
+    while (tpr * SSL < fa.nss) tpr <<= 1;
+    const int row = tid / tpr, j0 = (tid % tpr) * SSL;
+#pragma unroll
+    for (int i = 0; i < SSL; ++i)
+      ssv[i] = (fa.ss_in != nullptr && row < M && j0 + i < fa.nss) ? fa.ss_in[(int64_t)(j0 + i) * fa.ss_ld + row] : 0.f;
+  }
 
   bf16x8 xr[XL];
   auto load_x = [&](int ch) {
@@ -172,11 +391,89 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
           for (int i = 0; i < 16; ++i) acc[mt][i] += red[((((j - 1) * 4 + ct) * MT + mt) * 16 + i) * 64 + lane];
     }
   }
+  if constexpr (FIN == FIN_RES || FIN == FIN_ROPE) {
+    __shared__ int s_last;
+    __shared__ float s_r[FIN == FIN_ROPE ? ROWS : 1];
+    __shared__ int s_pos[FIN == FIN_ROPE ? ROWS : 1];
+    __shared__ int64_t s_slot[FIN == FIN_ROPE ? ROWS : 1];
+    const int S = gridDim.y, by = blockIdx.y;
+    float* tp = reinterpret_cast<float*>(&xs[0][0]);  // [4][ROWS][32] fp32: this split's tile (the X stage is dead)
+    if constexpr (FIN == FIN_ROPE) {
+      // every split loads the per-row scale / position / slot (their latency overlaps the slab store drain below;
+      // the finisher is not known yet)
+      if (tid < M) {
+        float s = 0.f;
+        if (fa.ss_in != nullptr)
+          for (int j = 0; j < fa.nss; ++j) s += fa.ss_in[(int64_t)j * fa.ss_ld + tid];
+        s_r[tid] = fa.ss_in != nullptr ? rsqrtf(s * fa.inv_d + fa.eps) : 1.f;
+        s_pos[tid] = (int)fa.positions[tid];
+        s_slot[tid] = fa.slots != nullptr ? fa.slots[tid] : -1;
+      }
+    }
+    __syncthreads();  // (the K-part fold's LDS reads are done)
+    if (kh == 0) {
+      float* tw = tp + ct * (ROWS * 32);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tw[(mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = acc[mt][i];
+      if (S > 1) {
+        // (one wave's LDS accesses complete in order: the reads below see its writes)
+#pragma unroll
+        for (int j = 0; j < ROWS / 8; ++j) {
+          const int q = j * 64 + lane, row = q >> 3, c4 = q & 7;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(tw + row * 32 + 4 * c4);
+          if (row < M) store16_slab(P + ((int64_t)by * Mtot + row) * N + cb * 128 + ct * 32 + 4 * c4, v);
+        }
+      }
+    }
+    if (S > 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this split's slab has reached the coherent level
+      __syncthreads();
+      if (tid == 0) {
+        int* tk = fa.tickets + cb;
+        const int t = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = t == S - 1;
+        if (t == S - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+      }
+      __syncthreads();
+      if (!s_last) return;  // workgroup-uniform
+    } else {
+      __syncthreads();
+    }
+#define KAFKA_FIN_S(S_)                                                                          \
+  case S_:                                                                                       \
+    if constexpr (FIN == FIN_RES)                                                                \
+      fin_res<S_, ROWS, NTH>(tp, P, by, M, Mtot, N, cb, fa, tid);                                \
+    else                                                                                         \
+      fin_rope<S_, ROWS, NTH>(tp, P, by, M, Mtot, N, cb, fa, tid, s_r, s_pos, s_slot);          \
+    break;
+    switch (S) {
+      KAFKA_FIN_S(1)
+      KAFKA_FIN_S(2)
+      KAFKA_FIN_S(4)
+      KAFKA_FIN_S(8)
+      default: break;  // (host-checked: S in {1, 2, 4, 8})
+    }
+#undef KAFKA_FIN_S
+    return;
+  }
   if (glu && P == nullptr) {
     // fused SwiGLU epilogue (weight tiles GLU-interleaved: tile 2j = gate rows [32j, 32j+32), tile 2j+1 = the
     // matching up rows): odd waves hand their up tile to the even wave of the pair through LDS, which writes
     // silu(gate) * up straight from the fp32 accumulators into Y [M, N/2]
     float* red = reinterpret_cast<float*>(&xs[0][0]);
+    // FIN_GLU: deferred RMSNorm of X, r[row] from the partials loaded at kernel start (1 without ss_in)
+    __shared__ float s_rg[FIN == FIN_GLU ? ROWS : 1];
+    if constexpr (FIN == FIN_GLU) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < SSL; ++i) s += ssv[i];
+      for (int o = tpr >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      const int row = tid / tpr;
+      if (tid % tpr == 0 && row < ROWS) s_rg[row] = fa.ss_in != nullptr ? rsqrtf(s * fa.inv_d + fa.eps) : 1.f;
+    }
+    auto rrow = [&](int m) { return FIN == FIN_GLU ? s_rg[m < ROWS ? m : ROWS - 1] : 1.f; };
     __syncthreads();
     if (kh == 0 && (ct & 1)) {
 #pragma unroll
@@ -193,8 +490,10 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            const float g = acc[mt][i], u = red[(((ct >> 1) * MT + mt) * 16 + i) * 64 + lane];
-            ty[(mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h) * 64 + (ct >> 1) * 32 + r] = (bf16)(g / (1.0f + __expf(-g)) * u);
+            const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            const float rr = rrow(m);
+            const float g = acc[mt][i] * rr, u = red[(((ct >> 1) * MT + mt) * 16 + i) * 64 + lane] * rr;
+            ty[m * 64 + (ct >> 1) * 32 + r] = (bf16)(g / (1.0f + __expf(-g)) * u);
           }
       }
       __syncthreads();
@@ -213,7 +512,8 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
         for (int i = 0; i < 16; ++i) {
           const int m = mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
           if (m < M) {
-            const float g = acc[mt][i], u = red[(((ct >> 1) * MT + mt) * 16 + i) * 64 + lane];
+            const float rr = rrow(m);
+            const float g = acc[mt][i] * rr, u = red[(((ct >> 1) * MT + mt) * 16 + i) * 64 + lane] * rr;
             Y[(int64_t)m * ldy + n] = (bf16)(g / (1.0f + __expf(-g)) * u);
           }
         }
@@ -501,10 +801,10 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   do {                                                                                                          \
     if (nt)                                                                                                     \
       wstream_gemm_kernel<MT_, KC_, true, KW_, PIN_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, \
-                                                                              glu, rt, wide);                   \
+                                                                              glu, rt, wide, FinArgs{});        \
     else                                                                                                        \
       wstream_gemm_kernel<MT_, KC_, false, KW_, PIN_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, \
-                                                                               glu, rt, wide);                  \
+                                                                               glu, rt, wide, FinArgs{});       \
   } while (0)
 #define KAFKA_WS_IF(MT_, KC_, KW_)                                      \
   if (mt == MT_ && kc == KC_ && kw == KW_) {                           \
@@ -523,6 +823,73 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   else return hipErrorInvalidValue;
 #undef KAFKA_WS_IF
 #undef KAFKA_WS
+  return hipGetLastError();
+}
+
+extern "C" int kafka_fin_args_size() { return (int)sizeof(FinArgs); }
+
+// Fused decode-layer GEMMs (FIN_RES / FIN_ROPE / FIN_GLU above): one row tile (M <= 128), N % 128 == 0, S in
+// {1, 2, 4, 8}; P = [S][M][N] fp32 scratch (unused for S == 1); FIN_GLU needs S == 1.
+extern "C" hipError_t kafka_launch_wstream_fin(int fin, const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K,
+                                              int mt, int kc, int splits, int kw, int pin, bf16* Y, int64_t ldy,
+                                              float* P, const FinArgs* fa_in, hipStream_t st) {
+  if (M < 1) return hipSuccess;
+  const FinArgs fa = *fa_in;
+  if (M > 32 * mt || M > 128 || N % 128 != 0 || K % (kc * splits) != 0) return hipErrorInvalidValue;
+  if (!(splits == 1 || splits == 2 || splits == 4 || splits == 8)) return hipErrorInvalidValue;
+  if (fin == FIN_GLU) {
+    const int ssl = 4096 / (256 * kw);
+    int tpr = 1;
+    while (tpr * ssl < fa.nss) tpr <<= 1;
+    if (splits != 1 || Y == nullptr || tpr > 64 || M * tpr > 256 * kw) return hipErrorInvalidValue;
+  } else if (fin == FIN_RES) {
+    if (fa.resid == nullptr || fa.nw == nullptr || fa.xn == nullptr || fa.ss_out == nullptr) return hipErrorInvalidValue;
+  } else if (fin == FIN_ROPE) {
+    if (fa.positions == nullptr || fa.cos_sin == nullptr || fa.q_out == nullptr || N != (fa.Hq + 2 * fa.Hkv) * 128 ||
+        (fa.slots != nullptr && (fa.k_cache == nullptr || fa.v_cache == nullptr)))
+      return hipErrorInvalidValue;
+  } else {
+    return hipErrorInvalidValue;
+  }
+  if (fin != FIN_GLU && ((splits > 1 && (P == nullptr || fa.tickets == nullptr))))
+    return hipErrorInvalidValue;
+  const dim3 grid(N / 128, splits);
+  const int ks = K / splits;
+  const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
+  float* p = splits > 1 ? P : nullptr;
+  static const int slab16 = [] {
+    const char* e = getenv("KAFKA_WSTREAM_SLAB16");
+    return e ? atoi(e) : 3;
+  }();
+  const int wide = (Y != nullptr && (ldy % 8 != 0 || reinterpret_cast<uintptr_t>(Y) % 16 != 0)) ? 0 : (slab16 & 2);
+  const int glu = fin == FIN_GLU ? 1 : 0;
+#define KAFKA_WF(MT_, KC_, KW_, PIN_, FIN_)                                                                      \
+  wstream_gemm_kernel<MT_, KC_, true, KW_, PIN_, FIN_><<<grid, 256 * KW_, 0, st>>>(X, ldx, wt, M, N, K, ks, Y, ldy, p, \
+                                                                                  glu, 1, wide, fa)
+#define KAFKA_WF_FIN(MT_, KC_, KW_, PIN_)                                    \
+  do {                                                                       \
+    if (fin == FIN_RES) KAFKA_WF(MT_, KC_, KW_, PIN_, FIN_RES);              \
+    else if (fin == FIN_ROPE) KAFKA_WF(MT_, KC_, KW_, PIN_, FIN_ROPE);       \
+    else KAFKA_WF(MT_, KC_, KW_, PIN_, FIN_GLU);                             \
+  } while (0)
+#define KAFKA_WF_IF(MT_, KC_, KW_)                                \
+  if (mt == MT_ && kc == KC_ && kw == KW_) {                      \
+    if (pin)                                                      \
+      KAFKA_WF_FIN(MT_, KC_, KW_, true);                          \
+    else                                                          \
+      KAFKA_WF_FIN(MT_, KC_, KW_, false);                         \
+  }
+  KAFKA_WF_IF(1, 256, 1)
+  else KAFKA_WF_IF(1, 256, 2)
+  else KAFKA_WF_IF(2, 256, 1)
+  else KAFKA_WF_IF(2, 256, 2)
+  else KAFKA_WF_IF(3, 256, 1)
+  else KAFKA_WF_IF(4, 128, 1)
+  else KAFKA_WF_IF(4, 128, 2)
+  else return hipErrorInvalidValue;
+#undef KAFKA_WF_IF
+#undef KAFKA_WF_FIN
+#undef KAFKA_WF
   return hipGetLastError();
 }
 

@@ -251,6 +251,76 @@ def test_stream_decode_gemm_matches_oracle():
     _check_against_oracle(m, prompts, outs)
 
 
+def test_fused_decode_layer_matches_unfused(monkeypatch):
+    """The fused decode layer (deferred RMSNorm in the GEMMs, RoPE + KV write in the QKV finisher, residual add in the
+    o / down finishers; models/llama.py _forward_fused) takes every decode step of the stream mode, and generation
+    agrees with the unfused layer and with the dense oracle."""
+    from kafka_llm_service_amd import ops
+    from kafka_llm_service_amd.models import llama
+
+    calls = {"qkv": 0, "res": 0, "glu": 0}
+    for name, key in (("linear_qkv_rope", "qkv"), ("linear_res", "res"), ("linear_glu_rs", "glu")):
+        orig = getattr(ops, name)
+
+        def wrap(*a, _o=orig, _k=key, **kw):
+            calls[_k] += 1
+            return _o(*a, **kw)
+        monkeypatch.setattr(ops, name, wrap)
+    eng = _engine(decode_gemm="stream")
+    prompts = _prompts(seed=10)
+    fused = eng.generate(prompts, GREEDY)
+    L = eng.model_cfg.num_layers
+    assert calls["qkv"] >= L and calls["res"] >= 2 * L - 1 and calls["glu"] >= L
+    _check_against_oracle(eng.model, prompts, fused)
+    monkeypatch.setattr(llama, "FUSED", False)
+    n = calls["qkv"]
+    plain = _engine(decode_gemm="stream", model=eng.model).generate(prompts, GREEDY)
+    assert calls["qkv"] == n  # the unfused path never enters the fused ops
+    assert plain == fused
+
+
+def test_fused_ops_cpu_reference():
+    """ops.linear_res / linear_qkv_rope / linear_glu_rs (CPU reference of the FIN epilogues) against the unfused op
+    chain: residual add + RMSNorm, then the projection of the normalised rows (RMSNorm deferred through ``ss``)."""
+    from kafka_llm_service_amd import ops
+    from kafka_llm_service_amd.ops import reference as ref
+
+    torch.manual_seed(3)
+    M, d, F, Hq, Hkv = 5, 512, 256, 2, 1
+    eps = 1e-5
+    resid = torch.randn(M, d).to(torch.bfloat16)
+    a = torch.randn(M, F).to(torch.bfloat16)
+    w_down = (torch.randn(d, F) * F ** -0.5).to(torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(d)).to(torch.bfloat16)
+    r0 = resid.clone()
+    xn = torch.empty(M, d, dtype=torch.bfloat16)
+    ss = torch.empty(d // 128, M)
+    ops.linear_res(a, ops.tile_weight(w_down), resid, nw, xn, ss)
+    s_ref = (r0.float() + a.float() @ w_down.float().t()).to(torch.bfloat16)
+    assert (resid.float() - s_ref.float()).abs().max() < 2e-2
+    assert torch.allclose(ss.sum(0), s_ref.float().pow(2).sum(1), rtol=1e-3)
+    normed = ref.rmsnorm(s_ref, nw, eps).float()
+    r = ops.fin_row_scale(ss, M, d, eps)
+    assert (xn.float() * r[:, None] - normed).abs().max() < 0.05
+    # QKV + RoPE of the deferred-normalised rows == rope_kv_write of the normalised rows' projection
+    w_qkv = (torch.randn((Hq + 2 * Hkv) * 128, d) * d ** -0.5).to(torch.bfloat16)
+    cs = ref.rope_cos_sin(256, 128, 500000.0)
+    pos = torch.tensor([3, 9, 0, 100, 255])
+    slots = torch.tensor([0, 17, -1, 5, 40])
+    q1, q2 = torch.empty(M, Hq, 128, dtype=torch.bfloat16), torch.empty(M, Hq, 128, dtype=torch.bfloat16)
+    k1, v1 = torch.zeros(4, Hkv, 16, 128, dtype=torch.bfloat16), torch.zeros(4, Hkv, 128, 16, dtype=torch.bfloat16)
+    k2, v2 = k1.clone(), v1.clone()
+    ops.linear_qkv_rope(xn, ops.tile_weight(w_qkv), ss, eps, pos, cs, q1, k1, v1, slots, Hq, Hkv)
+    ref.rope_kv_write((normed @ w_qkv.float().t()), pos, cs, q2, k2, v2, slots, Hq, Hkv)
+    for x1, x2 in ((q1, q2), (k1, k2), (v1, v2)):
+        assert (x1.float() - x2.float()).abs().max() < 0.05
+    # gate_up with the row scale == SwiGLU of the normalised rows' projection
+    w_gu = (torch.randn(2 * F, d) * d ** -0.5).to(torch.bfloat16)
+    y = ops.linear_glu_rs(xn, ops.tile_weight(w_gu, glu=True), ss, eps)
+    y_ref = ref.silu_mul(normed @ w_gu.float().t())
+    assert (y.float() - y_ref.float()).abs().max() < 0.05
+
+
 def test_stream_plan_rules(monkeypatch):
     """The decode GEMM plan (ops.stream_plan, mirrored from csrc kafka_wstream_plan): row tiles by step size (1 / 2 /
     3 / 4 x 32 rows), 128-deep chunks for four tiles, split-K grown toward the grid target."""

@@ -1,0 +1,202 @@
+"""The fused decode layer's GEMM epilogues (csrc/wstream_gemm.hip FIN_RES / FIN_ROPE / FIN_GLU) against plain
+PyTorch fp32 references of the unfused op chains, their buffers rewritten after readers on every XCD cached them, and
+the engine on the fused layer against the unfused one."""
+import pytest
+import torch
+
+from kafka_llm_service_amd import ops
+from kafka_llm_service_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+EPS = 1e-5
+
+
+def _close(a, b, atol, rtol=0.0, msg=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    tol = atol + rtol * b.abs().max().item()
+    assert err <= tol, f"{msg} max err {err} > {tol}"
+
+
+def _res_ref(a, w, resid, nw):
+    """fp32 reference of FIN_RES: (new residual bf16, xn = bf16(h * nw), per-128-column sums of h^2)."""
+    s = (resid.float().cpu() + a.float().cpu() @ w.float().cpu().t()).to(torch.bfloat16)
+    M, N = s.shape
+    return s, (s.float() * nw.float().cpu()).to(torch.bfloat16), s.float().pow(2).view(M, N // 128, 128).sum(-1).t()
+
+
+@pytest.mark.parametrize("M", [1, 17, 64, 96, 128])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336), (512, 1024)])
+def test_linear_res(cuda, M, N, K):
+    """o / down projection + residual add + the next norm's producer half, vs fp32."""
+    torch.manual_seed(21)
+    a = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) * K ** -0.5).to(torch.bfloat16)
+    resid = torch.randn(M, N, device=cuda, dtype=torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(N, device=cuda)).to(torch.bfloat16)
+    s_ref, xn_ref, ss_ref = _res_ref(a, w, resid, nw)
+    xn = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    ss = torch.full((N // 128, M + 3), float("nan"), device=cuda)
+    ops.linear_res(a, ops.tile_weight(w), resid, nw, xn, ss)
+    _close(resid, s_ref, atol=0.02, rtol=0.01, msg="residual")
+    _close(xn, xn_ref, atol=0.03, rtol=0.01, msg="xn")
+    _close(ss[:, :M], ss_ref, atol=1e-2, rtol=2e-3, msg="ss")
+    torch.cuda.synchronize()
+
+
+def _qkv_case(cuda, M, Hq, Hkv, d, seed):
+    g = torch.Generator().manual_seed(seed)
+    h = torch.randn(M, d, generator=g).to(torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(d, generator=g)).to(torch.bfloat16)
+    w = (torch.randn((Hq + 2 * Hkv) * 128, d, generator=g) * d ** -0.5).to(torch.bfloat16)
+    pos = torch.randint(0, 8000, (M,), generator=g)
+    nb = (M + 15) // 16 + 4
+    slots = torch.randperm(nb * 16, generator=g)[:M]
+    slots[::5] = -1  # rows whose KV is not written (e.g. a prefix-cached position)
+    return h, nw, w, pos, slots, nb
+
+
+@pytest.mark.parametrize("M", [1, 20, 64, 100, 128])
+@pytest.mark.parametrize("Hq,Hkv,d", [(32, 8, 4096), (4, 1, 512), (8, 2, 1024)])
+@pytest.mark.parametrize("deferred", [True, False])
+def test_linear_qkv_rope(cuda, M, Hq, Hkv, d, deferred):
+    """QKV GEMM with RoPE + paged KV write in its split-K finisher, on deferred-normalised rows (bf16(h * w) with the
+    row partials) or already-normalised ones, vs fp32 RMSNorm -> projection -> rope_kv_write."""
+    h, nw, w, pos, slots, nb = _qkv_case(cuda, M, Hq, Hkv, d, seed=M + d)
+    cs = ref.rope_cos_sin(8192, 128, 500000.0, {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                                 "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    normed = ref.rmsnorm(h, nw, EPS).float()
+    if deferred:
+        x = (h.float() * nw.float()).to(torch.bfloat16)
+        ss = torch.full((d // 128, M + 1), float("nan"))
+        ss[:, :M] = h.float().pow(2).view(M, d // 128, 128).sum(-1).t()
+        x_ref = normed
+    else:
+        x, ss = normed.to(torch.bfloat16), None
+        x_ref = x.float()
+    qr = torch.empty(M, Hq, 128, dtype=torch.bfloat16)
+    kr, vr = torch.zeros(nb, Hkv, 16, 128, dtype=torch.bfloat16), torch.zeros(nb, Hkv, 128, 16, dtype=torch.bfloat16)
+    ref.rope_kv_write(x_ref @ w.float().t(), pos, cs, qr, kr, vr, slots, Hq, Hkv)
+    q = torch.empty(M, Hq, 128, device=cuda, dtype=torch.bfloat16)
+    k = torch.zeros(nb, Hkv, 16, 128, device=cuda, dtype=torch.bfloat16)
+    v = torch.zeros(nb, Hkv, 128, 16, device=cuda, dtype=torch.bfloat16)
+    ops.linear_qkv_rope(x.to(cuda), ops.tile_weight(w.to(cuda)), None if ss is None else ss.to(cuda), EPS,
+                        pos.to(cuda), cs.to(cuda), q, k, v, slots.to(cuda), Hq, Hkv)
+    _close(q, qr, atol=0.04, rtol=0.01, msg="q")
+    _close(k, kr, atol=0.04, rtol=0.01, msg="k cache")
+    _close(v, vr, atol=0.04, rtol=0.01, msg="v cache")
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("M", [1, 33, 64, 100, 128])
+@pytest.mark.parametrize("N,K", [(28672, 4096), (2048, 512), (7168, 1024)])
+def test_linear_glu_rs(cuda, M, N, K):
+    """gate_up with the deferred row scale in the SwiGLU epilogue vs fp32 RMSNorm -> projection -> SwiGLU."""
+    g = torch.Generator().manual_seed(M + N)
+    h = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(K, generator=g)).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16)
+    ss = h.float().pow(2).view(M, K // 128, 128).sum(-1).t().contiguous()
+    x = (h.float() * nw.float()).to(torch.bfloat16)
+    y_ref = ref.silu_mul(ref.rmsnorm(h, nw, EPS).float() @ w.float().t())
+    y = ops.linear_glu_rs(x.to(cuda), ops.tile_weight(w.to(cuda), glu=True), ss.to(cuda), EPS)
+    _close(y, y_ref, atol=0.03, rtol=0.02, msg=f"glu_rs M={M}")
+    # without partials it is the plain fused SwiGLU
+    y1 = ops.linear_glu_rs(x.to(cuda), ops.tile_weight(w.to(cuda), glu=True), None, EPS)
+    _close(y1, ref.silu_mul(x.float() @ w.float().t()), atol=0.03, rtol=0.02, msg="glu no scale")
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("M", [17, 64, 128])
+def test_fused_layer_reused_buffers(cuda, M):
+    """One layer's fused chain — o (FIN_RES) -> gate_up (FIN_GLU) -> down (FIN_RES) -> qkv (FIN_ROPE) — run six times
+    over the SAME residual / xn / ss / q / cache buffers (and the allocator's recycled slab scratch), as the engine
+    does layer after layer, with torch kernels on every XCD reading (caching) each buffer between rounds; every round
+    is checked against fp32. The finishers read other splits' slabs with sc1 loads after a relaxed ticket: a stale
+    line anywhere would show here."""
+    torch.manual_seed(31)
+    d, F, Hq, Hkv = 4096, 14336, 32, 8
+    wo = (torch.randn(d, Hq * 128, device=cuda) * d ** -0.5).to(torch.bfloat16)
+    wgu = (torch.randn(2 * F, d, device=cuda) * d ** -0.5).to(torch.bfloat16)
+    wd = (torch.randn(d, F, device=cuda) * F ** -0.5).to(torch.bfloat16)
+    wqkv = (torch.randn((Hq + 2 * Hkv) * 128, d, device=cuda) * d ** -0.5).to(torch.bfloat16)
+    wot, wgut, wdt, wqt = ops.tile_weight(wo), ops.tile_weight(wgu, glu=True), ops.tile_weight(wd), ops.tile_weight(wqkv)
+    n1 = (1 + 0.1 * torch.randn(d, device=cuda)).to(torch.bfloat16)
+    n2 = (1 + 0.1 * torch.randn(d, device=cuda)).to(torch.bfloat16)
+    cs = ref.rope_cos_sin(4096, 128, 500000.0).to(cuda)
+    resid = torch.randn(M, d, device=cuda, dtype=torch.bfloat16)
+    xn = torch.empty(M, d, device=cuda, dtype=torch.bfloat16)
+    ss = torch.empty(2, d // 128, M, device=cuda)
+    q = torch.empty(M, Hq, 128, device=cuda, dtype=torch.bfloat16)
+    nb = (M + 15) // 16
+    kc = torch.zeros(nb, Hkv, 16, 128, device=cuda, dtype=torch.bfloat16)
+    vc = torch.zeros(nb, Hkv, 128, 16, device=cuda, dtype=torch.bfloat16)
+    pos = torch.arange(M, device=cuda) * 7
+    slots = torch.arange(M, device=cuda)
+    g = torch.Generator(device=cuda).manual_seed(8)
+    for it in range(6):
+        attn = torch.randn(M, Hq * 128, device=cuda, dtype=torch.bfloat16, generator=g)
+        r0 = resid.clone()
+        ops.linear_res(attn, wot, resid, n1, xn, ss[0], pool="fin_o")
+        s1, x1, ss1 = _res_ref(attn, wo, r0, n1)
+        _close(resid, s1, atol=0.02, rtol=0.01, msg=f"o residual round {it}")
+        _close(ss[0], ss1, atol=1e-2, rtol=2e-3, msg=f"o ss round {it}")
+        _ = (resid.float().sum() + xn.float().sum() + ss.sum()).item()  # readers on every XCD
+        a = ops.linear_glu_rs(xn, wgut, ss[0], EPS)
+        a_ref = ref.silu_mul(ref.rmsnorm(s1, n1.cpu(), EPS).float() @ wgu.float().cpu().t())
+        _close(a, a_ref, atol=0.03, rtol=0.02, msg=f"gate_up round {it}")
+        r1 = resid.clone()
+        ops.linear_res(a, wdt, resid, n2, xn, ss[1], pool="fin_down")
+        s2, x2, ss2 = _res_ref(a, wd, r1, n2)
+        _close(resid, s2, atol=0.02, rtol=0.01, msg=f"down residual round {it}")
+        _close(xn, x2, atol=0.03, rtol=0.01, msg=f"down xn round {it}")
+        _ = (resid.float().sum() + xn.float().sum() + ss.sum()).item()
+        ops.linear_qkv_rope(xn, wqt, ss[1], EPS, pos, cs, q, kc, vc, slots, Hq, Hkv)
+        qr = torch.empty(M, Hq, 128, dtype=torch.bfloat16)
+        kr, vr = torch.zeros_like(kc, device="cpu"), torch.zeros_like(vc, device="cpu")
+        ref.rope_kv_write(ref.rmsnorm(s2, n2.cpu(), EPS).float() @ wqkv.float().cpu().t(), pos.cpu(), cs.cpu(), qr,
+                          kr, vr, slots.cpu(), Hq, Hkv)
+        _close(q, qr, atol=0.04, rtol=0.01, msg=f"q round {it}")
+        _close(kc, kr, atol=0.04, rtol=0.01, msg=f"k round {it}")
+        _close(vc, vr, atol=0.04, rtol=0.01, msg=f"v round {it}")
+        _ = (q.float().sum() + kc.float().sum() + vc.float().sum()).item()
+    torch.cuda.synchronize()
+
+
+def test_engine_fused_layer_matches_unfused(cuda, monkeypatch):
+    """small-llama engine: the decode steps run the fused layer (the FIN ops are called), and every step's logits stay
+    within a bf16-rounding distance of the unfused layer's on the same inputs (same weights, same prompts, greedy)."""
+    from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
+    from kafka_llm_service_amd.engine.sequence import SamplingParams
+    from kafka_llm_service_amd.models import llama
+
+    n = {"qkv": 0}
+    orig = ops.linear_qkv_rope
+
+    def count(*a, **kw):
+        n["qkv"] += 1
+        return orig(*a, **kw)
+    monkeypatch.setattr(ops, "linear_qkv_rope", count)
+    sp = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
+    g = torch.Generator().manual_seed(4)
+    prompts = [torch.randint(0, 50000, (L,), generator=g).tolist() for L in (40, 300, 77)]
+    e1 = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", num_kv_blocks=2048, max_model_len=4096))
+    seen1 = []
+    o1 = e1.runner.sample_device
+    e1.runner.sample_device = lambda lg, s: (seen1.append(lg.float().cpu()), o1(lg, s))[1]
+    out1 = e1.generate(prompts, sp)
+    assert n["qkv"] >= e1.model_cfg.num_layers
+    monkeypatch.setattr(llama, "FUSED", False)
+    e2 = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", num_kv_blocks=2048, max_model_len=4096),
+                   model=e1.model)
+    seen2 = []
+    o2 = e2.runner.sample_device
+    e2.runner.sample_device = lambda lg, s: (seen2.append(lg.float().cpu()), o2(lg, s))[1]
+    out2 = e2.generate(prompts, sp)
+    # logits of the first decode step (identical inputs: same prompts, same prefill kernels) within bf16 noise
+    i = next(j for j, t in enumerate(seen1) if t.shape[0] == 3 and j > 0)
+    diff = (seen1[i] - seen2[i]).abs().max().item()
+    assert diff <= 0.1 * seen2[i].std().item() + 0.05, f"fused vs unfused logits differ by {diff}"
+    agree = sum(a == b for x, y in zip(out1, out2) for a, b in zip(x, y))
+    assert agree >= 0.8 * sum(len(x) for x in out2), (out1, out2)
