@@ -279,6 +279,11 @@ def main(argv=None):
         st = pstate.init_dp_attention(world, device=dev)
     else:
         st = pstate.init(tp=tp, device=dev) if world > 1 else pstate.get()
+        if tp > 1 and dev.startswith("cuda") and st.custom_status.get("tp") != "registered" and \
+                not os.environ.get("KAFKA_ALLOW_AR_FALLBACK"):
+            # the TP configuration is measured on the custom xGMI all-reduce; a silent RCCL fallback would report a
+            # different system (KAFKA_ALLOW_AR_FALLBACK=1 runs it anyway)
+            raise SystemExit(f"bench.py: TP={tp} custom all-reduce not registered ({st.custom_status.get('tp')})")
     from kafka_llm_service_amd.engine import tp_worker
     from kafka_llm_service_amd.engine.engine import EngineConfig, LLMEngine
     from kafka_llm_service_amd.engine.sequence import SamplingParams
@@ -477,6 +482,7 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
     me = _rank_record(args, rank, dev, timing, elapsed, eng)
     ranks = [me]
     dist_info = {"initialized": False}
+    pre = pstate.preflight()
     if world > 1:
         import torch.distributed as dist
 
@@ -554,6 +560,9 @@ def _report(args, world, rank, dev, eng, timing, elapsed, setup_s):
         "ranks": world,
         "per_rank": ranks,
         "dist": dist_info,
+        # pre-flight of the multi-GPU paths (parallel/state.py preflight): peer-access matrix of the visible devices,
+        # custom collective registration per group (or the fallback reason), RCCL version, group sizes
+        "preflight": pre,
     }
     if rank == 0:
         line = json.dumps(res)

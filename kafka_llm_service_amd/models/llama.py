@@ -48,9 +48,13 @@ PIPE_CHUNKS = max(1, int(os.environ.get("KAFKA_TP_PIPE_CHUNKS", "4")))
 PIPE_ROWS = 256
 SKINNY = frozenset(p for p in os.environ.get("KAFKA_SKINNY", "qkv,o,down").replace("+", ",").split(",")
                    if p in ("qkv", "o", "down", "gate_up"))  # gate_up: fused SwiGLU epilogue (A/B, not default)
-# Fused decode layer (forward -> _forward_fused; env KAFKA_FUSED_DECODE=0 turns it off for A/B runs): 6 launches per
-# layer instead of 9 — deferred RMSNorm and RoPE + KV write inside the streaming GEMMs' epilogues.
-FUSED = os.environ.get("KAFKA_FUSED_DECODE", "1") != "0"
+# Fused decode layer (forward -> _forward_fused; env KAFKA_FUSED_DECODE=1): 6 launches per layer instead of 9 —
+# deferred RMSNorm and RoPE + KV write inside the streaming GEMMs' split-K finishers. Correct (fp32-reference and
+# buffer-reuse tests) but OFF by default: each finisher is one workgroup reducing its column block's slabs at the
+# launch's tail (~220 KB through one CU at ~64 B/clk, plus drain / ticket / load round trips: 4-7 us), which costs
+# more than the RMSNorm / RoPE launches it removes — headline 8,231 vs 8,671 tok/s same box
+# (profiles/r06/fused/README.md).
+FUSED = os.environ.get("KAFKA_FUSED_DECODE", "0") == "1"
 _OVL: dict = {}
 _SEAM_DONE = object()  # forward(): the previous layer's overlapped seam already produced this layer's input
 

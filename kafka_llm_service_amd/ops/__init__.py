@@ -346,6 +346,21 @@ def fin_row_scale(ss: torch.Tensor | None, M: int, d: int, eps: float) -> torch.
     return torch.rsqrt(ss[:, :M].float().sum(0) / d + eps)
 
 
+FIN_POOLS = ("fin", "fin_o", "fin_down", "fin_qkv")
+
+
+def fin_errors(dev: torch.device) -> int:
+    """Error words of the fused GEMM finishers (the last int of each ticket pool; csrc FinArgs::err): nonzero if a
+    finisher ran on another XCD than the splits that kept their slabs in their home L2 — the result of that launch is
+    unreliable. Checked by the tests, smoke() and the bench (a host sync: not for the hot path)."""
+    n = 0
+    for pool in FIN_POOLS:
+        t = _TICKETS.get((dev, pool))
+        if t is not None:
+            n |= int(t[-1].item())
+    return n
+
+
 def _fin_scratch(x: torch.Tensor, N: int, max_splits: int) -> tuple[int, torch.Tensor | None]:
     M, K = x.shape
     plan = stream_plan(M, N, K, max_splits)
@@ -413,7 +428,8 @@ def linear_glu_rs(x: torch.Tensor, wt: torch.Tensor, ss_in: torch.Tensor | None,
 def fin_supported(M: int, d: int, n_qkv: int, n_gu: int, head_dim: int, kw_gate_up: int = 2) -> bool:
     """Shapes the fused decode layer takes (else the model runs the unfused kernels): one row tile, 128-column heads,
     the gate_up row-scale partials fit its threads."""
-    if not (1 <= M <= 128 and head_dim == 128 and d % 128 == 0 and n_qkv % 128 == 0 and n_gu % 128 == 0):
+    if not (1 <= M <= 128 and head_dim == 128 and d % 128 == 0 and d <= 4096 and n_qkv % 128 == 0 and
+            n_gu % 128 == 0):
         return False
     if stream_plan(M, n_gu, d, 1) is None or stream_plan(M, n_qkv, d) is None or stream_plan(M, d, d) is None:
         return False

@@ -67,6 +67,8 @@ struct FinArgs {
   bf16* v_cache;
   const int64_t* slots;
   int Hq, Hkv;
+  uint64_t* stamps;
+  int* err;
 };
 int kafka_fin_args_size();
 hipError_t kafka_launch_wstream_fin(int fin, const bf16* X, int64_t ldx, const bf16* Wt, int M, int N, int K, int mt,
@@ -511,7 +513,8 @@ static void wstream_fin(int64_t fin, at::Tensor x, at::Tensor wt, c10::optional<
                         c10::optional<at::Tensor> ss_out, c10::optional<at::Tensor> positions,
                         c10::optional<at::Tensor> cos_sin, c10::optional<at::Tensor> q_out,
                         c10::optional<at::Tensor> k_cache, c10::optional<at::Tensor> v_cache,
-                        c10::optional<at::Tensor> slots, int64_t Hq, int64_t Hkv, int64_t max_splits) {
+                        c10::optional<at::Tensor> slots, int64_t Hq, int64_t Hkv, int64_t max_splits,
+                        c10::optional<at::Tensor> stamps) {
   static const bool abi_ok = kafka_fin_args_size() == (int)sizeof(FinArgs);
   TORCH_CHECK(abi_ok, "wstream_fin: FinArgs layout differs between the kernel and the bindings");
   TORCH_CHECK(fin >= 1 && fin <= 3, "wstream_fin: fin must be 1, 2 or 3");
@@ -528,12 +531,15 @@ static void wstream_fin(int64_t fin, at::Tensor x, at::Tensor wt, c10::optional<
   TORCH_CHECK(tickets.is_cuda() && tickets.is_contiguous() && tickets.numel() >= N / 128, "wstream_fin: tickets");
   FinArgs fa{};
   fa.tickets = tickets.data_ptr<int>();
+  TORCH_CHECK(tickets.numel() >= N / 128 + 1, "wstream_fin: tickets need N/128 + 1 entries (the last one is the error word)");
+  fa.err = tickets.data_ptr<int>() + (tickets.numel() - 1);
   fa.eps = (float)eps;
   fa.inv_d = 1.f / (float)K;
   if (ss_in.has_value()) {
     CHECK_DT(ss_in.value(), at::kFloat);
-    TORCH_CHECK(ss_in->is_cuda() && ss_in->dim() == 2 && ss_in->stride(1) == 1 && ss_in->size(0) * 128 == K &&
-                    ss_in->size(1) >= M, "wstream_fin: ss_in must be fp32 [K/128, >= M]");
+    TORCH_CHECK(ss_in->is_cuda() && ss_in->dim() == 2 && (ss_in->stride(1) == 1 || ss_in->size(1) == 1) &&
+                    ss_in->size(0) * 128 == K && ss_in->size(1) >= M && ss_in->stride(0) >= M,
+                "wstream_fin: ss_in must be fp32 [K/128, >= M] with unit column stride");
     fa.ss_in = ss_in->data_ptr<float>();
     fa.nss = ss_in->size(0);
     fa.ss_ld = ss_in->stride(0);
@@ -597,6 +603,11 @@ static void wstream_fin(int64_t fin, at::Tensor x, at::Tensor wt, c10::optional<
     TORCH_CHECK(y->dim() == 2 && y->size(0) == M && y->size(1) == N / 2, "wstream_fin: y must be [M, N/2]");
     yp = bptr(y.value());
     ldy = y->stride(0);
+  }
+  if (stamps.has_value()) {
+    TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == at::kLong && stamps->is_contiguous() &&
+                    stamps->numel() >= (int64_t)(N / 128) * s * 8, "wstream_fin: stamps must be int64 [grid * 8]");
+    fa.stamps = reinterpret_cast<uint64_t*>(stamps->data_ptr<int64_t>());
   }
   CHECK_HIP(kafka_launch_wstream_fin((int)fin, bptr(x), x.stride(0), bptr(wt), M, N, K, mt, kc, s, kw, pin, yp, ldy, pp,
                                      &fa, cur_stream()));
@@ -974,7 +985,8 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("wstream_fin", &wstream_fin, py::arg("fin"), py::arg("x"), py::arg("wt"), py::arg("y"), py::arg("p"),
         py::arg("tickets"), py::arg("ss_in"), py::arg("eps"), py::arg("resid"), py::arg("nw"), py::arg("xn"),
         py::arg("ss_out"), py::arg("positions"), py::arg("cos_sin"), py::arg("q_out"), py::arg("k_cache"),
-        py::arg("v_cache"), py::arg("slots"), py::arg("Hq"), py::arg("Hkv"), py::arg("max_splits"));
+        py::arg("v_cache"), py::arg("slots"), py::arg("Hq"), py::arg("Hkv"), py::arg("max_splits"),
+        py::arg("stamps") = py::none());
   m.def("skinny_plan", &skinny_plan);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("wstream_gemm_cfg", &wstream_gemm_cfg);

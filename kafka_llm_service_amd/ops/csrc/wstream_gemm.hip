@@ -67,6 +67,8 @@ struct FinArgs {
   bf16* v_cache;                // [blocks, Hkv, 128, 16] V^T, key o at vt_pos(o)
   const int64_t* slots;         // [M] (-1: no KV write) or nullptr
   int Hq, Hkv;
+  uint64_t* stamps;             // optional phase stamps [grid][8] (100 MHz clock; benchmarks/fused_bench.py)
+  int* err;                     // bit 0 set if a finisher could not reach a split's slab (see "home XCD" below)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
@@ -79,13 +81,25 @@ __device__ __forceinline__ f32x4 load16_sc1(__amdgpu_buffer_rsrc_t rs, int byte_
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16));
 }
 
+__device__ __forceinline__ f32x4 load16_plain(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 0));
+}
+// split s's 16 B: from this XCD's L2 (the split stored it there: same XCD) or, flagged, agent-coherent (sc1)
+template <bool MIXED>
+__device__ __forceinline__ f32x4 load16_split(__amdgpu_buffer_rsrc_t rs, int byte_off, unsigned flags, int s) {
+  if constexpr (MIXED) {
+    if ((flags >> s) & 1u) return load16_sc1(rs, byte_off);
+  }
+  return load16_plain(rs, byte_off);
+}
+
 __device__ __forceinline__ int vt_pos16(int o) { return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1); }
 
 // tp: this split's tile [4 column tiles][ROWS][32] fp32 in LDS; own column c of row m at tp[((c >> 5) * ROWS + m) * 32
 // + (c & 31)]. P: slabs [S][Mtot][N]; the finisher is split `by`.
-template <int S, int ROWS, int NTH>
+template <int S, int ROWS, int NTH, bool MIXED>
 __device__ __forceinline__ void fin_res(const float* tp, const float* P, int by, int M, int Mtot, int N, int cb,
-                                        const FinArgs& fa, int tid) {
+                                        const FinArgs& fa, int tid, unsigned flags) {
   constexpr int O = S - 1;                                  // the other splits' slabs
   constexpr int UB = O == 0 ? 8 : (28 / O >= 8 ? 8 : (28 / O < 1 ? 1 : 28 / O));  // <= 28 loads in flight
   const auto rs = buf_rsrc(P);
@@ -99,7 +113,7 @@ __device__ __forceinline__ void fin_res(const float* tp, const float* P, int by,
 #pragma unroll
       for (int j = 0; j < O; ++j) {
         const int s = j < by ? j : j + 1;
-        pv[u][j] = load16_sc1(rs, (int)((((int64_t)s * Mtot + row) * N + c0 + 4 * g) * 4));
+        pv[u][j] = load16_split<MIXED>(rs, (int)((((int64_t)s * Mtot + row) * N + c0 + 4 * g) * 4), flags, s);
       }
     }
 #pragma unroll
@@ -133,10 +147,10 @@ __device__ __forceinline__ void fin_res(const float* tp, const float* P, int by,
   }
 }
 
-template <int S, int ROWS, int NTH>
+template <int S, int ROWS, int NTH, bool MIXED>
 __device__ __forceinline__ void fin_rope(const float* tp, const float* P, int by, int M, int Mtot, int N, int cb,
                                          const FinArgs& fa, int tid, const float* s_r, const int* s_pos,
-                                         const int64_t* s_slot) {
+                                         const int64_t* s_slot, unsigned flags) {
   constexpr int O = S - 1;
   const auto rs = buf_rsrc(P);
   const int head = cb, c0 = cb * 128;
@@ -155,8 +169,8 @@ __device__ __forceinline__ void fin_rope(const float* tp, const float* P, int by
         for (int j = 0; j < O; ++j) {
           const int s = j < by ? j : j + 1;
           const int64_t base = ((int64_t)s * Mtot + row) * N + c0 + 4 * g;
-          pa[u][j] = load16_sc1(rs, (int)(base * 4));
-          pb[u][j] = load16_sc1(rs, (int)((base + 64) * 4));
+          pa[u][j] = load16_split<MIXED>(rs, (int)(base * 4), flags, s);
+          pb[u][j] = load16_split<MIXED>(rs, (int)((base + 64) * 4), flags, s);
         }
       }
 #pragma unroll
@@ -211,7 +225,7 @@ __device__ __forceinline__ void fin_rope(const float* tp, const float* P, int by
 #pragma unroll
         for (int j = 0; j < O; ++j) {
           const int s = j < by ? j : j + 1;
-          pv[u][j] = load16_sc1(rs, (int)((((int64_t)s * Mtot + row) * N + c0 + 4 * g) * 4));
+          pv[u][j] = load16_split<MIXED>(rs, (int)((((int64_t)s * Mtot + row) * N + c0 + 4 * g) * 4), flags, s);
         }
       }
 #pragma unroll
@@ -278,6 +292,14 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
   const bf16x8* wp =
       Wt + ((int64_t)(active ? nb : (N >> 5) - 1) * (K >> 4) + (k0 >> 4) + kh * KSW) * 64 + lane;
 
+  // phase stamps (FinArgs::stamps, benchmarks only): 0 start, 1 main loop done, 2 slab stores drained, 3 ticket
+  // taken (finisher), 4 finisher done
+  auto stamp = [&](int k) {
+    if constexpr (FIN != FIN_NONE)
+      if (fa.stamps != nullptr && tid == 0)
+        fa.stamps[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   // FIN_GLU: this thread's share of the row-scale partials ss_in[j][row], issued before the stream (host-checked:
   // tpr = a power of two >= nss / SSL threads per row, M * tpr <= NTH)
   constexpr int SSL = FIN == FIN_GLU ? 4096 / NTH : 1;
@@ -398,16 +420,39 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
     __shared__ int64_t s_slot[FIN == FIN_ROPE ? ROWS : 1];
     const int S = gridDim.y, by = blockIdx.y;
     float* tp = reinterpret_cast<float*>(&xs[0][0]);  // [4][ROWS][32] fp32: this split's tile (the X stage is dead)
+    // Home XCD: workgroups are dealt to the 8 XCDs round-robin (linear id % 8), so with N / 128 a multiple of 8 every
+    // split of column block cb runs on XCD cb % 8 and the finisher is one of them: the slabs can go through that XCD's
+    // L2 (plain stores, L2-hit loads) instead of the agent-coherent level. Each split CHECKS it (hardware XCC_ID);
+    // one that is not home stores sc1 and flags its bit in the ticket (bits 8 + s), so the finisher loads that slab
+    // sc1. A finisher that is itself not home cannot reach the home L2 of the others: it sets fa.err.
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xfu;  // hwreg(HW_REG_XCC_ID, 0, 4)
+    const bool home = (gridDim.x & 7) == 0 && (int)xcc == (lin & 7);
+    __shared__ unsigned s_flags;
+    stamp(1);
+    // FIN_ROPE: every split loads the per-row partials / position / slot (the finisher is not known yet) into
+    // registers before its slab stores and parks them in LDS after issuing them, so the load round trip overlaps the
+    // store drain. Thread (row = tid % ROWS, part = tid / ROWS) sums partials part, part + PARTS, ... (nss <= 32,
+    // host-checked); the PARTS sums of a row are added in a fixed order (deterministic).
+    constexpr int PARTS = NTH / ROWS >= 8 ? 8 : (NTH / ROWS >= 4 ? 4 : (NTH / ROWS >= 2 ? 2 : 1));
+    constexpr int JL = FIN == FIN_ROPE ? 32 / PARTS : 1;
+    __shared__ float s_ssp[FIN == FIN_ROPE ? PARTS : 1][FIN == FIN_ROPE ? ROWS : 1];
+    const int prow = tid % ROWS, ppart = tid / ROWS;
+    const bool pact = FIN == FIN_ROPE && ppart < PARTS && prow < M;
+    float ssv2[JL];
+    int posv = 0;
+    int64_t slotv = -1;
     if constexpr (FIN == FIN_ROPE) {
-      // every split loads the per-row scale / position / slot (their latency overlaps the slab store drain below;
-      // the finisher is not known yet)
-      if (tid < M) {
-        float s = 0.f;
-        if (fa.ss_in != nullptr)
-          for (int j = 0; j < fa.nss; ++j) s += fa.ss_in[(int64_t)j * fa.ss_ld + tid];
-        s_r[tid] = fa.ss_in != nullptr ? rsqrtf(s * fa.inv_d + fa.eps) : 1.f;
-        s_pos[tid] = (int)fa.positions[tid];
-        s_slot[tid] = fa.slots != nullptr ? fa.slots[tid] : -1;
+      if (pact) {
+#pragma unroll
+        for (int u = 0; u < JL; ++u) {
+          const int j = ppart + PARTS * u;
+          ssv2[u] = (fa.ss_in != nullptr && j < fa.nss) ? fa.ss_in[(int64_t)j * fa.ss_ld + prow] : 0.f;
+        }
+        if (ppart == 0) {
+          posv = (int)fa.positions[prow];
+          slotv = fa.slots != nullptr ? fa.slots[prow] : -1;
+        }
       }
     }
     __syncthreads();  // (the K-part fold's LDS reads are done)
@@ -423,30 +468,73 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
         for (int j = 0; j < ROWS / 8; ++j) {
           const int q = j * 64 + lane, row = q >> 3, c4 = q & 7;
           const f32x4 v = *reinterpret_cast<const f32x4*>(tw + row * 32 + 4 * c4);
-          if (row < M) store16_slab(P + ((int64_t)by * Mtot + row) * N + cb * 128 + ct * 32 + 4 * c4, v);
+          if (row < M) {
+            float* dst = P + ((int64_t)by * Mtot + row) * N + cb * 128 + ct * 32 + 4 * c4;
+            if (home)
+              *reinterpret_cast<f32x4*>(dst) = v;  // into this XCD's L2, where the finisher will read it
+            else
+              store16_slab(dst, v);
+          }
         }
+      }
+    }
+    if constexpr (FIN == FIN_ROPE) {
+      if (pact) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int u = 0; u < JL; ++u) sacc += ssv2[u];
+        s_ssp[ppart][prow] = sacc;
+        if (ppart == 0) {
+          s_pos[prow] = posv;
+          s_slot[prow] = slotv;
+        }
+      }
+      __syncthreads();
+      if (tid < M) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int p = 0; p < PARTS; ++p) sacc += s_ssp[p][tid];
+        s_r[tid] = fa.ss_in != nullptr ? rsqrtf(sacc * fa.inv_d + fa.eps) : 1.f;
       }
     }
     if (S > 1) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this split's slab has reached the coherent level
+      stamp(2);
       __syncthreads();
       if (tid == 0) {
         int* tk = fa.tickets + cb;
-        const int t = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = t == S - 1;
-        if (t == S - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+        const int add = 1 + (home ? 0 : (256 << by));
+        const int t = __hip_atomic_fetch_add(tk, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int tot = t + add;
+        s_last = (tot & 255) == S;
+        s_flags = (unsigned)(tot >> 8) & 255u;
+        if ((tot & 255) == S) {
+          __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+          const unsigned others = ((1u << S) - 1u) & ~(1u << by);
+          if (!home && (s_flags & others) != others && fa.err != nullptr) atomicOr(fa.err, 1);
+        }
       }
       __syncthreads();
       if (!s_last) return;  // workgroup-uniform
+      stamp(3);
     } else {
+      if (tid == 0) s_flags = 0;
       __syncthreads();
     }
-#define KAFKA_FIN_S(S_)                                                                          \
-  case S_:                                                                                       \
-    if constexpr (FIN == FIN_RES)                                                                \
-      fin_res<S_, ROWS, NTH>(tp, P, by, M, Mtot, N, cb, fa, tid);                                \
-    else                                                                                         \
-      fin_rope<S_, ROWS, NTH>(tp, P, by, M, Mtot, N, cb, fa, tid, s_r, s_pos, s_slot);          \
+    const unsigned flags = s_flags;
+#define KAFKA_FIN_S(S_)                                                                                     \
+  case S_:                                                                                                  \
+    if constexpr (FIN == FIN_RES) {                                                                         \
+      if (flags == 0)                                                                                       \
+        fin_res<S_, ROWS, NTH, false>(tp, P, by, M, Mtot, N, cb, fa, tid, 0u);                              \
+      else                                                                                                  \
+        fin_res<S_, ROWS, NTH, true>(tp, P, by, M, Mtot, N, cb, fa, tid, flags);                            \
+    } else {                                                                                                \
+      if (flags == 0)                                                                                       \
+        fin_rope<S_, ROWS, NTH, false>(tp, P, by, M, Mtot, N, cb, fa, tid, s_r, s_pos, s_slot, 0u);         \
+      else                                                                                                  \
+        fin_rope<S_, ROWS, NTH, true>(tp, P, by, M, Mtot, N, cb, fa, tid, s_r, s_pos, s_slot, flags);       \
+    }                                                                                                       \
     break;
     switch (S) {
       KAFKA_FIN_S(1)
@@ -456,6 +544,10 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
       default: break;  // (host-checked: S in {1, 2, 4, 8})
     }
 #undef KAFKA_FIN_S
+    if (fa.stamps != nullptr) {
+      __syncthreads();
+      stamp(4);
+    }
     return;
   }
   if (glu && P == nullptr) {
@@ -845,7 +937,7 @@ extern "C" hipError_t kafka_launch_wstream_fin(int fin, const bf16* X, int64_t l
   } else if (fin == FIN_RES) {
     if (fa.resid == nullptr || fa.nw == nullptr || fa.xn == nullptr || fa.ss_out == nullptr) return hipErrorInvalidValue;
   } else if (fin == FIN_ROPE) {
-    if (fa.positions == nullptr || fa.cos_sin == nullptr || fa.q_out == nullptr || N != (fa.Hq + 2 * fa.Hkv) * 128 ||
+    if (fa.nss > 32 || fa.positions == nullptr || fa.cos_sin == nullptr || fa.q_out == nullptr || N != (fa.Hq + 2 * fa.Hkv) * 128 ||
         (fa.slots != nullptr && (fa.k_cache == nullptr || fa.v_cache == nullptr)))
       return hipErrorInvalidValue;
   } else {

@@ -16,7 +16,7 @@ The reference service has no collectives at all; this module i
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from datetime import timedelta
 
 import torch
@@ -40,6 +40,8 @@ class ParallelState:
     ep_rank: int = 0
     ep_group: object = None
     ep_cpu_group: object = None  # gloo: the per-step agreement on the all-to-all capacity
+    # custom IPC collective per group: "registered", "off (...)" or "fallback: <reason>" (preflight())
+    custom_status: dict = field(default_factory=dict)
 
     @property
     def is_tp_leader(self) -> bool:
@@ -87,7 +89,13 @@ def init(tp: int = 1, backend: str | None = None, device: str | None = None) -> 
                 if rank in ranks:
                     st.tp_group, st.cpu_group = pg, cpg
             on_gpu = (device or "").startswith("cuda") or (device is None and torch.cuda.is_available())
-            if on_gpu and tp in (2, 4, 8) and os.environ.get("KAFKA_CUSTOM_AR", "1") == "1":
+            if not on_gpu:
+                st.custom_status["tp"] = "off (not a GPU group)"
+            elif tp not in (2, 4, 8):
+                st.custom_status["tp"] = f"off (tp={tp} unsupported)"
+            elif os.environ.get("KAFKA_CUSTOM_AR", "1") != "1":
+                st.custom_status["tp"] = "off (KAFKA_CUSTOM_AR=0)"
+            else:
                 _register_custom_ar(st, tp)
     _STATE = st
     return st
@@ -113,6 +121,7 @@ def init_dp_attention(ep: int, backend: str | None = None, device: str | None = 
         if st.rank in ranks:
             st.ep_group, st.ep_cpu_group = pg, cpg
     on_gpu = (device or "").startswith("cuda") or (device is None and torch.cuda.is_available())
+    st.custom_status["ep"] = "off (not a GPU group)" if not on_gpu else f"off (ep={ep} unsupported)"
     if on_gpu and ep in (2, 4, 8) and os.environ.get("KAFKA_CUSTOM_AR", "1") == "1":
         import logging
 
@@ -121,7 +130,9 @@ def init_dp_attention(ep: int, backend: str | None = None, device: str | None = 
 
         try:
             comm.register_custom(st.ep_group, CustomAllReduce(st.ep_cpu_group, st.ep_rank, ep))
-        except CustomAllReduceUnavailable:
+            st.custom_status["ep"] = "registered"
+        except CustomAllReduceUnavailable as e:
+            st.custom_status["ep"] = f"fallback: {e}"
             logging.getLogger("kafka.parallel").exception("IPC all-to-all unavailable; using the library collective")
     _STATE = st
     return st
@@ -139,8 +150,41 @@ def _register_custom_ar(st: ParallelState, tp: int) -> None:
 
     try:
         comm.register_custom(st.tp_group, CustomAllReduce(st.cpu_group, st.tp_rank, tp))
-    except CustomAllReduceUnavailable:
+        st.custom_status["tp"] = "registered"
+    except CustomAllReduceUnavailable as e:
+        st.custom_status["tp"] = f"fallback: {e}"
         logging.getLogger("kafka.parallel").exception("custom all-reduce unavailable; using RCCL for every message")
+        if os.environ.get("KAFKA_REQUIRE_CUSTOM_AR", "0") == "1":
+            raise
+
+
+def preflight() -> dict:
+    """What a first multi-GPU run needs to explain itself (bench.py puts it in its JSON line): the peer-access matrix
+    of the visible devices (xGMI P2P, which the custom all-reduce's IPC buffers need), each group's custom-collective
+    status (registered / off / fallback with the reason), the RCCL version and the group sizes."""
+    st = _STATE
+    out: dict = {"custom_collectives": dict(st.custom_status), "tp": st.tp, "ep": st.ep, "world": st.world}
+    try:
+        v = torch.cuda.nccl.version() if torch.cuda.is_available() else None
+        out["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else v
+    except Exception as e:  # noqa: BLE001 — informational
+        out["rccl_version"] = f"unavailable: {type(e).__name__}"
+    if torch.cuda.is_available():
+        n = torch.cuda.device_count()
+        out["visible_devices"] = n
+        out["peer_access"] = [[1 if i == j else int(torch.cuda.can_device_access_peer(i, j)) for j in range(n)]
+                              for i in range(n)]
+    else:
+        out["visible_devices"] = 0
+        out["peer_access"] = []
+    if dist.is_initialized():
+        out["world_backend"] = dist.get_backend()
+        for name in ("tp", "ep"):
+            g = getattr(st, f"{name}_group", None)
+            if g is not None:
+                out[f"{name}_backend"] = dist.get_backend(g)
+                out[f"{name}_group_size"] = dist.get_world_size(g)
+    return out
 
 
 def custom_ar():

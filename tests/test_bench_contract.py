@@ -64,6 +64,13 @@ def _check_ranks(d, n, tp):
         assert d["dist"]["tp_group_size"] == tp
     else:
         assert "tp_group_size" not in d["dist"]
+    # pre-flight fields a first 8-GPU run explains itself with: peer matrix, collective registration, RCCL version
+    pre = d["preflight"]
+    assert pre["world"] == n and pre["tp"] == tp and "rccl_version" in pre
+    assert isinstance(pre["peer_access"], list) and pre["visible_devices"] == len(pre["peer_access"])
+    assert pre["world_backend"] == "gloo"
+    if tp > 1:
+        assert pre["tp_group_size"] == tp and pre["custom_collectives"]["tp"].startswith("off")
 
 
 @pytest.mark.timeout(900)

@@ -266,6 +266,7 @@ def test_fused_decode_layer_matches_unfused(monkeypatch):
             calls[_k] += 1
             return _o(*a, **kw)
         monkeypatch.setattr(ops, name, wrap)
+    monkeypatch.setattr(llama, "FUSED", True)
     eng = _engine(decode_gemm="stream")
     prompts = _prompts(seed=10)
     fused = eng.generate(prompts, GREEDY)

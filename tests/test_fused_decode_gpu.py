@@ -42,7 +42,7 @@ def test_linear_res(cuda, M, N, K):
     _close(resid, s_ref, atol=0.02, rtol=0.01, msg="residual")
     _close(xn, xn_ref, atol=0.03, rtol=0.01, msg="xn")
     _close(ss[:, :M], ss_ref, atol=1e-2, rtol=2e-3, msg="ss")
-    torch.cuda.synchronize()
+    assert ops.fin_errors(cuda) == 0
 
 
 def _qkv_case(cuda, M, Hq, Hkv, d, seed):
@@ -86,7 +86,7 @@ def test_linear_qkv_rope(cuda, M, Hq, Hkv, d, deferred):
     _close(q, qr, atol=0.04, rtol=0.01, msg="q")
     _close(k, kr, atol=0.04, rtol=0.01, msg="k cache")
     _close(v, vr, atol=0.04, rtol=0.01, msg="v cache")
-    torch.cuda.synchronize()
+    assert ops.fin_errors(cuda) == 0
 
 
 @pytest.mark.parametrize("M", [1, 33, 64, 100, 128])
@@ -113,8 +113,8 @@ def test_fused_layer_reused_buffers(cuda, M):
     """One layer's fused chain — o (FIN_RES) -> gate_up (FIN_GLU) -> down (FIN_RES) -> qkv (FIN_ROPE) — run six times
     over the SAME residual / xn / ss / q / cache buffers (and the allocator's recycled slab scratch), as the engine
     does layer after layer, with torch kernels on every XCD reading (caching) each buffer between rounds; every round
-    is checked against fp32. The finishers read other splits' slabs with sc1 loads after a relaxed ticket: a stale
-    line anywhere would show here."""
+    is checked against fp32. The finishers read other splits' slabs from their home XCD's L2 (or, flagged, sc1) after
+    a relaxed ticket: a stale line anywhere would show here."""
     torch.manual_seed(31)
     d, F, Hq, Hkv = 4096, 14336, 32, 8
     wo = (torch.randn(d, Hq * 128, device=cuda) * d ** -0.5).to(torch.bfloat16)
@@ -161,7 +161,7 @@ def test_fused_layer_reused_buffers(cuda, M):
         _close(kc, kr, atol=0.04, rtol=0.01, msg=f"k round {it}")
         _close(vc, vr, atol=0.04, rtol=0.01, msg=f"v round {it}")
         _ = (q.float().sum() + kc.float().sum() + vc.float().sum()).item()
-    torch.cuda.synchronize()
+    assert ops.fin_errors(cuda) == 0
 
 
 def test_engine_fused_layer_matches_unfused(cuda, monkeypatch):
@@ -178,6 +178,7 @@ def test_engine_fused_layer_matches_unfused(cuda, monkeypatch):
         n["qkv"] += 1
         return orig(*a, **kw)
     monkeypatch.setattr(ops, "linear_qkv_rope", count)
+    monkeypatch.setattr(llama, "FUSED", True)
     sp = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
     g = torch.Generator().manual_seed(4)
     prompts = [torch.randint(0, 50000, (L,), generator=g).tolist() for L in (40, 300, 77)]
@@ -198,5 +199,6 @@ def test_engine_fused_layer_matches_unfused(cuda, monkeypatch):
     i = next(j for j, t in enumerate(seen1) if t.shape[0] == 3 and j > 0)
     diff = (seen1[i] - seen2[i]).abs().max().item()
     assert diff <= 0.1 * seen2[i].std().item() + 0.05, f"fused vs unfused logits differ by {diff}"
+    assert ops.fin_errors(cuda) == 0
     agree = sum(a == b for x, y in zip(out1, out2) for a, b in zip(x, y))
     assert agree >= 0.8 * sum(len(x) for x in out2), (out1, out2)
