@@ -361,6 +361,47 @@ def fin_errors(dev: torch.device) -> int:
     return n
 
 
+# KAFKA_FIN_STAMPS=<file.json>: every fused GEMM launch records per-workgroup phase stamps (csrc FinArgs::stamps) and
+# the anatomy of the last launches per kind is written to that file at exit (benchmarks/fused_bench.py reads the same
+# stamps in isolation; this is the in-engine view)
+_FIN_STAMPS = os.environ.get("KAFKA_FIN_STAMPS")
+_STAMP_LOG: list = []
+
+
+def _stamps_for(kind: str, grid: int, dev: torch.device):
+    if not _FIN_STAMPS:
+        return None
+    if not _STAMP_LOG:
+        import atexit
+        atexit.register(_dump_stamps)
+    t = torch.zeros(grid * 8 + 8, dtype=torch.long, device=dev)
+    _STAMP_LOG.append((kind, grid, t))
+    del _STAMP_LOG[:-2000]
+    return t
+
+
+def _dump_stamps() -> None:
+    import json
+    import statistics
+    out: dict = {}
+    for kind, grid, t in _STAMP_LOG:
+        a = t[:grid * 8].view(grid, 8).cpu().double() / 100.0
+        a = a - a[:, 0].min()
+        fin = a[:, 4] > 0
+        rec = {"loop_max": float((a[:, 1] - a[:, 0]).max()), "last_loop_end": float(a[:, 1].max()),
+               "first_start_to_last_start": float(a[:, 0].max())}
+        if fin.any():
+            rec.update(end=float(a[fin, 4].max()), tail=float(a[fin, 4].max() - a[:, 1].max()),
+                       fin_med=float((a[fin, 4] - a[fin, 3]).median()),
+                       drain_med=float((a[a[:, 2] > 0, 2] - a[a[:, 2] > 0, 1]).median()) if (a[:, 2] > 0).any() else 0.0,
+                       ticket_med=float((a[fin, 3] - a[fin, 2]).median()))
+        out.setdefault(f"{kind}/grid{grid}", []).append(rec)
+    summary = {k: {f: round(statistics.median(r[f] for r in v if f in r), 2) for f in v[-1]} | {"calls": len(v)}
+               for k, v in out.items()}
+    with open(_FIN_STAMPS, "w") as f:
+        json.dump(summary, f, indent=1)
+
+
 def _fin_scratch(x: torch.Tensor, N: int, max_splits: int) -> tuple[int, torch.Tensor | None]:
     M, K = x.shape
     plan = stream_plan(M, N, K, max_splits)
@@ -378,7 +419,8 @@ def linear_res(x: torch.Tensor, wt: torch.Tensor, resid: torch.Tensor, nw: torch
     if _gpu(x):
         S, p = _fin_scratch(x, N, max_splits)
         ext().wstream_fin(1, x, wt, None, p, _tickets(x.device, N // 128 + 1, pool), None, 0.0, resid, nw, xn, ss_out,
-                          None, None, None, None, None, None, 0, 0, int(max_splits))
+                          None, None, None, None, None, None, 0, 0, int(max_splits),
+                          _stamps_for(pool, N // 128 * S, x.device))
         return
     M = x.shape[0]
     y = x.float() @ untile_weight(wt).float().t()
@@ -399,7 +441,7 @@ def linear_qkv_rope(x: torch.Tensor, wt: torch.Tensor, ss_in: torch.Tensor | Non
         S, p = _fin_scratch(x, N, max_splits)
         ext().wstream_fin(2, x, wt, None, p, _tickets(x.device, N // 128 + 1, pool), ss_in, float(eps), None, None,
                           None, None, positions, cos_sin, q_out, k_cache, v_cache, slot_mapping, int(Hq), int(Hkv),
-                          int(max_splits))
+                          int(max_splits), _stamps_for(pool, N // 128 * S, x.device))
         return
     y = x.float() @ untile_weight(wt).float().t()
     r = fin_row_scale(ss_in, M, K, eps)
@@ -415,7 +457,7 @@ def linear_glu_rs(x: torch.Tensor, wt: torch.Tensor, ss_in: torch.Tensor | None,
     if _gpu(x):
         y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
         ext().wstream_fin(3, x, wt, y, None, _tickets(x.device, 1, "fin"), ss_in, float(eps), None, None, None, None,
-                          None, None, None, None, None, None, 0, 0, 1)
+                          None, None, None, None, None, None, 0, 0, 1, _stamps_for("glu", N // 128, x.device))
         return y
     y = x.float() @ untile_weight(wt, glu=True).float().t()
     r = fin_row_scale(ss_in, M, K, eps)

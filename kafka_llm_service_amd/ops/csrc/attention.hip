@@ -590,13 +590,10 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   __syncthreads();
   if (!sm.s_last) return;
   auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  // 16-B agent-coherent loads (sc1: not served from this XCD's possibly stale L2); inline asm, so the group below
-  // waits for them itself
-  auto ld4 = [](const float* p) {
-    f32x4 r;
-    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
-    return r;
-  };
+  // 16-B agent-coherent loads (sc1: not served from this XCD's possibly stale L2) as compiler builtins over a buffer
+  // of out_part, so hipcc's waitcnt pass tracks them (out_part < 2 GiB: host-checked)
+  const auto prs = buf_rsrc(out_part);
+  auto ld4 = [&](const float* p) { return load16_sc1(prs, (int)((p - out_part) * 4)); };
   const int n = split_offset + S;  // <= 64 (host-checked)
   for (int g = w; g < G; g += 4) {
     const int64_t pbase = ((int64_t)b * Hq + kvh * G + g) * S_total;
@@ -641,7 +638,6 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
         acc4 += f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]} * sW[g][s0];
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the inline-asm loads above are not tracked by hipcc)
 #pragma unroll
     for (int j = 0; j < PQ; ++j)
       if (p0 + j < n) acc4 += pv[j] * sW[g][p0 + j];
@@ -650,7 +646,6 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
       f32x4 v[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) v[j] = ld4(pp + min(s2 + j, n - 1) * D);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
       for (int j = 0; j < 16; ++j)
         if (s2 + j < n) acc4 += v[j] * sW[g][s2 + j];

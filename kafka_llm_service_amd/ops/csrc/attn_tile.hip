@@ -415,7 +415,7 @@ __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __res
           if (PST && pbf) {
             float* d = reinterpret_cast<float*>(reinterpret_cast<bf16*>(out_part) +
                                                 (((int64_t)tok2 * Hq + head2) * S_total + it.split) * D + 64 * rd + 8 * cc);
-            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(d), "v"(v) : "memory");
+            store16_slab(d, v);  // (common.h: asm store + its hazard wait state)
             continue;
           }
           if (part && !pbf)

@@ -286,6 +286,7 @@ static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at
                     tickets->numel() >= (int64_t)B * Hkv,
                 "attn_decode: the fused merge needs an int32 ticket buffer of >= B * Hkv zeros");
     tp = tickets->data_ptr<int>();
+    TORCH_CHECK(out_part.numel() * 4 < 0x7fffffffLL, "attn_decode: the ticket merge addresses out_part as a < 2 GiB buffer");
   }
   const bf16* pre = nullptr;  // bf16 cascade prefix partials (slots < npre), same [B, Hq, S_total, 128] indexing
   if (pre_part.has_value()) {

@@ -65,12 +65,39 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 
 __device__ __forceinline__ bf16x8 load_bf16x8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 __device__ __forceinline__ void store_bf16x8(bf16* p, bf16x8 v) { *reinterpret_cast<bf16x8*>(p) = v; }
-// 16-B fp32 store that bypasses this XCD's L2 (sc1). Used for split-K slabs and GEMM outputs (write-only in their
-// kernel, whole 128-B lines per instruction, read by the next kernel: profiles/r05/bench_ab_wstream_slab16_sc1.jsonl)
-// and for the decode ticket merge's partial rows (read back in the same launch with sc1 loads); sc1 outputs in
-// RMSNorm / RoPE / tile kernels left readers stale data (README "Measured and removed")
+// ---- Store / load scopes on gfx950 (8 XCDs, one L2 each; the MALL and HBM behind them are shared) ---------------
+// What the kernels here rely on, and the evidence for it:
+//   * plain store  -> the writer XCD's L2 (write-back). Visible to other XCDs in LATER kernels (the kernel-end release
+//     writes dirty lines back, a kernel start drops other XCDs' stale copies). Within one launch it is visible to
+//     workgroups of the SAME XCD only (they share the L2): the fused finishers in wstream_gemm.hip rely on this and
+//     check it (hardware XCC_ID, flagged fallback).
+//   * sc1 store (agent scope) -> written through to the coherent level. Readable in the same launch by sc1 loads
+//     from any XCD once the writer's vmcnt reached 0 (decode ticket merge, GEMM finishers' flagged slabs; the ticket
+//     itself is a relaxed agent-scope atomic issued after that wait — no release fence, which would write back the
+//     writer's whole L2). In later kernels it is read with plain loads like any other data (decode-GEMM slabs, GEMM
+//     bf16 outputs, cascade bf16 partials: tests/test_sc1_reuse_gpu.py rewrites each buffer after readers on every
+//     XCD cached it).
+//   * sc1 load -> not served from this XCD's (possibly stale) L2.
+// Round 5 saw sc1 stores at other sites (RMSNorm / RoPE / tile outputs) leave wrong data (21 GPU tests, NaN in
+// test_rope_kv_write). The cause was the STORE INSTRUCTION, not the scope: an inline-asm global_store_dwordx4 is
+// opaque to hipcc's hazard recognizer, and on gfx9 a VMEM store of more than 8 bytes followed by a VALU write of its
+// data VGPRs needs one wait state — hipcc inserts it for its own stores, never after an asm one, so a loop that
+// reuses the data registers at once stored garbage. Every asm store below therefore carries its own s_nop.
 __device__ __forceinline__ void store16_slab(float* p, f32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 0" ::"v"(p), "v"(v) : "memory");
+}
+
+// raw buffer over 2 GiB from a wave-uniform base (gfx9 dword3: untyped 32-bit data); loads through it are compiler
+// builtins, so hipcc's waitcnt and hazard passes see them (unlike inline asm)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+// 16-B agent-coherent load (cache policy sc1)
+__device__ __forceinline__ f32x4 load16_sc1(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16));
+}
+__device__ __forceinline__ f32x4 load16_plain(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 0));
 }
 
 // 8 consecutive fp32 values at element offset `off` of a bf16 tensor x, or — when xp is set — the sum of S fp32

@@ -8,13 +8,15 @@
 // Split-K slab inputs: the decode GEMM (wstream_gemm.hip) leaves its output as S fp32 partial slabs
 // P[S][T][n]; every kernel here can take such a slab instead of a bf16 input and sums the S partials while
 // loading (load_in8 in common.h), so the split-K combine costs no launch of its own.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace kafka {
 
 // y = x * rsqrt(mean(x^2) + eps) * w     (x: [T, d] with row stride, out: [T, d] contiguous)
 // If RESID: r = x + r (rounded to bf16, written back to r), y = norm(r) * w.
-template <int NV, bool RESID, int NT = 256>
+template <int NV, bool RESID, int NT = 256, bool SC1 = false>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int64_t out_stride,
                                                        const bf16* __restrict__ x, const float* __restrict__ xp,
                                                        int S, int64_t ps, int64_t x_stride,
@@ -45,7 +47,10 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int
           s[j] = (bf16)(v[i][j] + (float)b[j]);
           v[i][j] = (float)s[j];
         }
-        store_bf16x8(resid + row * r_stride + vi * 8, s);
+        if constexpr (SC1)
+          store16_slab(reinterpret_cast<float*>(resid + row * r_stride + vi * 8), __builtin_bit_cast(f32x4, s));
+        else
+          store_bf16x8(resid + row * r_stride + vi * 8, s);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
@@ -60,7 +65,10 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, int
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[i][j] * r * (float)wv[i][j]);
-      store_bf16x8(out + row * out_stride + vi * 8, o);
+      if constexpr (SC1)
+        store16_slab(reinterpret_cast<float*>(out + row * out_stride + vi * 8), __builtin_bit_cast(f32x4, o));
+      else
+        store_bf16x8(out + row * out_stride + vi * 8, o);
     }
   }
 }
@@ -90,8 +98,18 @@ static hipError_t launch_rmsnorm_t(bf16* out, int64_t os, const bf16* x, const f
   const int nv = (nvec + 255) / 256;
   dim3 grid(T), block(256);
   if (T == 0) return hipSuccess;
+  // KAFKA_SC1_NORM=1: outputs as 16-B sc1 stores (an A/B of the store scope now that asm stores carry their hazard
+  // wait state, common.h); needs 16-B aligned rows
+  static const bool sc1 = [] {
+    const char* e = getenv("KAFKA_SC1_NORM");
+    return e != nullptr && e[0] == '1';
+  }();
   if (nvec <= 512 && nvec > 256) {  // e.g. d = 4096: one 16-B vector per thread, twice the loads in flight per row
-    rmsnorm_kernel<1, RESID, 512><<<grid, 512, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps);
+    if (sc1 && os % 8 == 0 && rs % 8 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
+        (!RESID || reinterpret_cast<uintptr_t>(r) % 16 == 0))
+      rmsnorm_kernel<1, RESID, 512, true><<<grid, 512, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps);
+    else
+      rmsnorm_kernel<1, RESID, 512><<<grid, 512, 0, st>>>(out, os, x, xp, S, ps, xs, r, rs, w, d, eps);
     return hipGetLastError();
   }
   switch (nv) {

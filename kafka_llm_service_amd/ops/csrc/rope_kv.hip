@@ -32,7 +32,7 @@ namespace kafka {
 
 __device__ __forceinline__ int vt_pos(int o) { return (o & ~15) | (o & 3) | ((o & 4) << 1) | ((o & 8) >> 1); }
 
-template <int D>
+template <int D, bool SC1 = false>
 __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ qkv, const float* __restrict__ qp,
                                                        int S, int64_t ps, int64_t qkv_stride,
                                                        const int64_t* __restrict__ positions,
@@ -73,15 +73,21 @@ __global__ __launch_bounds__(1024) void rope_kv_kernel(const bf16* __restrict__ 
         o1[j] = (bf16)(a * cv[j] - b * sv[j]);
         o2[j] = (bf16)(b * cv[j] + a * sv[j]);
       }
+      auto st16 = [](bf16* p, bf16x8 v) {
+        if constexpr (SC1)
+          store16_slab(reinterpret_cast<float*>(p), __builtin_bit_cast(f32x4, v));
+        else
+          store_bf16x8(p, v);
+      };
       if (head < Hq) {
         bf16* dst = q_out + t * q_stride + head * D;
-        store_bf16x8(dst + c, o1);
-        store_bf16x8(dst + HALF + c, o2);
+        st16(dst + c, o1);
+        st16(dst + HALF + c, o2);
       } else if (slot >= 0) {
         const int kh = head - Hq;
         bf16* dst = k_cache + (blk * Hkv + kh) * (int64_t)block_size * D + off * 8;
-        store_bf16x8(dst + (c >> 3) * block_size * 8, o1);
-        store_bf16x8(dst + ((HALF + c) >> 3) * block_size * 8, o2);
+        st16(dst + (c >> 3) * block_size * 8, o1);
+        st16(dst + ((HALF + c) >> 3) * block_size * 8, o2);
       }
     } else if (slot >= 0) {
       const int v = u - n_rope;
@@ -249,7 +255,15 @@ extern "C" hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int
   const int units = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
   const int nt = 64, ny = (units + nt - 1) / nt;
   const dim3 grid(T, ny);
-  if (D == 128)
+  // KAFKA_SC1_ROPE=1: q and K rows as 16-B sc1 stores (store-scope A/B, see common.h)
+  static const bool sc1 = [] {
+    const char* e = getenv("KAFKA_SC1_ROPE");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (D == 128 && sc1 && q_stride % 8 == 0)
+    rope_kv_kernel<128, true><<<grid, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride,
+                                                k_cache, v_cache, slot_mapping, Hq, Hkv, block_size);
+  else if (D == 128)
     rope_kv_kernel<128><<<grid, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride, k_cache,
                                           v_cache, slot_mapping, Hq, Hkv, block_size);
   else

@@ -71,19 +71,6 @@ struct FinArgs {
   int* err;                     // bit 0 set if a finisher could not reach a split's slab (see "home XCD" below)
 };
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
-  // raw buffer over 2 GiB from p (gfx9 dword3: untyped 32-bit data)
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
-}
-// 16-B agent-coherent load (cache policy sc1): not served from this XCD's L2. A compiler builtin, so hipcc's
-// waitcnt pass tracks it (unlike an inline-asm load).
-__device__ __forceinline__ f32x4 load16_sc1(__amdgpu_buffer_rsrc_t rs, int byte_off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16));
-}
-
-__device__ __forceinline__ f32x4 load16_plain(__amdgpu_buffer_rsrc_t rs, int byte_off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 0));
-}
 // split s's 16 B: from this XCD's L2 (the split stored it there: same XCD) or, flagged, agent-coherent (sc1)
 template <bool MIXED>
 __device__ __forceinline__ f32x4 load16_split(__amdgpu_buffer_rsrc_t rs, int byte_off, unsigned flags, int s) {
