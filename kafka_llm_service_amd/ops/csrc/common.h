@@ -82,9 +82,13 @@ __device__ __forceinline__ void store_bf16x8(bf16* p, bf16x8 v) { *reinterpret_c
 // test_rope_kv_write). The cause was the STORE INSTRUCTION, not the scope: an inline-asm global_store_dwordx4 is
 // opaque to hipcc's hazard recognizer, and on gfx9 a VMEM store of more than 8 bytes followed by a VALU write of its
 // data VGPRs needs one wait state — hipcc inserts it for its own stores, never after an asm one, so a loop that
-// reuses the data registers at once stored garbage. Every asm store below therefore carries its own s_nop.
+// reuses the data registers at once stored garbage. The same blindness holds on the way in: a VALU result read by
+// the store too early (gfx950 forwarding hazards after dst_sel / op_sel writes such as the bf16 packs of a
+// conversion, or after a transcendental) needs wait states hipcc does not insert in front of an asm consumer —
+// round 6 measured garbage (1e30) in RMSNorm's in-place residual stored this way. Every asm store below therefore
+// carries wait states on both sides.
 __device__ __forceinline__ void store16_slab(float* p, f32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 0" ::"v"(p), "v"(v) : "memory");
+  asm volatile("s_nop 4\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 0" ::"v"(p), "v"(v) : "memory");
 }
 
 // raw buffer over 2 GiB from a wave-uniform base (gfx9 dword3: untyped 32-bit data); loads through it are compiler

@@ -585,3 +585,17 @@ def test_plan_prefill_items_with_prefix_offset():
     assert min(it[3] for it in mine if it[0] == 0) == 18000 and max(it[4] for it in mine if it[0] == 0) >= 20000
     assert splits == max(it[5] for it in items) + 1
     assert any(lo <= 0 and hi >= 100 for lo, hi in ranges)
+
+
+def test_engine_logits_bounded_by_fp32_forward_cpu(base_engine):
+    """The composed-numerics bound of tests/test_numerics_gpu.py on the CPU reference ops (tiny-llama): prefill,
+    decode, prefix-cached and cascade rows within K_STD of the fp32 forward and within RATIO of the bf16 forward's
+    own error."""
+    from tests.test_numerics_gpu import _check, composed_errors
+
+    eng = _engine(model=base_engine.model, cascade_min_prefix=16)
+    g = torch.Generator().manual_seed(12)
+    _check(composed_errors(eng, [torch.randint(0, 5000, (n,), generator=g).tolist() for n in (9, 33)]), "cpu cold")
+    prefix = torch.randint(0, 5000, (96,), generator=g).tolist()
+    warm = [prefix + torch.randint(0, 5000, (n,), generator=g).tolist() for n in (3, 20)]
+    _check(composed_errors(eng, warm, warm_prefix=prefix), "cpu cascade")
