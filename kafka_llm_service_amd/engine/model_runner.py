@@ -417,11 +417,13 @@ class _Stager:
         return dev.view(a.shape)
 
     def upload_into(self, arrays: list[np.ndarray | None], offs: list[int], dst: torch.Tensor) -> None:
-        """Arrays staged at their byte offsets of ``dst`` (a uint8 device buffer whose layout the caller fixed; None
-        leaves a range untouched) and moved by ONE async copy of the whole range — a hipGraph's static inputs refreshed
-        with one copy launch instead of an upload plus a device copy per array."""
+        """Arrays staged at their byte offsets of ``dst`` (a uint8 device buffer whose layout the caller fixed) and moved
+        by ONE async copy of the whole range — a hipGraph's static inputs refreshed with one copy launch instead of an
+        upload plus a device copy per array. Every byte of ``dst`` is written: the ranges of None arrays (and any
+        padding) become zeros, never stale bytes of an earlier upload."""
         n = dst.numel()
         if self.device.type != "cuda":
+            dst.zero_()
             for a, o in zip(arrays, offs):
                 if a is not None:
                     dst[o:o + a.nbytes].copy_(torch.from_numpy(np.ascontiguousarray(a).reshape(-1).view(np.uint8)))
@@ -431,6 +433,7 @@ class _Stager:
         if buf is None or base + n > buf.numel():
             self.bufs[self.i] = buf = torch.empty(max(self.nbytes, 2 * (base + n)), dtype=torch.uint8, pin_memory=True)
         host = buf.numpy()
+        host[base:base + n] = 0
         for a, o in zip(arrays, offs):
             if a is not None:
                 a = np.ascontiguousarray(a)

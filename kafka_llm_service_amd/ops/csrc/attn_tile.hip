@@ -125,6 +125,9 @@ __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __res
   uint64_t ph[5] = {0, 0, 0, 0, 0};
   if constexpr (ABL == 8) ph[0] = t3_rt();
   const TileItem it = items[blockIdx.y];
+  // an item flagged alt without an alt buffer (host bug) would write row B + q of the main buffer, past its end:
+  // dropped (workgroup-uniform), as the decode kernel drops malformed items
+  if (it.alt != 0 && ap.part == nullptr) return;
   const int kvh = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;

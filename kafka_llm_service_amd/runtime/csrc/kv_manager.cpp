@@ -420,7 +420,9 @@ class KVManager {
   // next-fit: the first free page at or after the cursor (wrapping)
   int pop_block() {
     if (free_.empty()) {
-      if (lru_.empty()) reclaim_reserves();
+      // idle speculative reserves go back before any cached prefix page is evicted (a reserve is only a guess at
+      // a sequence's next pages; an evicted prefix page is a recompute for the next request that shares it)
+      if (n_reserved_ > 0) reclaim_reserves();
       if (free_.empty()) {
         if (lru_.empty()) throw std::runtime_error("KV pool exhausted");
         evict_one();

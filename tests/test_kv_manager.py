@@ -270,3 +270,23 @@ def test_page_runs_contiguous_and_invariants():
             del live[sid]
         assert kv.check_invariants(), step
     assert kv.available() >= kv.num_free()
+
+
+def test_reserves_reclaimed_before_cached_pages_are_evicted():
+    """A sequence's speculative page reserve (run > 1) goes back to the pool before any cached prefix page is evicted
+    (the cache exists for the agent workloads' shared prefixes; a reserve is only a guess)."""
+    kv = KVManager(48, 16, True, 16)
+    pre = list(range(1, 65))
+    kv.add_sequence(1, pre)
+    assert kv.ensure_capacity(1, 64)
+    kv.commit(1, 64)
+    kv.free_sequence(1)
+    assert kv.num_evictable() == 4
+    kv.add_sequence(2, [7])
+    assert kv.ensure_capacity(2, 1) and kv.ensure_capacity(2, 17)  # decode growth: a run, most of it reserved
+    assert kv.num_reserved() > 0
+    kv.add_sequence(3, list(range(1000, 1000 + 16 * 30)))
+    assert kv.ensure_capacity(3, 16 * 30)  # needs more than the free set: reserves first
+    assert kv.stats()["evictions"] == 0 and kv.num_reserved() == 0
+    assert kv.add_sequence(4, pre + [5]) == 64  # the cached prefix survived
+    assert kv.check_invariants()
