@@ -200,5 +200,11 @@ def test_engine_fused_layer_matches_unfused(cuda, monkeypatch):
     diff = (seen1[i] - seen2[i]).abs().max().item()
     assert diff <= 0.1 * seen2[i].std().item() + 0.05, f"fused vs unfused logits differ by {diff}"
     assert ops.fin_errors(cuda) == 0
-    agree = sum(a == b for x, y in zip(out1, out2) for a, b in zip(x, y))
-    assert agree >= 0.8 * sum(len(x) for x in out2), (out1, out2)
+    # greedy tokens of flat random-init logits may flip between the two summation orders after the first decode
+    # step; what must hold is that every fused-path token is the dense oracle's argmax up to bf16 rounding
+    from kafka_llm_service_amd.models.oracle import dense_logits
+    for p, o in zip(prompts, out1):
+        lg = dense_logits(e1.model, p + o)
+        for i, tok in enumerate(o):
+            row = lg[len(p) - 1 + i]
+            assert (row.max() - row[tok]).item() < 0.15, f"fused token {i}: gap {(row.max() - row[tok]).item()}"
