@@ -28,10 +28,13 @@ def composed_errors(eng, prompts, warm_prefix=None, max_tokens=6):
         return orig(lg, sp)
 
     eng.runner.sample_device = keep
+    budget = eng.sched.cfg.prefill_cost_budget
+    eng.sched.cfg.prefill_cost_budget = 0  # every prompt admitted in the first step: row j of each step = prompt j
     try:
         outs = eng.generate(prompts, SamplingParams(temperature=0.0, max_tokens=max_tokens, ignore_eos=True))
     finally:
         eng.runner.sample_device = orig
+        eng.sched.cfg.prefill_cost_budget = budget
     steps = [t for t in seen if t.shape[0] == len(prompts)]
     assert len(steps) == max_tokens, [t.shape for t in seen]
     rows = []
