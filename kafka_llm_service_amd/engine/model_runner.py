@@ -485,7 +485,9 @@ class ModelRunner:
         # rows whose token was still being sampled at launch gather their input ids from it on the stream
         self.tok_buf = torch.zeros(max_num_seqs * 2 + 64, dtype=torch.int64, device=self.device)
         self.graphs = None  # engine/graphs.py DecodeGraphs when hipGraph decode is enabled
-        self.fixed_decode_items = False  # decode_items_fixed without graphs too (equivalence tests)
+        # decode_items_fixed without graphs too (equivalence tests; KAFKA_FIXED_DECODE_ITEMS=1 separates the graph
+        # plan's cost from the replay's in an eager A/B)
+        self.fixed_decode_items = os.environ.get("KAFKA_FIXED_DECODE_ITEMS", "0") == "1"
         self.step_events: list | None = None  # (start, end) timing events per launched step when a list is set
         # grammar masks / forced tokens / penalties inside the sampler kernel (tables allocated on first use)
         self.lp = LogitsProcessor(self.device, self.vocab, max_slots=max(256, max_num_seqs))
