@@ -7,6 +7,8 @@
   seqsplit  prefix pass (fp32 partials) -> decode kernel (suffix partials only) -> attn_merge
   seqsplit_bf16  as seqsplit with the prefix partials in bf16 (attn_merge reads slots < npre from them)
   conc      prefix pass on a second stream CONCURRENT with the decode kernel (suffix partials), then attn_merge
+  cumask    as conc, but on two CU-MASKED streams (hipExtStreamCreateWithCUMask): the prefix pass on --cascade-cus
+            CUs, the decode kernel on the other ones (no co-residency: each kernel keeps its own CUs), then attn_merge
   cascade / decode_fused / decode_part / merge   each launch of the above alone (inputs left by a previous run)
 
 The prefix pass is a short-lived launch with fixed phases (prologue, first tile, epilogue) during which HBM idles;
@@ -35,6 +37,10 @@ def main():
     ap.add_argument("--layers", type=int, default=4)
     ap.add_argument("--chunks", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--cascade-cus", type=str, default="96,112,128",
+                    help="cumask modes: CUs (of 256) given to the prefix pass")
+    ap.add_argument("--mask-order", choices=("stripe", "block"), default="stripe",
+                    help="stripe: CU-mask bits taken round-robin (bit i, i + 8, ...); block: the lowest bits")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     Hq, Hkv, D, G = 32, 8, 128, 4
@@ -77,6 +83,36 @@ def main():
                                                                                    "conc")}
     side = torch.cuda.Stream(dev)
     main_s = torch.cuda.current_stream(dev)
+    masked = {}  # C -> (cascade stream, decode stream)
+
+    def cu_streams(C):
+        if C not in masked:
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+            if args.mask_order == "stripe":
+                # bit i = (a, b, c) = (i // 32, i // 8 % 4, i % 8): whether a bit's XCD is i % 8 or i // 32, taking
+                # (a + c) % 8 < k plus b < j where it equals k gives every XCD C / 8 CUs (C = 32 k + 8 j)
+                k, j = C // 32, (C % 32) // 8
+                sel = set(i for i in range(ncu) if ((i // 32 + i % 8) % 8 < k) or
+                          ((i // 32 + i % 8) % 8 == k and (i // 8) % 4 < j))
+            else:
+                sel = set(range(C))
+            words = []
+            for which in (sel, set(range(ncu)) - sel):
+                m = [0] * ((ncu + 31) // 32)
+                for i in which:
+                    m[i // 32] |= 1 << (i % 32)
+                words.append(m)
+            out = []
+            for m in words:
+                st = ctypes.c_void_p()
+                arr = (ctypes.c_uint32 * len(m))(*m)
+                rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), len(m), arr)
+                assert rc == 0, f"hipExtStreamCreateWithCUMask: {rc}"
+                out.append(torch.cuda.ExternalStream(st.value, device=dev))
+            masked[C] = tuple(out)
+        return masked[C]
 
     def cascade(i, op, stream=None):
         kc, vc = caches[i % args.layers]
@@ -108,6 +144,30 @@ def main():
             ops.attn_decode_items(q, kc, vc, btd, dit, part, lse, scale)
         elif mode == "merge":
             ops.attn_merge(part, lse, outs["seqsplit"])
+        elif mode.startswith("cumask"):
+            C = int(mode[6:])
+            sa, sb = cu_streams(C)
+            sa.wait_stream(main_s)
+            sb.wait_stream(main_s)
+            with torch.cuda.stream(sa):
+                cascade(i, pre)
+            with torch.cuda.stream(sb):
+                ops.attn_decode_items(q, kc, vc, btd, dit, part, lse, scale)
+            main_s.wait_stream(sa)
+            main_s.wait_stream(sb)
+            ops.attn_merge(part, lse, outs["conc"], pre=pre, npre=npre)
+        elif mode.startswith("cascade_cu"):  # the prefix pass alone on its masked stream
+            sa, _ = cu_streams(int(mode[10:]))
+            sa.wait_stream(main_s)
+            with torch.cuda.stream(sa):
+                cascade(i, pre)
+            main_s.wait_stream(sa)
+        elif mode.startswith("decode_cu"):  # the decode kernel alone on the complement
+            _, sb = cu_streams(int(mode[9:]))
+            sb.wait_stream(main_s)
+            with torch.cuda.stream(sb):
+                ops.attn_decode_items(q, kc, vc, btd, dit, part, lse, scale)
+            main_s.wait_stream(sb)
         else:
             side.wait_stream(main_s)
             with torch.cuda.stream(side):
@@ -116,8 +176,12 @@ def main():
             main_s.wait_stream(side)
             ops.attn_merge(part, lse, outs[mode])
 
-    for mode in ("seq", "seq_fp32", "seqsplit", "seqsplit_bf16", "conc", "cascade", "decode_fused", "decode_part", "merge",
-                 "merge_bf16"):
+    cus = [int(x) for x in args.cascade_cus.split(",") if x]
+    modes = ["seq", "seq_fp32", "seqsplit", "seqsplit_bf16", "conc", "cascade", "decode_fused", "decode_part", "merge",
+             "merge_bf16"]
+    for C in cus:
+        modes += [f"cascade_cu{C}", f"decode_cu{C}", f"cumask{C}"]
+    for mode in modes:
         res = []
         for _ in range(5):
             run(mode, 0)
@@ -131,8 +195,9 @@ def main():
             res.append(s.elapsed_time(e) * 1e3 / args.iters)
         run(mode, 0)
         torch.cuda.synchronize()
-        err = (outs[mode].float() - outs["seq"].float()).abs().max().item() if mode in ("seq_fp32", "seqsplit", "seqsplit_bf16", "conc") \
-            else 0.0
+        om = "conc" if mode.startswith("cumask") else mode
+        err = (outs[om].float() - outs["seq"].float()).abs().max().item() \
+            if om in ("seq_fp32", "seqsplit", "seqsplit_bf16", "conc") else 0.0
         print(json.dumps({"mode": mode, "us": round(statistics.median(res), 1), "S": S, "prefix_items": npre,
                           "decode_items": int(ditems.shape[0]), "err_vs_seq": round(err, 4)}), flush=True)
 

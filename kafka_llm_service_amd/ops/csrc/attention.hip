@@ -55,9 +55,12 @@ struct AttnWorkItem {
 // Reductions with the partner lane l ^ 32 on gfx950's v_permlane32_swap (one VALU op, no LDS crossbar round trip
 // through ds_bpermute — which also queued behind the K/V fragment reads): swapping a register with itself leaves
 // x[l] in one result and x[l ^ 32] in the other, so a symmetric op of the two is the xor-32 reduction on every lane.
+// max as llvm.maximum (gfx950 v_maximum3_f32, 3 inputs, no NaN-quieting v_max x, x of each MFMA result that fmaxf
+// costs in IEEE mode; attn_tile.hip t3_max)
+__device__ __forceinline__ float vmax(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 __device__ __forceinline__ float xor32_max(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  return vmax(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 __device__ __forceinline__ float xor32_sum(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -181,11 +184,14 @@ __device__ __forceinline__ void softmax_pv(f32x16& s, bool masked, int key0, int
       if (!((key >= lo) & (key < hi) & (key <= limit))) s[i] = -INFINITY;
     }
   }
-  float mx = s[0];
+  float ma = vmax(s[0], s[1]), mb = vmax(s[2], s[3]);
 #pragma unroll
-  for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[i]);
-  mx = xor32_max(mx);
-  const float m_new = fmaxf(acc.m, mx * scale_log2);
+  for (int i = 4; i < 16; i += 4) {
+    ma = vmax(vmax(ma, s[i]), s[i + 1]);
+    mb = vmax(vmax(mb, s[i + 2]), s[i + 3]);
+  }
+  const float mx = xor32_max(vmax(ma, mb));
+  const float m_new = vmax(acc.m, mx * scale_log2);
   const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
   if (!__all(m_new == acc.m)) {
     const float alpha = exp2f(acc.m - m_use);
@@ -339,12 +345,29 @@ struct DecodeSmem {
   float sW[8][65];
   float sWt[8];
   int s_last;
+  bf16 so[8][D];  // OST: the final bf16 rows, stored from here as 16-B sc1 stores
 };
+
+// the workgroup's G final rows from sm.so to out (every thread of the workgroup calls it)
+template <int D>
+__device__ __forceinline__ void store_rows_sc1(DecodeSmem<D>& sm, bf16* __restrict__ out, int64_t out_stride, int b,
+                                               int kvh, int G) {
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < G * (D / 8)) {
+    const int g = t / (D / 8), c = (t % (D / 8)) * 8;
+    store16_slab(reinterpret_cast<float*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c),
+                 *reinterpret_cast<const f32x4*>(&sm.so[g][c]));
+  }
+}
 
 // One decode piece: keys [lo, hi) of row b, kv head kvh, piece `split` of S, partial slots from split_offset. Every
 // thread of the workgroup calls it with the same arguments (it synchronises the workgroup); returns when the
 // piece's partial or final rows are written.
-template <int D, bool FP8>
+// OST: the final bf16 rows leave through LDS as 16-B sc1 stores (one instruction per 16 B of a row instead of one
+// 8-B plain store per thread: the lines leave this XCD's L2, so the launch ends with no dirty output lines to write
+// back; the o GEMM reads them on every XCD). Needs 16-B aligned rows (host-checked).
+template <int D, bool FP8, bool OST = false>
 __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __restrict__ q, int64_t q_stride,
                                              const void* __restrict__ k_cache, const void* __restrict__ v_cache,
                                              int Hkv, int G, const int* __restrict__ block_tables, int bt_stride,
@@ -517,8 +540,12 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
       bf16x4 o4;
 #pragma unroll
       for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc4[j] * inv);
-      *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
+      if constexpr (OST)
+        *reinterpret_cast<bf16x4*>(&sm.so[g][c]) = o4;
+      else
+        *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
     }
+    if constexpr (OST) store_rows_sc1<D>(sm, out, out_stride, b, kvh, G);
     return;
   }
   if (out != nullptr) {
@@ -654,14 +681,18 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
     bf16x4 o4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc4[j] * inv);
-    *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
+    if constexpr (OST)
+      *reinterpret_cast<bf16x4*>(&sm.so[g][c]) = o4;
+    else
+      *reinterpret_cast<bf16x4*>(out + (int64_t)b * out_stride + (int64_t)(kvh * G + g) * D + c) = o4;
   }
+  if constexpr (OST) store_rows_sc1<D>(sm, out, out_stride, b, kvh, G);
 }
 
 // grid (Hkv, items): the Hkv heads of an item are consecutive workgroups, dealt to different XCDs, reading one page
 // row together (heads-fast: +7 % over items-fast, three workgroups per CU +5 % over two,
 // profiles/r04/bench_ab_decode_placement_occ.jsonl)
-template <int D, bool FP8>
+template <int D, bool FP8, bool OST = false>
 __global__ __launch_bounds__(256, FP8 ? 2 : 3) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
                                                                       const void* __restrict__ k_cache,
                                                                       const void* __restrict__ v_cache, int Hkv, int G,
@@ -680,7 +711,7 @@ __global__ __launch_bounds__(256, FP8 ? 2 : 3) void attn_decode_kernel(const bf1
   if (b < 0 || b >= B || split < 0 || split >= S || split_offset < 0 || split_offset + S > S_total ||
       (out != nullptr && split_offset + S > 64))
     return;
-  decode_piece<D, FP8>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, it.lo, it.hi,
+  decode_piece<D, FP8, OST>(sm, q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride, b, kvh, it.lo, it.hi,
                        split, S, split_offset, out_part, lse_part, S_total, scale_log2, out, out_stride, tickets,
                        pre_bf16);
 }
@@ -1180,7 +1211,17 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
   const float scale_log2 = scale * 1.4426950408889634f;
   const auto* di = reinterpret_cast<const DecodeItem*>(items);
   const dim3 grid(Hkv, n_items);
-  if (fp8)
+  // KAFKA_SC1_ATTN (default 1): the bf16 rows as 16-B sc1 stores through LDS (decode_piece OST)
+  static const bool sc1 = [] {
+    const char* e = getenv("KAFKA_SC1_ATTN");
+    return e == nullptr || e[0] != '0';
+  }();
+  const bool ost = sc1 && out != nullptr && out_stride % 8 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  if (ost && !fp8)
+    attn_decode_kernel<128, false, true><<<grid, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables,
+                                                                bt_stride, di, B, out_part, lse_part, S_total,
+                                                                scale_log2, out, out_stride, tickets, pre_bf16);
+  else if (fp8)
     attn_decode_kernel<128, true><<<grid, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride,
                                                          di, B, out_part, lse_part, S_total, scale_log2, out,
                                                          out_stride, tickets, pre_bf16);

@@ -60,9 +60,13 @@ __device__ __forceinline__ void dma16(const void* g, char* lds) {
   __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds, 16, 0, AUX);
 }
 
+// max without fmaxf's NaN-quieting: IEEE-mode v_max_f32 needs each MFMA result canonicalised first (a v_max x, x
+// per value: 3 VALU ops per pair of scores); llvm.maximum lowers to gfx950's v_maximum3_f32, 3 inputs per op, no
+// canonicalisation (it propagates NaN instead of dropping it: a NaN score poisons its row either way)
+__device__ __forceinline__ float t3_max(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 __device__ __forceinline__ float t3_xor32_max(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  return t3_max(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 __device__ __forceinline__ float t3_xor32_sum(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -306,10 +310,14 @@ __global__ __launch_bounds__(512, 2) void attn_tile_kernel(const TileItem* __res
     float smax[2];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
-      float mx = fmaxf(s[rb][0][0], s[rb][1][0]);
+      // two chains of v_maximum3_f32 (m = max3(m, a, b)): 16 VALU ops for the 32 scores of a lane
+      float ma = t3_max(s[rb][0][0], s[rb][1][0]), mb = t3_max(s[rb][0][1], s[rb][1][1]);
 #pragma unroll
-      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, fmaxf(s[rb][0][i], s[rb][1][i]));
-      smax[rb] = t3_xor32_max(mx) * scale_log2;
+      for (int i = 2; i < 16; i += 2) {
+        ma = t3_max(t3_max(ma, s[rb][0][i]), s[rb][1][i]);
+        mb = t3_max(t3_max(mb, s[rb][0][i + 1]), s[rb][1][i + 1]);
+      }
+      smax[rb] = t3_xor32_max(t3_max(ma, mb)) * scale_log2;
     }
     bool need = false;
 #pragma unroll

@@ -86,9 +86,13 @@ __device__ __forceinline__ void store_bf16x8(bf16* p, bf16x8 v) { *reinterpret_c
 // the store too early (gfx950 forwarding hazards after dst_sel / op_sel writes such as the bf16 packs of a
 // conversion, or after a transcendental) needs wait states hipcc does not insert in front of an asm consumer —
 // round 6 measured garbage (1e30) in RMSNorm's in-place residual stored this way. Every asm store below therefore
-// carries wait states on both sides.
+// carries wait states on both sides — and FIVE after it, not the one hipcc itself puts behind a compiler-emitted
+// dwordx4 store: with `s_nop 0` after the sc1 store the residual row (whose data VGPRs the next instruction, a
+// v_pk_mul_f32 of the sum of squares, overwrites) still came out as garbage in 8 GPU tests; with `s_nop 4` all 60
+// store-scope tests pass (profiles/r06/sc1/). The sites that passed with one wait state never rewrote the data
+// registers right after the store.
 __device__ __forceinline__ void store16_slab(float* p, f32x4 v) {
-  asm volatile("s_nop 4\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 0" ::"v"(p), "v"(v) : "memory");
+  asm volatile("s_nop 4\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 4" ::"v"(p), "v"(v) : "memory");
 }
 
 // raw buffer over 2 GiB from a wave-uniform base (gfx9 dword3: untyped 32-bit data); loads through it are compiler

@@ -98,11 +98,12 @@ static hipError_t launch_rmsnorm_t(bf16* out, int64_t os, const bf16* x, const f
   const int nv = (nvec + 255) / 256;
   dim3 grid(T), block(256);
   if (T == 0) return hipSuccess;
-  // KAFKA_SC1_NORM=1: outputs as 16-B sc1 stores (an A/B of the store scope now that asm stores carry their hazard
-  // wait state, common.h); needs 16-B aligned rows
+  // outputs (normalised rows and the in-place residual) as 16-B sc1 stores — the lines leave this XCD's L2, so the
+  // launch ends with none of them dirty (+2.1 % on the headline with RoPE's, profiles/r06/ab/); KAFKA_SC1_NORM=0 keeps
+  // plain stores. Needs 16-B aligned rows. common.h "Store / load scopes"
   static const bool sc1 = [] {
     const char* e = getenv("KAFKA_SC1_NORM");
-    return e != nullptr && e[0] == '1';
+    return e == nullptr || e[0] != '0';
   }();
   if (nvec <= 512 && nvec > 256) {  // e.g. d = 4096: one 16-B vector per thread, twice the loads in flight per row
     if (sc1 && os % 8 == 0 && rs % 8 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&

@@ -255,10 +255,10 @@ extern "C" hipError_t kafka_launch_rope_kv(const bf16* qkv, const float* qp, int
   const int units = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
   const int nt = 64, ny = (units + nt - 1) / nt;
   const dim3 grid(T, ny);
-  // KAFKA_SC1_ROPE=1: q and K rows as 16-B sc1 stores (store-scope A/B, see common.h)
+  // q and K rows as 16-B sc1 stores (KAFKA_SC1_ROPE=0: plain; with the RMSNorm outputs +2.1 %, common.h)
   static const bool sc1 = [] {
     const char* e = getenv("KAFKA_SC1_ROPE");
-    return e != nullptr && e[0] == '1';
+    return e == nullptr || e[0] != '0';
   }();
   if (D == 128 && sc1 && q_stride % 8 == 0)
     rope_kv_kernel<128, true><<<grid, nt, 0, st>>>(qkv, qp, S, ps, qkv_stride, positions, cos_sin, q_out, q_stride,

@@ -142,3 +142,62 @@ def test_ticket_merge_partials_reused_buffer(cuda, S):
         _close(out, o_ref, atol=0.02, msg=f"ticket merge S={S} round {it}")
         _ = (part.sum() + lse.sum()).item()
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("T", [1, 64])
+def test_norm_rope_attn_outputs_reused_buffers(cuda, T):
+    """The layer chain's small kernels with their default 16-B sc1 stores, on ONE set of buffers rewritten six times
+    (the engine's layer after layer): fused_add_rmsnorm (normalised rows + the in-place residual), rope_kv_write (q rows
+    and the K cache rows) and the decode kernel's final bf16 rows (through LDS, decode_piece OST). Between rounds torch
+    and our decode GEMM (every XCD) read each buffer; every round is checked against fp32 references."""
+    g = torch.Generator(device=cuda).manual_seed(11)
+    d, Hq, Hkv, D = 4096, 32, 8, 128
+    nb = 20 * T  # 20 pages per row, none shared
+    eps = 1e-5
+    wn = (1 + 0.1 * torch.randn(d, device=cuda, generator=g)).to(torch.bfloat16)
+    wo = (torch.randn(d, d, device=cuda, generator=g) * d ** -0.5).to(torch.bfloat16)
+    wot = ops.tile_weight(wo)
+    cs = ref.rope_cos_sin(8192, D, 500000.0, None, device=cuda)
+    resid = torch.randn(T, d, device=cuda, dtype=torch.bfloat16, generator=g)
+    x = torch.empty(T, d, device=cuda, dtype=torch.bfloat16)
+    q = torch.empty(T, Hq, D, device=cuda, dtype=torch.bfloat16)
+    kc = torch.zeros(nb, Hkv, 16, D, device=cuda, dtype=torch.bfloat16)
+    vc = torch.zeros(nb, Hkv, D, 16, device=cuda, dtype=torch.bfloat16)
+    out = torch.empty(T, Hq, D, device=cuda, dtype=torch.bfloat16)
+    L = 16 * 20  # keys per row: 20 pages of its own
+    bt = torch.arange(T * 20, dtype=torch.int32, device=cuda).view(T, 20)
+    lens = torch.full((T,), L, dtype=torch.int32, device=cuda)
+    S = 2
+    part = torch.empty(T, Hq, S, D, device=cuda)
+    lse = torch.empty(T, Hq, S, device=cuda)
+    dit = ops.uniform_decode_items(lens, None, S, 0)
+    for it in range(6):
+        delta = torch.randn(T, d, device=cuda, dtype=torch.bfloat16, generator=g)
+        r0 = resid.clone()
+        ops.fused_add_rmsnorm(delta, resid, wn, eps, out=x)
+        y_ref, s_ref = ref.fused_add_rmsnorm(delta.cpu(), r0.cpu(), wn.cpu(), eps)
+        _close(resid, s_ref, atol=0.0, msg=f"residual round {it}")
+        _close(x, y_ref, atol=0.02, rtol=0.01, msg=f"rmsnorm round {it}")
+        # readers: torch and the decode GEMM on every XCD
+        _ = (x.float().sum() + resid.float().sum()).item()
+        _close(ops.slab_reduce(ops.linear_stream(x, wot)), x.float() @ wo.float().t(), atol=0.03, rtol=0.02,
+               msg=f"gemm of x round {it}")
+        # RoPE + KV write: every row writes its key at a new position of its own pages
+        qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=cuda, dtype=torch.bfloat16, generator=g)
+        pos = torch.full((T,), it, dtype=torch.long, device=cuda)
+        slots = (bt[:, it // 16].long() * 16 + it % 16)
+        kc_ref, vc_ref = kc.cpu().clone(), vc.cpu().clone()
+        ops.rope_kv_write(qkv, pos, cs, q, kc, vc, slots, Hq, Hkv)
+        q_ref = torch.empty(T, Hq, D, dtype=torch.bfloat16)
+        ref.rope_kv_write(qkv.cpu(), pos.cpu(), cs.cpu(), q_ref, kc_ref, vc_ref, slots.cpu(), Hq, Hkv)
+        _close(q, q_ref, atol=0.03, rtol=0.01, msg=f"q round {it}")
+        _close(kc, kc_ref, atol=0.03, rtol=0.01, msg=f"k cache round {it}")
+        assert torch.equal(vc.cpu(), vc_ref), f"v cache round {it}"
+        _ = (q.float().sum() + kc.float().sum()).item()
+        # decode over the rows' pages (keys written so far and zeros beyond: both are keys), one output buffer
+        ops.attn_decode_items(q, kc, vc, bt, dit, part, lse, D ** -0.5, out=out)
+        o_ref, _ = ref.attn_decode_full(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), lens.cpu(), D ** -0.5)
+        _close(out, o_ref, atol=0.03, msg=f"decode out round {it}")
+        _close(ops.slab_reduce(ops.linear_stream(out.view(T, -1), wot)), out.view(T, -1).float() @ wo.float().t(),
+               atol=0.03, rtol=0.02, msg=f"gemm of decode out round {it}")
+    torch.cuda.synchronize()
