@@ -88,7 +88,9 @@ def main():
     def cu_streams(C):
         if C not in masked:
             import ctypes
-            hip = ctypes.CDLL("libamdhip64.so")
+            # the HIP runtime torch already loaded (a second copy would not know torch's device context)
+            libs = [ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64.so" in ln]
+            hip = ctypes.CDLL(libs[0] if libs else "libamdhip64.so")
             ncu = torch.cuda.get_device_properties(dev).multi_processor_count
             if args.mask_order == "stripe":
                 # bit i = (a, b, c) = (i // 32, i // 8 % 4, i % 8): whether a bit's XCD is i % 8 or i // 32, taking

@@ -729,7 +729,11 @@ __global__ __launch_bounds__(256) void wstream_grouped_kernel(const bf16* __rest
     for (int t = 0; t < KSTEP; ++t) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        if (mt < mt_used) {
+        // MT = 4 computes every row tile (rows past the segment hold a valid row, never stored): with the MFMAs of
+        // unused tiles skipped behind a branch, the last accumulator register of tile 0 was read before its final
+        // MFMA had written it (row 27 / 31 of a 28..32-row expert wrong at K = 512; the 128-row tile's MFMAs are
+        // cheap next to its weight stream)
+        if (MT == 4 || mt < mt_used) {
           const int m = mt * 32 + r, c = 2 * t + h;
           const bf16x8 xf = *reinterpret_cast<const bf16x8*>(&xs[buf][m * KC + 8 * (c ^ (m & 15))]);
           acc[mt] = mfma32(xf, wv[t], acc[mt]);
@@ -994,25 +998,40 @@ extern "C" hipError_t kafka_launch_wstream_grouped(const bf16* X, int64_t ldx, c
                                                   hipStream_t st) {
   if (max_rows < 1 || e_local < 1) return hipSuccess;
   if (N % 64 != 0 || K % 256 != 0 || (out == nullptr) == (Y == nullptr)) return hipErrorInvalidValue;
-  const int MT = max_rows <= 32 ? 1 : 2;
+  // MT = 4 (128-row tiles on 128-deep K chunks) for large steps: with 64-row tiles every
+  // row tile of an expert re-streams its weights, and those tiles run far apart in dispatch order (blockIdx.z is the
+  // slowest dimension), so no cache keeps the slice between them — an expert with 65..128 rows read its 352 MB twice.
+  // KAFKA_MOE_MT4=0 keeps 64-row tiles (A/B).
+  static const bool mt4 = [] {
+    const char* e = getenv("KAFKA_MOE_MT4");
+    return e == nullptr || e[0] != '0';
+  }();
+  // (64-row tiles stay below 193 rows: an expert then rarely fills a second tile, and they stream faster there —
+  // benchmarks/moe_bench.py T = 128 / 192: 493 / 522 vs 517 / 551 us per layer; T = 256 / 384 / 512: 761 / 1002 /
+  // 1303 vs 601 / 691 / 1004, profiles/r06/mixtral/)
+  const int MT = max_rows <= 32 ? 1 : ((max_rows <= 192 || !mt4) ? 2 : 4);
   const dim3 grid((N + 127) / 128, e_local, (max_rows + 32 * MT - 1) / (32 * MT));
   const auto* wt = reinterpret_cast<const bf16x8*>(Wt);
 #define KAFKA_WG(MT_, G_, C_)                                                                                   \
   do {                                                                                                         \
+    constexpr int KC_ = MT_ == 4 ? 128 : 256;                                                                  \
     if (pin)                                                                                                   \
-      wstream_grouped_kernel<MT_, 256, G_, C_, true><<<grid, 256, 0, st>>>(X, ldx, wt, N, K, perm_tok, perm_w,      \
+      wstream_grouped_kernel<MT_, KC_, G_, C_, true><<<grid, 256, 0, st>>>(X, ldx, wt, N, K, perm_tok, perm_w,      \
                                                                            expert_off, e_lo, Y, ldy, out, ldo);  \
     else                                                                                                       \
-      wstream_grouped_kernel<MT_, 256, G_, C_, false><<<grid, 256, 0, st>>>(X, ldx, wt, N, K, perm_tok, perm_w,     \
+      wstream_grouped_kernel<MT_, KC_, G_, C_, false><<<grid, 256, 0, st>>>(X, ldx, wt, N, K, perm_tok, perm_w,     \
                                                                             expert_off, e_lo, Y, ldy, out, ldo); \
   } while (0)
   const bool comb = out != nullptr;
   if (MT == 1) {
     if (gather) { if (comb) KAFKA_WG(1, true, true); else KAFKA_WG(1, true, false); }
     else { if (comb) KAFKA_WG(1, false, true); else KAFKA_WG(1, false, false); }
-  } else {
+  } else if (MT == 2) {
     if (gather) { if (comb) KAFKA_WG(2, true, true); else KAFKA_WG(2, true, false); }
     else { if (comb) KAFKA_WG(2, false, true); else KAFKA_WG(2, false, false); }
+  } else {
+    if (gather) { if (comb) KAFKA_WG(4, true, true); else KAFKA_WG(4, true, false); }
+    else { if (comb) KAFKA_WG(4, false, true); else KAFKA_WG(4, false, false); }
   }
 #undef KAFKA_WG
   return hipGetLastError();

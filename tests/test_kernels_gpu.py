@@ -398,7 +398,8 @@ def test_grouped_gemm(cuda, T, d, N, E, e_lo, e_n):
 @pytest.mark.parametrize("T,d,F,E,e_lo,e_n", [(1, 512, 512, 8, 0, 8), (37, 1024, 768, 8, 0, 8),
                                               (64, 4096, 1792, 8, 0, 8), (128, 512, 1024, 8, 2, 4),
                                               (100, 768, 256, 8, 4, 4), (300, 1024, 512, 8, 0, 8),
-                                              (640, 512, 512, 8, 0, 8)])
+                                              (640, 512, 512, 8, 0, 8), (256, 512, 1024, 8, 0, 8),
+                                              (200, 512, 1024, 8, 2, 4), (400, 4096, 1792, 8, 0, 8)])
 def test_wstream_grouped(cuda, T, d, F, E, e_lo, e_n):
     """Expert MLP on the grouped weight-streaming kernel (GLU-tiled w13 with fused SwiGLU, w2 with the fused weighted
     combine) vs the fp32 reference of the same routing, including an expert-parallel subset of experts."""
