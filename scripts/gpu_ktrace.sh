@@ -8,4 +8,7 @@ mkdir -p $O && cd /tmp
 env ${KT_ENV:-KAFKA_X=0} timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O -o run --output-format csv -- \
   python3 $R/bench.py --steps ${KT_STEPS:-60} --warmup 20 ${KT_ARGS} > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
 cd $R && python scripts/ktrace_shapes.py $O/run_kernel_trace.csv ${KT_STEPS:-60} > $O/shapes.txt 2>&1
+python scripts/ktrace_gaps.py $O/run_kernel_trace.csv ${KT_STEPS:-60} > $O/gaps.txt 2>&1
+# the raw trace (tens of MB) would push gpurun_out past what a call copies back: keep it only when asked
+[[ -n $KT_KEEP_CSV ]] || rm -f $O/run_kernel_trace.csv
 head -${KT_HEAD:-25} $O/shapes.txt
