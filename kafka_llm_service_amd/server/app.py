@@ -121,9 +121,14 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
             prof = cProfile.Profile()
             prof.enable()
         await st.start()
+        lag_task = None
+        if trace.tracer() is not None:  # API event-loop lag (a blocked loop delays every request before its handler)
+            lag_task = asyncio.get_running_loop().create_task(_loop_lag_monitor())
         try:
             yield
         finally:
+            if lag_task is not None:
+                lag_task.cancel()
             await st.stop()
             if prof is not None:
                 import pstats
@@ -133,6 +138,17 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
                     ps = pstats.Stats(prof, stream=f)
                     ps.sort_stats("tottime").print_stats(45)
                     ps.sort_stats("cumtime").print_stats(60)
+
+    async def _loop_lag_monitor(period: float = 0.002) -> None:
+        """Sleep `period` over and over; every wake-up later than 2 ms past its deadline is an `api_loop_lag` span
+        (the time the event loop was busy elsewhere: a request arriving then waits that long before its handler)."""
+        tr = trace.tracer()
+        while True:
+            t = time.perf_counter()
+            await asyncio.sleep(period)
+            late = time.perf_counter() - t - period
+            if late > 0.002:
+                tr.complete("api_loop_lag", "api", t + period, t + period + late, "loop")
 
     app = FastAPI(title="kafka-llm-service-amd", lifespan=lifespan)
     app.state.kafka = st

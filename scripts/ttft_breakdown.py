@@ -38,6 +38,16 @@ def main():
             continue
         print(f"{n:20s} {len(d):6d} {d[len(d) // 2]:9.2f} {d[min(len(d) - 1, int(0.99 * len(d)))]:9.2f} "
               f"{statistics.fmean(d):9.2f}")
+    lag = sorted((e["ts"] / 1e3, e["dur"] / 1e3) for e in evs if e["name"] == "api_loop_lag")
+    if lag:  # API event loop blocked (> 2 ms late wake-ups): total, longest, and the busiest 100 ms window
+        tot = sum(d for _, d in lag)
+        best, j = 0.0, 0
+        for i in range(len(lag)):
+            while lag[i][0] - lag[j][0] > 100.0:
+                j += 1
+            best = max(best, sum(d for _, d in lag[j:i + 1]))
+        print(f"api loop lag: {len(lag)} stalls > 2 ms, {tot:.1f} ms in all, longest {max(d for _, d in lag):.1f} ms, "
+              f"busiest 100 ms window {best:.1f} ms blocked")
     steps = sorted(e["dur"] / 1e3 for e in evs if e["name"] == "launch")
     if steps:
         print(f"engine launch spans: {len(steps)}, p50 {steps[len(steps) // 2]:.2f} ms")
