@@ -15,6 +15,7 @@ import itertools
 import logging
 import multiprocessing as mp
 import os
+import queue
 import threading
 import time
 from dataclasses import asdict
@@ -240,6 +241,11 @@ class DPClient:
         self.procs: list = [None] * n_replicas
         self._group_procs: list[list] = [[] for _ in range(n_replicas)]
         self._send_locks = [threading.Lock() for _ in range(n_replicas)]
+        # the request path's messages (add / abort) leave through one sender thread per replica: Connection.send
+        # blocks once the pipe buffer is full, and the replica drains its pipe only between steps — a burst of new
+        # turns sent from the event loop stalled the whole API for up to a step of a busy engine (175 ms measured,
+        # profiles/r06/serve/). FIFO per replica keeps add -> abort order; tagged with the replica generation
+        self._outq = [queue.SimpleQueue() for _ in range(n_replicas)]
         self._streams: dict[str, tuple[asyncio.AbstractEventLoop, asyncio.Queue, int]] = {}
         self._lock = threading.Lock()
         self._loads = [0] * n_replicas
@@ -262,6 +268,8 @@ class DPClient:
             self._await_ready(r, conns)
         self._monitor_thread = threading.Thread(target=self._monitor, daemon=True, name="kafka-dp-monitor")
         self._monitor_thread.start()
+        for r in range(n_replicas):
+            threading.Thread(target=self._sender, args=(r,), daemon=True, name=f"kafka-dp-sender{r}").start()
 
     # ---- replica lifecycle -------------------------------------------------------------------------------------
     def _spawn(self, r: int, port: int) -> list:
@@ -374,6 +382,28 @@ class DPClient:
         with self._send_locks[r]:
             self.conns[r].send(msg)
 
+    def _post(self, r: int, msg) -> None:
+        """Queue msg for replica r's sender thread (never blocks the caller)."""
+        self._outq[r].put((self._gen[r], msg))
+
+    def _sender(self, r: int) -> None:
+        while True:
+            gen, msg = self._outq[r].get()
+            if msg is None:
+                return
+            if gen != self._gen[r]:
+                continue  # for a replica process that has been replaced: its streams were failed with it
+            try:
+                self._send(r, msg)
+            except (OSError, BrokenPipeError, EOFError, AttributeError):
+                if msg[0] == "add":  # the replica died between routing and this send: fail the stream now
+                    with self._lock:
+                        st = self._streams.pop(msg[1], None)
+                        if st is not None:
+                            self._loads[r] -= 1
+                    if st is not None:
+                        st[0].call_soon_threadsafe(st[1].put_nowait, EngineUnavailable(f"engine replica {r} is down"))
+
     def _send_quiet(self, r: int, msg) -> None:
         """Best-effort control message (aborts): a replica that is down has nothing to abort."""
         try:
@@ -452,12 +482,7 @@ class DPClient:
             payload = ("ref", n, list(prompt_ids[n:]))
         else:
             payload = list(prompt_ids)
-        try:
-            self._send(r, ("add", request_id, payload, pd, time.perf_counter()))
-        except (OSError, BrokenPipeError):
-            with self._lock:
-                self._streams.pop(request_id, None)
-            raise EngineUnavailable(f"engine replica {r} is down")
+        self._post(r, ("add", request_id, payload, pd, time.perf_counter()))
         done = False
         try:
             while True:
@@ -473,13 +498,13 @@ class DPClient:
                 with self._lock:
                     if self._streams.pop(request_id, None) is not None:
                         self._loads[r] -= 1
-                self._send_quiet(r, ("abort", request_id))
+                self._post(r, ("abort", request_id))
 
     def abort(self, request_id: str) -> None:
         with self._lock:
             s = self._streams.get(request_id)
         if s is not None:
-            self._send_quiet(s[2], ("abort", request_id))
+            self._post(s[2], ("abort", request_id))
 
     async def warm_prefix(self, token_ids: list[int]) -> None:
         """Prefill the shared prefix on EVERY live replica (bypassing thread routing), then pin it everywhere."""
@@ -516,10 +541,7 @@ class DPClient:
 
     def health(self) -> dict:
         for r in range(self.n_replicas):
-            try:
-                self._send(r, ("health",))
-            except (OSError, BrokenPipeError):
-                pass
+            self._post(r, ("health",))  # (answered asynchronously: the reader stores it for the next call)
         out = {"replicas": self.n_replicas}
         for r in range(self.n_replicas):
             out[f"replica{r}"] = dict(self._health[r], active=self._loads[r], alive=bool(self._alive[r]),
@@ -528,6 +550,8 @@ class DPClient:
 
     async def close(self) -> None:
         self._closing = True
+        for r in range(self.n_replicas):
+            self._outq[r].put((self._gen[r], None))  # stops the sender thread
         for r in range(self.n_replicas):
             try:
                 self._send(r, ("stop",))

@@ -55,6 +55,10 @@ class FakeEngine:
     def kv_stats(self) -> dict:
         return {"num_blocks": 1 << 16, "free": 1 << 16, "evictable": 0, "hit_tokens": 0}
 
+    def perf_stats(self) -> dict:
+        """The health message's perf block (LLMEngine.perf_stats): no GPU, only the step count."""
+        return {"device": "fake", "steps": self.stats["steps"]}
+
     def step(self) -> list[StepOutput]:
         cost = self.step_s
         while self.waiting:

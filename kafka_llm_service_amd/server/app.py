@@ -28,6 +28,7 @@ SSE behaviour (SURVEY.md §2.5.1/2.5.2, quirks Q1-Q3, Q6-Q8 fixed):
 from __future__ import annotations
 
 import asyncio
+import gc
 import json
 import os
 import logging
@@ -121,6 +122,12 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
             prof = cProfile.Profile()
             prof.enable()
         await st.start()
+        # everything loaded so far (tokenizer tables, prompt sections, engine client, route closures: hundreds of
+        # thousands of long-lived objects) leaves the cyclic GC's view: a full collection walking them stalled the
+        # event loop for ~180 ms in the middle of a burst of new turns (profiles/r06/serve/: the loop-lag watchdog
+        # caught the loop inside a collection's finalizers)
+        gc.collect()
+        gc.freeze()
         lag_task = None
         if trace.tracer() is not None:  # API event-loop lag (a blocked loop delays every request before its handler)
             lag_task = asyncio.get_running_loop().create_task(_loop_lag_monitor())
@@ -143,10 +150,38 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
         """Sleep `period` over and over; every wake-up later than 2 ms past its deadline is an `api_loop_lag` span
         (the time the event loop was busy elsewhere: a request arriving then waits that long before its handler)."""
         tr = trace.tracer()
+        beat = [time.perf_counter()]
+        dump = os.environ.get("KAFKA_LOOP_STALL_DUMP")
+        if dump:  # diagnosis: a watchdog thread writes the loop thread's stack whenever it misses its beat by 50 ms
+            import sys
+            import threading
+            import traceback
+
+            loop_tid = threading.get_ident()
+
+            def _watch():
+                seen = 0.0
+                with open(dump, "a") as f:
+                    while True:
+                        time.sleep(0.01)
+                        b = beat[0]
+                        if time.perf_counter() - b > 0.05 and b != seen:
+                            seen = b
+                            names = {t.ident: t.name for t in threading.enumerate()}
+                            f.write(f"--- loop stalled {1e3 * (time.perf_counter() - b):.0f} ms\n")
+                            for tid, fr in sys._current_frames().items():  # every thread: who holds the GIL?
+                                if tid == threading.get_ident():
+                                    continue
+                                tag = "LOOP" if tid == loop_tid else names.get(tid, str(tid))
+                                f.write(f"[{tag}]\n" + "".join(traceback.format_stack(fr)[-6:]))
+                            f.flush()
+
+            threading.Thread(target=_watch, daemon=True, name="loop-stall-dump").start()
         while True:
             t = time.perf_counter()
             await asyncio.sleep(period)
-            late = time.perf_counter() - t - period
+            beat[0] = time.perf_counter()
+            late = beat[0] - t - period
             if late > 0.002:
                 tr.complete("api_loop_lag", "api", t + period, t + period + late, "loop")
 
