@@ -663,8 +663,11 @@ __global__ __launch_bounds__(256 * KW) void wstream_gemm_kernel(const bf16* __re
 //   GATHER: A row = X[perm_tok[entry]] (token activations), else X[entry] (expert-sorted intermediate).
 //   Epilogue GLU (GLU-interleaved tiles): Y[entry, :N/2] = silu(gate) * up, bf16 — the SwiGLU of the expert MLP.
 //   Epilogue COMBINE: out_f32[perm_tok[entry], n] += perm_w[entry] * y (a token gets exactly k contributions).
+// (MT = 4: at most 256 registers so two workgroups share a CU — left free the compiler took 316, one wave per SIMD:
+// the 128-row expert tiles streamed 8 % slower, Mixtral 128 threads 5,155 vs 5,234 tok/s, profiles/r06/mixtral/;
+// MT = 2 spills 32+ registers under the same bound and keeps its 324)
 template <int MT, int KC, bool GATHER, bool COMBINE, bool PIN>
-__global__ __launch_bounds__(256) void wstream_grouped_kernel(const bf16* __restrict__ X, int64_t ldx,
+__global__ __launch_bounds__(256, MT == 4 ? 2 : 1) void wstream_grouped_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                                const bf16x8* __restrict__ Wt, int N, int K,
                                                                const int* __restrict__ perm_tok,
                                                                const float* __restrict__ perm_w,
