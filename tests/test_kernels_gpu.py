@@ -357,7 +357,7 @@ def test_sample_distribution(cuda):
     assert set(tok.tolist()) <= allowed
 
 
-@pytest.mark.parametrize("T,E,k", [(1, 8, 2), (128, 8, 2), (3000, 8, 2), (77, 16, 4)])
+@pytest.mark.parametrize("T,E,k", [(1, 8, 2), (128, 8, 2), (3000, 8, 2), (77, 16, 4), (2048, 8, 4), (5000, 8, 2)])
 def test_moe_route(cuda, T, E, k):
     torch.manual_seed(7)
     logits = torch.randn(T, E, device=cuda).to(torch.bfloat16)
