@@ -374,7 +374,9 @@ def main(argv=None):
         ts = time.perf_counter()
         outs = step()
         if steplog is not None:
-            steplog.append((ts, len(outs), sum(1 for o in outs if o.num_output_tokens == 1)))
+            st = getattr(eng.runner, "last_stats", None) or {}  # the step launched by this call (outs lag one step)
+            steplog.append((ts, len(outs), sum(1 for o in outs if o.num_output_tokens == 1), st.get("T"),
+                            st.get("s_total")))
         for o in outs:
             th, seq, resumed = req_thread[o.request_id]
             if record:
@@ -411,7 +413,9 @@ def main(argv=None):
     if ev:
         # GPU time inside the timed steps' spans (plan upload .. token download, kernel gaps included) vs the GPU
         # time between consecutive spans (idle unless the host had already queued the next step)
-        inside = sum(a.elapsed_time(b) for a, b in ev)
+        per_step = [a.elapsed_time(b) for a, b in ev]
+        timing["gpu_per_step"] = per_step  # (KAFKA_BENCH_STEPLOG: the per-step trace carries them)
+        inside = sum(per_step)
         between = [ev[i][1].elapsed_time(ev[i + 1][0]) for i in range(len(ev) - 1)]
         timing["gpu_ms"] = {"in_step": round(inside / len(ev), 3),
                             "between_steps": round(sum(max(0.0, x) for x in between) / max(1, len(between)), 3)}
@@ -437,10 +441,15 @@ def main(argv=None):
     _barrier(leaders)
     if steplog is not None:
         with open(os.environ["KAFKA_BENCH_STEPLOG"], "w") as f:
-            for i, (ts, n, first) in enumerate(steplog):
+            for i, (ts, n, first, rows, ctx) in enumerate(steplog):
                 nxt = steplog[i + 1][0] if i + 1 < len(steplog) else ts
-                f.write(json.dumps({"i": i, "timed": args.warmup <= i < args.warmup + args.steps,
-                                    "ms": round((nxt - ts) * 1e3, 3), "outs": n, "first_tokens": first}) + "\n")
+                rec = {"i": i, "timed": args.warmup <= i < args.warmup + args.steps,
+                       "ms": round((nxt - ts) * 1e3, 3), "outs": n, "first_tokens": first, "rows": rows,
+                       "s_total": ctx}
+                g = timing.get("gpu_per_step") or []
+                if rec["timed"] and i - args.warmup < len(g):
+                    rec["gpu_ms"] = round(g[i - args.warmup], 3)
+                f.write(json.dumps(rec) + "\n")
     if tp > 1:
         tp_worker.release_followers()
     return _report(args, world, rank, dev, eng, timing, t1 - t0, setup_s)

@@ -228,6 +228,17 @@ def plan_prefill_items(tiles: list[tuple], hkv: int, target_wgs: int, min_chunk:
     return items, splits, ranges
 
 
+def merge_ranges(ranges: list[tuple[int, int]]) -> list[tuple[int, int]]:
+    """Sorted union of half-open row ranges, touching ones joined (one attn_merge launch per range)."""
+    out: list[tuple[int, int]] = []
+    for lo, hi in sorted(ranges):
+        if out and lo <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], hi))
+        else:
+            out.append((lo, hi))
+    return out
+
+
 def prefix_groups(bt: np.ndarray, nfull: np.ndarray, min_blocks: int) -> tuple[list[int], list[tuple[int, int]]]:
     """Cascade groups of decode rows: rows whose block tables start with the same pages share that KV prefix.
 
@@ -488,6 +499,8 @@ class ModelRunner:
         # decode_items_fixed without graphs too (equivalence tests; KAFKA_FIXED_DECODE_ITEMS=1 separates the graph
         # plan's cost from the replay's in an eager A/B)
         self.fixed_decode_items = os.environ.get("KAFKA_FIXED_DECODE_ITEMS", "0") == "1"
+        # a joined new turn's own keys (its history behind the shared prefix) ride in the cascade launch too
+        self.join_suffix = os.environ.get("KAFKA_JOIN_SUFFIX", "1") == "1"
         self.step_events: list | None = None  # (start, end) timing events per launched step when a list is set
         # grammar masks / forced tokens / penalties inside the sampler kernel (tables allocated on first use)
         self.lp = LogitsProcessor(self.device, self.vocab, max_slots=max(256, max_num_seqs))
@@ -577,21 +590,26 @@ class ModelRunner:
         # system prompt every new turn of a thread re-attends): their tokens join the group's prefix pass — one read
         # of the prefix pages per step for all rows — and their own tiles attend only the keys behind the prefix
         joins = self._prefix_joins(bt, B, pre, groups, tiles) if groups and self.variant == 3 else {}
+        sfx_slots, sfx_rows = 0, []  # joined tiles whose own keys are planned into the prefix pass: slots, rows
         if B:
             kv_start = np.zeros(B, dtype=np.int64)
             npre = np.zeros(B, dtype=np.int64)
             pit = []
             if groups:
+                # joined tiles' own key spans (behind the prefix): with join_suffix they are items of this launch too
+                spans = {ti: tiles[ti][3] - groups[gi][1] * PAGE for gi, js in joins.items() for ti in js} \
+                    if self.join_suffix else {}
                 # key chunks sized so the prefix pass launches ~target_wgs workgroups over all groups together
                 work = sum(-(-n // self.tile) * p * PAGE for n, p in groups) + \
-                    sum(len(js) * groups[gi][1] * PAGE for gi, js in joins.items())
+                    sum(len(js) * groups[gi][1] * PAGE for gi, js in joins.items()) + sum(spans.values())
                 want = max(1, self.target_wgs // self.model.hkv)
                 chunk = min(MAX_ITEM_KEYS, max(256, -(-work // (want * 32)) * 32))
                 # one round of workgroups: per-group rounding up can overshoot the target by a few items, and a
                 # second round of a handful of workgroups doubles the launch
                 tiles_per_group = [-(-n // self.tile) + len(joins.get(gi, ())) for gi, (n, _) in enumerate(groups)]
                 while chunk < MAX_ITEM_KEYS and sum(t * -(-(p * PAGE) // chunk) for t, (_, p) in
-                                                    zip(tiles_per_group, groups)) > want:
+                                                    zip(tiles_per_group, groups)) + \
+                        sum(-(-sp // chunk) for sp in spans.values()) > want:
                     chunk += 32
                 r0 = 0
                 for gi, (n, p) in enumerate(groups):
@@ -609,6 +627,18 @@ class ModelRunner:
                             pit.append((B + q0, cnt, r0, c * ck, min(P, (c + 1) * ck), c, 1, 0))
                     for ti in joins.get(gi, ()):
                         tiles[ti] = tiles[ti][:5] + (P, nc)
+                        if ti in spans:
+                            # the tile's keys [P, extent) in pieces of ~chunk keys: alt partials at slots nc, nc + 1..
+                            # (beside its prefix pieces' slots 0..nc-1), so the step needs no separate prefill launch
+                            # for it; attn_merge combines all of the row's slots as before
+                            q0, cnt, btr, ext, hi = tiles[ti][:5]
+                            nsp = max(1, -(-spans[ti] // chunk))
+                            ps = -(-spans[ti] // (nsp * 32)) * 32
+                            nsp = -(-spans[ti] // ps)
+                            pit += [(B + q0, cnt, btr, P + c * ps, min(hi, P + (c + 1) * ps), nc + c, 1, 0)
+                                    for c in range(nsp)]
+                            sfx_slots = max(sfx_slots, nc + nsp)
+                            sfx_rows.append((q0, q0 + cnt))
                     kv_start[r0:r0 + n] = P
                     npre[r0:r0 + n] = nc
                     h.cascade_prefix = max(h.cascade_prefix, P)
@@ -617,11 +647,17 @@ class ModelRunner:
             if pit:
                 h.n_prefix_items = len(pit)
                 i32_parts.append(np.asarray(pit, dtype=np.int32).reshape(-1))
-        if tiles:
+        if sfx_rows:  # (their suffix items are in the prefix pass)
+            done = {ti for js in joins.values() for ti in js}
+            tiles = [t for ti, t in enumerate(tiles) if ti not in done]
+        if tiles or sfx_rows:
             # long tiles (a new turn against a ~20k-token cached context, the late tiles of a causal prompt) are
             # split along the key range so the launch is balanced; their partials are merged afterwards
             items, h.prefill_splits, ranges = plan_prefill_items(tiles, self.model.hkv, self.target_wgs,
                                                                  min(256, self.prefill_kv_chunk))
+            if sfx_rows:
+                h.prefill_splits = max(h.prefill_splits, sfx_slots)
+                ranges = merge_ranges(ranges + sfx_rows)
             h.n_items = len(items)
             i32_parts.append(np.asarray(items, dtype=np.int32).reshape(-1))
             if ranges:
@@ -633,7 +669,7 @@ class ModelRunner:
         h.stats = {"B": B, "T": T, "cascade_prefix": h.cascade_prefix, "cascade_groups": len(groups),
                    "prefix_joined_tiles": h.prefix_joined,
                    "decode_items": h.n_dec_items, "prefix_items": h.n_prefix_items, "s_total": h.s_total,
-                   "prefill_splits": h.prefill_splits}
+                   "prefill_splits": h.prefill_splits, "prefill_items": h.n_items}
         return h, sample_seqs
 
     @staticmethod
@@ -715,9 +751,10 @@ class ModelRunner:
             if h.n_prefix_items and self.cascade_bf16:
                 meta.pre_part = torch.empty(B, Hq, h.s_total, D, dtype=torch.bfloat16, device=self.device)
             meta.extra["cascade_prefix"] = h.cascade_prefix
-        if h.n_items:
-            meta.prefill_items = d32[o:o + h.n_items * 8].view(-1, 8)
-            o += h.n_items * 8
+        if h.n_items or h.n_merge:
+            if h.n_items:
+                meta.prefill_items = d32[o:o + h.n_items * 8].view(-1, 8)
+                o += h.n_items * 8
             if h.prefill_splits:
                 Tp = T - B
                 meta.prefill_splits = h.prefill_splits

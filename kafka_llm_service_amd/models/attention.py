@@ -10,7 +10,9 @@ chunk tokens. Per layer:
     covers only the per-row suffix [P, len), folding the prefix partials into its merge. Rows with different system
     prompts form different groups (model_runner.prefix_groups); rows without a group read their whole context.
   * prefill rows: work items of up to 256 (token, head) rows against the causal key range (``attn_prefill``)
-    write bf16 output directly.
+    write bf16 output directly, or (long ranges) fp32 partials merged by ``attn_merge``. A new turn behind a cascade
+    group's prefix rides in the group's prefix pass twice over: its prefix pieces and its own keys' pieces are items
+    of the same launch (model_runner.build_host ``join_suffix``), leaving only the merge.
 
 ``AttnMeta`` holds only device tensors that the model runner prepares once per step (shared by all layers), so
 the decode path is hipGraph-capturable (fixed shapes per batch bucket).
@@ -54,15 +56,13 @@ class AttnMeta:
 
 def _prefill_part(q, k_cache, v_cache, meta: AttnMeta, out: torch.Tensor) -> None:
     B = meta.num_decode
-    if meta.prefill_splits:
+    if meta.prefill_items is not None:  # (None when every prefill tile rode in the cascade launch)
+        split = bool(meta.prefill_splits)
         ops.attn_prefill(meta.prefill_items, q[B:], k_cache, v_cache, meta.block_tables, meta.q_limit[B:],
-                         meta.scale, out=out[B:], out_part=meta.prefill_part, lse_part=meta.prefill_lse,
-                         variant=meta.variant)
-        for lo, hi in meta.prefill_merge:
-            ops.attn_merge(meta.prefill_part[lo:hi], meta.prefill_lse[lo:hi], out[B + lo:B + hi])
-    else:
-        ops.attn_prefill(meta.prefill_items, q[B:], k_cache, v_cache, meta.block_tables, meta.q_limit[B:],
-                         meta.scale, out=out[B:], variant=meta.variant)
+                         meta.scale, out=out[B:], out_part=meta.prefill_part if split else None,
+                         lse_part=meta.prefill_lse if split else None, variant=meta.variant)
+    for lo, hi in meta.prefill_merge:
+        ops.attn_merge(meta.prefill_part[lo:hi], meta.prefill_lse[lo:hi], out[B + lo:B + hi])
 
 
 def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, meta: AttnMeta,
@@ -83,7 +83,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         # the decode kernel merges each row's prefix partials and its own pieces and writes the final rows
         ops.attn_decode_items(qd, k_cache, v_cache, meta.block_tables, meta.decode_items, meta.part, meta.lse,
                               meta.scale, out=out[:B], pre_part=meta.pre_part)
-    if meta.prefill_items is not None and meta.num_tokens > B:
+    if meta.num_tokens > B and (meta.prefill_items is not None or meta.prefill_merge):
         _prefill_part(q, k_cache, v_cache, meta, out)
 
 

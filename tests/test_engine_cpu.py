@@ -547,11 +547,13 @@ def test_bf16_cascade_partials_close_to_fp32(base_engine, monkeypatch):
     assert (a - b).abs().max().item() < 0.05 * a.abs().max().item() + 0.05
 
 
-def test_new_turn_rows_join_the_prefix_pass(base_engine):
+@pytest.mark.parametrize("join_suffix", [False, True])
+def test_new_turn_rows_join_the_prefix_pass(base_engine, join_suffix):
     """New-turn prefill chunks that start behind a cascade group's cached prefix take part in the group's prefix
     pass (model_runner._prefix_joins: one read of the shared pages per step for decode AND prefill rows, fp32
     partials merged with the chunk's own tiles over the keys behind the prefix): the tokens equal plain per-row
-    attention, and the joined path actually ran (steps with joined tiles)."""
+    attention, and the joined path actually ran (steps with joined tiles). With ``join_suffix`` the chunk's own
+    keys are items of the same cascade launch too: steps with joined tiles then launch no prefill tile kernel."""
     prompts = _prompts(seed=41, shared=160, tails=(5, 23, 40))
     late = _prompts(seed=42, shared=0, tails=(37, 90))  # new turns arriving while the group decodes
     late = [prompts[0][:160] + t for t in late]
@@ -560,6 +562,7 @@ def test_new_turn_rows_join_the_prefix_pass(base_engine):
     for cascade in (False, True):
         e = _engine(model=base_engine.model, use_cascade=cascade, cascade_min_prefix=16, prefill_kv_chunk=64)
         e.runner.cascade_bf16 = False  # fp32 prefix partials: token-exact against the plain path
+        e.runner.join_suffix = join_suffix
         e.generate([prompts[0][:160] + [7]], GREEDY)  # the shared prefix is cached
         seqs = [e.add_request(f"r{i}", p, sp) for i, p in enumerate(prompts)]
         for _ in range(3):
@@ -571,6 +574,8 @@ def test_new_turn_rows_join_the_prefix_pass(base_engine):
         if cascade:
             joined = [st.get("prefix_joined_tiles", 0) for st in e.runner.recent_stats]
             assert max(joined) >= 2, joined
+            items = [st["prefill_items"] for st in e.runner.recent_stats if st.get("prefix_joined_tiles")]
+            assert (max(items) == 0) if join_suffix else (min(items) > 0), items
     assert outs[0] == outs[1]
 
 
