@@ -20,11 +20,15 @@ the decode path is hipGraph-capturable (fixed shapes per batch bucket).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
 
 from kafka_llm_service_amd import ops
+
+# KAFKA_FUSED_PREFILL_MERGE=0: prefill rows' partials merged by their own attn_merge launch, never by the decode launch
+FUSE_PREFILL_MERGE = os.environ.get("KAFKA_FUSED_PREFILL_MERGE", "1") == "1"
 
 
 @dataclass
@@ -80,9 +84,16 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                              out_part=meta.pre_part if meta.pre_part is not None else meta.part, lse_part=meta.lse,
                              variant=meta.variant, alt_part=meta.prefill_part if joined else None,
                              alt_lse=meta.prefill_lse if joined else None, alt_tok_off=B)
-        # the decode kernel merges each row's prefix partials and its own pieces and writes the final rows
+        # the decode kernel merges each row's prefix partials and its own pieces and writes the final rows; when
+        # every prefill tile rode in the cascade launch, its extra workgroups also merge the prefill rows' partials
+        merge = None
+        if meta.prefill_items is None and len(meta.prefill_merge) == 1 and FUSE_PREFILL_MERGE:
+            lo, hi = meta.prefill_merge[0]
+            merge = (meta.prefill_part[lo:hi], meta.prefill_lse[lo:hi], out[B + lo:B + hi])
         ops.attn_decode_items(qd, k_cache, v_cache, meta.block_tables, meta.decode_items, meta.part, meta.lse,
-                              meta.scale, out=out[:B], pre_part=meta.pre_part)
+                              meta.scale, out=out[:B], pre_part=meta.pre_part, merge=merge)
+        if merge is not None:
+            return
     if meta.num_tokens > B and (meta.prefill_items is not None or meta.prefill_merge):
         _prefill_part(q, k_cache, v_cache, meta, out)
 

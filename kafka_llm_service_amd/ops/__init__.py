@@ -106,19 +106,24 @@ DECODE_ITEM = 8  # int32 fields of a decode work item: (b, lo, hi, split, nsplit
 
 
 def attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale: float, out=None,
-                      pre_part=None) -> None:
+                      pre_part=None, merge=None) -> None:
     """Paged decode attention over work items (int32 [n, 8]: row b, key range [lo, hi), piece ``split`` of
     ``nsplit``, ``npre`` prefix partials in front). Each item writes its (O, lse2) partial to slot npre + split of
     [B, Hq, S_total, D]; with ``out`` (npre + nsplit <= 64 per row) the rows are instead merged with their prefix
     partials and written as final bf16 — a one-piece row directly, a split row by the last piece to finish (ticket
     counters, no merge kernel). ``pre_part``: bf16 prefix partials written by the tile-v3 cascade (slots < npre,
-    out_part's shape) — half the bytes of the fp32 round trip."""
+    out_part's shape) — half the bytes of the fp32 round trip. ``merge`` = (part [rows, Hq, S2, D], lse [rows, Hq,
+    S2], out [rows, Hq, D]): other rows' fp32 partials (a step's prefill rows) merged into ``out`` by extra
+    workgroups of the same launch, as ``attn_merge`` would."""
     if _gpu(q):
         tk = _tickets(q.device, q.shape[0] * k_cache.shape[1]) if out is not None else None
+        mp, ml, mo = merge if merge is not None else (None, None, None)
         ext().attn_decode(q, k_cache, v_cache, block_tables, items, out_part, lse_part, float(scale), out, tk,
-                          pre_part)
+                          pre_part, mp, ml, mo)
         return
     ref.attn_decode_items(q, k_cache, v_cache, block_tables, items, out_part, lse_part, scale, out, pre_part)
+    if merge is not None:
+        ref.attn_merge(*merge)
 
 
 def uniform_decode_items(seq_lens: torch.Tensor, kv_start: torch.Tensor | None, num_splits: int,

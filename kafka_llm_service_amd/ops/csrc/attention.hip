@@ -689,8 +689,48 @@ __device__ __forceinline__ void decode_piece(DecodeSmem<D>& sm, const bf16* __re
   if constexpr (OST) store_rows_sc1<D>(sm, out, out_stride, b, kvh, G);
 }
 
-// grid (Hkv, items): the Hkv heads of an item are consecutive workgroups, dealt to different XCDs, reading one page
-// row together (heads-fast: +7 % over items-fast, three workgroups per CU +5 % over two,
+// Prefill rows merged by the decode launch (grid rows past the decode items): a step whose new-turn rows rode in the
+// cascade launch (prefix AND own keys, model_runner join_suffix) has no prefill launch left, only the log-sum-exp
+// merge of those rows' fp32 partials — done by extra workgroups of this launch instead of an attn_merge launch of its
+// own (one kernel boundary and ramp less per layer). Workgroup (kvh, n_items + m): rows RPW m .. RPW m + RPW - 1,
+// heads kvh G .. kvh G + G - 1, 32 lanes x float4 columns per (row, head) as attn_merge_kernel.
+struct FusedMerge {
+  const float* part = nullptr;  // [rows, Hq, S, 128]
+  const float* lse = nullptr;   // [rows, Hq, S]
+  int S = 0;
+  int rows = 0;
+  bf16* out = nullptr;          // row r at out + r * out_stride
+  int64_t out_stride = 0;
+};
+
+__device__ __forceinline__ void fused_merge_rows(const FusedMerge& fm, int m, int kvh, int G, int Hq) {
+  constexpr int D = 128;
+  const int t = threadIdx.x >> 5, rpw = (8 % G == 0) ? 8 / G : 1;
+  const int rr = t / G, row = m * rpw + rr;
+  if (rr >= rpw || row >= fm.rows) return;
+  const int hh = kvh * G + t % G, c = (threadIdx.x & 31) * 4, S = fm.S;
+  const float* l = fm.lse + ((int64_t)row * Hq + hh) * S;
+  const float* p = fm.part + ((int64_t)row * Hq + hh) * S * D + c;
+  float M = -INFINITY;
+  for (int s = 0; s < S; ++s) M = fmaxf(M, l[s]);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float L = 0.f;
+  if (M != -INFINITY) {
+    for (int s = 0; s < S; ++s) {
+      const float w = exp2f(l[s] - M);
+      if (w > 0.f) acc += *reinterpret_cast<const f32x4*>(p + s * D) * w;  // (an unwritten slot has lse -inf)
+      L += w;
+    }
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  bf16x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = (bf16)(acc[j] * inv);
+  *reinterpret_cast<bf16x4*>(fm.out + (int64_t)row * fm.out_stride + (int64_t)hh * D + c) = o;
+}
+
+// grid (Hkv, items [+ merge workgroups]): the Hkv heads of an item are consecutive workgroups, dealt to different
+// XCDs, reading one page row together (heads-fast: +7 % over items-fast, three workgroups per CU +5 % over two,
 // profiles/r04/bench_ab_decode_placement_occ.jsonl)
 template <int D, bool FP8, bool OST = false>
 __global__ __launch_bounds__(256, FP8 ? 2 : 3) void attn_decode_kernel(const bf16* __restrict__ q, int64_t q_stride,
@@ -703,8 +743,13 @@ __global__ __launch_bounds__(256, FP8 ? 2 : 3) void attn_decode_kernel(const bf1
                                                                       float* __restrict__ lse_part, int S_total,
                                                                       float scale_log2, bf16* __restrict__ out,
                                                                       int64_t out_stride, int* __restrict__ tickets,
-                                                                      const bf16* __restrict__ pre_bf16) {
+                                                                      const bf16* __restrict__ pre_bf16, int n_items,
+                                                                      FusedMerge fm) {
   __shared__ DecodeSmem<D> sm;
+  if ((int)blockIdx.y >= n_items) {  // (workgroup-uniform)
+    fused_merge_rows(fm, blockIdx.y - n_items, blockIdx.x, G, Hkv * G);
+    return;
+  }
   const DecodeItem it = items[blockIdx.y];
   const int b = it.b, kvh = blockIdx.x, split = it.split, S = it.nsplit, split_offset = it.npre;
   // a malformed item (host bug) is dropped instead of indexing out of bounds (workgroup-uniform)
@@ -1204,13 +1249,20 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
                                               const void* v_cache, int fp8, int n_items, int B, int Hkv, int G, int D,
                                               const int* block_tables, int bt_stride, const int* items,
                                               float* out_part, float* lse_part, int S_total, float scale, bf16* out,
-                                              int64_t out_stride, int* tickets, const bf16* pre_bf16, hipStream_t st) {
+                                              int64_t out_stride, int* tickets, const bf16* pre_bf16,
+                                              const float* m_part, const float* m_lse, int m_S, int m_rows,
+                                              bf16* m_out, int64_t m_out_stride, hipStream_t st) {
   if (n_items == 0) return hipSuccess;
-  if (D != 128 || G > 8 || G < 1 || n_items > 65535) return hipErrorInvalidValue;
+  if (D != 128 || G > 8 || G < 1) return hipErrorInvalidValue;
   if (out != nullptr && tickets == nullptr) return hipErrorInvalidValue;
+  if (m_rows > 0 && (m_part == nullptr || m_lse == nullptr || m_out == nullptr || m_S < 1)) return hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
   const auto* di = reinterpret_cast<const DecodeItem*>(items);
-  const dim3 grid(Hkv, n_items);
+  const int rpw = (8 % G == 0) ? 8 / G : 1;
+  const int n_mwg = m_rows > 0 ? (m_rows + rpw - 1) / rpw : 0;
+  if (n_items + n_mwg > 65535) return hipErrorInvalidValue;
+  const FusedMerge fm{m_part, m_lse, m_S, m_rows, m_out, m_out_stride};
+  const dim3 grid(Hkv, n_items + n_mwg);
   // KAFKA_SC1_ATTN (default 1): the bf16 rows as 16-B sc1 stores through LDS (decode_piece OST)
   static const bool sc1 = [] {
     const char* e = getenv("KAFKA_SC1_ATTN");
@@ -1220,15 +1272,16 @@ extern "C" hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, 
   if (ost && !fp8)
     attn_decode_kernel<128, false, true><<<grid, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables,
                                                                 bt_stride, di, B, out_part, lse_part, S_total,
-                                                                scale_log2, out, out_stride, tickets, pre_bf16);
+                                                                scale_log2, out, out_stride, tickets, pre_bf16,
+                                                                n_items, fm);
   else if (fp8)
     attn_decode_kernel<128, true><<<grid, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables, bt_stride,
                                                          di, B, out_part, lse_part, S_total, scale_log2, out,
-                                                         out_stride, tickets, pre_bf16);
+                                                         out_stride, tickets, pre_bf16, n_items, fm);
   else
     attn_decode_kernel<128, false><<<grid, 256, 0, st>>>(q, q_stride, k_cache, v_cache, Hkv, G, block_tables,
                                                           bt_stride, di, B, out_part, lse_part, S_total, scale_log2,
-                                                          out, out_stride, tickets, pre_bf16);
+                                                          out, out_stride, tickets, pre_bf16, n_items, fm);
   return hipGetLastError();
 }
 

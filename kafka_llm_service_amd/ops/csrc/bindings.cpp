@@ -28,7 +28,8 @@ hipError_t kafka_launch_attn_decode(const bf16* q, int64_t q_stride, const void*
                                     int n_items, int B, int Hkv, int G, int D, const int* block_tables, int bt_stride,
                                     const int* items, float* out_part, float* lse_part, int S_total, float scale,
                                     bf16* out, int64_t out_stride, int* tickets, const bf16* pre_bf16,
-                                    hipStream_t st);
+                                    const float* m_part, const float* m_lse, int m_S, int m_rows, bf16* m_out,
+                                    int64_t m_out_stride, hipStream_t st);
 hipError_t kafka_launch_attn_prefill(const void* items, int n_items, const bf16* q, int64_t q_stride,
                                      const void* k_cache, const void* v_cache, int fp8, int Hkv, int G, int D,
                                      const int* block_tables, int bt_stride, const int* q_limit, bf16* out,
@@ -258,7 +259,8 @@ static void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_s
 static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
                         at::Tensor items, at::Tensor out_part, at::Tensor lse_part, double scale,
                         c10::optional<at::Tensor> out, c10::optional<at::Tensor> tickets,
-                        c10::optional<at::Tensor> pre_part) {
+                        c10::optional<at::Tensor> pre_part, c10::optional<at::Tensor> m_part,
+                        c10::optional<at::Tensor> m_lse, c10::optional<at::Tensor> m_out) {
   CHECK_CUDA(q); CHECK_DT(q, at::kBFloat16); check_cache_pair(k_cache, v_cache);
   CHECK_DT(block_tables, at::kInt); CHECK_DT(items, at::kInt); CHECK_DT(out_part, at::kFloat);
   CHECK_DT(lse_part, at::kFloat);
@@ -295,11 +297,35 @@ static void attn_decode(at::Tensor q, at::Tensor k_cache, at::Tensor v_cache, at
                 "attn_decode: pre_part must match out_part's shape");
     pre = bptr(pre_part.value());
   }
+  // fused merge of prefill rows (attention.hip FusedMerge): m_part [rows, Hq, S2, 128] / m_lse [rows, Hq, S2] fp32
+  // -> m_out [rows, Hq, 128] bf16
+  const float *mp = nullptr, *ml = nullptr;
+  bf16* mo = nullptr;
+  int mS = 0, mrows = 0;
+  int64_t mstride = 0;
+  if (m_part.has_value()) {
+    TORCH_CHECK(m_lse.has_value() && m_out.has_value(), "attn_decode: a fused merge needs m_part, m_lse and m_out");
+    CHECK_CUDA(m_part.value()); CHECK_DT(m_part.value(), at::kFloat); CHECK_DT(m_lse.value(), at::kFloat);
+    CHECK_DT(m_out.value(), at::kBFloat16);
+    TORCH_CHECK(m_part->is_contiguous() && m_part->dim() == 4 && m_part->size(1) == Hq && m_part->size(3) == 128,
+                "attn_decode: m_part must be contiguous [rows, Hq, S, 128]");
+    mrows = m_part->size(0);
+    mS = m_part->size(2);
+    TORCH_CHECK(m_lse->is_contiguous() && m_lse->numel() == (int64_t)mrows * Hq * mS, "attn_decode: m_lse");
+    TORCH_CHECK(m_out->dim() == 3 && m_out->size(0) == mrows && m_out->size(1) == Hq && m_out->size(2) == 128 &&
+                    m_out->stride(2) == 1 && m_out->stride(1) == 128,
+                "attn_decode: m_out must be [rows, Hq, 128] with 128-element head rows");
+    mp = m_part->data_ptr<float>();
+    ml = m_lse->data_ptr<float>();
+    mo = bptr(m_out.value());
+    mstride = m_out->stride(0);
+  }
   CHECK_HIP(kafka_launch_attn_decode(bptr(q), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                       is_fp8_cache(k_cache) ? 1 : 0, items.size(0), B, Hkv,
                                       Hq / Hkv, 128, block_tables.data_ptr<int>(), block_tables.stride(0),
                                       items.data_ptr<int>(), out_part.data_ptr<float>(), lse_part.data_ptr<float>(),
-                                      S_total, scale, op, ostride, tp, pre, cur_stream()));
+                                      S_total, scale, op, ostride, tp, pre, mp, ml, mS, mrows, mo, mstride,
+                                      cur_stream()));
 }
 
 static void attn_prefill(at::Tensor items, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
@@ -970,7 +996,8 @@ PYBIND11_MODULE(_kafka_ops, m) {
   m.def("rope_kv_write", &rope_kv_write);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("items"), py::arg("out_part"), py::arg("lse_part"), py::arg("scale"), py::arg("out"),
-        py::arg("tickets"), py::arg("pre_part") = py::none());
+        py::arg("tickets"), py::arg("pre_part") = py::none(), py::arg("m_part") = py::none(),
+        py::arg("m_lse") = py::none(), py::arg("m_out") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("items"), py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("block_tables"), py::arg("q_limit"), py::arg("out"), py::arg("out_part"), py::arg("lse_part"),
         py::arg("scale"), py::arg("variant") = 0, py::arg("alt_part") = py::none(), py::arg("alt_lse") = py::none(),

@@ -157,6 +157,38 @@ def test_attn_decode_fused_merge(cuda, n_pre, S):
         _close(out, o_ref, atol=0.02, msg=f"fused merge n_pre={n_pre} S={S} launch {it}")
 
 
+@pytest.mark.parametrize("Hkv,G,rows,S2", [(8, 4, 105, 13), (4, 8, 3, 1), (8, 2, 9, 40), (2, 3, 5, 4)])
+def test_attn_decode_merges_prefill_rows(cuda, Hkv, G, rows, S2):
+    """Extra workgroups of the decode launch merge other rows' fp32 partials (attention.hip FusedMerge: a step's
+    prefill rows once every prefill tile rode in the cascade launch) as attn_merge does — unwritten slots (lse -inf,
+    NaN data) weigh nothing, rows outside the range stay untouched — and the decode rows are unchanged."""
+    torch.manual_seed(11)
+    D, Hq = 128, Hkv * G
+    lens = [40, 300, 17]
+    B = len(lens)
+    k, v, bt = _random_paged(B, lens, Hkv, cuda)
+    q = torch.randn(B, Hq, D, device=cuda, dtype=torch.bfloat16)
+    sl = torch.tensor(lens, dtype=torch.int32, device=cuda)
+    scale = 1 / math.sqrt(D)
+    items = ops.uniform_decode_items(sl, None, 1, 0)
+    part = torch.empty(B, Hq, 1, D, device=cuda)
+    lse = torch.empty(B, Hq, 1, device=cuda)
+    mp = torch.randn(rows, Hq, S2, D, device=cuda)
+    ml = torch.randn(rows, Hq, S2, device=cuda) * 4
+    if S2 > 1:
+        ml[:, :, -1] = float("-inf")
+        mp[:, :, -1] = float("nan")
+    out = torch.full((B + 1 + rows + 1, Hq, D), float("nan"), device=cuda, dtype=torch.bfloat16)
+    ops.attn_decode_items(q, k, v, bt, items, part, lse, scale, out=out[:B], merge=(mp, ml, out[B + 1:B + 1 + rows]))
+    torch.cuda.synchronize()
+    o_ref, _ = ref.attn_decode_full(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), sl.cpu(), scale)
+    _close(out[:B], o_ref, atol=0.02, msg="decode rows")
+    m_ref = torch.empty(rows, Hq, D)
+    ref.attn_merge(mp.cpu(), ml.cpu(), m_ref)
+    _close(out[B + 1:B + 1 + rows], m_ref, atol=0.02, msg="merged prefill rows")
+    assert torch.isnan(out[B].float()).all() and torch.isnan(out[-1].float()).all(), "rows outside the merge range"
+
+
 def test_attn_decode_multi_group_cascade(cuda):
     """Three prefix groups (different shared prefixes of 208 / 320 / 96 tokens) + two ungrouped rows, planned by the
     engine's own planner (model_runner.prefix_groups / decode_items, long suffixes split into pieces), run as
