@@ -237,9 +237,11 @@ def untile_weight(wt: torch.Tensor, glu: bool = False) -> torch.Tensor:
 
 
 # Steps of up to this many rows run the dense projections on the weight-streaming kernel (csrc/wstream_gemm.hip).
-# The kernel takes up to 256 rows (beyond 128 as two row tiles whose workgroups share each weight slice through the
-# MALL) but there it loses to hipBLASLt (gate_up 101 vs 66 us at 168..248 rows; bench 7,359 vs 7,546 tok/s,
-# profiles/r02/stream_max_m_256_rejected.jsonl), so the default stays 128. Env KAFKA_STREAM_MAX_M (1..256).
+# The kernel takes up to 256 rows: one 192-row tile (MT = 6) up to 192, beyond that two row tiles of 128 sharing each
+# weight slice through the MALL, where it loses to hipBLASLt (gate_up 101 vs 66 us at 168..248 rows; bench 7,359 vs
+# 7,546 tok/s, profiles/r02/stream_max_m_256_rejected.jsonl). The 192-row tile only ties the skinny GEMM + hipBLASLt
+# path of 129..192-row steps (8,725 vs 8,732 tok/s, profiles/r06/mt6/), so the default stays 128; tiled-only models
+# (no row-major copy for hipBLASLt) stream every step up to 256 rows. Env KAFKA_STREAM_MAX_M (1..256).
 STREAM_MAX_M = max(1, min(256, int(os.environ.get("KAFKA_STREAM_MAX_M", "128"))))
 STREAM_KERNEL_MAX_M = 256
 
@@ -249,8 +251,8 @@ def stream_plan(M: int, N: int, K: int, max_splits: int = 8) -> tuple[int, int, 
     kafka_wstream_plan in csrc/wstream_gemm.hip, mirrored so CPU runs take the same split decisions)."""
     if M < 1 or M > STREAM_KERNEL_MAX_M or N % 32 or N <= 0:
         return None
-    mt = 1 if M <= 32 else (2 if M <= 64 else (3 if M <= 96 else 4))
-    kc = 128 if mt == 4 else 256
+    mt = 1 if M <= 32 else (2 if M <= 64 else (3 if M <= 96 else (4 if M <= 128 or M > 192 else 6)))
+    kc = 128 if mt >= 4 else 256
     if K % kc or K <= 0:
         return None
     nx, chunks, s = (N + 127) // 128 * ((M + 32 * mt - 1) // (32 * mt)), K // kc, 1

@@ -832,14 +832,16 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 // ops.stream_plan). max_splits caps S (1 forces a direct bf16 output).
 //   MT: 1 tile up to 32 rows, 2 up to 64, 3 up to 96 (a decode batch plus a short new-turn chunk: three 32-row tiles
 //   on 256-deep chunks, 96 KB X stage; +0.24 % over four on 128-deep ones, profiles/r04/bench_ab_wstream_mt3.jsonl),
-//   else 4 (128-deep chunks: 256-deep ones lose 1.9 %, profiles/r04/bench_ab_wstream_mt4_kc256.jsonl). Beyond 128
-//   rows (tiled-only models) the rows are split over row tiles of 128.
+//   4 up to 128 (128-deep chunks: 256-deep ones lose 1.9 %, profiles/r04/bench_ab_wstream_mt4_kc256.jsonl), 6 up to
+//   192 (a decode batch plus a ~100-token new turn: one 192-row tile on 128-deep chunks, 96 KB X stage, ~210
+//   registers at one wave per SIMD; two 128-row tiles sharing the weight slice lost to hipBLASLt, r02/r05). Beyond
+//   192 rows (tiled-only models) the rows are split over row tiles of 128.
 //   Measured and rejected (profiles/r04/): 64-row tiles sharing a weight slice in one XCD's L2 beyond 64 rows (-0.6 %)
 //   and 33..64 rows as two 32-row tiles (-4.8 %).
 extern "C" int kafka_wstream_plan(int M, int N, int K, int max_splits, int* mt, int* kc, int* splits) {
   if (M < 1 || M > 256 || N % 32 != 0 || N <= 0) return 1;
-  const int MT = M <= 32 ? 1 : (M <= 64 ? 2 : (M <= 96 ? 3 : 4));
-  const int KC = MT == 4 ? 128 : 256;
+  const int MT = M <= 32 ? 1 : (M <= 64 ? 2 : (M <= 96 ? 3 : (M <= 128 || M > 192 ? 4 : 6)));
+  const int KC = MT >= 4 ? 128 : 256;
   if (K % KC != 0 || K <= 0) return 2;
   const int nx = (N + 127) / 128 * ((M + 32 * MT - 1) / (32 * MT));  // workgroups per split (x row tiles)
   const int chunks = K / KC;
@@ -906,6 +908,7 @@ extern "C" hipError_t kafka_launch_wstream_gemm(const bf16* X, int64_t ldx, cons
   else KAFKA_WS_IF(3, 256, 1)
   else KAFKA_WS_IF(4, 128, 1)
   else KAFKA_WS_IF(4, 128, 2)
+  else KAFKA_WS_IF(6, 128, 1)
   else return hipErrorInvalidValue;
 #undef KAFKA_WS_IF
 #undef KAFKA_WS

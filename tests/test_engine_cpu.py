@@ -327,7 +327,9 @@ def test_stream_plan_rules(monkeypatch):
     3 / 4 x 32 rows), 128-deep chunks for four tiles, split-K grown toward the grid target."""
     from kafka_llm_service_amd import ops
 
-    assert [ops.stream_plan(M, 28672, 4096)[0] for M in (1, 32, 33, 64, 65, 96, 97, 128)] == [1, 1, 2, 2, 3, 3, 4, 4]
+    assert [ops.stream_plan(M, 28672, 4096)[0] for M in (1, 32, 33, 64, 65, 96, 97, 128, 129, 192, 193, 256)] == \
+        [1, 1, 2, 2, 3, 3, 4, 4, 6, 6, 4, 4]  # 129..192: one 192-row tile; beyond: row tiles of 128
+    assert ops.stream_plan(169, 28672, 4096)[1:] == (128, 1) and ops.stream_plan(169, 6144, 4096)[2] == 4
     assert ops.stream_plan(128, 4096, 4096)[1] == 128 and ops.stream_plan(64, 4096, 4096)[1] == 256
     assert ops.stream_plan(64, 28672, 4096)[2] == 1 and ops.stream_plan(64, 6144, 4096)[2] == 4
     assert ops.stream_plan(114, 28672, 4096)[2] == 1  # gate_up unsplit at 97..128 rows (fused SwiGLU)
@@ -479,10 +481,12 @@ def test_plan_prefill_items_balances_causal_tiles():
     assert 200 <= len(items) * 8 <= 256, len(items) * 8
 
 
-def test_padded_mixed_steps_match_unpadded(base_engine):
-    """Steps of 129..256 token rows padded with inert rows (pad_step_rows) produce the same greedy tokens."""
+def test_padded_mixed_steps_match_unpadded(base_engine, monkeypatch):
+    """Steps beyond the streaming GEMM's rows (up to 256) padded with inert rows (pad_step_rows) produce the same
+    greedy tokens (checked with the streaming bound at 128, so a 150-row step is padded)."""
     from kafka_llm_service_amd.engine.model_runner import pad_step_rows
 
+    monkeypatch.setattr(ops, "STREAM_MAX_M", 128)
     assert [pad_step_rows(t) for t in (64, 128, 129, 160, 168, 170, 185, 192, 250, 256, 300)] == \
         [64, 128, 168, 168, 168, 184, 200, 200, 250, 256, 300]
     prompts = _prompts(seed=21, shared=100, tails=(50,))  # first step: one 150-token prefill -> padded to 168 rows
@@ -507,6 +511,7 @@ def test_skinny_projections_match_blas(monkeypatch):
     from kafka_llm_service_amd.models import llama
 
     prompts = _prompts(seed=23, shared=100, tails=(50,))  # first step: one 150-row prefill
+    monkeypatch.setattr(ops, "STREAM_MAX_M", 128)  # (150 rows would otherwise stream: 192-row tile)
     e0 = _engine(decode_gemm="stream")
     monkeypatch.setattr(llama, "SKINNY", frozenset())
     ref = e0.generate(prompts, GREEDY)

@@ -459,7 +459,7 @@ def test_wstream_grouped(cuda, T, d, F, E, e_lo, e_n):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("M", [1, 7, 32, 33, 64, 65, 80, 96, 97, 128, 129, 200, 256])
+@pytest.mark.parametrize("M", [1, 7, 32, 33, 64, 65, 80, 96, 97, 128, 129, 169, 192, 193, 200, 256])
 @pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1280, 8192), (16032, 1024), (96, 512)])
 def test_wstream_gemm(cuda, M, N, K):
     """Weight-streaming decode GEMM on wave-tiled weights (bf16 direct and split-K slabs) vs fp32 matmul."""
@@ -480,7 +480,7 @@ def test_wstream_gemm(cuda, M, N, K):
         torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("M", [17, 64, 128])
+@pytest.mark.parametrize("M", [17, 64, 128, 169])
 def test_wstream_slabs_reused_buffer(cuda, M):
     """The split-K slabs leave the GEMM as sc1 stores (their lines bypass the writer XCD's L2). Rewrite ONE slab buffer
     many times after consumers on every XCD have read (and cached) its previous contents, as the engine does layer
@@ -528,7 +528,7 @@ def test_skinny_slabs_reused_buffer(cuda, M):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("M", [1, 40, 64, 80, 100, 168, 256])
+@pytest.mark.parametrize("M", [1, 40, 64, 80, 100, 150, 168, 192, 256])
 @pytest.mark.parametrize("N,K", [(28672, 4096), (7168, 8192), (2048, 1024)])
 def test_wstream_glu(cuda, M, N, K):
     """GLU-tiled gate_up: fused silu(gate) * up epilogue (one split) and de-interleaved gate | up slabs (split plans)
