@@ -13,6 +13,8 @@ token ids so the agent can store them with the message (thread token cache).
 """
 from __future__ import annotations
 
+import asyncio
+import os
 import time
 import uuid
 from typing import Any, AsyncGenerator
@@ -25,6 +27,16 @@ from kafka_llm_service_amd.engine.tokenizer import IncrementalDetokenizer, token
 from kafka_llm_service_amd.llm.base import LLMProvider
 from kafka_llm_service_amd.llm.types import LLMProviderError, Message, StreamChunk, Usage
 from kafka_llm_service_amd.obs import trace
+
+
+def _gpu_host() -> bool:
+    """GPUs visible to this process (counting them does not initialise HIP here: the engine owns the devices)."""
+    try:
+        import torch
+
+        return torch.cuda.device_count() > 0
+    except Exception:
+        return False
 
 
 class EngineLLMProvider(LLMProvider):
@@ -71,7 +83,25 @@ class EngineLLMProvider(LLMProvider):
         if hasattr(self.client, "warm_prefix"):
             await self.client.warm_prefix(ids)
             self._pin = ids
+            n = int(os.environ.get("KAFKA_WARM_BURST", "64" if _gpu_host() else "0"))
+            if n > 0:
+                await self._warm_burst(ids, n)
         return len(ids)
+
+    async def _warm_burst(self, prefix: list[int], n: int) -> None:
+        """A burst of ``n`` short requests behind the pinned prefix (tails of 8..103 tokens, 8 sampled tokens each)
+        before the API opens: the decode steps of 1..n rows and the mixed steps of the many row counts a burst of new
+        turns produces run once, so their kernels are loaded and their GEMM shapes resolved (hipBLASLt heuristics on
+        the first call of a shape) before the first real burst instead of inside it."""
+        rng = np.random.default_rng(0)
+        sp = SamplingParams(temperature=0.7, max_tokens=8, ignore_eos=True, seed=1)
+        pre = list(prefix)
+
+        async def one(i: int) -> None:
+            tail = [pre[j] for j in rng.integers(0, len(pre), size=8 + (i * 7) % 96)]
+            async for _ in self.client.generate(f"warm-burst-{i}", pre + tail, sp, f"warm-burst-{i}"):
+                pass
+        await asyncio.gather(*(one(i) for i in range(n)))
 
     def _maybe_pin(self, messages: list[Message], tools: list[dict] | None) -> None:
         """Pin the shared system prefix (system prompt + tool schemas, ~18k tokens for Kafka) in the engine's prefix

@@ -31,13 +31,25 @@ def main():
     evs = load(paths)
     names = ["api_http_ttft", "api_db_load", "api_db_save", "api_render", "api_engine_first", "pipe_in", "first_token",
              "pipe_out"]
-    print(f"{'span':20s} {'n':>6s} {'p50 ms':>9s} {'p99 ms':>9s} {'mean ms':>9s}")
-    for n in names:
-        d = sorted(e["dur"] / 1e3 for e in evs if e["name"] == n)
-        if not d:
-            continue
-        print(f"{n:20s} {len(d):6d} {d[len(d) // 2]:9.2f} {d[min(len(d) - 1, int(0.99 * len(d)))]:9.2f} "
-              f"{statistics.fmean(d):9.2f}")
+
+    def table(sel):
+        print(f"{'span':20s} {'n':>6s} {'p50 ms':>9s} {'p99 ms':>9s} {'mean ms':>9s}")
+        for n in names:
+            d = sorted(e["dur"] / 1e3 for e in sel if e["name"] == n)
+            if not d:
+                continue
+            print(f"{n:20s} {len(d):6d} {d[len(d) // 2]:9.2f} {d[min(len(d) - 1, int(0.99 * len(d)))]:9.2f} "
+                  f"{statistics.fmean(d):9.2f}")
+    table(evs)
+    # the first burst (spans starting within 150 ms of the first request: every thread's first turn in a burst run)
+    t0 = min((e["ts"] for e in evs if e["name"] == "api_http_ttft"), default=None)
+    if t0 is not None:
+        first = [e for e in evs if t0 <= e["ts"] <= t0 + 150e3]
+        print("-- first burst (spans starting within 150 ms of the first request)")
+        table(first)
+        lag0 = [e["dur"] / 1e3 for e in evs if e["name"] == "api_loop_lag" and t0 - 50e3 <= e["ts"] <= t0 + 400e3]
+        print(f"   api loop lag in [-50, +400] ms: {len(lag0)} stalls, {sum(lag0):.1f} ms, longest "
+              f"{max(lag0, default=0.0):.1f} ms")
     lag = sorted((e["ts"] / 1e3, e["dur"] / 1e3) for e in evs if e["name"] == "api_loop_lag")
     if lag:  # API event loop blocked (> 2 ms late wake-ups): total, longest, and the busiest 100 ms window
         tot = sum(d for _, d in lag)
