@@ -41,9 +41,17 @@ def main():
             print(f"{n:20s} {len(d):6d} {d[len(d) // 2]:9.2f} {d[min(len(d) - 1, int(0.99 * len(d)))]:9.2f} "
                   f"{statistics.fmean(d):9.2f}")
     table(evs)
-    # the first burst (spans starting within 150 ms of the first request: every thread's first turn in a burst run)
-    t0 = min((e["ts"] for e in evs if e["name"] == "api_http_ttft"), default=None)
+    # the first burst: spans starting within 150 ms of the 8th request (every thread's first turn in a burst run;
+    # a lone earlier request, e.g. a readiness probe, does not start it)
+    starts = sorted(e["ts"] for e in evs if e["name"] == "api_http_ttft")
+    t0 = starts[min(7, len(starts) - 1)] - 20e3 if starts else None
     if t0 is not None:
+        print("-- request starts (ms after the first): " +
+              " ".join(f"{(t - starts[0]) / 1e3:.0f}" for t in starts[:12]) + " ...")
+        big = sorted(((e["dur"] / 1e3, (e["ts"] - starts[0]) / 1e3) for e in evs if e["name"] == "api_loop_lag"),
+                     reverse=True)[:6]
+        print("-- longest loop stalls (ms, at ms after the first request): " +
+              ", ".join(f"{d:.0f} @ {t:.0f}" for d, t in big))
         first = [e for e in evs if t0 <= e["ts"] <= t0 + 150e3]
         print("-- first burst (spans starting within 150 ms of the first request)")
         table(first)
