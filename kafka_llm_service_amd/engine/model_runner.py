@@ -228,6 +228,20 @@ def plan_prefill_items(tiles: list[tuple], hkv: int, target_wgs: int, min_chunk:
     return items, splits, ranges
 
 
+def retile(spans: list[tuple[int, int]], tile: int) -> list[tuple[int, int]]:
+    """(q0, count) token spans (ascending) -> the same tokens as (q0, count) tiles of at most ``tile`` tokens, contiguous
+    spans joined first: 8 new turns of 30 tokens back to back make 4 full tiles, not 8 half-empty ones."""
+    if tile <= 0:  # (off: the spans as they are)
+        return [tuple(t) for t in spans]
+    runs: list[list[int]] = []
+    for q0, cnt in spans:
+        if runs and runs[-1][0] + runs[-1][1] == q0:
+            runs[-1][1] += cnt
+        else:
+            runs.append([q0, cnt])
+    return [(q0 + t, min(tile, cnt - t)) for q0, cnt in runs for t in range(0, cnt, tile)]
+
+
 def merge_ranges(ranges: list[tuple[int, int]]) -> list[tuple[int, int]]:
     """Sorted union of half-open row ranges, touching ones joined (one attn_merge launch per range)."""
     out: list[tuple[int, int]] = []
@@ -501,6 +515,7 @@ class ModelRunner:
         self.fixed_decode_items = os.environ.get("KAFKA_FIXED_DECODE_ITEMS", "0") == "1"
         # a joined new turn's own keys (its history behind the shared prefix) ride in the cascade launch too
         self.join_suffix = os.environ.get("KAFKA_JOIN_SUFFIX", "1") == "1"
+        self.retile_joins = os.environ.get("KAFKA_RETILE_JOINS", "1") == "1"  # (model_runner.retile)
         self.step_events: list | None = None  # (start, end) timing events per launched step when a list is set
         # grammar masks / forced tokens / penalties inside the sampler kernel (tables allocated on first use)
         self.lp = LogitsProcessor(self.device, self.vocab, max_slots=max(256, max_num_seqs))
@@ -599,14 +614,19 @@ class ModelRunner:
                 # joined tiles' own key spans (behind the prefix): with join_suffix they are items of this launch too
                 spans = {ti: tiles[ti][3] - groups[gi][1] * PAGE for gi, js in joins.items() for ti in js} \
                     if self.join_suffix else {}
+                # the joined rows' prefix-pass tiles: the group's joined tokens re-tiled at token granularity (a burst
+                # of short new turns fills 64-token tiles instead of one mostly empty tile per turn; every key of the
+                # prefix is below every joined token's position, so tokens of different turns share a tile)
+                jt = {gi: retile([tiles[ti][:2] for ti in js], self.tile if self.retile_joins else 0)
+                      for gi, js in joins.items()}
                 # key chunks sized so the prefix pass launches ~target_wgs workgroups over all groups together
                 work = sum(-(-n // self.tile) * p * PAGE for n, p in groups) + \
-                    sum(len(js) * groups[gi][1] * PAGE for gi, js in joins.items()) + sum(spans.values())
+                    sum(len(t) * groups[gi][1] * PAGE for gi, t in jt.items()) + sum(spans.values())
                 want = max(1, self.target_wgs // self.model.hkv)
                 chunk = min(MAX_ITEM_KEYS, max(256, -(-work // (want * 32)) * 32))
                 # one round of workgroups: per-group rounding up can overshoot the target by a few items, and a
                 # second round of a handful of workgroups doubles the launch
-                tiles_per_group = [-(-n // self.tile) + len(joins.get(gi, ())) for gi, (n, _) in enumerate(groups)]
+                tiles_per_group = [-(-n // self.tile) + len(jt.get(gi, ())) for gi, (n, _) in enumerate(groups)]
                 while chunk < MAX_ITEM_KEYS and sum(t * -(-(p * PAGE) // chunk) for t, (_, p) in
                                                     zip(tiles_per_group, groups)) + \
                         sum(-(-sp // chunk) for sp in spans.values()) > want:
@@ -622,8 +642,7 @@ class ModelRunner:
                     for c in range(nc):  # chunk-major: the row tiles of one chunk run together (L2 sharing)
                         for g0 in range(r0, r0 + n, self.tile):
                             pit.append((g0, min(self.tile, r0 + n - g0), r0, c * ck, min(P, (c + 1) * ck), c, 0, 0))
-                        for ti in joins.get(gi, ()):  # prefill tiles: q rows B + q0, fp32 alt partials
-                            q0, cnt = tiles[ti][0], tiles[ti][1]
+                        for q0, cnt in jt.get(gi, ()):  # joined prefill rows: q rows B + q0, fp32 alt partials
                             pit.append((B + q0, cnt, r0, c * ck, min(P, (c + 1) * ck), c, 1, 0))
                     for ti in joins.get(gi, ()):
                         tiles[ti] = tiles[ti][:5] + (P, nc)

@@ -584,6 +584,16 @@ def test_new_turn_rows_join_the_prefix_pass(base_engine, join_suffix):
     assert outs[0] == outs[1]
 
 
+def test_retile_joins_contiguous_spans():
+    """The prefix pass re-tiles joined prefill tokens: contiguous spans are joined, then cut into full tiles."""
+    from kafka_llm_service_amd.engine.model_runner import retile
+
+    assert retile([(i * 30, 30) for i in range(8)], 64) == [(0, 64), (64, 64), (128, 64), (192, 48)]
+    assert retile([(0, 64), (64, 36), (200, 10)], 64) == [(0, 64), (64, 36), (200, 10)]
+    assert retile([(0, 37), (37, 90)], 64) == [(0, 64), (64, 63)]
+    assert retile([], 64) == []
+
+
 def test_plan_prefill_items_with_prefix_offset():
     """A tile behind a cascade prefix (lo > 0) attends only [lo, extent) and writes partials from slot s0 on."""
     from kafka_llm_service_amd.engine.model_runner import plan_prefill_items
