@@ -131,6 +131,7 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
         lag_task = None
         if trace.tracer() is not None:  # API event-loop lag (a blocked loop delays every request before its handler)
             lag_task = asyncio.get_running_loop().create_task(_loop_lag_monitor())
+            _trace_gc(trace.tracer())
         try:
             yield
         finally:
@@ -145,6 +146,18 @@ def create_app(config: ServerConfig | None = None, state: ServerState | None = N
                     ps = pstats.Stats(prof, stream=f)
                     ps.sort_stats("tottime").print_stats(45)
                     ps.sort_stats("cumtime").print_stats(60)
+
+    def _trace_gc(tr) -> None:
+        """Every cyclic-GC collection of this process as a `gc_gen<N>` span (a collection runs inside whatever
+        allocation triggered it, so a stall dump shows only the allocating frame)."""
+        t0 = [0.0]
+
+        def cb(phase, info):
+            if phase == "start":
+                t0[0] = time.perf_counter()
+            else:
+                tr.complete(f"gc_gen{info.get('generation')}", "gc", t0[0], time.perf_counter(), "gc")
+        gc.callbacks.append(cb)
 
     async def _loop_lag_monitor(period: float = 0.002) -> None:
         """Sleep `period` over and over; every wake-up later than 2 ms past its deadline is an `api_loop_lag` span

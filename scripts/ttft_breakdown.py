@@ -52,6 +52,11 @@ def main():
                      reverse=True)[:6]
         print("-- longest loop stalls (ms, at ms after the first request): " +
               ", ".join(f"{d:.0f} @ {t:.0f}" for d, t in big))
+        gcs = sorted(((e["dur"] / 1e3, (e["ts"] - starts[0]) / 1e3, e["name"]) for e in evs
+                      if e["name"].startswith("gc_gen")), reverse=True)
+        if gcs:
+            print(f"-- cyclic GC: {len(gcs)} collections, {sum(g[0] for g in gcs):.1f} ms; longest: " +
+                  ", ".join(f"{n} {d:.1f} @ {t:.0f}" for d, t, n in gcs[:5]))
         first = [e for e in evs if t0 <= e["ts"] <= t0 + 150e3]
         print("-- first burst (spans starting within 150 ms of the first request)")
         table(first)
