@@ -226,7 +226,12 @@ __global__ __launch_bounds__(SNT) void sample_kernel(const T* __restrict__ logit
     int* part = ws + SAMPLE_MAX_ROWS + ((int64_t)row * nsplit + sp) * 2;
     __hip_atomic_store(part, __float_as_int(a.v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(part + 1, a.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int t = __hip_atomic_fetch_add(tk_row, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    // the ticket as the decode kernel's (attention.hip): the agent-scope stores above have completed at the coherent
+    // level once vmcnt is 0, then a RELAXED ticket — an acq_rel one compiles to buffer_wbl2 + buffer_inv (write back
+    // and drop this XCD's whole L2) in every one of the B x nsplit workgroups; the last one reads the partials with
+    // agent-scope (sc1) loads, which do not hit a stale L2 line
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(tk_row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t != nsplit - 1) return;
     __hip_atomic_store(tk_row, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int* p0 = ws + SAMPLE_MAX_ROWS + (int64_t)row * nsplit * 2;
